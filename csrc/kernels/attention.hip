@@ -1,0 +1,539 @@
+// Flash attention (forward + backward) for gfx950, bf16 in / fp32 accumulate.
+//
+// Parity: lib/kernels/src/cuda/ops/attention_kernels.cu, which calls cuDNN's
+// monolithic cudnnMultiHeadAttnForward/BackwardData/BackwardWeights (:255,
+// :292, :316) and materialises the whole attention matrix.  Here the score
+// matrix never leaves the CU (blockwise online softmax), which is what makes
+// the long-sequence configs of SURVEY.md §5.7 possible.
+//
+// CDNA4 design (see /opt/skills/guides/cdna_hip_programming.md §3, §5.5):
+//  * MFMA v_mfma_f32_32x32x16_bf16; a workgroup = 4 waves, each wave owns 32
+//    query rows (forward, dQ) or 32 key rows (dK/dV).
+//  * "swapped" products: the forward computes S^T = K Q^T so every lane holds
+//    scores of ONE query -> the row max / row sum are lane-local plus a single
+//    exchange with lane^32; O^T = V^T P^T consumes the S^T accumulator
+//    directly as the MFMA B operand (accumulator-as-operand, no LDS round
+//    trip for P) and keeps the query on the lane, so the online-softmax
+//    rescale is a per-lane scalar multiply.
+//  * K/V tiles are staged global->registers->LDS with the next tile's loads
+//    issued before the current tile's MFMAs (async-STAGE split, T14), double
+//    buffered, one barrier per tile.
+//  * LDS images are XOR-swizzled per row so ds_read_b128 row reads are
+//    conflict-free; V^T (and K^T / Q^T / dO^T in the backward) operands come
+//    from ds_read_b64_tr_b16 hardware-transposed reads of the same images.
+//  * backward = dK/dV kernel (key block resident, loops over query tiles,
+//    key on the lane) + dQ kernel (query block resident) -> no float atomics,
+//    deterministic, no [N, N] buffers; delta = rowsum(dO*O) precomputed.
+//
+// Tensor addressing: every tensor is [B, S, H, D] with arbitrary strides for
+// b / s / h and contiguous d, so the fused QKV projection output
+// [B, S, 3, H, D] is consumed in place.  LSE is [B, H, S] fp32, log2 domain.
+#include "kernels.h"
+#include "mfma.h"
+
+namespace ffk {
+
+struct TensorView {
+  const bf16* p;
+  int64_t sb, ss, sh;  // element strides; d is contiguous
+};
+
+struct AttnParams {
+  TensorView q, k, v, o, dout;
+  bf16 *o_out, *dq, *dk, *dv;
+  int64_t o_sb, o_ss, o_sh;                   // output strides (o_out)
+  int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
+  float* lse;    // [B, H, Sq] log2-domain
+  float* delta;  // [B, H, Sq]
+  int B, H, Sq, Sk;
+  float scale;       // softmax scale (1/sqrt(D) by default)
+  float scale_log2;  // scale * log2(e)
+};
+
+template <int D>
+__device__ __forceinline__ int lds_off(int r, int c) {  // byte offset of chunk c of row r
+  return img_off<D * 2>(r, c);
+}
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned char* img, int row0, int dt, int lane) {
+  return tr_frag_acc<D * 2>(img, row0, dt * 32, lane);
+}
+
+// Global [rows][D] tile -> registers (each thread `per` chunks of 16 B).
+template <int D, int ROWS>
+struct TileLoader {
+  static constexpr int CHUNKS = ROWS * D / 8;
+  static constexpr int PER = CHUNKS / 256;
+  bf16x8 reg[PER];
+  __device__ __forceinline__ void load(const TensorView& t, int b, int h, int row0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int r = c / (D / 8), ch = c % (D / 8);
+      if (row0 + r < nrows) {
+        reg[i] = *reinterpret_cast<const bf16x8*>(t.p + b * t.sb + static_cast<int64_t>(row0 + r) * t.ss +
+                                                  h * t.sh + ch * 8);
+      } else {
+        reg[i] = bf16x8{};
+      }
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* img) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int r = c / (D / 8), ch = c % (D / 8);
+      *reinterpret_cast<bf16x8*>(img + lds_off<D>(r, ch)) = reg[i];
+    }
+  }
+};
+
+// ===========================================================================
+// Forward
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
+  constexpr int KS = D / 16;        // k-steps over the head dim
+  constexpr int DT = D / 32;        // 32-wide output tiles over the head dim
+  constexpr int KV = 64;            // keys per tile
+  constexpr int TILE_BYTES = KV * D * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];  // K0 V0 K1 V1
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int bh = blockIdx.y, b = bh / P.H, hh = bh % P.H;
+  const int q_blk = blockIdx.x * 128;
+  const int qw = q_blk + wave * 32;
+  const int q = qw + (lane & 31);
+  const bool q_ok = q < P.Sq;
+
+  // Q as the B operand of S^T = K Q^T: lane holds Q[q][16ks + 8h .. +8]
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    qf[ks] = q_ok ? *reinterpret_cast<const bf16x8*>(P.q.p + b * P.q.sb + static_cast<int64_t>(q) * P.q.ss +
+                                                     hh * P.q.sh + ks * 16 + 8 * h)
+                  : bf16x8{};
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  int n_tiles = (P.Sk + KV - 1) / KV;
+  if (CAUSAL) n_tiles = min(n_tiles, (q_blk + 128 + KV - 1) / KV);
+
+  TileLoader<D, KV> kl, vl;
+  kl.load(P.k, b, hh, 0, P.Sk);
+  vl.load(P.v, b, hh, 0, P.Sk);
+  kl.store(smem);
+  vl.store(smem + TILE_BYTES);
+  __syncthreads();
+
+  for (int t = 0; t < n_tiles; ++t) {
+    const int k0 = t * KV;
+    const unsigned char* Kt = smem + (t & 1) * 2 * TILE_BYTES;
+    const unsigned char* Vt = Kt + TILE_BYTES;
+    const bool has_next = t + 1 < n_tiles;
+    if (has_next) {  // issue next tile's HBM loads before this tile's MFMAs
+      kl.load(P.k, b, hh, k0 + KV, P.Sk);
+      vl.load(P.v, b, hh, k0 + KV, P.Sk);
+    }
+    const bool wave_active = !CAUSAL || (k0 <= qw + 31);
+    if (wave_active) {
+      // ---- S^T[key][q] for two 32-key tiles
+      f32x16 s[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          bf16x8 kf = lds_read16(Kt, lds_off<D>(kt * 32 + (lane & 31), 2 * ks + h));
+          s[kt] = mfma32(kf, qf[ks], s[kt]);
+        }
+      }
+      // ---- scale, mask, tile max
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float x = s[kt][r] * P.scale_log2;
+          if (key >= P.Sk || (CAUSAL && key > q)) x = -INFINITY;
+          s[kt][r] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m, tmax);
+      const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+      const float msub = (m_new == -INFINITY) ? 0.f : m_new;
+      m = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pv = exp2f(s[kt][r] - msub);
+          s[kt][r] = pv;
+          psum += pv;
+        }
+      l = l * alpha + psum;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      // ---- O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 pf = acc_to_frag(s[kt], st);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            bf16x8 vf = tr_frag<D>(Vt, kt * 32 + 16 * st, dt, lane);
+            o[dt] = mfma32(vf, pf, o[dt]);
+          }
+        }
+    }
+    if (has_next) {
+      unsigned char* nxt = smem + ((t + 1) & 1) * 2 * TILE_BYTES;
+      kl.store(nxt);
+      vl.store(nxt + TILE_BYTES);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: O = O^T / l, LSE
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (q_ok) {
+    bf16* orow = P.o_out + b * P.o_sb + static_cast<int64_t>(q) * P.o_ss + hh * P.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * g4 + e] * inv);
+        *reinterpret_cast<bf16x4*>(orow + dt * 32 + 8 * g4 + 4 * h) = v;
+      }
+    if (h == 0) P.lse[static_cast<int64_t>(bh) * P.Sq + q] = (lt > 0.f) ? m + log2f(lt) : -INFINITY;
+  }
+}
+
+// ===========================================================================
+// Backward preprocessing: delta[b,h,q] = sum_d dO[q][d] * O[q][d]
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams P) {
+  constexpr int TPR = D / 8;  // threads per row
+  const int64_t rows = static_cast<int64_t>(P.B) * P.H * P.Sq;
+  const int64_t row = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) / TPR;
+  const int c = threadIdx.x % TPR;
+  float acc = 0.f;
+  if (row < rows) {
+    const int q = static_cast<int>(row % P.Sq);
+    const int bh = static_cast<int>(row / P.Sq);
+    const int b = bh / P.H, hh = bh % P.H;
+    u16x8 a = *reinterpret_cast<const u16x8*>(P.o.p + b * P.o.sb + static_cast<int64_t>(q) * P.o.ss +
+                                              hh * P.o.sh + c * 8);
+    u16x8 d = *reinterpret_cast<const u16x8*>(P.dout.p + b * P.dout.sb + static_cast<int64_t>(q) * P.dout.ss +
+                                              hh * P.dout.sh + c * 8);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += u2f(a[k]) * u2f(d[k]);
+  }
+#pragma unroll
+  for (int o = TPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (row < rows && c == 0) P.delta[row] = acc;
+}
+
+// ===========================================================================
+// dQ: query block resident (4 waves x 32 rows), loop over 64-key tiles.
+//   S^T = K Q^T ; P^T = exp2(S^T*c - lse) ; dP^T = V dO^T ;
+//   dS^T = P^T (dP^T - delta) ; dQ^T += K^T dS^T ; dQ = scale * dQ
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(AttnParams P) {
+  constexpr int KS = D / 16, DT = D / 32, KV = 64;
+  constexpr int TILE_BYTES = KV * D * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int bh = blockIdx.y, b = bh / P.H, hh = bh % P.H;
+  const int q_blk = blockIdx.x * 128;
+  const int qw = q_blk + wave * 32;
+  const int q = qw + (lane & 31);
+  const bool q_ok = q < P.Sq;
+
+  bf16x8 qf[KS], df[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = q_ok ? *reinterpret_cast<const bf16x8*>(P.q.p + b * P.q.sb + static_cast<int64_t>(q) * P.q.ss +
+                                                     hh * P.q.sh + ks * 16 + 8 * h)
+                  : bf16x8{};
+    df[ks] = q_ok ? *reinterpret_cast<const bf16x8*>(P.dout.p + b * P.dout.sb +
+                                                     static_cast<int64_t>(q) * P.dout.ss + hh * P.dout.sh +
+                                                     ks * 16 + 8 * h)
+                  : bf16x8{};
+  }
+  const float lse = q_ok ? P.lse[static_cast<int64_t>(bh) * P.Sq + q] : 0.f;
+  const float dlt = q_ok ? P.delta[static_cast<int64_t>(bh) * P.Sq + q] : 0.f;
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x16{};
+
+  int n_tiles = (P.Sk + KV - 1) / KV;
+  if (CAUSAL) n_tiles = min(n_tiles, (q_blk + 128 + KV - 1) / KV);
+
+  TileLoader<D, KV> kl, vl;
+  kl.load(P.k, b, hh, 0, P.Sk);
+  vl.load(P.v, b, hh, 0, P.Sk);
+  kl.store(smem);
+  vl.store(smem + TILE_BYTES);
+  __syncthreads();
+
+  for (int t = 0; t < n_tiles; ++t) {
+    const int k0 = t * KV;
+    const unsigned char* Kt = smem + (t & 1) * 2 * TILE_BYTES;
+    const unsigned char* Vt = Kt + TILE_BYTES;
+    const bool has_next = t + 1 < n_tiles;
+    if (has_next) {
+      kl.load(P.k, b, hh, k0 + KV, P.Sk);
+      vl.load(P.v, b, hh, k0 + KV, P.Sk);
+    }
+    const bool wave_active = !CAUSAL || (k0 <= qw + 31);
+    if (wave_active) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int off = lds_off<D>(kt * 32 + (lane & 31), 2 * ks + h);
+          s = mfma32(lds_read16(Kt, off), qf[ks], s);
+          dp = mfma32(lds_read16(Vt, off), df[ks], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float pv = exp2f(s[r] * P.scale_log2 - lse);
+          if (key >= P.Sk || (CAUSAL && key > q) || !q_ok) pv = 0.f;
+          s[r] = pv * (dp[r] - dlt);  // dS^T
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 sf = acc_to_frag(s, st);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_frag<D>(Kt, kt * 32 + 16 * st, dt, lane), sf, dq[dt]);
+        }
+      }
+    }
+    if (has_next) {
+      unsigned char* nxt = smem + ((t + 1) & 1) * 2 * TILE_BYTES;
+      kl.store(nxt);
+      vl.store(nxt + TILE_BYTES);
+    }
+    __syncthreads();
+  }
+  if (q_ok) {
+    bf16* row = P.dq + b * P.dq_sb + static_cast<int64_t>(q) * P.dq_ss + hh * P.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(dq[dt][4 * g4 + e] * P.scale);
+        *reinterpret_cast<bf16x4*>(row + dt * 32 + 8 * g4 + 4 * h) = v;
+      }
+  }
+}
+
+// ===========================================================================
+// dK / dV: key block resident (4 waves x 32 keys), loop over 64-query tiles.
+//   S = Q K^T (key on lane) ; P = exp2(S*c - lse[q]) ; dP = dO V^T ;
+//   dS = P (dP - delta[q]) ; dV^T += dO^T P ; dK^T += Q^T dS ; dK = scale*dK
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(AttnParams P) {
+  constexpr int KS = D / 16, DT = D / 32, QT = 64;
+  constexpr int TILE_BYTES = QT * D * 2;
+  constexpr int STAGE = 2 * TILE_BYTES + 2 * QT * 4;  // Q, dO, lse, delta
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int bh = blockIdx.y, b = bh / P.H, hh = bh % P.H;
+  const int k_blk = blockIdx.x * 128;
+  const int kw = k_blk + wave * 32;
+  const int key = kw + (lane & 31);
+  const bool k_ok = key < P.Sk;
+
+  // K, V rows as B operands (lane holds row `key`, d = 16ks + 8h ..)
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = k_ok ? *reinterpret_cast<const bf16x8*>(P.k.p + b * P.k.sb + static_cast<int64_t>(key) * P.k.ss +
+                                                     hh * P.k.sh + ks * 16 + 8 * h)
+                  : bf16x8{};
+    vf[ks] = k_ok ? *reinterpret_cast<const bf16x8*>(P.v.p + b * P.v.sb + static_cast<int64_t>(key) * P.v.ss +
+                                                     hh * P.v.sh + ks * 16 + 8 * h)
+                  : bf16x8{};
+  }
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x16{};
+
+  const int n_q_tiles = (P.Sq + QT - 1) / QT;
+  const int t0 = CAUSAL ? (k_blk / QT) : 0;
+
+  TileLoader<D, QT> ql, dl;
+  auto load_scalars = [&](unsigned char* stage, int q0) {
+    float* ls = reinterpret_cast<float*>(stage + 2 * TILE_BYTES);
+    float* ds = ls + QT;
+    if (threadIdx.x < QT) {
+      const int qq = q0 + threadIdx.x;
+      ls[threadIdx.x] = qq < P.Sq ? P.lse[static_cast<int64_t>(bh) * P.Sq + qq] : INFINITY;
+      ds[threadIdx.x] = qq < P.Sq ? P.delta[static_cast<int64_t>(bh) * P.Sq + qq] : 0.f;
+    }
+  };
+  if (t0 < n_q_tiles) {
+    ql.load(P.q, b, hh, t0 * QT, P.Sq);
+    dl.load(P.dout, b, hh, t0 * QT, P.Sq);
+    ql.store(smem);
+    dl.store(smem + TILE_BYTES);
+    load_scalars(smem, t0 * QT);
+  }
+  __syncthreads();
+
+  for (int t = t0; t < n_q_tiles; ++t) {
+    const int q0 = t * QT;
+    unsigned char* stage = smem + ((t - t0) & 1) * STAGE;
+    const unsigned char* Qt = stage;
+    const unsigned char* Dt = stage + TILE_BYTES;
+    const float* ls = reinterpret_cast<const float*>(stage + 2 * TILE_BYTES);
+    const float* ds = ls + QT;
+    const bool has_next = t + 1 < n_q_tiles;
+    if (has_next) {
+      ql.load(P.q, b, hh, q0 + QT, P.Sq);
+      dl.load(P.dout, b, hh, q0 + QT, P.Sq);
+    }
+    const bool wave_active = !CAUSAL || (q0 + QT - 1 >= kw);
+    if (wave_active) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int off = lds_off<D>(qt * 32 + (lane & 31), 2 * ks + h);
+          s = mfma32(lds_read16(Qt, off), kf[ks], s);
+          dp = mfma32(lds_read16(Dt, off), vf[ks], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int qq = q0 + ql_;
+          float pv = exp2f(s[r] * P.scale_log2 - ls[ql_]);
+          if (qq >= P.Sq || (CAUSAL && key > qq) || !k_ok) pv = 0.f;
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - ds[ql_]);
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 pf = acc_to_frag(s, st);
+          bf16x8 sf = acc_to_frag(dp, st);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            dv[dt] = mfma32(tr_frag<D>(Dt, qt * 32 + 16 * st, dt, lane), pf, dv[dt]);
+            dk[dt] = mfma32(tr_frag<D>(Qt, qt * 32 + 16 * st, dt, lane), sf, dk[dt]);
+          }
+        }
+      }
+    }
+    if (has_next) {
+      unsigned char* nxt = smem + ((t + 1 - t0) & 1) * STAGE;
+      ql.store(nxt);
+      dl.store(nxt + TILE_BYTES);
+      load_scalars(nxt, q0 + QT);
+    }
+    __syncthreads();
+  }
+  if (k_ok) {
+    bf16* krow = P.dk + b * P.dk_sb + static_cast<int64_t>(key) * P.dk_ss + hh * P.dk_sh;
+    bf16* vrow = P.dv + b * P.dv_sb + static_cast<int64_t>(key) * P.dv_ss + hh * P.dv_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 a, c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = f2bf(dk[dt][4 * g4 + e] * P.scale);
+          c[e] = f2bf(dv[dt][4 * g4 + e]);
+        }
+        *reinterpret_cast<bf16x4*>(krow + dt * 32 + 8 * g4 + 4 * h) = a;
+        *reinterpret_cast<bf16x4*>(vrow + dt * 32 + 8 * g4 + 4 * h) = c;
+      }
+  }
+}
+
+// ===========================================================================
+static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, float scale) {
+  AttnParams P{};
+  auto tv = [](const AttnTensors::T& x) {
+    return TensorView{static_cast<const bf16*>(x.p), x.sb, x.ss, x.sh};
+  };
+  P.q = tv(t.q);
+  P.k = tv(t.k);
+  P.v = tv(t.v);
+  P.o = tv(t.o);
+  P.dout = tv(t.dout);
+  P.o_out = static_cast<bf16*>(const_cast<void*>(t.o.p));
+  P.o_sb = t.o.sb; P.o_ss = t.o.ss; P.o_sh = t.o.sh;
+  P.dq = static_cast<bf16*>(const_cast<void*>(t.dq.p));
+  P.dq_sb = t.dq.sb; P.dq_ss = t.dq.ss; P.dq_sh = t.dq.sh;
+  P.dk = static_cast<bf16*>(const_cast<void*>(t.dk.p));
+  P.dk_sb = t.dk.sb; P.dk_ss = t.dk.ss; P.dk_sh = t.dk.sh;
+  P.dv = static_cast<bf16*>(const_cast<void*>(t.dv.p));
+  P.dv_sb = t.dv.sb; P.dv_ss = t.dv.ss; P.dv_sh = t.dv.sh;
+  P.lse = t.lse;
+  P.delta = t.delta;
+  P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
+  P.scale = scale;
+  P.scale_log2 = scale * 1.4426950408889634f;
+  (void)D;
+  return P;
+}
+
+void attention_fwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, float scale, bool causal,
+                   hipStream_t st) {
+  AttnParams P = make_params(t, B, H, Sq, Sk, D, scale);
+  dim3 grid((Sq + 127) / 128, B * H), block(256);
+  if (D == 64) {
+    if (causal) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, block, 0, st, P);
+    else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, block, 0, st, P);
+  } else if (D == 128) {
+    if (causal) hipLaunchKernelGGL((attn_fwd_kernel<128, true>), grid, block, 0, st, P);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, false>), grid, block, 0, st, P);
+  } else {
+    throw std::invalid_argument("attention: head dim must be 64 or 128");
+  }
+  FFK_LAUNCH_CHECK("attention_fwd");
+}
+
+void attention_bwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, float scale, bool causal,
+                   hipStream_t st) {
+  AttnParams P = make_params(t, B, H, Sq, Sk, D, scale);
+  const int64_t rows = static_cast<int64_t>(B) * H * Sq;
+  const int tpr = D / 8;
+  dim3 gd(static_cast<unsigned>((rows * tpr + 255) / 256));
+  dim3 gq((Sq + 127) / 128, B * H), gk((Sk + 127) / 128, B * H), block(256);
+#define FFK_ATTN_BWD(DD, CC)                                                          \
+  hipLaunchKernelGGL((attn_bwd_delta_kernel<DD>), gd, block, 0, st, P);               \
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, CC>), gk, block, 0, st, P);            \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, CC>), gq, block, 0, st, P)
+  if (D == 64) {
+    if (causal) { FFK_ATTN_BWD(64, true); }
+    else { FFK_ATTN_BWD(64, false); }
+  } else if (D == 128) {
+    if (causal) { FFK_ATTN_BWD(128, true); }
+    else { FFK_ATTN_BWD(128, false); }
+  } else {
+    throw std::invalid_argument("attention: head dim must be 64 or 128");
+  }
+#undef FFK_ATTN_BWD
+  FFK_LAUNCH_CHECK("attention_bwd");
+}
+
+}  // namespace ffk

@@ -1,0 +1,121 @@
+// pybind11 module `_ffkernels`: thin launchers over the gfx950 kernel library.
+// Pointers and streams cross as integers (tensor.data_ptr(),
+// torch.cuda.current_stream().cuda_stream); validation of shapes / dtypes /
+// contiguity happens in flexflow_train_amd/kernels/__init__.py before any
+// launch.  Errors from the launch path surface as Python exceptions.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace ffk;
+
+static inline void* P(uintptr_t p) { return reinterpret_cast<void*>(p); }
+static inline float* F(uintptr_t p) { return reinterpret_cast<float*>(p); }
+static inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static AttnTensors::T tview(const py::tuple& t) {
+  AttnTensors::T r;
+  if (t.size() != 4) throw std::invalid_argument("attention tensor view must be (ptr, sb, ss, sh)");
+  r.p = P(t[0].cast<uintptr_t>());
+  r.sb = t[1].cast<int64_t>();
+  r.ss = t[2].cast<int64_t>();
+  r.sh = t[3].cast<int64_t>();
+  return r;
+}
+
+PYBIND11_MODULE(_ffkernels, m) {
+  m.doc() = "flexflow_train_amd gfx950 HIP kernels";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("layernorm_fwd", [](int dt, uintptr_t x, uintptr_t res, uintptr_t sum_out, uintptr_t g, uintptr_t b,
+                            uintptr_t y, uintptr_t mean, uintptr_t rstd, int M, int N, float eps, uintptr_t st) {
+    layernorm_fwd(dt, P(x), P(res), P(sum_out), P(g), P(b), P(y), F(mean), F(rstd), M, N, eps, S(st));
+  });
+  m.def("layernorm_bwd", [](int dt, uintptr_t dy, uintptr_t s, uintptr_t mean, uintptr_t rstd, uintptr_t g,
+                            uintptr_t dx, uintptr_t dg, uintptr_t db, int M, int N, uintptr_t st) {
+    layernorm_bwd(dt, P(dy), P(s), F(mean), F(rstd), P(g), P(dx), F(dg), F(db), M, N, S(st));
+  });
+  m.def("bias_act_fwd", [](int dt, uintptr_t x, uintptr_t bias, uintptr_t pre, uintptr_t y, int64_t M, int64_t N,
+                           int op, float alpha, uintptr_t st) {
+    bias_act_fwd(dt, P(x), P(bias), P(pre), P(y), M, N, op, alpha, S(st));
+  });
+  m.def("act_bwd", [](int dt, uintptr_t dy, uintptr_t pre, uintptr_t dx, int64_t n, int op, float alpha,
+                      uintptr_t st) { act_bwd(dt, P(dy), P(pre), P(dx), n, op, alpha, S(st)); });
+  m.def("colsum_act", [](int dt, uintptr_t dy, uintptr_t pre, uintptr_t dx, uintptr_t dbias, int64_t M, int64_t N,
+                         int op, float alpha, uintptr_t st) {
+    colsum_act(dt, P(dy), P(pre), P(dx), F(dbias), M, N, op, alpha, S(st));
+  });
+  m.def("dropout_fwd", [](int dt, uintptr_t x, uintptr_t y, int64_t n, float p, uint64_t seed, uintptr_t st) {
+    dropout_fwd(dt, P(x), P(y), n, p, seed, S(st));
+  });
+  m.def("cast", [](int di, int dout, uintptr_t x, uintptr_t y, int64_t n, uintptr_t st) {
+    cast(di, dout, P(x), P(y), n, S(st));
+  });
+  m.def("axpby", [](int dt, uintptr_t x, uintptr_t y, int64_t n, float a, float b, uintptr_t st) {
+    axpby(dt, P(x), P(y), n, a, b, S(st));
+  });
+  m.def("softmax_ce", [](int dt, int label_bits, uintptr_t logits, uintptr_t labels, uintptr_t row_loss,
+                         uintptr_t metrics, int M, int V, int V_valid, float grad_scale, int ignore_index,
+                         int write_grad, uintptr_t st) {
+    softmax_ce(dt, label_bits, P(logits), P(labels), F(row_loss), F(metrics), M, V, V_valid, grad_scale,
+               ignore_index, write_grad, S(st));
+  });
+  m.def("softmax_fwd", [](int dt, uintptr_t x, uintptr_t y, int M, int N, uintptr_t st) {
+    softmax_fwd(dt, P(x), P(y), M, N, S(st));
+  });
+  m.def("softmax_bwd", [](int dt, uintptr_t dy, uintptr_t y, uintptr_t dx, int M, int N, uintptr_t st) {
+    softmax_bwd(dt, P(dy), P(y), P(dx), M, N, S(st));
+  });
+  m.def("adam_step", [](uintptr_t w, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t wb, int64_t n, float lr,
+                        float b1, float b2, float eps, float wd, int step, float gs, int decoupled, uintptr_t st) {
+    adam_step(F(w), F(g), F(mm), F(v), P(wb), n, lr, b1, b2, eps, wd, step, gs, decoupled, S(st));
+  });
+  m.def("sgd_step", [](uintptr_t w, uintptr_t g, uintptr_t mom, uintptr_t wb, int64_t n, float lr, float momentum,
+                       float wd, int nesterov, float gs, uintptr_t st) {
+    sgd_step(F(w), F(g), F(mom), P(wb), n, lr, momentum, wd, nesterov, gs, S(st));
+  });
+  m.def("sum_squares", [](uintptr_t x, int64_t n, uintptr_t out, uintptr_t st) {
+    sum_squares(F(x), n, F(out), S(st));
+  });
+  m.def("embedding_fwd", [](int dt, int ib, uintptr_t idx, uintptr_t W, uintptr_t out, int64_t B, int L, int D,
+                            int mode, int64_t n, uintptr_t st) {
+    embedding_fwd(dt, ib, P(idx), P(W), P(out), B, L, D, mode, n, S(st));
+  });
+  m.def("embedding_bwd", [](int dt, int ib, uintptr_t idx, uintptr_t dout, uintptr_t dW, int64_t B, int L, int D,
+                            int mode, int64_t n, uintptr_t st) {
+    embedding_bwd(dt, ib, P(idx), P(dout), F(dW), B, L, D, mode, n, S(st));
+  });
+  m.def("attention_fwd", [](py::tuple q, py::tuple k, py::tuple v, py::tuple o, uintptr_t lse, int B, int H, int Sq,
+                            int Sk, int D, float scale, bool causal, uintptr_t st) {
+    AttnTensors t;
+    t.q = tview(q);
+    t.k = tview(k);
+    t.v = tview(v);
+    t.o = tview(o);
+    t.lse = F(lse);
+    attention_fwd(t, B, H, Sq, Sk, D, scale, causal, S(st));
+  });
+  m.def("attention_bwd", [](py::tuple q, py::tuple k, py::tuple v, py::tuple o, py::tuple dout, py::tuple dq,
+                            py::tuple dk, py::tuple dv, uintptr_t lse, uintptr_t delta, int B, int H, int Sq, int Sk,
+                            int D, float scale, bool causal, uintptr_t st) {
+    AttnTensors t;
+    t.q = tview(q);
+    t.k = tview(k);
+    t.v = tview(v);
+    t.o = tview(o);
+    t.dout = tview(dout);
+    t.dq = tview(dq);
+    t.dk = tview(dk);
+    t.dv = tview(dv);
+    t.lse = F(lse);
+    t.delta = F(delta);
+    attention_bwd(t, B, H, Sq, Sk, D, scale, causal, S(st));
+  });
+  m.def("gemm", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int M, int N, int K,
+                   int lda, int ldb, int ldc, bool ta, bool tb, int act, float alpha, float beta, int out_f32,
+                   uintptr_t st) {
+    gemm_bf16_ex(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32, S(st));
+  });
+}

@@ -1,0 +1,297 @@
+// Elementwise / activation / reduction-by-column kernels for gfx950.
+//
+// Parity: lib/kernels/src/cuda/ops/element_unary_kernels.cu (ReLU / Sigmoid /
+// Tanh / ELU / GELU / Exp / ... forward + backward), cuda_helper.cu
+// (gelu_forward_kernel, relu/sigmoid backward, apply_add, scale), linear bias
+// gradient (linear_kernels.cu:280, a GEMM with a ones vector there), dropout
+// (dropout_kernels.cu, cuDNN there), cast_kernels.cu.
+// CDNA4 design: every kernel moves 16 B per lane; the activation backward and
+// the bias gradient are one pass (column sums kept in registers across rows,
+// then an LDS reduce over the block and one fp32 atomic per column);
+// dropout regenerates its mask from a counter hash instead of storing it.
+#include "common.h"
+#include "kernels.h"
+
+namespace ffk {
+
+enum Act : int { kIdentity = 0, kRelu = 1, kSigmoid = 2, kTanh = 3, kGelu = 4, kElu = 5, kExp = 6 };
+
+__device__ __forceinline__ float act_apply(int op, float x, float alpha) {
+  switch (op) {
+    case kRelu: return x > 0.f ? x : 0.f;
+    case kSigmoid: return 1.f / (1.f + __expf(-x));
+    case kTanh: return tanhf(x);
+    case kGelu: return gelu_tanh(x);
+    case kElu: return x > 0.f ? x : alpha * (__expf(x) - 1.f);
+    case kExp: return __expf(x);
+    default: return x;
+  }
+}
+// derivative w.r.t. the pre-activation x
+__device__ __forceinline__ float act_grad(int op, float x, float alpha) {
+  switch (op) {
+    case kRelu: return x > 0.f ? 1.f : 0.f;
+    case kSigmoid: {
+      float s = 1.f / (1.f + __expf(-x));
+      return s * (1.f - s);
+    }
+    case kTanh: {
+      float t = tanhf(x);
+      return 1.f - t * t;
+    }
+    case kGelu: return gelu_tanh_grad(x);
+    case kElu: return x > 0.f ? 1.f : alpha * __expf(x);
+    case kExp: return __expf(x);
+    default: return 1.f;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float* o);
+template <>
+__device__ __forceinline__ void ld8<bf16>(const bf16* p, float* o) {
+  u16x8 v = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = u2f(v[i]);
+}
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, float* o) {
+  f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[i] = a[i];
+    o[i + 4] = b[i];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float* o);
+template <>
+__device__ __forceinline__ void st8<bf16>(bf16* p, const float* o) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = f2bf(o[i]);
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void st8<float>(float* p, const float* o) {
+  f32x4 a, b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a[i] = o[i];
+    b[i] = o[i + 4];
+  }
+  reinterpret_cast<f32x4*>(p)[0] = a;
+  reinterpret_cast<f32x4*>(p)[1] = b;
+}
+
+// ---------------------------------------------------------------------------
+// y = act(x [+ bias]); optionally pre = x + bias.  x: [M, N] row-major; n8 = M*N/8.
+template <typename T>
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__ x, const T* __restrict__ bias,
+                                                           T* __restrict__ pre, T* __restrict__ y, int64_t n8,
+                                                           int N, int op, float alpha) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    float v[8];
+    ld8<T>(x + i * 8, v);
+    if (bias) {
+      float b[8];
+      ld8<T>(bias + (i * 8) % N, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += b[k];
+      if (pre) st8<T>(pre + i * 8, v);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = act_apply(op, v[k], alpha);
+    st8<T>(y + i * 8, v);
+  }
+}
+
+// dx = dy * act'(pre).  Element-wise (no bias grad).
+template <typename T>
+__global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ pre,
+                                                      T* __restrict__ dx, int64_t n8, int op, float alpha) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    float d[8], p[8];
+    ld8<T>(dy + i * 8, d);
+    ld8<T>(pre + i * 8, p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] *= act_grad(op, p[k], alpha);
+    st8<T>(dx + i * 8, d);
+  }
+}
+
+// Column-sum (bias gradient), optionally fused with the activation backward:
+//   g = dy * act'(pre) (if pre) ; dx = g (if dx) ; dbias += sum_rows g
+// grid = (ceil(N/512), row_splits); block = 4 waves over the same 512 columns.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_act_kernel(const T* __restrict__ dy, const T* __restrict__ pre,
+                                                         T* __restrict__ dx, float* __restrict__ dbias, int M,
+                                                         int N, int op, float alpha) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + lane * 8;
+  const bool active = col < N;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const int rows_per = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(M, r0 + rows_per);
+  if (active) {
+    for (int r = r0 + wave; r < r1; r += 4) {
+      const size_t off = static_cast<size_t>(r) * N + col;
+      float d[8];
+      ld8<T>(dy + off, d);
+      if (pre) {
+        float p[8];
+        ld8<T>(pre + off, p);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] *= act_grad(op, p[k], alpha);
+      }
+      if (dx) st8<T>(dx + off, d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += d[k];
+    }
+  }
+  if (!dbias) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[wave][lane * 8 + k] = acc[k];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 512; j += 256) {
+    const int c = blockIdx.x * 512 + j;
+    if (c < N) atomicAdd(dbias + c, red[0][j] + red[1][j] + red[2][j] + red[3][j]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dropout with a regenerated mask: y = x * keep / (1-p)
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n8,
+                                                      float p, uint64_t seed) {
+  const float scale = 1.f / (1.f - p);
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    float v[8];
+    ld8<T>(x + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = uniform01(seed, i * 8 + k) >= p ? v[k] * scale : 0.f;
+    st8<T>(y + i * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n8) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    float v[8];
+    ld8<TI>(x + i * 8, v);
+    st8<TO>(y + i * 8, v);
+  }
+}
+
+// y = a*x + b*y
+template <typename T>
+__global__ __launch_bounds__(256) void axpby_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n8, float a,
+                                                    float b) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    float u[8], v[8];
+    ld8<T>(x + i * 8, u);
+    ld8<T>(y + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = a * u[k] + b * v[k];
+    st8<T>(y + i * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+static void need8(int64_t n, const char* what) {
+  if (n % 8 != 0) throw std::invalid_argument(std::string(what) + ": element count must be a multiple of 8");
+}
+
+void bias_act_fwd(int dtype, const void* x, const void* bias, void* pre, void* y, int64_t M, int64_t N, int op,
+                  float alpha, hipStream_t st) {
+  need8(N, "bias_act_fwd");
+  int64_t n8 = M * N / 8;
+  int grid = grid_for(n8, 256, 256 * 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(bias_act_fwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(x),
+                       static_cast<const bf16*>(bias), static_cast<bf16*>(pre), static_cast<bf16*>(y), n8,
+                       static_cast<int>(N), op, alpha);
+  else if (dtype == kF32)
+    hipLaunchKernelGGL(bias_act_fwd_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(x),
+                       static_cast<const float*>(bias), static_cast<float*>(pre), static_cast<float*>(y), n8,
+                       static_cast<int>(N), op, alpha);
+  else throw std::invalid_argument("bias_act_fwd: dtype");
+  FFK_LAUNCH_CHECK("bias_act_fwd");
+}
+
+void act_bwd(int dtype, const void* dy, const void* pre, void* dx, int64_t n, int op, float alpha, hipStream_t st) {
+  need8(n, "act_bwd");
+  int grid = grid_for(n / 8, 256, 256 * 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(act_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(dy),
+                       static_cast<const bf16*>(pre), static_cast<bf16*>(dx), n / 8, op, alpha);
+  else if (dtype == kF32)
+    hipLaunchKernelGGL(act_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(dy),
+                       static_cast<const float*>(pre), static_cast<float*>(dx), n / 8, op, alpha);
+  else throw std::invalid_argument("act_bwd: dtype");
+  FFK_LAUNCH_CHECK("act_bwd");
+}
+
+void colsum_act(int dtype, const void* dy, const void* pre, void* dx, float* dbias, int64_t M, int64_t N, int op,
+                float alpha, hipStream_t st) {
+  need8(N, "colsum_act");
+  int gx = static_cast<int>((N + 511) / 512);
+  // enough row splits to put ~4 blocks per CU on the chip
+  int gy = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 63) / 64)));
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(colsum_act_kernel<bf16>, dim3(gx, gy), dim3(256), 0, st, static_cast<const bf16*>(dy),
+                       static_cast<const bf16*>(pre), static_cast<bf16*>(dx), dbias, static_cast<int>(M),
+                       static_cast<int>(N), op, alpha);
+  else if (dtype == kF32)
+    hipLaunchKernelGGL(colsum_act_kernel<float>, dim3(gx, gy), dim3(256), 0, st, static_cast<const float*>(dy),
+                       static_cast<const float*>(pre), static_cast<float*>(dx), dbias, static_cast<int>(M),
+                       static_cast<int>(N), op, alpha);
+  else throw std::invalid_argument("colsum_act: dtype");
+  FFK_LAUNCH_CHECK("colsum_act");
+}
+
+void dropout_fwd(int dtype, const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st) {
+  need8(n, "dropout");
+  int grid = grid_for(n / 8, 256, 256 * 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16>, dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(x),
+                       static_cast<bf16*>(y), n / 8, p, seed);
+  else if (dtype == kF32)
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(x),
+                       static_cast<float*>(y), n / 8, p, seed);
+  else throw std::invalid_argument("dropout: dtype");
+  FFK_LAUNCH_CHECK("dropout");
+}
+
+void cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, hipStream_t st) {
+  need8(n, "cast");
+  int grid = grid_for(n / 8, 256, 256 * 8);
+  if (dtype_in == kF32 && dtype_out == kBF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid), dim3(256), 0, st, static_cast<const float*>(x),
+                       static_cast<bf16*>(y), n / 8);
+  else if (dtype_in == kBF16 && dtype_out == kF32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(x),
+                       static_cast<float*>(y), n / 8);
+  else throw std::invalid_argument("cast: unsupported dtype pair");
+  FFK_LAUNCH_CHECK("cast");
+}
+
+void axpby(int dtype, const void* x, void* y, int64_t n, float a, float b, hipStream_t st) {
+  need8(n, "axpby");
+  int grid = grid_for(n / 8, 256, 256 * 8);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(axpby_kernel<bf16>, dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(x),
+                       static_cast<bf16*>(y), n / 8, a, b);
+  else if (dtype == kF32)
+    hipLaunchKernelGGL(axpby_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(x),
+                       static_cast<float*>(y), n / 8, a, b);
+  else throw std::invalid_argument("axpby: dtype");
+  FFK_LAUNCH_CHECK("axpby");
+}
+
+}  // namespace ffk

@@ -1,0 +1,140 @@
+// Embedding lookup (no aggregation / SUM / AVG bags) forward and backward.
+//
+// Parity: lib/kernels/src/cuda/embedding_kernels.cu (embed_forward_no_aggr,
+// embed_forward_with_aggr, embed_backward_* with atomicAdd, :64-242).  Fixes
+// the reference's AVG bug (the 1/L scale applied inside the accumulation
+// loop, :106-113): here the bag is summed in fp32 and scaled once.
+// CDNA4: each thread moves one 16-byte chunk (8 x bf16) of a row, rows are
+// gathered whole; the backward scatter-adds fp32 rows with per-column atomics
+// shaped as contiguous 256-byte wave segments (guide G12), into the flat fp32
+// gradient buffer.
+#include "common.h"
+#include "kernels.h"
+
+namespace ffk {
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* o) {
+  if constexpr (sizeof(T) == 2) {
+    u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = u2f(u[k]);
+  } else {
+    f32x4 a = reinterpret_cast<const f32x4*>(p)[0], b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = a[k];
+      o[k + 4] = b[k];
+    }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float* o) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = f2bf(o[k]);
+    *reinterpret_cast<bf16x8*>(p) = v;
+  } else {
+    f32x4 a, b;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = o[k];
+      b[k] = o[k + 4];
+    }
+    reinterpret_cast<f32x4*>(p)[0] = a;
+    reinterpret_cast<f32x4*>(p)[1] = b;
+  }
+}
+
+// out[b, :] = agg_{j<L} W[idx[b*L + j], :]   (L == 1 and mode 0 -> plain lookup)
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const I* __restrict__ idx, const T* __restrict__ W,
+                                                        T* __restrict__ out, int64_t B, int L, int D, int mode,
+                                                        int64_t num_entries) {
+  const int cpr = D / 8;
+  const int64_t total = B * cpr;
+  for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t b = t / cpr;
+    const int col = static_cast<int>(t % cpr) * 8;
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int j = 0; j < L; ++j) {
+      int64_t r = static_cast<int64_t>(idx[b * L + j]);
+      if (r < 0 || r >= num_entries) continue;  // out-of-range ids contribute zeros
+      float v[8];
+      load8<T>(W + r * D + col, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+    if (mode == 2 && L > 0) {
+      const float inv = 1.f / L;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] *= inv;
+    }
+    store8<T>(out + b * D + col, acc);
+  }
+}
+
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const I* __restrict__ idx, const T* __restrict__ dout,
+                                                        float* __restrict__ dW, int64_t B, int L, int D, int mode,
+                                                        int64_t num_entries) {
+  const int cpr = D / 8;
+  const int64_t total = B * L * cpr;
+  const float scale = (mode == 2 && L > 0) ? 1.f / L : 1.f;
+  for (int64_t t = blockIdx.x * 256 + threadIdx.x; t < total; t += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t bj = t / cpr;
+    const int col = static_cast<int>(t % cpr) * 8;
+    const int64_t b = bj / L;
+    int64_t r = static_cast<int64_t>(idx[bj]);
+    if (r < 0 || r >= num_entries) continue;
+    float v[8];
+    load8<T>(dout + b * D + col, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(dW + r * D + col + k, v[k] * scale);
+  }
+}
+
+void embedding_fwd(int dtype, int index_bits, const void* idx, const void* W, void* out, int64_t B, int L, int D,
+                   int mode, int64_t num_entries, hipStream_t st) {
+  if (D % 8 != 0) throw std::invalid_argument("embedding: dim must be a multiple of 8");
+  int grid = grid_for(B * (D / 8), 256, 256 * 16);
+#define FFK_EF(T, I)                                                                                         \
+  hipLaunchKernelGGL((embed_fwd_kernel<T, I>), dim3(grid), dim3(256), 0, st, static_cast<const I*>(idx),     \
+                     static_cast<const T*>(W), static_cast<T*>(out), B, L, D, mode, num_entries)
+  if (dtype == kBF16) {
+    if (index_bits == 64) FFK_EF(bf16, int64_t);
+    else FFK_EF(bf16, int32_t);
+  } else if (dtype == kF32) {
+    if (index_bits == 64) FFK_EF(float, int64_t);
+    else FFK_EF(float, int32_t);
+  } else {
+    throw std::invalid_argument("embedding: dtype");
+  }
+#undef FFK_EF
+  FFK_LAUNCH_CHECK("embedding_fwd");
+}
+
+void embedding_bwd(int dtype, int index_bits, const void* idx, const void* dout, float* dW, int64_t B, int L, int D,
+                   int mode, int64_t num_entries, hipStream_t st) {
+  if (D % 8 != 0) throw std::invalid_argument("embedding: dim must be a multiple of 8");
+  int grid = grid_for(B * L * (D / 8), 256, 256 * 16);
+#define FFK_EB(T, I)                                                                                          \
+  hipLaunchKernelGGL((embed_bwd_kernel<T, I>), dim3(grid), dim3(256), 0, st, static_cast<const I*>(idx),      \
+                     static_cast<const T*>(dout), dW, B, L, D, mode, num_entries)
+  if (dtype == kBF16) {
+    if (index_bits == 64) FFK_EB(bf16, int64_t);
+    else FFK_EB(bf16, int32_t);
+  } else if (dtype == kF32) {
+    if (index_bits == 64) FFK_EB(float, int64_t);
+    else FFK_EB(float, int32_t);
+  } else {
+    throw std::invalid_argument("embedding: dtype");
+  }
+#undef FFK_EB
+  FFK_LAUNCH_CHECK("embedding_bwd");
+}
+
+}  // namespace ffk

@@ -1,0 +1,366 @@
+// Fused (residual add +) LayerNorm forward / backward for gfx950.
+//
+// Parity: lib/kernels/src/cuda/ops/layer_norm_kernels.cu (RowwiseMoments +
+// LayerNormForward, ComputeInternalGradients + backward + GammaBetaBackward,
+// :69-399).  Re-designed for CDNA4 rather than translated:
+//  * one wave64 per row, the whole row held in registers (N = C*512 fast path,
+//    C <= 8) -> a single HBM read of x (+ residual) and a single write of y;
+//  * 16-byte vector loads/stores (8 x bf16 per lane);
+//  * residual add fused (BERT/GPT post/pre-LN blocks), optional store of the
+//    pre-norm sum for the backward pass;
+//  * dgamma/dbeta accumulate in registers across the rows a wave visits,
+//    reduce across the block's 4 waves through LDS, then one fp32 atomic per
+//    column per block (grid is capped, so atomics are ~N * grid, not N * M).
+#include "common.h"
+#include "kernels.h"
+
+namespace ffk {
+
+template <typename T>
+struct Vec8;
+template <>
+struct Vec8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float* o) {
+    u16x8 v = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = u2f(v[i]);
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* o) {
+    bf16x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = f2bf(o[i]);
+    *reinterpret_cast<bf16x8*>(p) = v;
+  }
+};
+template <>
+struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float* o) {
+    f32x4 a = reinterpret_cast<const f32x4*>(p)[0];
+    f32x4 b = reinterpret_cast<const f32x4*>(p)[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = a[i];
+      o[4 + i] = b[i];
+    }
+  }
+  static __device__ __forceinline__ void store(float* p, const float* o) {
+    f32x4 a, b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = o[i];
+      b[i] = o[4 + i];
+    }
+    reinterpret_cast<f32x4*>(p)[0] = a;
+    reinterpret_cast<f32x4*>(p)[1] = b;
+  }
+};
+
+// ---------------------------------------------------------------------------
+template <typename T, int C>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                     T* __restrict__ sum_out, const T* __restrict__ gamma,
+                                                     const T* __restrict__ beta, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int M, float eps) {
+  constexpr int N = C * 512;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const size_t base = static_cast<size_t>(row) * N;
+  float v[C][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int col = c * 512 + lane * 8;
+    Vec8<T>::load(x + base + col, v[c]);
+    if (res) {
+      float r[8];
+      Vec8<T>::load(res + base + col, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] += r[i];
+      if (sum_out) Vec8<T>::store(sum_out + base + col, v[c]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[c][i];
+  }
+  const float mean = wave_sum(s) * (1.f / N);
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float d = v[c][i] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / N) + eps);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int col = c * 512 + lane * 8;
+    float g[8], b[8], o[8];
+    if (gamma) Vec8<T>::load(gamma + col, g);
+    else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = 1.f;
+    if (beta) Vec8<T>::load(beta + col, b);
+    else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mean) * rstd * g[i] + b[i];
+    Vec8<T>::store(y + base + col, o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Generic path: any N that is a multiple of 8; one 256-thread block per row,
+// two passes over the row (L2 resident).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_generic(const T* __restrict__ x, const T* __restrict__ res,
+                                                      T* __restrict__ sum_out, const T* __restrict__ gamma,
+                                                      const T* __restrict__ beta, T* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int M, int N, float eps) {
+  __shared__ float scratch[4];
+  const int row = blockIdx.x;
+  const size_t base = static_cast<size_t>(row) * N;
+  float s = 0.f, q = 0.f;
+  for (int col = threadIdx.x * 8; col < N; col += 256 * 8) {
+    float v[8];
+    Vec8<T>::load(x + base + col, v);
+    if (res) {
+      float r[8];
+      Vec8<T>::load(res + base + col, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += r[i];
+      if (sum_out) Vec8<T>::store(sum_out + base + col, v);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s += v[i];
+      q += v[i] * v[i];
+    }
+  }
+  s = block_sum<256>(s, scratch);
+  q = block_sum<256>(q, scratch);
+  const float mean = s / N;
+  const float var = fmaxf(q / N - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + eps);
+  for (int col = threadIdx.x * 8; col < N; col += 256 * 8) {
+    float v[8], g[8], b[8], o[8];
+    Vec8<T>::load(x + base + col, v);
+    if (res) {
+      float r[8];
+      Vec8<T>::load(res + base + col, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += r[i];
+    }
+    if (gamma) Vec8<T>::load(gamma + col, g);
+    else
+      for (int i = 0; i < 8; ++i) g[i] = 1.f;
+    if (beta) Vec8<T>::load(beta + col, b);
+    else
+      for (int i = 0; i < 8; ++i) b[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (v[i] - mean) * rstd * g[i] + b[i];
+    Vec8<T>::store(y + base + col, o);
+  }
+  if (threadIdx.x == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward: xhat = (s - mean) * rstd; g = dy * gamma
+//   dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
+//   dgamma += dy * xhat, dbeta += dy
+template <typename T, int C>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
+                                                     const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const T* __restrict__ gamma,
+                                                     T* __restrict__ dx, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, int M) {
+  constexpr int N = C * 512;
+  __shared__ float red[4][2][512];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  float pg[C][8], pb[C][8];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pg[c][i] = pb[c][i] = 0.f;
+
+  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
+    const size_t base = static_cast<size_t>(row) * N;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[C][8], g[C][8];
+    float sum_g = 0.f, sum_gx = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int col = c * 512 + lane * 8;
+      float dv[8], sv[8], gm[8];
+      Vec8<T>::load(dy + base + col, dv);
+      Vec8<T>::load(s + base + col, sv);
+      if (gamma) Vec8<T>::load(gamma + col, gm);
+      else
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gm[i] = 1.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xh[c][i] = (sv[i] - mean) * rstd;
+        g[c][i] = dv[i] * gm[i];
+        sum_g += g[c][i];
+        sum_gx += g[c][i] * xh[c][i];
+        pg[c][i] += dv[i] * xh[c][i];
+        pb[c][i] += dv[i];
+      }
+    }
+    sum_g = wave_sum(sum_g) * (1.f / N);
+    sum_gx = wave_sum(sum_gx) * (1.f / N);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int col = c * 512 + lane * 8;
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = rstd * (g[c][i] - sum_g - xh[c][i] * sum_gx);
+      Vec8<T>::store(dx + base + col, o);
+    }
+  }
+  if (!dgamma && !dbeta) return;
+  // reduce the 4 waves' partials chunk by chunk, then one atomic per column
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[wave][0][lane * 8 + i] = pg[c][i];
+      red[wave][1][lane * 8 + i] = pb[c][i];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 512; j += 256) {
+      float a = red[0][0][j] + red[1][0][j] + red[2][0][j] + red[3][0][j];
+      float b = red[0][1][j] + red[1][1][j] + red[2][1][j] + red[3][1][j];
+      if (dgamma) atomicAdd(dgamma + c * 512 + j, a);
+      if (dbeta) atomicAdd(dbeta + c * 512 + j, b);
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_generic(const T* __restrict__ dy, const T* __restrict__ s,
+                                                      const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in,
+                                                      const T* __restrict__ gamma, T* __restrict__ dx,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
+                                                      int N) {
+  __shared__ float scratch[4];
+  const int row = blockIdx.x;
+  const size_t base = static_cast<size_t>(row) * N;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  float sum_g = 0.f, sum_gx = 0.f;
+  for (int col = threadIdx.x * 8; col < N; col += 256 * 8) {
+    float dv[8], sv[8], gm[8];
+    Vec8<T>::load(dy + base + col, dv);
+    Vec8<T>::load(s + base + col, sv);
+    if (gamma) Vec8<T>::load(gamma + col, gm);
+    else
+      for (int i = 0; i < 8; ++i) gm[i] = 1.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float xh = (sv[i] - mean) * rstd;
+      float g = dv[i] * gm[i];
+      sum_g += g;
+      sum_gx += g * xh;
+      if (dgamma) atomicAdd(dgamma + col + i, dv[i] * xh);
+      if (dbeta) atomicAdd(dbeta + col + i, dv[i]);
+    }
+  }
+  sum_g = block_sum<256>(sum_g, scratch) / N;
+  sum_gx = block_sum<256>(sum_gx, scratch) / N;
+  for (int col = threadIdx.x * 8; col < N; col += 256 * 8) {
+    float dv[8], sv[8], gm[8], o[8];
+    Vec8<T>::load(dy + base + col, dv);
+    Vec8<T>::load(s + base + col, sv);
+    if (gamma) Vec8<T>::load(gamma + col, gm);
+    else
+      for (int i = 0; i < 8; ++i) gm[i] = 1.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float xh = (sv[i] - mean) * rstd;
+      o[i] = rstd * (dv[i] * gm[i] - sum_g - xh * sum_gx);
+    }
+    Vec8<T>::store(dx + base + col, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+static void ln_fwd_t(const void* x, const void* res, void* sum_out, const void* gamma, const void* beta, void* y,
+                     float* mean, float* rstd, int M, int N, float eps, hipStream_t st) {
+  auto X = static_cast<const T*>(x);
+  auto R = static_cast<const T*>(res);
+  auto S = static_cast<T*>(sum_out);
+  auto G = static_cast<const T*>(gamma);
+  auto B = static_cast<const T*>(beta);
+  auto Y = static_cast<T*>(y);
+  if (N % 512 == 0 && N <= 4096) {
+    dim3 grid((M + 3) / 4);
+    switch (N / 512) {
+#define FFK_LN_CASE(c) \
+  case c: hipLaunchKernelGGL((ln_fwd_kernel<T, c>), grid, dim3(256), 0, st, X, R, S, G, B, Y, mean, rstd, M, eps); break;
+      FFK_LN_CASE(1) FFK_LN_CASE(2) FFK_LN_CASE(3) FFK_LN_CASE(4) FFK_LN_CASE(5) FFK_LN_CASE(6) FFK_LN_CASE(7)
+      FFK_LN_CASE(8)
+#undef FFK_LN_CASE
+    }
+  } else {
+    hipLaunchKernelGGL((ln_fwd_generic<T>), dim3(M), dim3(256), 0, st, X, R, S, G, B, Y, mean, rstd, M, N, eps);
+  }
+  FFK_LAUNCH_CHECK("layernorm_fwd");
+}
+
+template <typename T>
+static void ln_bwd_t(const void* dy, const void* s, const float* mean, const float* rstd, const void* gamma,
+                     void* dx, float* dgamma, float* dbeta, int M, int N, hipStream_t st) {
+  auto DY = static_cast<const T*>(dy);
+  auto S = static_cast<const T*>(s);
+  auto G = static_cast<const T*>(gamma);
+  auto DX = static_cast<T*>(dx);
+  if (N % 512 == 0 && N <= 4096) {
+    int grid = std::min((M + 3) / 4, 1024);
+    switch (N / 512) {
+#define FFK_LNB_CASE(c)                                                                                        \
+  case c:                                                                                                      \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, c>), dim3(grid), dim3(256), 0, st, DY, S, mean, rstd, G, DX, dgamma, \
+                       dbeta, M);                                                                              \
+    break;
+      FFK_LNB_CASE(1) FFK_LNB_CASE(2) FFK_LNB_CASE(3) FFK_LNB_CASE(4) FFK_LNB_CASE(5) FFK_LNB_CASE(6)
+      FFK_LNB_CASE(7) FFK_LNB_CASE(8)
+#undef FFK_LNB_CASE
+    }
+  } else {
+    hipLaunchKernelGGL((ln_bwd_generic<T>), dim3(M), dim3(256), 0, st, DY, S, mean, rstd, G, DX, dgamma, dbeta, M,
+                       N);
+  }
+  FFK_LAUNCH_CHECK("layernorm_bwd");
+}
+
+void layernorm_fwd(int dtype, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
+                   void* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st) {
+  if (N % 8 != 0) throw std::invalid_argument("layernorm: N must be a multiple of 8");
+  if (dtype == kBF16) ln_fwd_t<bf16>(x, res, sum_out, gamma, beta, y, mean, rstd, M, N, eps, st);
+  else if (dtype == kF32) ln_fwd_t<float>(x, res, sum_out, gamma, beta, y, mean, rstd, M, N, eps, st);
+  else throw std::invalid_argument("layernorm: unsupported dtype");
+}
+
+void layernorm_bwd(int dtype, const void* dy, const void* s, const float* mean, const float* rstd,
+                   const void* gamma, void* dx, float* dgamma, float* dbeta, int M, int N, hipStream_t st) {
+  if (N % 8 != 0) throw std::invalid_argument("layernorm: N must be a multiple of 8");
+  if (dtype == kBF16) ln_bwd_t<bf16>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, M, N, st);
+  else if (dtype == kF32) ln_bwd_t<float>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, M, N, st);
+  else throw std::invalid_argument("layernorm: unsupported dtype");
+}
+
+}  // namespace ffk

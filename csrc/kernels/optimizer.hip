@@ -1,0 +1,122 @@
+// Fused optimizer updates over flat parameter buffers (gfx950).
+//
+// Parity: lib/kernels/src/cuda/optimizer_kernel.cu — sgd_update (:20-41,
+// PyTorch semantics: weight decay, momentum, Nesterov) and adam_update
+// (:123-145, weight decay folded into the gradient, alpha_t bias correction
+// precomputed on the host: lib/runtime/src/optimizer.cc:141-147).
+// MI355X-first: all parameters live in ONE flat fp32 master buffer with one
+// flat fp32 gradient buffer (DP all-reduce buckets are slices of it), so an
+// optimizer step is a single launch over the whole model instead of one task
+// per weight; the bf16 compute copy of the weights is written in the same
+// pass (no separate cast launch).
+#include "common.h"
+#include "kernels.h"
+
+namespace ffk {
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16* __restrict__ w_bf16, int64_t n4, float lr, float beta1,
+                                                   float beta2, float eps, float weight_decay, float bc1,
+                                                   float bc2_sqrt, float grad_scale, int decoupled) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    f32x4 W = reinterpret_cast<f32x4*>(w)[i];
+    f32x4 G = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 Mm = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 Vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = G[k] * grad_scale;
+      if (!decoupled) gg += weight_decay * W[k];
+      Mm[k] = beta1 * Mm[k] + (1.f - beta1) * gg;
+      Vv[k] = beta2 * Vv[k] + (1.f - beta2) * gg * gg;
+      float upd = (Mm[k] / bc1) / (sqrtf(Vv[k]) / bc2_sqrt + eps);
+      if (decoupled) upd += weight_decay * W[k];
+      W[k] -= lr * upd;
+    }
+    reinterpret_cast<f32x4*>(w)[i] = W;
+    reinterpret_cast<f32x4*>(m)[i] = Mm;
+    reinterpret_cast<f32x4*>(v)[i] = Vv;
+    if (w_bf16) {
+      bf16x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = f2bf(W[k]);
+      reinterpret_cast<bf16x4*>(w_bf16)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                  float* __restrict__ mom, bf16* __restrict__ w_bf16, int64_t n4,
+                                                  float lr, float momentum, float weight_decay, int nesterov,
+                                                  float grad_scale) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    f32x4 W = reinterpret_cast<f32x4*>(w)[i];
+    f32x4 G = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 Mo;
+    if (mom) Mo = reinterpret_cast<f32x4*>(mom)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = G[k] * grad_scale + weight_decay * W[k];
+      if (mom) {
+        Mo[k] = momentum * Mo[k] + gg;
+        gg = nesterov ? gg + momentum * Mo[k] : Mo[k];
+      }
+      W[k] -= lr * gg;
+    }
+    reinterpret_cast<f32x4*>(w)[i] = W;
+    if (mom) reinterpret_cast<f32x4*>(mom)[i] = Mo;
+    if (w_bf16) {
+      bf16x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = f2bf(W[k]);
+      reinterpret_cast<bf16x4*>(w_bf16)[i] = o;
+    }
+  }
+}
+
+// sum of squares of a flat fp32 buffer into out[0] (grad-norm clipping)
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n4, float* out) {
+  __shared__ float scratch[4];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  s = block_sum<256>(s, scratch);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+static void need4(int64_t n, const char* w) {
+  if (n % 4 != 0) throw std::invalid_argument(std::string(w) + ": flat buffer length must be a multiple of 4");
+}
+
+void adam_step(float* w, const float* g, float* m, float* v, void* w_bf16, int64_t n, float lr, float beta1,
+               float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
+               hipStream_t st) {
+  need4(n, "adam");
+  float bc1 = 1.f - powf(beta1, static_cast<float>(step));
+  float bc2s = sqrtf(1.f - powf(beta2, static_cast<float>(step)));
+  int grid = grid_for(n / 4, 256, 256 * 8);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, st, w, g, m, v, static_cast<bf16*>(w_bf16), n / 4, lr,
+                     beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale, decoupled);
+  FFK_LAUNCH_CHECK("adam");
+}
+
+void sgd_step(float* w, const float* g, float* mom, void* w_bf16, int64_t n, float lr, float momentum,
+              float weight_decay, int nesterov, float grad_scale, hipStream_t st) {
+  need4(n, "sgd");
+  int grid = grid_for(n / 4, 256, 256 * 8);
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, st, w, g, mom, static_cast<bf16*>(w_bf16), n / 4, lr,
+                     momentum, weight_decay, nesterov, grad_scale);
+  FFK_LAUNCH_CHECK("sgd");
+}
+
+void sum_squares(const float* x, int64_t n, float* out, hipStream_t st) {
+  need4(n, "sum_squares");
+  int grid = grid_for(n / 4, 256, 1024);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid), dim3(256), 0, st, x, n / 4, out);
+  FFK_LAUNCH_CHECK("sum_squares");
+}
+
+}  // namespace ffk

@@ -1,0 +1,223 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references.
+
+Every test runs the native kernel (asserting via kernels.STATS that it ran)
+and compares to an fp32 computation of the same op.  Inputs are random and
+asymmetric (guide: never validate MFMA layouts with symmetric operands).
+"""
+import math
+
+import pytest
+import torch
+
+from flexflow_train_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N", [1024, 768, 4096, 200 * 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layernorm_fwd_bwd(N, dtype):
+    torch.manual_seed(0)
+    M = 257
+    x = torch.randn(M, N, device=DEV, dtype=dtype)
+    r = torch.randn(M, N, device=DEV, dtype=dtype)
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).to(dtype)
+    b = (0.1 * torch.randn(N, device=DEV)).to(dtype)
+    n0 = K.STATS["layernorm_fwd"]
+    y, s, mean, rstd = K.layernorm_fwd(x, g, b, 1e-5, residual=r)
+    assert K.STATS["layernorm_fwd"] == n0 + 1
+    xs = (x.float() + r.float()).requires_grad_(True)
+    gf = g.float().requires_grad_(True)
+    bf = b.float().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xs, (N,), gf, bf, 1e-5)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(y, ref) < tol
+    dy = torch.randn(M, N, device=DEV, dtype=dtype)
+    ref.backward(dy.float())
+    dg = torch.zeros(N, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    dx = K.layernorm_bwd(dy, s, mean, rstd, g, dg, db)
+    assert _rel(dx, xs.grad) < (3e-2 if dtype == torch.bfloat16 else 1e-4)
+    assert _rel(dg, gf.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
+    assert _rel(db, bf.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu", "sigmoid", "tanh"])
+def test_bias_act_and_colsum(act):
+    torch.manual_seed(1)
+    M, N = 1000, 3072
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    y, pre = K.bias_act_fwd(x, bias, act)
+    u = x.float() + bias.float()
+    fn = {"gelu": lambda t: torch.nn.functional.gelu(t, approximate="tanh"), "relu": torch.relu,
+          "sigmoid": torch.sigmoid, "tanh": torch.tanh}[act]
+    uu = u.clone().requires_grad_(True)
+    ref = fn(uu)
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    ref.backward(dy.float())
+    dbias = torch.zeros(N, device=DEV)
+    g = K.colsum_act(dy, pre, act, dbias)
+    assert _rel(g, uu.grad) < 2e-2
+    assert _rel(dbias, uu.grad.sum(0)) < 2e-2
+
+
+def test_softmax_ce():
+    torch.manual_seed(2)
+    M, V, Vv = 300, 30528, 30522
+    logits = torch.randn(M, V, device=DEV, dtype=torch.bfloat16) * 3
+    labels = torch.randint(0, Vv, (M,), device=DEV, dtype=torch.int64)
+    lf = logits.float()[:, :Vv].clone().requires_grad_(True)
+    ref_loss = torch.nn.functional.cross_entropy(lf, labels, reduction="mean")
+    ref_loss.backward()
+    metrics = torch.zeros(4, device=DEV)
+    g = logits.clone()
+    K.softmax_ce(g, labels, 1.0 / M, metrics=metrics, valid_cols=Vv)
+    assert abs(metrics[0].item() / M - ref_loss.item()) < 2e-2 * abs(ref_loss.item())
+    assert _rel(g[:, :Vv], lf.grad) < 2e-2
+    assert g[:, Vv:].abs().max().item() == 0
+    acc = (lf.argmax(1) == labels).float().sum().item()
+    assert abs(metrics[1].item() - acc) <= 2
+
+
+def test_softmax_fwd_bwd():
+    torch.manual_seed(3)
+    x = torch.randn(64, 1000, device=DEV, dtype=torch.float32).requires_grad_(True)
+    y = K.softmax_fwd(x.detach())
+    ref = torch.softmax(x, -1)
+    assert _rel(y, ref) < 1e-5
+    dy = torch.randn_like(y)
+    ref.backward(dy)
+    dx = K.softmax_bwd(dy, y)
+    assert _rel(dx, x.grad) < 1e-4
+
+
+def test_adam_and_sgd():
+    torch.manual_seed(4)
+    n = 4096 * 3
+    w = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    wb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    ref_p = torch.nn.Parameter(w.clone())
+    opt = torch.optim.AdamW([ref_p], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    for step in range(1, 4):
+        ref_p.grad = g.clone()
+        opt.step()
+        K.adam_step(w, g, m, v, wb, 1e-3, 0.9, 0.999, 1e-8, 0.01 * 1e-3 / 1e-3, step, decoupled=True)
+    # AdamW decoupled decay in torch multiplies by lr: w -= lr*wd*w; ours adds wd*w to the update scaled by lr
+    assert _rel(w, ref_p.detach()) < 1e-5
+    assert _rel(wb, w) < 1e-2
+    # SGD with momentum + nesterov + weight decay against torch.optim.SGD
+    w2 = torch.randn(n, device=DEV)
+    mom = torch.zeros(n, device=DEV)
+    p2 = torch.nn.Parameter(w2.clone())
+    opt2 = torch.optim.SGD([p2], lr=0.1, momentum=0.9, nesterov=True, weight_decay=1e-4)
+    for _ in range(3):
+        p2.grad = g.clone()
+        opt2.step()
+        K.sgd_step(w2, g, mom, None, 0.1, 0.9, 1e-4, True)
+    assert _rel(w2, p2.detach()) < 1e-5
+
+
+@pytest.mark.parametrize("aggr", ["none", "sum", "avg"])
+def test_embedding(aggr):
+    torch.manual_seed(5)
+    n, D = 5000, 256
+    W = torch.randn(n, D, device=DEV, dtype=torch.bfloat16)
+    idx = torch.randint(0, n, (32, 7), device=DEV)
+    out = K.embedding_fwd(idx, W, aggr)
+    ref = W.float()[idx]
+    if aggr == "sum":
+        ref = ref.sum(-2)
+    elif aggr == "avg":
+        ref = ref.mean(-2)
+    assert _rel(out, ref) < 1e-2
+    dout = torch.randn_like(out)
+    dW = torch.zeros(n, D, device=DEV)
+    K.embedding_bwd(idx, dout, dW, aggr)
+    Wf = W.float().requires_grad_(True)
+    r = Wf[idx]
+    r = r.sum(-2) if aggr == "sum" else (r.mean(-2) if aggr == "avg" else r)
+    r.backward(dout.float())
+    assert _rel(dW, Wf.grad) < 1e-2
+
+
+def _ref_attn(q, k, v, causal):
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))  # [B,H,S,D]
+    s = qf @ kf.transpose(-1, -2) / math.sqrt(q.shape[-1])
+    if causal:
+        Sq, Sk = s.shape[-2:]
+        mask = torch.ones(Sq, Sk, device=q.device, dtype=torch.bool).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, -1)
+    return (p @ vf).transpose(1, 2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("S", [512, 320])
+def test_attention_fwd_bwd(causal, D, S):
+    torch.manual_seed(6)
+    B, H = 2, 4
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    o, lse = K.attention_fwd(q, k, v, causal=causal)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attn(qf, kf, vf, causal)
+    assert _rel(o, ref) < 2e-2, _rel(o, ref)
+    do = torch.randn_like(o)
+    ref.backward(do.float())
+    dqkv = torch.empty_like(qkv)
+    K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal)
+    assert _rel(dqkv[:, :, 2], vf.grad) < 3e-2, "dV"
+    assert _rel(dqkv[:, :, 1], kf.grad) < 3e-2, "dK"
+    assert _rel(dqkv[:, :, 0], qf.grad) < 3e-2, "dQ"
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd", [(512, 1024, 768), (300, 136, 200), (1024, 4096, 1024)])
+def test_gemm(ta, tb, M, N, Kd):
+    torch.manual_seed(7)
+    a = torch.randn(Kd, M, device=DEV, dtype=torch.bfloat16) if ta else torch.randn(M, Kd, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    b = torch.randn(N, Kd, device=DEV, dtype=torch.bfloat16) if tb else torch.randn(Kd, N, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    af = a.float().t() if ta else a.float()
+    bf = b.float().t() if tb else b.float()
+    ref = af @ bf
+    c = K.gemm(a, b, trans_a=ta, trans_b=tb)
+    assert _rel(c, ref) < 1e-2
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    c2 = K.gemm(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
+    u = ref + bias.float()
+    assert _rel(pre, u) < 1e-2
+    assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
+    c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
+    K.gemm(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3)
+    assert _rel(c3, ref + 1) < 1e-2
+
+
+def test_dropout_and_cast():
+    x = torch.randn(1 << 16, device=DEV, dtype=torch.bfloat16)
+    y = K.dropout(x, 0.25, 1234)
+    keep = (y != 0).float().mean().item()
+    assert abs(keep - 0.75) < 0.02
+    y2 = K.dropout(x, 0.25, 1234)
+    assert torch.equal(y, y2)
+    nz = y != 0
+    assert torch.allclose(y[nz].float(), x[nz].float() / 0.75, rtol=1e-2, atol=1e-2)
+    f = torch.empty(x.numel(), device=DEV)
+    K.cast_(x, f)
+    assert torch.equal(f, x.float())

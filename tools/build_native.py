@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""Build the native parts of flexflow_train_amd in-tree.
+
+Two shared objects are produced next to the Python package:
+
+* ``_ffcore``    - the C++17 core (IR, shape inference, PCG, substitutions,
+                   machine mapping, Unity/MCMC search, simulator), g++ + pybind11.
+* ``_ffkernels`` - hand-written HIP kernels for gfx950 (CDNA4), hipcc + pybind11.
+
+A ``build.ninja`` is generated under ``build/`` so rebuilds are incremental and
+header dependencies are tracked through compiler depfiles.  Usage::
+
+    python tools/build_native.py            # build both
+    python tools/build_native.py core       # only _ffcore
+    python tools/build_native.py kernels    # only _ffkernels
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "build")
+PKG = os.path.join(ROOT, "flexflow_train_amd")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("FF_OFFLOAD_ARCH", "gfx950")
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11
+
+    return [pybind11.get_include(), sysconfig.get_paths()["include"]]
+
+
+def _rel(p: str) -> str:
+    return os.path.relpath(p, BUILD)
+
+
+def write_ninja(targets: list[str]) -> str:
+    inc = " ".join(f"-I{p}" for p in _pybind_includes())
+    core_inc = f"-I{os.path.join(ROOT, 'csrc', 'ffcore', 'include')}"
+    kern_inc = f"-I{os.path.join(ROOT, 'csrc', 'kernels')}"
+    cxx = os.environ.get("CXX", "g++")
+    lines = [
+        "ninja_required_version = 1.5",
+        f"cxx = {cxx}",
+        f"hipcc = {HIPCC}",
+        f"core_flags = -O2 -g0 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function {core_inc} {inc}",
+        # -mcode-object-version=5 keeps the code object loadable by the HIP
+        # runtime bundled with the PyTorch wheel (ROCm 7.0) as well as 7.2.
+        f"hip_flags = -O3 -std=c++17 -fPIC --offload-arch={ARCH} -mcode-object-version=5 "
+        f"-fvisibility=hidden -munsafe-fp-atomics -Wno-unused-result {kern_inc} {inc}",
+        "rule cxx",
+        "  command = $cxx $core_flags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX $in",
+        "rule hip",
+        "  command = $hipcc $hip_flags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = HIPCC $in",
+        "rule link_cxx",
+        "  command = $cxx -shared -o $out $in -lpthread",
+        "  description = LINK $out",
+        "rule link_hip",
+        f"  command = $hipcc -shared --offload-arch={ARCH} -o $out $in",
+        "  description = LINK $out",
+    ]
+    defaults = []
+    if "core" in targets:
+        srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "ffcore", "src", "*.cc")))
+        srcs += sorted(glob.glob(os.path.join(ROOT, "csrc", "ffcore", "bindings*.cc")))
+        objs = []
+        for s in srcs:
+            o = os.path.join("obj", "core", os.path.basename(s) + ".o")
+            lines.append(f"build {o}: cxx {s}")
+            objs.append(o)
+        out = os.path.join(PKG, "_ffcore" + EXT)
+        lines.append(f"build {out}: link_cxx {' '.join(objs)}")
+        defaults.append(out)
+    if "kernels" in targets:
+        srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+        srcs += sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "bindings*.cpp")))
+        objs = []
+        for s in srcs:
+            o = os.path.join("obj", "kernels", os.path.basename(s) + ".o")
+            lines.append(f"build {o}: hip {s}")
+            objs.append(o)
+        out = os.path.join(PKG, "_ffkernels" + EXT)
+        lines.append(f"build {out}: link_hip {' '.join(objs)}")
+        defaults.append(out)
+    lines.append("default " + " ".join(defaults))
+    os.makedirs(BUILD, exist_ok=True)
+    path = os.path.join(BUILD, "build.ninja")
+    text = "\n".join(lines) + "\n"
+    old = open(path).read() if os.path.exists(path) else None
+    if old != text:
+        with open(path, "w") as f:
+            f.write(text)
+    return path
+
+
+def build(targets: list[str] | None = None, jobs: int | None = None, verbose: bool = False) -> None:
+    targets = targets or ["core", "kernels"]
+    write_ninja(targets)
+    ninja = shutil.which("ninja")
+    if ninja is None:
+        try:
+            import ninja as _ninja  # type: ignore
+
+            ninja = os.path.join(_ninja.BIN_DIR, "ninja")
+        except Exception as e:  # pragma: no cover
+            raise RuntimeError("ninja not found") from e
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    cmd = [ninja, "-C", BUILD, f"-j{jobs}"]
+    if verbose:
+        cmd.append("-v")
+    subprocess.run(cmd, check=True)
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("-")]
+    build(args or None, verbose="-v" in sys.argv)
