@@ -1,0 +1,102 @@
+"""LINEAR and BATCHMATMUL operators.
+
+Parity: lib/local-execution/src/ops/linear.cc + lib/kernels/src/cuda/ops/
+linear_kernels.cu (forward GEMM + bias + activation, backward activation
+grad in place, dW += X dY^T, db += sum dY, dX += W dY — gradients accumulate,
+:109-327); batch_matmul_kernels.cu.  The local-execution bug
+`in_dim = shape[0] + 1` (linear.cc:99-101) is not reproduced.
+
+Parallel semantics (op-attrs linear.cc:73-140): a row-parallel shard
+(input last dim sharded -> output partial sums) adds the bias only on the
+partial-sum replica 0, so the Reduction that follows sums it once.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import kernels as K
+from .base import OpContext, OpImpl, acc_grad, register
+from .gemm import matmul
+
+_ACT_T = {
+    "none": lambda t: t,
+    "relu": torch.relu,
+    "sigmoid": torch.sigmoid,
+    "tanh": torch.tanh,
+    "gelu": lambda t: torch.nn.functional.gelu(t, approximate="tanh"),
+}
+
+
+@register("LINEAR")
+class LinearOp(OpImpl):
+    def forward(self, ctx: OpContext, inputs, weights):
+        x = inputs[0]
+        W = weights[0]
+        b = weights[1] if len(weights) > 1 and ctx.sum_index == 0 else None
+        act = ctx.a("activation", "none")
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        if x2.is_cuda and x2.dtype == torch.bfloat16:
+            pre = torch.empty(x2.shape[0], W.shape[1], device=x2.device, dtype=x2.dtype) if act != "none" else None
+            y = matmul(x2, W, bias=b, act=act, pre=pre)
+        else:
+            u = x2 @ W.to(x2.dtype)
+            if b is not None:
+                u = u + b.to(u.dtype)
+            pre = u if act != "none" else None
+            y = _ACT_T[act](u)
+        return [y.reshape(*lead, W.shape[1])], (x2, pre, W)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        x2, pre, W = saved
+        dy = grad_outputs[0]
+        act = ctx.a("activation", "none")
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        has_bias = len(weight_grads) > 1
+        db = weight_grads[1] if has_bias and ctx.sum_index == 0 else None
+        dW = weight_grads[0]
+        if dy2.is_cuda and dy2.dtype == torch.bfloat16 and K.available() and dy2.shape[1] % 8 == 0:
+            if act != "none":
+                g = K.colsum_act(dy2, pre, act, db, write_dx=True)
+            else:
+                g = dy2
+                if db is not None:
+                    K.colsum_act(dy2, None, "none", db, write_dx=False)
+        else:
+            if act != "none":
+                p = pre.float().detach().requires_grad_(True)
+                y = _ACT_T[act](p)
+                y.backward(dy2.float())
+                g = p.grad.to(dy2.dtype)
+            else:
+                g = dy2
+            if db is not None:
+                acc_grad(db, g.float().sum(0))
+        if dW is not None:
+            if dW.is_cuda and g.dtype == torch.bfloat16:
+                matmul(x2, g, trans_a=True, out=dW, beta=1.0)
+            else:
+                acc_grad(dW, x2.float().t() @ g.float())
+        dx = None
+        if need_input_grad[0]:
+            dx = matmul(g, W, trans_b=True) if g.is_cuda else (g @ W.to(g.dtype).t())
+            dx = dx.reshape(*dy.shape[:-1], W.shape[0])
+        return [dx]
+
+
+@register("BATCHMATMUL", "MATMUL")
+class BatchMatmulOp(OpImpl):
+    def forward(self, ctx, inputs, weights):
+        a, b = inputs
+        return [torch.matmul(a, b)], (a, b)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        a, b = saved
+        d = grad_outputs[0]
+        da = torch.matmul(d, b.transpose(-1, -2)) if need_input_grad[0] else None
+        db = torch.matmul(a.transpose(-1, -2), d) if need_input_grad[1] else None
+        return [da, db]
