@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Headline benchmark: BERT-large training throughput (samples/s, whole node).
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Metric / config from BASELINE.json: "samples/sec (whole node) + speedup-over-
+DP after search, BERT-large 8xMI355X".  The model is BERT-large (24 layers,
+hidden 1024, 16 heads, FFN 4096, seq 512, vocab 30522 padded to 30528) with
+a full MLM head, bf16 compute / fp32 master weights + Adam, random-init
+weights and synthetic token ids (no datasets on this pool).  The per-GPU
+batch is fixed (weak scaling); the strategy comes from the framework's
+compile() (searched, or --strategy dp for the data-parallel baseline).
+Each timed step = forward + loss + backward + gradient all-reduce + Adam
+update over all parameters.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-per-gpu", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--model", default="bert-large")
+    ap.add_argument("--layers", type=int, default=None, help="override (debug only; invalidates the metric)")
+    ap.add_argument("--strategy", default="search", choices=["search", "dp"])
+    ap.add_argument("--gemm", default=os.environ.get("FF_GEMM", "auto"))
+    ap.add_argument("--profile", action="store_true")
+    args = ap.parse_args()
+
+    os.environ["FF_GEMM"] = args.gemm
+    import torch
+
+    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType)
+    from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    global_batch = args.batch_per_gpu * world
+    mk = bert_large if args.model == "bert-large" else bert_base
+    kw = dict(batch_size=global_batch, sequence_length=args.seq)
+    if args.layers:
+        kw["num_encoder_layers"] = args.layers
+    bcfg = mk(**kw)
+
+    cfg = FFConfig()
+    cfg.batch_size = global_batch
+    cfg.print_freq = 0
+    cfg.profiling = args.profile
+    cfg.only_data_parallel = args.strategy == "dp"
+    model = FFModel(cfg)
+    inputs, out = build_bert(model, bcfg)
+    t0 = time.time()
+    model.compile(optimizer=AdamOptimizer(model, alpha=1e-4, weight_decay=0.01, decoupled=True),
+                  loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY, MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+    compile_s = time.time() - t0
+    ex = model.executor
+    dev = ex.cfg.device
+
+    # synthetic data: this rank's piece of every input, generated on device once
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    feeds = {}
+    for name in ex.inputs:
+        shp = ex.local_input_shape(name)
+        if name == "input_ids":
+            feeds[name] = torch.randint(0, bcfg.vocab_size, shp, generator=g, device=dev, dtype=torch.int32)
+        elif name == "position_ids":
+            feeds[name] = torch.arange(shp[-1], device=dev, dtype=torch.int32).expand(shp).contiguous()
+        else:
+            feeds[name] = torch.randint(0, bcfg.type_vocab_size, shp, generator=g, device=dev, dtype=torch.int32)
+    lshape = ex._loss_layout().piece_shape[:-1]
+    labels = torch.randint(0, bcfg.vocab_size, lshape, generator=g, device=dev, dtype=torch.int64)
+
+    def step():
+        ex.train_step(feeds, labels)
+
+    for _ in range(args.warmup):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ex.dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ex.dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = ex.dist.max_scalar(time.perf_counter() - t0)
+    ms = elapsed / args.steps * 1000.0
+    sps = global_batch * args.steps / elapsed
+    pm = ex.perf_metrics()
+    if rank == 0:
+        par = model.search_report.get("source", "")
+        res = {
+            "metric": "samples_per_sec_whole_node",
+            "value": round(sps, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic token ids, random-init weights",
+            "config": {
+                "model": args.model + ("" if not args.layers else f"-{args.layers}L(debug)"),
+                "global_batch": global_batch,
+                "seq_len": args.seq,
+                "parallelism": ("dp%d" % world) if par in ("data_parallel", "single_device",
+                                                            "data_parallel_fallback") else par,
+                "strategy_source": par,
+                "layers": bcfg.num_encoder_layers,
+                "hidden": bcfg.hidden_size,
+                "heads": bcfg.num_heads,
+                "vocab": bcfg.vocab_size,
+                "optimizer": "adamw",
+                "compile_s": round(compile_s, 2),
+                "tokens_per_sec": round(sps * args.seq, 1),
+                "final_loss": round(pm.loss, 4),
+            },
+        }
+        print(json.dumps(res), flush=True)
+        if args.profile:
+            rep = ex.profile_report()
+            print(json.dumps({"profile_ms_total": {k: round(v, 3) for k, v in list(rep.items())[:40]}}),
+                  file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,8 @@
+"""flexflow.core-compatible API: FFConfig, FFModel, optimizers, initializers,
+data loaders and enums."""
+from .config import FFConfig  # noqa: F401
+from .initializers import (ConstantInitializer, GlorotNormalInitializer, GlorotUniformInitializer,  # noqa: F401
+                           NormInitializer, TruncatedNormalInitializer, UniformInitializer, ZeroInitializer)
+from .model import (AdamOptimizer, FFModel, Layer, Parameter, SGDOptimizer, SingleDataLoader,  # noqa: F401
+                    Tensor)
+from .types import *  # noqa: F401,F403

@@ -1,0 +1,145 @@
+"""FFConfig: runtime configuration + the reference's command-line flag set.
+
+Parity: lib/local-execution/include/local-execution/config.h:51-107 (FFConfig
+fields) and bin/arg_parser/arg_parser.cc:5-153 (flags), python
+FFConfig (python/flexflow/core/flexflow_cffi.py:526-566).  Legion-only flags
+(-ll:*, -lg:*) are accepted and ignored; -ll:gpu maps to the number of GPUs
+of the node (one process per GPU here: the world comes from torchrun's env).
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+import sys
+import time
+from typing import List, Optional
+
+
+@dataclasses.dataclass
+class FFConfig:
+    epochs: int = 1
+    batch_size: int = 64
+    num_nodes: int = 1
+    cpus_per_node: int = 1
+    workers_per_node: int = 0          # GPUs per node (0 = from WORLD_SIZE / LOCAL_WORLD_SIZE)
+    learning_rate: float = 0.01
+    weight_decay: float = 0.0001
+    print_freq: int = 10
+    dataset_path: str = ""
+    profiling: bool = False
+    perform_fusion: bool = True
+    search_budget: int = -1
+    search_alpha: float = 1.2
+    search_overlap_backward_update: bool = True
+    only_data_parallel: bool = False
+    enable_parameter_parallel: bool = False
+    enable_attribute_parallel: bool = False
+    enable_inplace_optimizations: bool = False
+    allow_tensor_op_math_conversion: bool = True
+    import_strategy_file: str = ""
+    export_strategy_file: str = ""
+    export_strategy_task_graph_file: str = ""
+    include_costs_dot_graph: bool = False
+    export_strategy_computation_graph_file: str = ""
+    substitution_json_path: str = ""
+    machine_model_version: int = 0
+    machine_model_file: str = ""
+    simulator_segment_size: int = 16777216
+    simulator_max_num_segments: int = 1
+    simulator_work_space_size: int = 2 << 30
+    search_num_nodes: int = -1
+    search_num_workers: int = -1
+    base_optimize_threshold: int = 10
+    enable_control_replication: bool = True
+    python_data_loader_type: int = 2
+    enable_propagation: bool = False
+    search_algorithm: str = "unity"    # unity | mcmc | data_parallel
+    compute_dtype: str = "bfloat16"    # bfloat16 on GPU; CPU runs float unless asked
+    seed: int = 0
+    _start_time: float = dataclasses.field(default_factory=time.time)
+
+    def __post_init__(self):
+        pass
+
+    # -- reference accessors -------------------------------------------------
+    def parse_args(self, argv: Optional[List[str]] = None):
+        argv = sys.argv[1:] if argv is None else argv
+        p = build_arg_parser()
+        ns, _unknown = p.parse_known_args(argv)
+        for k, v in vars(ns).items():
+            if v is not None and hasattr(self, k):
+                setattr(self, k, v)
+        return self
+
+    def get_batch_size(self):
+        return self.batch_size
+
+    def get_workers_per_node(self):
+        if self.workers_per_node:
+            return self.workers_per_node
+        return int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+
+    def get_num_nodes(self):
+        return self.num_nodes
+
+    def get_epochs(self):
+        return self.epochs
+
+    def get_current_time(self):
+        return (time.time() - self._start_time) * 1e6   # microseconds, like Legion's timer
+
+    def begin_trace(self, trace_id: int):
+        """Legion trace capture; the MI355X executor captures hipGraphs itself."""
+
+    def end_trace(self, trace_id: int):
+        pass
+
+
+def build_arg_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(add_help=False, allow_abbrev=False)
+    a = p.add_argument
+    a("-e", "--epochs", dest="epochs", type=int)
+    a("-b", "--batch-size", dest="batch_size", type=int)
+    a("--lr", "--learning-rate", dest="learning_rate", type=float)
+    a("--wd", "--weight-decay", dest="weight_decay", type=float)
+    a("-p", "--print-freq", dest="print_freq", type=int)
+    a("-d", "--dataset", dest="dataset_path", type=str)
+    a("--budget", "--search-budget", dest="search_budget", type=int)
+    a("--alpha", "--search-alpha", dest="search_alpha", type=float)
+    a("--simulator-workspace-size", dest="simulator_work_space_size", type=int)
+    a("--import", "--import-strategy", dest="import_strategy_file", type=str)
+    a("--export", "--export-strategy", dest="export_strategy_file", type=str)
+    a("--only-data-parallel", dest="only_data_parallel", action="store_const", const=True)
+    a("--enable-parameter-parallel", dest="enable_parameter_parallel", action="store_const", const=True)
+    a("--enable-attribute-parallel", dest="enable_attribute_parallel", action="store_const", const=True)
+    a("-ll:gpu", dest="workers_per_node", type=int)
+    a("--nodes", dest="num_nodes", type=int)
+    a("-ll:cpu", dest="cpus_per_node", type=int)
+    a("--profiling", dest="profiling", action="store_const", const=True)
+    a("--allow-tensor-op-math-conversion", dest="allow_tensor_op_math_conversion", action="store_const",
+      const=True)
+    a("--fusion", dest="perform_fusion", action="store_const", const=True)
+    a("--overlap", dest="search_overlap_backward_update", action="store_const", const=True)
+    a("--taskgraph", dest="export_strategy_task_graph_file", type=str)
+    a("--include-costs-dot-graph", dest="include_costs_dot_graph", action="store_const", const=True)
+    a("--compgraph", dest="export_strategy_computation_graph_file", type=str)
+    a("--machine-model-version", dest="machine_model_version", type=int)
+    a("--machine-model-file", dest="machine_model_file", type=str)
+    a("--simulator-segment-size", dest="simulator_segment_size", type=int)
+    a("--simulator-max-num-segments", dest="simulator_max_num_segments", type=int)
+    a("--enable-propagation", dest="enable_propagation", action="store_const", const=True)
+    a("--enable-inplace-optimizations", dest="enable_inplace_optimizations", action="store_const", const=True)
+    a("--search-num-nodes", dest="search_num_nodes", type=int)
+    a("--search-num-workers", dest="search_num_workers", type=int)
+    a("--base-optimize-threshold", dest="base_optimize_threshold", type=int)
+    a("--disable-control-replication", dest="enable_control_replication", action="store_const", const=False)
+    a("--python-data-loader-type", dest="python_data_loader_type", type=int)
+    a("--substitution-json", dest="substitution_json_path", type=str)
+    a("--search-algorithm", dest="search_algorithm", type=str)
+    a("--compute-dtype", dest="compute_dtype", type=str)
+    a("--seed", dest="seed", type=int)
+    # Legion / Realm flags: accepted, ignored
+    for f in ("-ll:fsize", "-ll:zsize", "-ll:util", "-ll:bgwork", "-ll:csize", "-lg:prof", "-lg:prof_logfile"):
+        a(f, dest="_ignored_" + f.strip("-").replace(":", "_"), type=str)
+    return p

@@ -1,0 +1,606 @@
+"""FFModel: the user-facing model-building / training API.
+
+Parity: python/flexflow/core/flexflow_cffi.py (FFModel :883-2300, Tensor
+:574-846, Parameter :849-881, SGDOptimizer/AdamOptimizer :2303-2330,
+SingleDataLoader :2449-2490) and the C++ FFModel (lib/runtime/src/
+model.h:41-127).  Layers are recorded into the native ComputationGraph
+(flexflow_train_amd._ffcore, shape inference in C++); ``compile`` runs the
+strategy search (Unity / MCMC / data-parallel, or --import-strategy) to get a
+ParallelComputationGraph + machine views and lowers it onto this rank's
+Executor; ``fit`` / ``eval`` drive the training loop and report the
+reference's "THROUGHPUT = ... samples/s" metric.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from .. import _ffcore as C
+from ..ops.loss import normalize_loss_type, normalize_metric
+from ..parallel.comm import DistContext
+from ..runtime.executor import ExecConfig, Executor
+from ..runtime.optimizer import AdamConfig, SGDConfig
+from . import initializers as I
+from .config import FFConfig
+from .types import (ACTI_TO_STR, AGGR_TO_STR, DT_TO_STR, POOL_TO_STR, ActiMode, AggrMode, CompMode, DataType,
+                    LossType, MetricsType, PoolType, STR_TO_DT)
+
+_NP_DT = {"float": np.float32, "double": np.float64, "int32": np.int32, "int64": np.int64, "half": np.float16,
+          "bool": np.bool_, "bfloat16": np.float32}
+
+
+def _dt_str(dt) -> str:
+    if dt is None:
+        return "float"
+    if isinstance(dt, DataType):
+        return DT_TO_STR[dt]
+    return str(dt)
+
+
+def _act(a) -> str:
+    if a is None:
+        return "none"
+    if isinstance(a, ActiMode):
+        return ACTI_TO_STR[a]
+    return str(a)
+
+
+class Tensor:
+    def __init__(self, model: "FFModel", vref, name: Optional[str] = None):
+        self.model = model
+        self.vref = vref
+        self.name = name
+
+    @property
+    def dims(self):
+        return tuple(self.model.cg.shape(self.vref).dims)
+
+    @property
+    def num_dims(self):
+        return len(self.dims)
+
+    @property
+    def data_type(self):
+        return STR_TO_DT.get(C.datatype_to_string(self.model.cg.shape(self.vref).dtype), DataType.DT_FLOAT)
+
+    @property
+    def owner_layer(self):
+        return self.model._layer_of_node.get(self.vref.node)
+
+    def set_tensor(self, ffmodel, np_array):
+        """Attach a value: for inputs it is the next fed batch; for weights it
+        overwrites the parameter (see Parameter.set_weights)."""
+        ffmodel._pending_feeds[self.name or f"input_{self.vref.node}"] = np.asarray(np_array)
+
+    def get_tensor(self, ffmodel):
+        return ffmodel._get_value(self)
+
+    def get_gradients(self, ffmodel, comm_type=None):
+        return ffmodel._get_gradient(self)
+
+    def get_model_output_tensor(self, ffmodel):
+        return ffmodel._get_value(self)
+
+    def __repr__(self):
+        return f"Tensor({self.name}, dims={self.dims})"
+
+
+class Parameter(Tensor):
+    def set_weights(self, ffmodel, np_array):
+        ffmodel.executor.set_parameter(self.name, torch.as_tensor(np.asarray(np_array, dtype=np.float32)))
+        return True
+
+    def get_weights(self, ffmodel):
+        return ffmodel.executor.get_parameter(self.name).cpu().numpy()
+
+
+class Layer:
+    def __init__(self, model: "FFModel", node: int, name: str, op_type: str):
+        self.model = model
+        self.node = node
+        self.name = name
+        self.op_type = op_type
+
+    def _weights(self):
+        return [Parameter(self.model, v, self.model.cg.layer_name(v.node)) for v in self.model.cg.layer_weights(self.node)]
+
+    def get_number_parameters(self):
+        return len(self._weights())
+
+    def get_parameter_by_id(self, i):
+        return self._weights()[i]
+
+    def get_weight_tensor(self):
+        return self._weights()[0]
+
+    def get_bias_tensor(self):
+        w = self._weights()
+        return w[1] if len(w) > 1 else None
+
+    def get_number_inputs(self):
+        return len(self.model.cg.layer_data_inputs(self.node))
+
+    def get_input_by_id(self, i):
+        return Tensor(self.model, self.model.cg.layer_data_inputs(self.node)[i])
+
+    def get_input_tensor(self):
+        return self.get_input_by_id(0)
+
+    def get_number_outputs(self):
+        return self.model.cg.num_outputs(self.node)
+
+    def get_output_by_id(self, i):
+        return Tensor(self.model, C.ValueRef(self.node, i))
+
+    def get_output_tensor(self):
+        return self.get_output_by_id(0)
+
+    def __repr__(self):
+        return f"Layer({self.name}, {self.op_type})"
+
+
+class SGDOptimizer:
+    def __init__(self, ffmodel=None, lr=0.01, momentum=0.0, nesterov=False, weight_decay=0.0):
+        self.cfg = SGDConfig(lr, momentum, nesterov, weight_decay)
+
+    def set_learning_rate(self, learning_rate):
+        self.cfg.lr = learning_rate
+
+
+class AdamOptimizer:
+    def __init__(self, ffmodel=None, alpha=0.001, beta1=0.9, beta2=0.999, weight_decay=0.0, epsilon=1e-8,
+                 decoupled=False):
+        self.cfg = AdamConfig(alpha, beta1, beta2, weight_decay, epsilon, decoupled)
+
+    def set_learning_rate(self, learning_rate):
+        self.cfg.lr = learning_rate
+
+
+class SingleDataLoader:
+    """Holds the full dataset on the host and yields global batches (the
+    executor keeps only this rank's piece).  Parity: flexflow_cffi.py:2449."""
+
+    def __init__(self, ffmodel, input, full_input, num_samples=None, data_type=None):
+        self.model = ffmodel
+        self.tensor = input
+        self.full = np.asarray(full_input)
+        self._num_samples = int(num_samples if num_samples is not None else self.full.shape[0])
+        self.batch_size = ffmodel.ffconfig.batch_size
+        self.idx = 0
+
+    @property
+    def num_samples(self):
+        return self._num_samples
+
+    @num_samples.setter
+    def num_samples(self, v):
+        self._num_samples = int(v)
+
+    def reset(self):
+        self.idx = 0
+
+    def next_batch(self, ffmodel=None):
+        b = self.batch_size
+        if self.idx + b > self._num_samples:
+            self.idx = 0
+        out = self.full[self.idx:self.idx + b]
+        self.idx += b
+        return out
+
+
+class FFModel:
+    def __init__(self, ffconfig: Optional[FFConfig] = None):
+        self.ffconfig = ffconfig or FFConfig()
+        self.cg = C.ComputationGraph()
+        self._layers: List[Layer] = []
+        self._layer_of_node: Dict[int, Layer] = {}
+        self._inputs: List[Tensor] = []
+        self._optimizer = None
+        self.executor: Optional[Executor] = None
+        self.loss_type = None
+        self.metrics: List[str] = []
+        self._pending_feeds: Dict[str, np.ndarray] = {}
+        self._label_tensor: Optional[Tensor] = None
+        self._last_labels = None
+        self._name_counter = 0
+        self.dist: Optional[DistContext] = None
+        self.pcg = None
+        self.views = {}
+        self.search_report: Dict = {}
+        self.valid_classes = None
+
+    # ------------------------------------------------------------------ utils
+    def _uname(self, name, prefix):
+        if name:
+            return name
+        self._name_counter += 1
+        return f"{prefix}_{self._name_counter}"
+
+    def _add(self, op_type: str, inputs: Sequence[Tensor], name=None, inits=(), **attrs):
+        op = C.OpAttrs(op_type, **attrs)
+        nm = self._uname(name, op_type.lower())
+        outs = self.cg.add_layer(op, [t.vref for t in inputs], nm, [i.to_json() if hasattr(i, "to_json") else (i or "")
+                                                                    for i in inits])
+        node = outs[0].node
+        layer = Layer(self, node, nm, op_type)
+        self._layers.append(layer)
+        self._layer_of_node[node] = layer
+        res = [Tensor(self, v, nm) for v in outs]
+        return res[0] if len(res) == 1 else res
+
+    def get_layers(self):
+        return list(self._layers)
+
+    def get_layer_by_id(self, layer_id):
+        return self._layers[layer_id]
+
+    def get_last_layer(self):
+        return self._layers[-1]
+
+    def get_layer_by_name(self, layer_name):
+        for l in self._layers:
+            if l.name == layer_name:
+                return l
+        return None
+
+    def get_tensor_by_id(self, id):
+        return self._layers[id].get_output_tensor()
+
+    def print_layers(self, id=-1):
+        for i, l in enumerate(self._layers):
+            if id in (-1, i):
+                outs = [tuple(self.cg.shape(C.ValueRef(l.node, k)).dims) for k in range(self.cg.num_outputs(l.node))]
+                print(f"layer[{i}] {l.name} {l.op_type} outputs={outs}")
+
+    # --------------------------------------------------------------- inputs
+    def create_tensor(self, dims, data_type=DataType.DT_FLOAT, create_grad=True, name=None):
+        dt = _dt_str(data_type)
+        nm = self._uname(name, "input")
+        v = self.cg.create_input(C.TensorShape(list(dims), C.datatype_from_string(dt)), bool(create_grad), nm)
+        t = Tensor(self, v, nm)
+        self._inputs.append(t)
+        return t
+
+    def create_constant(self, dims, value, data_type=DataType.DT_FLOAT):
+        t = self.create_tensor(dims, data_type, create_grad=False)
+        self._pending_feeds[t.name] = np.full(dims, value, dtype=_NP_DT[_dt_str(data_type)])
+        t._constant = True
+        return t
+
+    # --------------------------------------------------------------- layers
+    def exp(self, x, name=None):
+        return self._add("EXP", [x], name)
+
+    def sin(self, x, name=None):
+        return self._add("SIN", [x], name)
+
+    def cos(self, x, name=None):
+        return self._add("COS", [x], name)
+
+    def add(self, x, y, inplace_a=False, name=None):
+        return self._add("EW_ADD", [x, y], name)
+
+    def subtract(self, x, y, inplace_a=False, name=None):
+        return self._add("EW_SUB", [x, y], name)
+
+    def multiply(self, x, y, inplace_a=False, name=None):
+        return self._add("EW_MUL", [x, y], name)
+
+    def divide(self, x, y, inplace_a=False, name=None):
+        return self._add("EW_DIV", [x, y], name)
+
+    def max(self, x, y, inplace_a=False, name=None):
+        return self._add("EW_MAX", [x, y], name)
+
+    def min(self, x, y, inplace_a=False, name=None):
+        return self._add("EW_MIN", [x, y], name)
+
+    def reduce_sum(self, input, axes, keepdims=False, name=None):
+        return self._add("REDUCE_SUM", [input], name, axes=list(axes), keepdims=keepdims)
+
+    def rsqrt(self, input, name=None):
+        return self._add("RSQRT", [input], name)
+
+    def pow(self, input, exponent, name=None):
+        return self._add("POW", [input], name, exponent=float(exponent))
+
+    def mean(self, input, dims, keepdims=False, name=None):
+        return self._add("REDUCE_MEAN", [input], name, axes=list(dims), keepdims=keepdims)
+
+    def conv2d(self, input, out_channels, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w,
+               activation=ActiMode.AC_MODE_NONE, groups=1, use_bias=True, shared_op=None, kernel_initializer=None,
+               bias_initializer=None, name=None):
+        return self._add("CONV2D", [input], name, (kernel_initializer, bias_initializer), out_channels=out_channels,
+                         kernel_h=kernel_h, kernel_w=kernel_w, stride_h=stride_h, stride_w=stride_w,
+                         padding_h=padding_h, padding_w=padding_w, activation=_act(activation), groups=groups,
+                         use_bias=use_bias)
+
+    def embedding(self, input, num_embeddings, embedding_dim, aggr=AggrMode.AGGR_MODE_NONE,
+                  dtype=DataType.DT_FLOAT, shared_op=None, kernel_initializer=None, name=None):
+        aggr_s = AGGR_TO_STR[aggr] if isinstance(aggr, AggrMode) else str(aggr)
+        return self._add("EMBEDDING", [input], name, (kernel_initializer,), num_entries=num_embeddings,
+                         out_channels=embedding_dim, aggr=aggr_s, data_type=_dt_str(dtype))
+
+    def pool2d(self, input, kernel_h, kernel_w, stride_h, stride_w, padding_h, padding_w, pool_type=PoolType.POOL_MAX,
+               activation=ActiMode.AC_MODE_NONE, name=None):
+        return self._add("POOL2D", [input], name, kernel_h=kernel_h, kernel_w=kernel_w, stride_h=stride_h,
+                         stride_w=stride_w, padding_h=padding_h, padding_w=padding_w,
+                         pool_type=POOL_TO_STR[pool_type] if isinstance(pool_type, PoolType) else str(pool_type),
+                         activation=_act(activation))
+
+    def batch_norm(self, input, relu=True, name=None):
+        return self._add("BATCHNORM", [input], name, relu=relu)
+
+    def layer_norm(self, input, axes, elementwise_affine=True, eps=1e-5, use_bias=True, name=None):
+        return self._add("LAYERNORM", [input], name, axes=list(axes), elementwise_affine=elementwise_affine,
+                         eps=float(eps), use_bias=use_bias)
+
+    def batch_matmul(self, A, B, a_seq_length_dim=None, b_seq_length_dim=None, name=None):
+        return self._add("BATCHMATMUL", [A, B], name,
+                         a_seq_length_dim=-1 if a_seq_length_dim is None else a_seq_length_dim,
+                         b_seq_length_dim=-1 if b_seq_length_dim is None else b_seq_length_dim)
+
+    def dense(self, input, out_dim, activation=ActiMode.AC_MODE_NONE, use_bias=True, datatype=None, shared_op=None,
+              kernel_initializer=None, bias_initializer=None, kernel_regularizer=None, name=None):
+        return self._add("LINEAR", [input], name, (kernel_initializer, bias_initializer), out_channels=out_dim,
+                         activation=_act(activation), use_bias=use_bias)
+
+    def concat(self, tensors, axis, name=None):
+        return self._add("CONCAT", list(tensors), name, axis=axis)
+
+    def split(self, input, sizes, axis, name=None):
+        if isinstance(sizes, int):
+            n = input.dims[axis]
+            sizes = [n // sizes] * sizes
+        out = self._add("SPLIT", [input], name, axis=axis, splits=list(sizes))
+        return out if isinstance(out, list) else [out]
+
+    def flat(self, input, name=None):
+        return self._add("FLAT", [input], name)
+
+    def softmax(self, input, axis=-1, name=None):
+        return self._add("SOFTMAX", [input], name, dim=axis)
+
+    def reshape(self, input, shape, name=None):
+        return self._add("RESHAPE", [input], name, shape=list(shape))
+
+    def gather(self, input, index, dim, name=None):
+        return self._add("GATHER", [input, index], name, dim=dim)
+
+    def transpose(self, input, perm, name=None):
+        return self._add("TRANSPOSE", [input], name, perm=list(perm))
+
+    def reverse(self, input, axis, name=None):
+        return self._add("REVERSE", [input], name, axis=axis)
+
+    def scalar_multiply(self, input, scalar, inplace=True, name=None):
+        return self._add("SCALAR_MULTIPLY", [input], name, scalar=float(scalar))
+
+    def scalar_add(self, input, scalar, inplace=True, name=None):
+        return self._add("SCALAR_ADD", [input], name, scalar=float(scalar))
+
+    def scalar_sub(self, input, scalar, inplace=True, name=None):
+        return self._add("SCALAR_SUB", [input], name, scalar=float(scalar))
+
+    def scalar_true_divide(self, input, scalar, inplace=True, name=None):
+        return self._add("SCALAR_TRUE_DIV", [input], name, scalar=float(scalar))
+
+    def gelu(self, input, inplace=True, name=None):
+        return self._add("GELU", [input], name)
+
+    def relu(self, input, inplace=True, name=None):
+        return self._add("RELU", [input], name)
+
+    def identity(self, input, name=None):
+        return self._add("IDENTITY", [input], name)
+
+    def sigmoid(self, input, name=None):
+        return self._add("SIGMOID", [input], name)
+
+    def tanh(self, input, name=None):
+        return self._add("TANH", [input], name)
+
+    def elu(self, input, inplace=True, name=None):
+        return self._add("ELU", [input], name)
+
+    def dropout(self, input, rate, seed, name=None):
+        return self._add("DROPOUT", [input], name, rate=float(rate), seed=int(seed))
+
+    def multihead_attention(self, query, key, value, embed_dim, num_heads, kdim=0, vdim=0, dropout=0.0, bias=True,
+                            add_bias_kv=False, add_zero_attn=False, kernel_initializer=None, causal=False, name=None):
+        return self._add("MULTIHEAD_ATTENTION", [query, key, value], name, (kernel_initializer,),
+                         embed_dim=embed_dim, num_heads=num_heads, kdim=kdim, vdim=vdim, dropout=float(dropout),
+                         bias=bias, add_bias_kv=add_bias_kv, add_zero_attn=add_zero_attn, causal=causal)
+
+    def cast(self, input, dtype, name=None):
+        return self._add("CAST", [input], name, dtype=_dt_str(dtype))
+
+    def top_k(self, input, k, sorted=True, name=None):
+        return self._add("TOPK", [input], name, k=k, sorted=sorted)
+
+    # ------------------------------------------------------------- training
+    @property
+    def optimizer(self):
+        return self._optimizer
+
+    @optimizer.setter
+    def optimizer(self, opt):
+        self._optimizer = opt
+
+    def set_optimizer(self, optimizer):
+        self._optimizer = optimizer
+
+    @property
+    def label_tensor(self):
+        return self._label_tensor
+
+    def compile(self, optimizer=None, loss_type=None, metrics=None, comp_mode=None, output=None):
+        from ..search import strategy as strat
+
+        if optimizer is not None:
+            self._optimizer = optimizer
+        if self._optimizer is None:
+            self._optimizer = SGDOptimizer(self, lr=self.ffconfig.learning_rate)
+        self.loss_type = loss_type
+        self.metrics = [normalize_metric(m) for m in (metrics or [])]
+        cuda = torch.cuda.is_available()
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        device = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
+        if cuda:
+            torch.cuda.set_device(device)
+        self.dist = DistContext.from_env(device=device)
+        world = self.dist.world
+        self.pcg, self.views, self.search_report = strat.build_pcg(self.cg, self.ffconfig, world)
+        if self.ffconfig.export_strategy_file:
+            strat.export_strategy(self.ffconfig.export_strategy_file, self.pcg, self.views, self.search_report)
+        dt = self.ffconfig.compute_dtype if cuda else ("float" if self.ffconfig.compute_dtype == "bfloat16"
+                                                         else self.ffconfig.compute_dtype)
+        cdt = {"bfloat16": torch.bfloat16, "float": torch.float32, "float32": torch.float32,
+               "half": torch.float16}[dt]
+        cfg = ExecConfig(compute_dtype=cdt, device=device, seed=self.ffconfig.seed,
+                         profiling=self.ffconfig.profiling, fuse_add_layernorm=self.ffconfig.perform_fusion)
+        out_v = None
+        if output is not None:
+            out_v = self._pcg_value_of(output)
+        self.executor = Executor(self.pcg, self.dist, cfg, views=self.views,
+                                 loss_type=normalize_loss_type(loss_type) if loss_type is not None else None,
+                                 metrics=self.metrics, optimizer=self._optimizer.cfg, output=out_v,
+                                 valid_classes=self.valid_classes)
+        self.executor.init_parameters()
+        # label tensor (reference: created in compile, [batch, 1] int32 for sparse CE)
+        out_lay = self.executor.value_layout[self.executor.loss_value]
+        if loss_type is not None and normalize_loss_type(loss_type) == "sparse_categorical_crossentropy":
+            ldims = list(out_lay.sizes[:-1]) + [1]
+            self._label_tensor = Tensor(self, None, "label")
+            self._label_tensor._dims = tuple(ldims)
+        return self
+
+    def _pcg_value_of(self, t: Tensor):
+        mapping = self.search_report.get("cg_to_pcg", {})
+        if t.vref.node in mapping:
+            return (mapping[t.vref.node], t.vref.idx)
+        return None
+
+    def init_layers(self):
+        if self.executor is None:
+            raise RuntimeError("call compile() first")
+
+    def reset_metrics(self):
+        self.executor.zero_metrics()
+
+    def get_perf_metrics(self):
+        return self.executor.perf_metrics()
+
+    def compute_metrics(self):
+        return self.get_perf_metrics()
+
+    def create_data_loader(self, batch_tensor, full_array):
+        return SingleDataLoader(self, batch_tensor, full_array, full_array.shape[0])
+
+    def _feeds_from(self, batch_inputs: Dict[str, np.ndarray]):
+        return {k: torch.as_tensor(v) for k, v in batch_inputs.items()}
+
+    def forward(self, seq_length=None):
+        feeds = dict(self._pending_feeds)
+        self.executor.forward(self._feeds_from(feeds), training=True)
+
+    def backward(self, seq_length=None):
+        lab = self._pending_feeds.get("label")
+        g = self.executor.compute_loss(torch.as_tensor(lab) if lab is not None else None)
+        self.executor.backward(g)
+
+    def update(self):
+        self.executor.update(lr=self._optimizer.cfg.lr)
+
+    def zero_gradients(self):
+        for f in self.executor.flats:
+            f["grad"].zero_()
+
+    def _input_name(self, t):
+        return t.name
+
+    def fit(self, x=None, y=None, batch_size=None, epochs=1):
+        """Training loop over data loaders (or arrays).  Prints the
+        reference's ``ELAPSED TIME = ..., THROUGHPUT = ... samples/s``."""
+        ex = self.executor
+        xs = x if isinstance(x, (list, tuple)) else [x]
+        loaders = [d if isinstance(d, SingleDataLoader) else SingleDataLoader(self, self._inputs[i], d)
+                   for i, d in enumerate(xs)]
+        ylo = y if isinstance(y, SingleDataLoader) else SingleDataLoader(self, self._label_tensor, y)
+        bs = batch_size or self.ffconfig.batch_size
+        for l in loaders + [ylo]:
+            l.batch_size = bs
+        num_samples = ylo.num_samples
+        iters = num_samples // bs
+        ex.zero_metrics()
+        if ex.cfg.device.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.time()
+        for epoch in range(epochs):
+            for l in loaders + [ylo]:
+                l.reset()
+            ex.zero_metrics()
+            for it in range(iters):
+                feeds = {self._inputs[i].name: torch.as_tensor(l.next_batch()) for i, l in enumerate(loaders)}
+                labels = torch.as_tensor(ylo.next_batch())
+                ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
+                if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0 and self.dist.rank == 0:
+                    print(f"epoch {epoch} iter {it + 1}/{iters}: {ex.perf_metrics()}", flush=True)
+            if self.dist.rank == 0 and iters:
+                print(f"epoch {epoch}: {ex.perf_metrics()}", flush=True)
+        if ex.cfg.device.type == "cuda":
+            torch.cuda.synchronize()
+        elapsed = time.time() - t0
+        thr = num_samples * epochs / max(elapsed, 1e-9)
+        if self.dist.rank == 0:
+            print(f"ELAPSED TIME = {elapsed:.4f}s, THROUGHPUT = {thr:.2f} samples/s", flush=True)
+        self.last_throughput = thr
+        return thr
+
+    def eval(self, x=None, y=None, batch_size=None):
+        ex = self.executor
+        xs = x if isinstance(x, (list, tuple)) else [x]
+        loaders = [d if isinstance(d, SingleDataLoader) else SingleDataLoader(self, self._inputs[i], d)
+                   for i, d in enumerate(xs)]
+        ylo = y if isinstance(y, SingleDataLoader) else SingleDataLoader(self, self._label_tensor, y)
+        bs = batch_size or self.ffconfig.batch_size
+        for l in loaders + [ylo]:
+            l.batch_size = bs
+            l.reset()
+        ex.zero_metrics()
+        iters = ylo.num_samples // bs
+        for _ in range(iters):
+            feeds = {self._inputs[i].name: torch.as_tensor(l.next_batch()) for i, l in enumerate(loaders)}
+            labels = torch.as_tensor(ylo.next_batch())
+            ex.forward(feeds, training=False)
+            # metrics without gradient: run the loss on the logits, discard grads
+            if ex.loss is not None:
+                ex._env[ex.loss_value] = ex._env.get(ex.loss_value)
+                ex.compute_loss(labels)
+        pm = ex.perf_metrics()
+        if self.dist.rank == 0:
+            print(f"eval: {pm}", flush=True)
+        return pm
+
+    def _get_value(self, t: Tensor):
+        raise NotImplementedError("get_tensor of activations is available through Executor.forward outputs")
+
+    def _get_gradient(self, t: Tensor):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------ checkpoint
+    def save_checkpoint(self, path: str):
+        from ..utils.checkpoint import save_checkpoint
+
+        save_checkpoint(self, path)
+
+    def load_checkpoint(self, path: str):
+        from ..utils.checkpoint import load_checkpoint
+
+        load_checkpoint(self, path)

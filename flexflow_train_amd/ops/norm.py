@@ -1,0 +1,114 @@
+"""LAYERNORM (optionally fused with the residual add) and BATCHNORM.
+
+Parity: lib/kernels/src/cuda/ops/layer_norm_kernels.cu, batch_norm_kernels.cu
+(cuDNN training-mode BN with running stats and optional fused ReLU).
+
+``FUSED_ADD_LAYERNORM`` is produced by the executor's fusion pass from
+EW_ADD -> LAYERNORM (the post-LN transformer block): one HIP kernel reads
+both operands once and writes y, the pre-norm sum and the row statistics.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import kernels as K
+from .base import OpImpl, acc_grad, register
+from .generic import AutogradOp
+
+
+def _ln_axes_are_trailing(ctx, x):
+    axes = sorted(int(a) % x.dim() for a in ctx.a("axes", [-1]))
+    return axes == list(range(x.dim() - len(axes), x.dim())), len(axes)
+
+
+class _LayerNormBase(OpImpl):
+    fused_add = False
+
+    def forward(self, ctx, inputs, weights):
+        x = inputs[0]
+        res = inputs[1] if self.fused_add else None
+        eps = float(ctx.a("eps", 1e-5))
+        gamma = weights[0] if len(weights) > 0 else None
+        beta = weights[1] if len(weights) > 1 else None
+        trailing, nax = _ln_axes_are_trailing(ctx, x)
+        N = int(math.prod(x.shape[x.dim() - nax:]))
+        if (x.is_cuda and trailing and N % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32) and K.available()):
+            xc = x.contiguous()
+            rc = res.contiguous() if res is not None else None
+            g = gamma.reshape(-1) if gamma is not None else None
+            b = beta.reshape(-1) if beta is not None else None
+            y, s, mean, rstd = K.layernorm_fwd(xc.view(-1, N), g, b, eps,
+                                               residual=rc.view(-1, N) if rc is not None else None)
+            return [y.view(x.shape)], ("hip", s, mean, rstd, gamma, N)
+        xs = x + res if res is not None else x
+        shape = x.shape[x.dim() - nax:] if trailing else None
+        if not trailing:
+            raise NotImplementedError("LAYERNORM over non-trailing axes")
+        with torch.no_grad():
+            y = torch.nn.functional.layer_norm(xs.float(), shape, gamma.float() if gamma is not None else None,
+                                               beta.float() if beta is not None else None, eps).to(x.dtype)
+        return [y], ("torch", xs, gamma, beta, shape, eps)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        dy = grad_outputs[0]
+        dg = weight_grads[0] if len(weight_grads) > 0 else None
+        db = weight_grads[1] if len(weight_grads) > 1 else None
+        if saved[0] == "hip":
+            _, s, mean, rstd, gamma, N = saved
+            dx = K.layernorm_bwd(dy.contiguous().view(-1, N), s, mean, rstd,
+                                 gamma.reshape(-1) if gamma is not None else None,
+                                 dg.reshape(-1) if dg is not None else None,
+                                 db.reshape(-1) if db is not None else None).view(dy.shape)
+        else:
+            _, xs, gamma, beta, shape, eps = saved
+            xf = xs.detach().float().requires_grad_(True)
+            gf = gamma.detach().float().requires_grad_(dg is not None) if gamma is not None else None
+            bf = beta.detach().float().requires_grad_(db is not None) if beta is not None else None
+            with torch.enable_grad():
+                y = torch.nn.functional.layer_norm(xf, shape, gf, bf, eps)
+            y.backward(dy.float())
+            dx = xf.grad.to(dy.dtype)
+            if dg is not None:
+                acc_grad(dg, gf.grad)
+            if db is not None:
+                acc_grad(db, bf.grad)
+        if self.fused_add:
+            return [dx, dx]
+        return [dx]
+
+
+@register("LAYERNORM")
+class LayerNormOp(_LayerNormBase):
+    fused_add = False
+
+
+@register("FUSED_ADD_LAYERNORM")
+class FusedAddLayerNormOp(_LayerNormBase):
+    fused_add = True
+
+
+@register("BATCHNORM")
+class BatchNormOp(AutogradOp):
+    """Training-mode batch norm over the sample + spatial dims, running stats
+    kept in the op's persistent state (ctx.extra['state'])."""
+
+    def compute(self, ctx, inputs, weights):
+        x = inputs[0]
+        state = ctx.extra.setdefault("state", {})
+        C = x.shape[1]
+        if "running_mean" not in state:
+            state["running_mean"] = torch.zeros(C, device=x.device, dtype=torch.float32)
+            state["running_var"] = torch.ones(C, device=x.device, dtype=torch.float32)
+        g = weights[0] if weights else None
+        b = weights[1] if len(weights) > 1 else None
+        train = ctx.training and not torch.is_grad_enabled()  # update stats only in the real forward
+        y = torch.nn.functional.batch_norm(
+            x.float(), state["running_mean"], state["running_var"],
+            g.float() if g is not None else None, b.float() if b is not None else None,
+            training=ctx.training, momentum=float(ctx.a("momentum", 0.1)) if train else 0.0,
+            eps=float(ctx.a("eps", 1e-5)))
+        if ctx.a("relu", False):
+            y = torch.relu(y)
+        return [y.to(x.dtype)]

@@ -1,0 +1,303 @@
+"""Distributed context and the layout-redistribution engine (RCCL over xGMI).
+
+One process per GPU (torchrun-style env: RANK / WORLD_SIZE / LOCAL_RANK /
+MASTER_ADDR / MASTER_PORT); torch.distributed's "nccl" backend is RCCL on
+ROCm; "gloo" serves the CPU tests.
+
+``redistribute(x, src, dst)`` moves a tensor between two layouts of the same
+logical shape.  Every rank computes the same global plan (deterministic), so
+sub-communicators can be created collectively up front.  The plan is lowered
+to the cheapest primitive that implements it:
+
+  * local slice / copy (no communication) — Replicate after a Reduction,
+    Repartition of a replicated tensor, matching views;
+  * all_reduce over a group — Reduction (sum of partials), the backward of
+    Replicate (sum of copy gradients);
+  * all_gather over a group — Combine;
+  * batched point-to-point (isend/irecv of the intersecting boxes) — any
+    other view change (different machine views, all-to-all style reshards).
+
+Parity: replaces Legion region copies + the NCCL weight-sync-only path of the
+reference (lib/runtime/src/legion_backing.cc:173-257, optimizer_kernel.cu:83);
+SURVEY §2.8 "MI355X-native equivalent".
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .layout import Box, Layout, intersect, rel_slices
+
+
+class DistContext:
+    """Process-group bookkeeping for one rank."""
+
+    def __init__(self, rank: int = 0, world: int = 1, device: Optional[torch.device] = None):
+        self.rank = rank
+        self.world = world
+        self.device = device or torch.device("cpu")
+        self._groups: Dict[Tuple[int, ...], object] = {}
+        self.stats = {"all_reduce": 0, "all_gather": 0, "p2p": 0, "local": 0, "bytes": 0}
+
+    @classmethod
+    def from_env(cls, device: Optional[torch.device] = None, backend: Optional[str] = None) -> "DistContext":
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        if world > 1 and not dist.is_initialized():
+            if backend is None:
+                backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
+            kw = {}
+            if backend == "nccl" and device is not None:
+                kw["device_id"] = device
+            dist.init_process_group(backend=backend, **kw)
+        if dist.is_initialized():
+            rank, world = dist.get_rank(), dist.get_world_size()
+        return cls(rank, world, device)
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1 and dist.is_initialized()
+
+    def group(self, ranks: Sequence[int]):
+        """Sub-communicator for ``ranks``; MUST be called in the same order on
+        every rank (plans are built identically everywhere)."""
+        key = tuple(sorted(ranks))
+        if len(key) == self.world:
+            return None  # default group
+        if key not in self._groups:
+            self._groups[key] = dist.new_group(list(key))
+        return self._groups[key]
+
+    def barrier(self):
+        if self.distributed:
+            dist.barrier()
+
+    def all_reduce_(self, t: torch.Tensor, ranks: Sequence[int], async_op: bool = False):
+        if len(ranks) <= 1 or not self.distributed:
+            return None
+        self.stats["all_reduce"] += 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+        return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
+
+    def max_scalar(self, v: float) -> float:
+        if not self.distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class Contribution:
+    src_rank: int
+    src_box: Box      # box of the source piece
+    part: Box         # intersection (global coordinates)
+
+
+@dataclasses.dataclass
+class Plan:
+    kind: str                                   # local | all_reduce | all_gather | p2p | none
+    contributions: Dict[int, List[Contribution]]
+    dst_boxes: Dict[int, Optional[Box]]
+    src_boxes: Dict[int, Optional[Box]]
+    groups: List[Tuple[int, ...]]
+    gather_dim: int = -1
+
+
+def _summed_sources(src: Layout, dst: Layout, s_d: int) -> List[int]:
+    Ss, Sd = src.sum_degree, dst.sum_degree
+    if Ss == Sd:
+        return [s_d]
+    if Ss % Sd == 0:
+        k = Ss // Sd
+        return [s_d * k + j for j in range(k)]
+    if Sd % Ss == 0:
+        k = Sd // Ss
+        return [s_d // k] if s_d % k == 0 else []
+    raise ValueError(f"incompatible summed degrees {Ss} -> {Sd}")
+
+
+def make_plan(src: Layout, dst: Layout, world: int) -> Plan:
+    if src.sizes != dst.sizes:
+        raise ValueError(f"redistribute: logical shapes differ {src.sizes} vs {dst.sizes}")
+    contributions: Dict[int, List[Contribution]] = {}
+    dst_boxes: Dict[int, Optional[Box]] = {}
+    src_boxes: Dict[int, Optional[Box]] = {}
+    for r in range(world):
+        cs = src.coord(r)
+        src_boxes[r] = src.box(cs.shard) if cs is not None else None
+        cd = dst.coord(r)
+        if cd is None:
+            dst_boxes[r] = None
+            continue
+        bd = dst.box(cd.shard)
+        dst_boxes[r] = bd
+        contribs = []
+        for s_s in _summed_sources(src, dst, dst.summed_index(cd)):
+            for shard in src.shards():
+                bs = src.box(shard)
+                part = intersect(bs, bd)
+                if part is None:
+                    continue
+                holders = src.holders(shard, s_s)
+                if r in holders:
+                    choice = r
+                else:
+                    # spread readers over holders deterministically
+                    choice = holders[(r + cd.rep) % len(holders)]
+                contribs.append(Contribution(choice, bs, part))
+        contributions[r] = contribs
+
+    # ---- classify
+    all_local = all(all(c.src_rank == r for c in cl) and len(cl) <= 1 for r, cl in contributions.items())
+    if all_local:
+        return Plan("local", contributions, dst_boxes, src_boxes, [])
+    # all_reduce: each rank's contributions are full-box copies from a group containing itself
+    groups = []
+    ok = True
+    for r, cl in contributions.items():
+        g = tuple(sorted(c.src_rank for c in cl))
+        if r not in g or len(set(g)) != len(g):
+            ok = False
+            break
+        if any(c.part != dst_boxes[r] or c.src_box != dst_boxes[r] for c in cl):
+            ok = False
+            break
+        for m in g:
+            cm = contributions.get(m)
+            if cm is None or tuple(sorted(c.src_rank for c in cm)) != g or dst_boxes[m] != dst_boxes[r]:
+                ok = False
+                break
+        if not ok:
+            break
+        if g not in groups:
+            groups.append(g)
+    if ok and src.sum_degree > dst.sum_degree:
+        return Plan("all_reduce", contributions, dst_boxes, src_boxes, groups)
+    # all_gather: each rank assembles its dst box from its group's own pieces
+    groups = []
+    ok = src.sum_degree == dst.sum_degree
+    gdim = -1
+    if ok:
+        for r, cl in contributions.items():
+            g = tuple(sorted(c.src_rank for c in cl))
+            if r not in g or len(set(g)) != len(g) or len(g) < 2:
+                ok = False
+                break
+            for c in cl:
+                if c.part != c.src_box or c.src_box != src_boxes[c.src_rank]:
+                    ok = False
+                    break
+                diff = [i for i, ((l1, h1), (l2, h2)) in enumerate(zip(c.src_box, dst_boxes[r])) if (l1, h1) != (l2, h2)]
+                if len(diff) != 1 or (gdim != -1 and diff[0] != gdim):
+                    ok = False
+                    break
+                gdim = diff[0]
+            if not ok:
+                break
+            for m in g:
+                cm = contributions.get(m)
+                if cm is None or tuple(sorted(c.src_rank for c in cm)) != g or dst_boxes[m] != dst_boxes[r]:
+                    ok = False
+                    break
+            if not ok:
+                break
+            if g not in groups:
+                groups.append(g)
+    if ok and gdim >= 0:
+        return Plan("all_gather", contributions, dst_boxes, src_boxes, groups, gather_dim=gdim)
+    return Plan("p2p", contributions, dst_boxes, src_boxes, [])
+
+
+def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_shape: Sequence[int],
+                 dtype: torch.dtype, device: torch.device) -> Optional[torch.Tensor]:
+    me = ctx.rank
+    my_dst = plan.dst_boxes.get(me)
+    my_src = plan.src_boxes.get(me)
+    if plan.kind == "local":
+        ctx.stats["local"] += 1
+        if my_dst is None:
+            return None
+        cl = plan.contributions[me]
+        if not cl:
+            return torch.zeros(dst_shape, dtype=dtype, device=device)
+        c = cl[0]
+        if c.part == my_src:
+            return x
+        return x[rel_slices(c.part, my_src)].contiguous()
+    if plan.kind == "all_reduce":
+        y = x.clone()
+        g = next(g for g in plan.groups if me in g)
+        ctx.all_reduce_(y, g)
+        return y
+    if plan.kind == "all_gather":
+        g = next(g for g in plan.groups if me in g)
+        ctx.stats["all_gather"] += 1
+        xs = x.contiguous()
+        outs = [torch.empty_like(xs) for _ in g]
+        dist.all_gather(outs, xs, group=ctx.group(g))
+        order = sorted(range(len(g)), key=lambda i: plan.src_boxes[g[i]][plan.gather_dim][0])
+        # members holding identical boxes (implicit replicas) appear once
+        seen, parts = set(), []
+        for i in order:
+            b = plan.src_boxes[g[i]]
+            if b in seen:
+                continue
+            seen.add(b)
+            parts.append(outs[i])
+        return torch.cat(parts, dim=plan.gather_dim)
+    # ---- generic point-to-point
+    ctx.stats["p2p"] += 1
+    ops = []
+    recv_bufs = []
+    for r, cl in plan.contributions.items():
+        for c in cl:
+            if c.src_rank == me and r != me:
+                piece = x[rel_slices(c.part, my_src)].contiguous()
+                ops.append(dist.P2POp(dist.isend, piece, r))
+    result = None
+    if my_dst is not None:
+        result = torch.zeros(dst_shape, dtype=dtype, device=device)
+        for c in plan.contributions[me]:
+            if c.src_rank == me:
+                result[rel_slices(c.part, my_dst)] += x[rel_slices(c.part, my_src)]
+            else:
+                buf = torch.empty([h - l for l, h in c.part], dtype=dtype, device=device)
+                ops.append(dist.P2POp(dist.irecv, buf, c.src_rank))
+                recv_bufs.append((c, buf))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for c, buf in recv_bufs:
+        result[rel_slices(c.part, my_dst)] += buf
+    return result
+
+
+class Redistributor:
+    """Caches plans and creates every sub-communicator they need up front."""
+
+    def __init__(self, ctx: DistContext):
+        self.ctx = ctx
+        self._plans: Dict[Tuple[Layout, Layout], Plan] = {}
+
+    def plan(self, src: Layout, dst: Layout) -> Plan:
+        key = (src, dst)
+        if key not in self._plans:
+            p = make_plan(src, dst, self.ctx.world)
+            for g in p.groups:
+                if self.ctx.distributed:
+                    self.ctx.group(g)
+            self._plans[key] = p
+        return self._plans[key]
+
+    def __call__(self, x: Optional[torch.Tensor], src: Layout, dst: Layout, dtype: torch.dtype,
+                 device: torch.device) -> Optional[torch.Tensor]:
+        p = self.plan(src, dst)
+        if p.kind != "local" and not self.ctx.distributed:
+            raise RuntimeError(f"redistribution {p.kind} needs torch.distributed (world={self.ctx.world})")
+        return execute_plan(p, x, self.ctx, dst.piece_shape, dtype, device)

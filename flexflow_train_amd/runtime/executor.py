@@ -1,0 +1,753 @@
+"""Per-rank executor of a ParallelComputationGraph.
+
+This is the MI355X replacement of the reference's Legion runtime
+(lib/runtime: FFModel/LegionBacking/FFMapper/NCCL communicators) and of the
+single-device LocalTrainingBacking (lib/local-execution/src/
+local_training_backing.cc:50-163):
+
+* one process per GPU; the PCG is lowered ONCE into a flat list of steps for
+  this rank (compute steps on local shards, redistribution steps for the
+  parallel operators and for machine-view changes), executed on the current
+  HIP stream; hipGraph capture of a whole iteration replaces Legion tracing;
+* weights: the WEIGHT -> Repartition/Replicate chains of the PCG are folded
+  into the parameter's resident layout; all parameter pieces of a rank live
+  in ONE flat fp32 master buffer (+ bf16 compute copy + fp32 gradient buffer)
+  per gradient-sync group; gradients are reduced with bucketed RCCL
+  all-reduces launched as soon as the backward pass finalises each bucket
+  (overlapped with the rest of the backward — the reference simulator's
+  "overlap backward and update" mode, simulator.cc:914-955);
+* the optimizer update is one fused launch per flat buffer;
+* loss + metrics are fused with the trailing softmax (loss.py).
+"""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import json
+import math
+import time
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import _ffcore as C
+from .. import ops as _ops_pkg  # noqa: F401  (registers operator impls)
+from ..ops import base as opbase
+from ..ops.loss import N_SLOTS, LossFunction, PerfMetrics
+from ..parallel.comm import DistContext, Redistributor
+from ..parallel.layout import Layout, layout_from_pshape
+from .optimizer import AdamConfig, FlatOptimizer, SGDConfig
+from .initializers import make_initializer_tensor
+
+Value = Tuple[int, int]
+_PAR_OPS = {"REPARTITION", "COMBINE", "REPLICATE", "REDUCTION", "ALLTOALL", "FUSED_PARALLEL"}
+_TORCH_DT = {"float": torch.float32, "double": torch.float64, "half": torch.float16, "bfloat16": torch.bfloat16,
+             "int32": torch.int32, "int64": torch.int64, "bool": torch.bool}
+
+
+@dataclasses.dataclass
+class ExecConfig:
+    compute_dtype: torch.dtype = torch.float32
+    device: torch.device = torch.device("cpu")
+    seed: int = 0
+    bucket_bytes: int = 64 << 20
+    fuse_add_layernorm: bool = True
+    profiling: bool = False
+    grad_clip: float = 0.0
+    overlap_grad_sync: bool = True
+
+
+@dataclasses.dataclass
+class ParamPiece:
+    name: str
+    node: int
+    terminal: Value
+    layout: Layout
+    logical_shape: Tuple[int, ...]
+    initializer: dict
+    group: Tuple[int, ...]
+    trainable: bool
+    consumer_op: str = ""
+    consumer_attrs: dict = dataclasses.field(default_factory=dict)
+    offset: int = 0
+    numel: int = 0
+    flat_id: int = 0
+    final_step: int = -1          # forward index of first consumer
+    master: Optional[torch.Tensor] = None
+    compute: Optional[torch.Tensor] = None
+    grad: Optional[torch.Tensor] = None
+
+
+@dataclasses.dataclass
+class Step:
+    kind: str                      # "compute" | "comm"
+    node: int
+    op_type: str
+    inputs: List[Value]
+    outputs: List[Value]
+    weights: List[Optional[ParamPiece]] = dataclasses.field(default_factory=list)
+    src: Optional[Layout] = None
+    dst: Optional[Layout] = None
+    ctx: Optional[opbase.OpContext] = None
+    active: bool = True            # this rank participates
+    name: str = ""
+
+
+def _stable_seed(*parts) -> int:
+    h = hashlib.sha256(("/".join(str(p) for p in parts)).encode()).digest()
+    return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
+
+
+class Executor:
+    def __init__(self, pcg, dist_ctx: DistContext, cfg: ExecConfig, views: Optional[Dict[int, Tuple[int, int]]] = None,
+                 loss_type=None, metrics: Sequence[str] = (), optimizer=None, output: Optional[Value] = None,
+                 label_dtype: Optional[torch.dtype] = None, valid_classes: Optional[int] = None):
+        self.pcg = pcg
+        self.dist = dist_ctx
+        self.cfg = cfg
+        self.views = dict(views or {})
+        self.world = dist_ctx.world
+        self.rank = dist_ctx.rank
+        self.redist = Redistributor(dist_ctx)
+        self.metrics_names = list(metrics)
+        self.optimizer_cfg = optimizer or SGDConfig()
+        self.valid_classes = valid_classes
+        self.step_num = 0
+        self._profile: Dict[str, float] = {}
+        self._build(output)
+        self.loss = LossFunction(loss_type, self._global_rows(), valid_cols=valid_classes) if loss_type else None
+        self.metrics_buf = torch.zeros(N_SLOTS, device=cfg.device, dtype=torch.float32)
+        self.metrics_start = time.time()
+        self._saved: Dict[int, Any] = {}
+        self._env: Dict[Value, torch.Tensor] = {}
+        self._works = []
+
+    # ------------------------------------------------------------------ build
+    def _view(self, node: int) -> Tuple[int, int]:
+        return self.views.get(node, (0, self.world))
+
+    def _layout(self, v: Value, node_for_view: Optional[int] = None) -> Layout:
+        start, block = self._view(v[0] if node_for_view is None else node_for_view)
+        return layout_from_pshape(self.pcg.shape(C.ValueRef(v[0], v[1])), block, start)
+
+    def _build(self, output: Optional[Value]):
+        pcg = self.pcg
+        order = list(pcg.topo_order())
+        self.order = order
+        optype = {n: pcg.layer_op(n).op_type for n in order}
+        attrs = {n: dict(pcg.layer_op(n).items()) for n in order}
+        names = {n: pcg.layer_name(n) for n in order}
+        inputs_of = {n: [(v.node, v.idx) for v in pcg.layer_inputs(n)] for n in order}
+        nout = {n: pcg.num_outputs(n) for n in order}
+        uses: Dict[Value, List[Tuple[int, int]]] = {}
+        for n in order:
+            for slot, v in enumerate(inputs_of[n]):
+                uses.setdefault(v, []).append((n, slot))
+        self._uses = uses
+        weight_path = {n: pcg.is_weight_path(n) for n in order}
+
+        def follow_chain(v: Value) -> List[Value]:
+            """Terminal values reached from v through parallel ops only."""
+            terms = []
+            for (c, _) in uses.get(v, []):
+                if optype[c] in _PAR_OPS and nout[c] == 1:
+                    terms.extend(follow_chain((c, 0)))
+                else:
+                    terms.append(v)
+            return sorted(set(terms))
+
+        # ---- parameters (folded weight paths)
+        self.params: List[ParamPiece] = []
+        self.param_of_value: Dict[Value, ParamPiece] = {}
+        folded = set()
+        for n in order:
+            if optype[n] != "WEIGHT":
+                continue
+            terms = follow_chain((n, 0))
+            if len(terms) != 1:
+                terms = [(n, 0)]  # shared weight with several layouts: keep the source layout
+            t = terms[0]
+            # fold the chain nodes
+            cur = t
+            while cur[0] != n:
+                folded.add(cur[0])
+                cur = inputs_of[cur[0]][0]
+            consumers = [c for (c, _) in uses.get(t, [])]
+            cnode = consumers[0] if consumers else n
+            lay = self._layout(t, node_for_view=cnode)
+            init = json.loads(attrs[n].get("initializer") or '{"type":"zero"}')
+            piece = ParamPiece(name=names[n] or f"weight_{n}", node=n, terminal=t, layout=lay,
+                               logical_shape=tuple(lay.sizes), initializer=init, group=(), trainable=bool(
+                                   pcg.create_grad(C.ValueRef(n, 0))),
+                               consumer_op=optype[cnode], consumer_attrs=attrs[cnode])
+            self.params.append(piece)
+            self.param_of_value[t] = piece
+            folded.add(n)
+
+        # ---- data inputs (folded repartition chains)
+        self.inputs: Dict[str, Tuple[Value, Layout, torch.dtype]] = {}
+        self.input_terminal: Dict[Value, str] = {}
+        for n in order:
+            if optype[n] != "INPUT":
+                continue
+            terms = follow_chain((n, 0))
+            if len(terms) != 1:
+                terms = [(n, 0)]
+            t = terms[0]
+            cur = t
+            while cur[0] != n:
+                folded.add(cur[0])
+                cur = inputs_of[cur[0]][0]
+            consumers = [c for (c, _) in uses.get(t, [])]
+            lay = self._layout(t, node_for_view=consumers[0] if consumers else n)
+            dt = _TORCH_DT.get(attrs[n].get("data_type", "float"), torch.float32)
+            nm = names[n] or f"input_{n}"
+            self.inputs[nm] = (t, lay, dt)
+            self.input_terminal[t] = nm
+            folded.add(n)
+
+        # ---- steps
+        self.steps: List[Step] = []
+        self.value_layout: Dict[Value, Layout] = {}
+        for nm, (t, lay, _) in self.inputs.items():
+            self.value_layout[t] = lay
+        for p in self.params:
+            self.value_layout[p.terminal] = p.layout
+        for n in order:
+            if n in folded or weight_path.get(n) and n in folded:
+                continue
+            t = optype[n]
+            if t in ("INPUT", "WEIGHT"):
+                continue
+            ins = inputs_of[n]
+            if t in _PAR_OPS:
+                src = self.value_layout[ins[0]]
+                start, block = self._view(n)
+                dst = layout_from_pshape(pcg.shape(C.ValueRef(n, 0)), block, start)
+                self.steps.append(Step("comm", n, t, [ins[0]], [(n, 0)], src=src, dst=dst, name=names[n]))
+                self.value_layout[(n, 0)] = dst
+                continue
+            nw = C.num_weights(pcg.layer_op(n))
+            data_ins, w_ins = ins[:len(ins) - nw], ins[len(ins) - nw:]
+            start, block = self._view(n)
+            # implicit view changes for data inputs
+            real_ins = []
+            for v in data_ins:
+                want = layout_from_pshape(pcg.shape(C.ValueRef(*v)), block, start)
+                have = self.value_layout[v]
+                if have != want:
+                    nv = (-(len(self.steps) + 1) * 1000 - v[0], v[1])  # synthetic value id
+                    self.steps.append(Step("comm", n, "VIEW_CHANGE", [v], [nv], src=have, dst=want,
+                                           name=f"{names[n]}.view"))
+                    self.value_layout[nv] = want
+                    v = nv
+                real_ins.append(v)
+            wpieces = []
+            for v in w_ins:
+                if v not in self.param_of_value:
+                    raise NotImplementedError(f"{names[n]}: weight input {v} is not a folded parameter")
+                wpieces.append(self.param_of_value[v])
+            outs = [(n, i) for i in range(nout[n])]
+            for o in outs:
+                self.value_layout[o] = layout_from_pshape(pcg.shape(C.ValueRef(*o)), block, start)
+            olay = self.value_layout[outs[0]]
+            coord = olay.coord(self.rank)
+            in0 = pcg.shape(C.ValueRef(*data_ins[0])) if data_ins else None
+            ctx = opbase.OpContext(
+                op_type=t, attrs=attrs[n], name=names[n],
+                sum_index=coord.a if coord else 0, sum_degree=olay.a_deg,
+                copy_index=coord.b if coord else 0,
+                input_copy_degree=int(in0.discard_copy_degree) if in0 is not None else 1,
+                input_sum_degree=int(in0.sum_degree) if in0 is not None else 1,
+                compute_dtype=self.cfg.compute_dtype, device=self.cfg.device,
+                seed=_stable_seed(self.cfg.seed, names[n], self.rank // max(1, olay.reps) if coord else 0),
+                output_shapes=[self.value_layout[o].piece_shape for o in outs])
+            if t in ("REDUCE_MEAN", "MEAN") and in0 is not None:
+                axes = [int(a) % len(in0.shard_dims) for a in attrs[n].get("axes", [])]
+                deg = math.prod(int(in0.shard_dims[a].degree) for a in axes)
+                if deg > 1:
+                    ctx.extra["mean_scale"] = 1.0 / deg
+            self.steps.append(Step("compute", n, t, real_ins, outs, weights=wpieces, ctx=ctx,
+                                   active=coord is not None, name=names[n]))
+
+        # ---- output / loss value
+        if output is None:
+            last = [s for s in self.steps if s.kind == "compute"][-1]
+            output = last.outputs[0]
+        self.output_value = output
+        self.loss_value = output
+        self.softmax_fused_step: Optional[Step] = None
+        prod_step = next((s for s in self.steps if output in s.outputs), None)
+        if prod_step is not None and prod_step.op_type == "SOFTMAX":
+            self.softmax_fused_step = prod_step
+            self.loss_value = prod_step.inputs[0]
+        if self.cfg.fuse_add_layernorm:
+            self._fuse_add_layernorm()
+        self._mark_requires_grad()
+        self._assign_params_to_buffers()
+
+    def _fuse_add_layernorm(self):
+        by_out = {o: s for s in self.steps for o in s.outputs}
+        keep = []
+        drop = set()
+        for s in self.steps:
+            if s.kind == "compute" and s.op_type == "LAYERNORM" and len(s.inputs) == 1:
+                v = s.inputs[0]
+                prod = by_out.get(v)
+                if (prod is not None and prod.kind == "compute" and prod.op_type == "EW_ADD"
+                        and len(self._uses.get(v, [])) == 1 and v != self.loss_value
+                        and self.value_layout[prod.inputs[0]] == self.value_layout[prod.inputs[1]]
+                        and self.value_layout[v] == self.value_layout[prod.inputs[0]]):
+                    s.op_type = "FUSED_ADD_LAYERNORM"
+                    s.ctx.op_type = "FUSED_ADD_LAYERNORM"
+                    s.inputs = list(prod.inputs)
+                    drop.add(id(prod))
+        for s in self.steps:
+            if id(s) not in drop:
+                keep.append(s)
+        self.steps = keep
+
+    def _mark_requires_grad(self):
+        rg: Dict[Value, bool] = {}
+        for p in self.params:
+            rg[p.terminal] = p.trainable
+        for nm, (t, _, dt) in self.inputs.items():
+            rg[t] = False
+        for idx, s in enumerate(self.steps):
+            need = any(rg.get(v, False) for v in s.inputs) or any(p.trainable for p in s.weights)
+            for o in s.outputs:
+                rg[o] = need
+            for p in s.weights:
+                if p.final_step < 0:
+                    p.final_step = idx
+        self.requires_grad = rg
+
+    def _assign_params_to_buffers(self):
+        dev = self.cfg.device
+        # gradient-sync group: same shard piece, same partial index, same
+        # implicit replica; all discard-copy indices (their grads add up).
+        for p in self.params:
+            lay = p.layout
+            c = lay.coord(self.rank)
+            if c is None:
+                p.group = ()
+                continue
+            grp = []
+            for b in range(lay.b_deg):
+                grp.append(lay.rank_of(dataclasses.replace(c, b=b)))
+            p.group = tuple(sorted(grp))
+        held = [p for p in self.params if p.group]
+        # flat order = the order in which backward finalises gradients
+        held.sort(key=lambda p: (-p.final_step, p.node))
+        groups: Dict[Tuple[int, ...], List[ParamPiece]] = {}
+        for p in held:
+            groups.setdefault(p.group, []).append(p)
+        self.flats = []
+        cd = self.cfg.compute_dtype
+        for fid, (g, plist) in enumerate(sorted(groups.items(), key=lambda kv: kv[0])):
+            off = 0
+            for p in plist:
+                p.numel = int(math.prod(p.layout.piece_shape))
+                p.offset = off
+                p.flat_id = fid
+                off += (p.numel + 63) // 64 * 64
+            master = torch.zeros(off, dtype=torch.float32, device=dev)
+            grad = torch.zeros(off, dtype=torch.float32, device=dev)
+            compute = torch.zeros(off, dtype=cd, device=dev) if cd != torch.float32 else None
+            for p in plist:
+                shp = p.layout.piece_shape
+                p.master = master[p.offset:p.offset + p.numel].view(shp)
+                p.grad = grad[p.offset:p.offset + p.numel].view(shp)
+                p.compute = (compute[p.offset:p.offset + p.numel].view(shp) if compute is not None else p.master)
+            # buckets: contiguous param ranges, finalised in backward order
+            buckets, cur, cur_bytes = [], [], 0
+            for p in plist:
+                cur.append(p)
+                cur_bytes += p.numel * 4
+                if cur_bytes >= self.cfg.bucket_bytes:
+                    buckets.append(cur)
+                    cur, cur_bytes = [], 0
+            if cur:
+                buckets.append(cur)
+            binfo = []
+            for b in buckets:
+                lo = b[0].offset
+                hi = b[-1].offset + (b[-1].numel + 63) // 64 * 64
+                binfo.append({"params": b, "lo": lo, "hi": hi, "pending": 0})
+            opt = FlatOptimizer(self.optimizer_cfg, master, grad, compute)
+            self.flats.append({"group": g, "params": plist, "master": master, "grad": grad, "compute": compute,
+                               "buckets": binfo, "opt": opt})
+        self._param_bucket = {}
+        for f in self.flats:
+            for bi, b in enumerate(f["buckets"]):
+                for p in b["params"]:
+                    self._param_bucket[id(p)] = (f, b)
+        # create every sub-communicator collectively, in a deterministic order
+        if self.dist.distributed:
+            all_groups = set()
+            for p in self.params:
+                lay = p.layout
+                for r in range(self.world):
+                    c = lay.coord(r)
+                    if c is None:
+                        continue
+                    all_groups.add(tuple(sorted(lay.rank_of(dataclasses.replace(c, b=b)) for b in range(lay.b_deg))))
+            for g in sorted(all_groups):
+                if len(g) > 1:
+                    self.dist.group(g)
+            for s in self.steps:
+                if s.kind == "comm":
+                    self.redist.plan(s.src, s.dst)
+                    self.redist.plan(s.dst.dual(), s.src.dual())
+
+    # ------------------------------------------------------------ weights
+    def init_parameters(self):
+        """Deterministic initialisation: every rank generates the full logical
+        weight from a seed derived from the weight name, then keeps its piece
+        (identical across replicas without any broadcast)."""
+        for p in self.params:
+            if not p.group:
+                continue
+            gen = torch.Generator().manual_seed(_stable_seed(self.cfg.seed, p.name))
+            impl = None
+            try:
+                impl = opbase.get_impl(p.consumer_op)
+            except NotImplementedError:
+                pass
+            full = None
+            if impl is not None:
+                ctx = opbase.OpContext(op_type=p.consumer_op, attrs=p.consumer_attrs, name=p.name)
+                widx = self._weight_index(p)
+                full = impl.init_weight(ctx, widx, p.logical_shape, p.initializer, gen)
+            if full is None:
+                full = make_initializer_tensor(p.initializer, p.logical_shape, gen)
+            self._set_piece(p, full)
+        for f in self.flats:
+            if f["compute"] is not None:
+                f["compute"].copy_(f["master"])
+
+    def _weight_index(self, p: ParamPiece) -> int:
+        for s in self.steps:
+            for i, w in enumerate(s.weights):
+                if w is p:
+                    return i
+        return 0
+
+    def _set_piece(self, p: ParamPiece, full: torch.Tensor):
+        c = p.layout.coord(self.rank)
+        box = p.layout.box(c.shard)
+        sl = tuple(slice(lo, hi) for lo, hi in box)
+        p.master.copy_(full.reshape(p.logical_shape)[sl].to(torch.float32))
+        if p.compute is not p.master:
+            p.compute.copy_(p.master)
+
+    def get_parameter(self, name: str) -> torch.Tensor:
+        """Full logical weight (gathered across ranks)."""
+        p = next(pp for pp in self.params if pp.name == name)
+        full = torch.zeros(p.logical_shape, dtype=torch.float32, device=self.cfg.device)
+        c = p.layout.coord(self.rank)
+        owner = c is not None and c.b == 0 and c.rep == 0 and c.a == 0
+        if owner:
+            box = p.layout.box(c.shard)
+            full[tuple(slice(lo, hi) for lo, hi in box)] = p.master
+        if self.dist.distributed:
+            import torch.distributed as dist
+            dist.all_reduce(full)
+        return full
+
+    def set_parameter(self, name: str, value: torch.Tensor):
+        p = next(pp for pp in self.params if pp.name == name)
+        if p.group:
+            self._set_piece(p, value.to(self.cfg.device).float())
+
+    def parameter_names(self) -> List[str]:
+        return [p.name for p in self.params]
+
+    # --------------------------------------------------------------- inputs
+    def local_input_shape(self, name: str) -> Tuple[int, ...]:
+        return self.inputs[name][1].piece_shape
+
+    def _local_piece(self, name: str, x: torch.Tensor) -> Optional[torch.Tensor]:
+        t, lay, dt = self.inputs[name]
+        c = lay.coord(self.rank)
+        if c is None:
+            return None
+        if tuple(x.shape) == tuple(lay.piece_shape) and tuple(lay.sizes) != tuple(lay.piece_shape):
+            piece = x  # already the local piece
+        elif tuple(x.shape) == tuple(lay.sizes):
+            piece = x[tuple(slice(lo, hi) for lo, hi in lay.box(c.shard))]
+        else:
+            raise ValueError(f"input {name}: shape {tuple(x.shape)} is neither global {lay.sizes} "
+                             f"nor local {lay.piece_shape}")
+        piece = piece.to(self.cfg.device, non_blocking=True)
+        if piece.is_floating_point():
+            piece = piece.to(self.cfg.compute_dtype)
+        return piece.contiguous()
+
+    def _global_rows(self) -> int:
+        lay = self.value_layout[self.loss_value]
+        return int(math.prod(lay.sizes[:-1])) if len(lay.sizes) > 1 else int(lay.sizes[0])
+
+    def label_layout(self) -> Layout:
+        lay = self.value_layout[self.loss_value]
+        return lay
+
+    def local_labels(self, y: torch.Tensor) -> Optional[torch.Tensor]:
+        lay = self._loss_layout()
+        c = lay.coord(self.rank)
+        if c is None:
+            return None
+        box = lay.box(c.shard)
+        sparse = self.loss is not None and self.loss.loss_type == "sparse_categorical_crossentropy"
+        gshape = tuple(lay.sizes[:-1]) if sparse else tuple(lay.sizes)
+        lshape = tuple(lay.piece_shape[:-1]) if sparse else tuple(lay.piece_shape)
+        nb = box[:-1] if sparse else box
+        if y.numel() == math.prod(gshape):
+            y = y.reshape(gshape)[tuple(slice(lo, hi) for lo, hi in nb)]
+        elif y.numel() == math.prod(lshape):
+            y = y.reshape(lshape)
+        else:
+            raise ValueError(f"labels of shape {tuple(y.shape)} match neither global {gshape} nor local {lshape}")
+        return y.to(self.cfg.device, non_blocking=True).contiguous()
+
+    def _loss_layout(self) -> Layout:
+        lay = self.value_layout[self.loss_value]
+        if lay.degrees[-1] != 1 or lay.a_deg != 1:
+            degs = tuple(lay.degrees[:-1]) + (1,)
+            lay = dataclasses.replace(lay, degrees=degs, a_deg=1)
+        return lay
+
+    # -------------------------------------------------------------- execution
+    def forward(self, feeds: Dict[str, torch.Tensor], training: bool = True, keep_outputs: bool = False):
+        env: Dict[Value, torch.Tensor] = {}
+        for name, x in feeds.items():
+            if name not in self.inputs:
+                raise KeyError(f"unknown input {name}; inputs are {list(self.inputs)}")
+            piece = self._local_piece(name, x)
+            if piece is not None:
+                env[self.inputs[name][0]] = piece
+        for p in self.params:
+            if p.group:
+                env[p.terminal] = p.compute
+        self._saved = {}
+        prof = self.cfg.profiling and self.cfg.device.type == "cuda"
+        for i, s in enumerate(self.steps):
+            if training and s is self.softmax_fused_step and self.loss is not None and self.loss.fuses_softmax:
+                continue
+            if s.kind == "comm":
+                x = env.get(s.inputs[0])
+                env[s.outputs[0]] = self.redist(x, s.src, s.dst, self._dtype_of(s.inputs[0], x), self.cfg.device)
+                continue
+            if not s.active:
+                continue
+            s.ctx.training = training
+            s.ctx.step = self.step_num
+            ins = [env[v] for v in s.inputs]
+            ws = [p.compute for p in s.weights]
+            impl = opbase.get_impl(s.op_type)
+            t0 = self._tick() if prof else None
+            outs, saved = impl.forward(s.ctx, ins, ws)
+            if prof:
+                self._tock(t0, f"{s.name}:fwd")
+            for o, t in zip(s.outputs, outs):
+                env[o] = t
+            if training:
+                self._saved[i] = saved
+        self._env = env
+        return env.get(self.output_value) if keep_outputs or not training else env.get(self.loss_value)
+
+    def _dtype_of(self, v: Value, x: Optional[torch.Tensor]) -> torch.dtype:
+        if x is not None:
+            return x.dtype
+        ps = self.pcg.shape(C.ValueRef(*v)) if v[0] >= 0 else None
+        if ps is not None and C.datatype_to_string(ps.dtype) in ("int32", "int64"):
+            return _TORCH_DT[C.datatype_to_string(ps.dtype)]
+        return self.cfg.compute_dtype
+
+    def compute_loss(self, labels: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        logits = self._env.get(self.loss_value)
+        lay = self.value_layout[self.loss_value]
+        want = self._loss_layout()
+        if want != lay:
+            logits = self.redist(logits, lay, want, logits.dtype if logits is not None else self.cfg.compute_dtype,
+                                 self.cfg.device)
+        c = want.coord(self.rank)
+        if c is None or logits is None:
+            return None
+        y = self.local_labels(labels)
+        if c.rep == 0 and c.b == 0:
+            mbuf = self.metrics_buf
+        else:
+            mbuf = torch.zeros(N_SLOTS, device=self.cfg.device)  # replicas do not double count
+        g = self.loss(logits, y, mbuf)
+        if want.b_deg > 1:
+            g = g / want.b_deg
+        if want != lay:
+            g = self.redist(g, want.dual(), lay.dual(), g.dtype, self.cfg.device)
+        return g
+
+    def backward(self, dlogits: Optional[torch.Tensor]):
+        grads: Dict[Value, torch.Tensor] = {}
+        if dlogits is not None:
+            grads[self.loss_value] = dlogits
+        for f in self.flats:
+            f["grad"].zero_()
+            for b in f["buckets"]:
+                b["pending"] = sum(1 for p in b["params"] if p.trainable)
+        self._works = []
+        prof = self.cfg.profiling and self.cfg.device.type == "cuda"
+        n = len(self.steps)
+        for i in range(n - 1, -1, -1):
+            s = self.steps[i]
+            if s is self.softmax_fused_step and self.loss is not None and self.loss.fuses_softmax:
+                continue
+            if s.kind == "comm":
+                g = grads.pop(s.outputs[0], None)
+                if not self.requires_grad.get(s.inputs[0], False):
+                    continue
+                if g is None and s.dst.coord(self.rank) is not None:
+                    g = torch.zeros(s.dst.piece_shape, dtype=self.cfg.compute_dtype, device=self.cfg.device)
+                gi = self.redist(g, s.dst.dual(), s.src.dual(), g.dtype if g is not None else self.cfg.compute_dtype,
+                                 self.cfg.device)
+                self._acc(grads, s.inputs[0], gi)
+                continue
+            saved = self._saved.pop(i, None)
+            if s.active:
+                gouts = [grads.pop(o, None) for o in s.outputs]
+                need = [self.requires_grad.get(v, False) for v in s.inputs]
+                if any(g is not None for g in gouts) and (any(need) or any(p.trainable for p in s.weights)):
+                    gouts = [g if g is not None else None for g in gouts]
+                    if gouts[0] is None:
+                        gouts[0] = torch.zeros(s.ctx.output_shapes[0], dtype=self.cfg.compute_dtype,
+                                               device=self.cfg.device)
+                    wgs = [p.grad if p.trainable else None for p in s.weights]
+                    impl = opbase.get_impl(s.op_type)
+                    t0 = self._tick() if prof else None
+                    gins = impl.backward(s.ctx, saved, gouts, wgs, need)
+                    if prof:
+                        self._tock(t0, f"{s.name}:bwd")
+                    for v, g, nd in zip(s.inputs, gins, need):
+                        if g is not None and nd:
+                            self._acc(grads, v, g)
+            for p in s.weights:
+                if p.final_step == i and p.trainable:
+                    self._param_done(p)
+        self._saved = {}
+        self._env = {}
+        self._finish_grad_sync()
+
+    def _acc(self, grads, v, g):
+        if g is None:
+            return
+        if v in grads:
+            grads[v] = grads[v] + g
+        else:
+            grads[v] = g
+
+    def _param_done(self, p: ParamPiece):
+        fb = self._param_bucket.get(id(p))
+        if fb is None:
+            return
+        f, b = fb
+        b["pending"] -= 1
+        if b["pending"] == 0 and self.cfg.overlap_grad_sync:
+            self._launch_bucket(f, b)
+
+    def _launch_bucket(self, f, b):
+        if len(f["group"]) > 1 and self.dist.distributed and not b.get("launched"):
+            w = self.dist.all_reduce_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
+            b["launched"] = True
+            if w is not None:
+                self._works.append(w)
+
+    def _finish_grad_sync(self):
+        for f in self.flats:
+            for b in f["buckets"]:
+                if not b.get("launched"):
+                    self._launch_bucket(f, b)
+        for w in self._works:
+            w.wait()
+        self._works = []
+        for f in self.flats:
+            for b in f["buckets"]:
+                b["launched"] = False
+
+    def update(self, lr: Optional[float] = None):
+        scale = 1.0
+        if self.cfg.grad_clip > 0:
+            norm = self.grad_norm()
+            if norm > self.cfg.grad_clip:
+                scale = self.cfg.grad_clip / (norm + 1e-6)
+        for f in self.flats:
+            f["opt"].step(lr=lr, grad_scale=scale)
+        self.step_num += 1
+
+    def grad_norm(self) -> float:
+        tot = torch.zeros(1, device=self.cfg.device, dtype=torch.float64)
+        for f in self.flats:
+            tot += f["grad"].double().pow(2).sum()
+        if self.dist.distributed:
+            import torch.distributed as dist
+            dist.all_reduce(tot)
+        return float(tot.sqrt().item())
+
+    def train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
+        self.forward(feeds, training=True)
+        g = self.compute_loss(labels)
+        self.backward(g)
+        self.update(lr)
+
+    def zero_metrics(self):
+        self.metrics_buf.zero_()
+        self.metrics_start = time.time()
+
+    def perf_metrics(self) -> PerfMetrics:
+        buf = self.metrics_buf.clone()
+        if self.dist.distributed:
+            import torch.distributed as dist
+            dist.all_reduce(buf)
+        out_dim = self.value_layout[self.loss_value].sizes[-1]
+        return PerfMetrics.from_buffer(buf, self.metrics_names, self.loss.loss_type if self.loss else "",
+                                       self.metrics_start, out_dim)
+
+    # --------------------------------------------------------------- profiling
+    def _tick(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _tock(self, start, key):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        e.synchronize()
+        self._profile[key] = self._profile.get(key, 0.0) + start.elapsed_time(e)
+
+    def profile_report(self) -> Dict[str, float]:
+        return dict(sorted(self._profile.items(), key=lambda kv: -kv[1]))
+
+    # ------------------------------------------------------------ checkpoint
+    def state_dict(self) -> Dict[str, Any]:
+        """Local (this rank's) shards + optimizer state + shard metadata."""
+        st = {"step": self.step_num, "rank": self.rank, "world": self.world, "params": {}, "optimizer": []}
+        for p in self.params:
+            if p.group:
+                c = p.layout.coord(self.rank)
+                st["params"][p.name] = {"tensor": p.master.detach().cpu().clone(),
+                                        "box": p.layout.box(c.shard), "logical_shape": p.logical_shape}
+        for f in self.flats:
+            st["optimizer"].append({"step": f["opt"].step_num,
+                                    **{k: t.detach().cpu().clone() for k, t in f["opt"].state_tensors().items()}})
+        return st
+
+    def load_state_dict(self, st: Dict[str, Any]):
+        for p in self.params:
+            if p.group and p.name in st["params"]:
+                p.master.copy_(st["params"][p.name]["tensor"].to(p.master.device))
+                if p.compute is not p.master:
+                    p.compute.copy_(p.master)
+        for f, o in zip(self.flats, st.get("optimizer", [])):
+            f["opt"].step_num = int(o["step"])
+            for k, t in f["opt"].state_tensors().items():
+                if k in o:
+                    t.copy_(o[k].to(t.device))
+        self.step_num = int(st.get("step", 0))
