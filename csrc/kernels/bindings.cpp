@@ -33,9 +33,10 @@ PYBIND11_MODULE(_ffkernels, m) {
                             uintptr_t y, uintptr_t mean, uintptr_t rstd, int M, int N, float eps, uintptr_t st) {
     layernorm_fwd(dt, P(x), P(res), P(sum_out), P(g), P(b), P(y), F(mean), F(rstd), M, N, eps, S(st));
   });
+  m.def("layernorm_bwd_grid", &layernorm_bwd_grid);
   m.def("layernorm_bwd", [](int dt, uintptr_t dy, uintptr_t s, uintptr_t mean, uintptr_t rstd, uintptr_t g,
-                            uintptr_t dx, uintptr_t dg, uintptr_t db, int M, int N, uintptr_t st) {
-    layernorm_bwd(dt, P(dy), P(s), F(mean), F(rstd), P(g), P(dx), F(dg), F(db), M, N, S(st));
+                            uintptr_t dx, uintptr_t dg, uintptr_t db, uintptr_t ws, int M, int N, uintptr_t st) {
+    layernorm_bwd(dt, P(dy), P(s), F(mean), F(rstd), P(g), P(dx), F(dg), F(db), F(ws), M, N, S(st));
   });
   m.def("bias_act_fwd", [](int dt, uintptr_t x, uintptr_t bias, uintptr_t pre, uintptr_t y, int64_t M, int64_t N,
                            int op, float alpha, uintptr_t st) {
@@ -84,8 +85,8 @@ PYBIND11_MODULE(_ffkernels, m) {
     embedding_fwd(dt, ib, P(idx), P(W), P(out), B, L, D, mode, n, S(st));
   });
   m.def("embedding_bwd", [](int dt, int ib, uintptr_t idx, uintptr_t dout, uintptr_t dW, int64_t B, int L, int D,
-                            int mode, int64_t n, uintptr_t st) {
-    embedding_bwd(dt, ib, P(idx), P(dout), F(dW), B, L, D, mode, n, S(st));
+                            int mode, int64_t n, uintptr_t ws, int copies, uintptr_t st) {
+    embedding_bwd(dt, ib, P(idx), P(dout), F(dW), B, L, D, mode, n, F(ws), copies, S(st));
   });
   m.def("attention_fwd", [](py::tuple q, py::tuple k, py::tuple v, py::tuple o, uintptr_t lse, int B, int H, int Sq,
                             int Sk, int D, float scale, bool causal, uintptr_t st) {

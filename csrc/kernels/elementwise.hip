@@ -138,19 +138,31 @@ __global__ __launch_bounds__(256) void colsum_act_kernel(const T* __restrict__ d
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(M, r0 + rows_per);
   if (active) {
-    for (int r = r0 + wave; r < r1; r += 4) {
-      const size_t off = static_cast<size_t>(r) * N + col;
-      float d[8];
-      ld8<T>(dy + off, d);
-      if (pre) {
-        float p[8];
-        ld8<T>(pre + off, p);
+    // 4 rows per wave per iteration: all loads issued before any use
+    for (int r = r0 + wave; r < r1; r += 16) {
+      float d[4][8], p[4][8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d[k] *= act_grad(op, p[k], alpha);
+      for (int u = 0; u < 4; ++u) {
+        const int rr = r + 4 * u;
+        if (rr < r1) {
+          const size_t off = static_cast<size_t>(rr) * N + col;
+          ld8<T>(dy + off, d[u]);
+          if (pre) ld8<T>(pre + off, p[u]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[u][k] = p[u][k] = 0.f;
+        }
       }
-      if (dx) st8<T>(dx + off, d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += d[k];
+      for (int u = 0; u < 4; ++u) {
+        const int rr = r + 4 * u;
+        if (pre)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[u][k] *= act_grad(op, p[u][k], alpha);
+        if (dx && rr < r1) st8<T>(dx + static_cast<size_t>(rr) * N + col, d[u]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += d[u][k];
+      }
     }
   }
   if (!dbias) return;

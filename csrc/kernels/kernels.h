@@ -10,8 +10,11 @@ namespace ffk {
 // ---- layernorm.hip
 void layernorm_fwd(int dtype, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
                    void* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st);
+// ws: 2 * layernorm_bwd_grid(M, N) * N floats (block partials of dgamma/dbeta)
+int layernorm_bwd_grid(int M, int N);
 void layernorm_bwd(int dtype, const void* dy, const void* s, const float* mean, const float* rstd,
-                   const void* gamma, void* dx, float* dgamma, float* dbeta, int M, int N, hipStream_t st);
+                   const void* gamma, void* dx, float* dgamma, float* dbeta, float* ws, int M, int N,
+                   hipStream_t st);
 
 // ---- elementwise.hip  (op: 0 identity, 1 relu, 2 sigmoid, 3 tanh, 4 gelu, 5 elu, 6 exp)
 void bias_act_fwd(int dtype, const void* x, const void* bias, void* pre, void* y, int64_t M, int64_t N, int op,
@@ -41,7 +44,7 @@ void sum_squares(const float* x, int64_t n, float* out, hipStream_t st);
 void embedding_fwd(int dtype, int index_bits, const void* idx, const void* W, void* out, int64_t B, int L, int D,
                    int mode, int64_t num_entries, hipStream_t st);
 void embedding_bwd(int dtype, int index_bits, const void* idx, const void* dout, float* dW, int64_t B, int L, int D,
-                   int mode, int64_t num_entries, hipStream_t st);
+                   int mode, int64_t num_entries, float* workspace, int copies, hipStream_t st);
 
 // ---- attention.hip
 struct AttnTensors {

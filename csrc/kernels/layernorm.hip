@@ -177,60 +177,87 @@ __global__ __launch_bounds__(256) void ln_fwd_generic(const T* __restrict__ x, c
 // Backward: xhat = (s - mean) * rstd; g = dy * gamma
 //   dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
 //   dgamma += dy * xhat, dbeta += dy
+// One wave per row, two rows in flight per wave (their loads are issued
+// together to hide HBM latency); dgamma / dbeta partials accumulate in
+// registers across the rows a wave visits, are reduced over the block's 4
+// waves in LDS and stored (plain stores, no atomics) as block partials
+// ws[2][gridDim.x][N]; a column-sum pass finishes them.
 template <typename T, int C>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                      const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const T* __restrict__ gamma,
-                                                     T* __restrict__ dx, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, int M) {
+                                                     T* __restrict__ dx, float* __restrict__ ws, int M) {
   constexpr int N = C * 512;
   __shared__ float red[4][2][512];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  float pg[C][8], pb[C][8];
+  float pg[C][8], pb[C][8], gm[C][8];
 #pragma unroll
-  for (int c = 0; c < C; ++c)
+  for (int c = 0; c < C; ++c) {
+    if (gamma) Vec8<T>::load(gamma + c * 512 + lane * 8, gm[c]);
+    else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) gm[c][i] = 1.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) pg[c][i] = pb[c][i] = 0.f;
-
-  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
-    const size_t base = static_cast<size_t>(row) * N;
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[C][8], g[C][8];
-    float sum_g = 0.f, sum_gx = 0.f;
+  }
+  const int stride = gridDim.x * 4;
+  for (int row0 = blockIdx.x * 4 + wave; row0 < M; row0 += 2 * stride) {
+    const int rows[2] = {row0, row0 + stride};
+    float dv[2][C][8], sv[2][C][8];
+    float mean[2], rstd[2];
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int col = c * 512 + lane * 8;
-      float dv[8], sv[8], gm[8];
-      Vec8<T>::load(dy + base + col, dv);
-      Vec8<T>::load(s + base + col, sv);
-      if (gamma) Vec8<T>::load(gamma + col, gm);
-      else
+    for (int k = 0; k < 2; ++k) {
+      const bool ok = rows[k] < M;
+      const size_t base = static_cast<size_t>(ok ? rows[k] : row0) * N;
+      mean[k] = mean_in[ok ? rows[k] : row0];
+      rstd[k] = rstd_in[ok ? rows[k] : row0];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) gm[i] = 1.f;
+      for (int c = 0; c < C; ++c) {
+        Vec8<T>::load(dy + base + c * 512 + lane * 8, dv[k][c]);
+        Vec8<T>::load(s + base + c * 512 + lane * 8, sv[k][c]);
+      }
+      if (!ok)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        xh[c][i] = (sv[i] - mean) * rstd;
-        g[c][i] = dv[i] * gm[i];
-        sum_g += g[c][i];
-        sum_gx += g[c][i] * xh[c][i];
-        pg[c][i] += dv[i] * xh[c][i];
-        pb[c][i] += dv[i];
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dv[k][c][i] = 0.f;
+    }
+    float sum_g[2] = {0.f, 0.f}, sum_gx[2] = {0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xh = (sv[k][c][i] - mean[k]) * rstd[k];
+          const float g = dv[k][c][i] * gm[c][i];
+          sv[k][c][i] = xh;  // keep xhat
+          sum_g[k] += g;
+          sum_gx[k] += g * xh;
+          pg[c][i] += dv[k][c][i] * xh;
+          pb[c][i] += dv[k][c][i];
+        }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      sum_g[k] = wave_sum(sum_g[k]) * (1.f / N);
+      sum_gx[k] = wave_sum(sum_gx[k]) * (1.f / N);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (rows[k] >= M) continue;
+      const size_t base = static_cast<size_t>(rows[k]) * N;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          o[i] = rstd[k] * (dv[k][c][i] * gm[c][i] - sum_g[k] - sv[k][c][i] * sum_gx[k]);
+        Vec8<T>::store(dx + base + c * 512 + lane * 8, o);
       }
     }
-    sum_g = wave_sum(sum_g) * (1.f / N);
-    sum_gx = wave_sum(sum_gx) * (1.f / N);
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int col = c * 512 + lane * 8;
-      float o[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = rstd * (g[c][i] - sum_g - xh[c][i] * sum_gx);
-      Vec8<T>::store(dx + base + col, o);
-    }
   }
-  if (!dgamma && !dbeta) return;
-  // reduce the 4 waves' partials chunk by chunk, then one atomic per column
+  if (!ws) return;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
 #pragma unroll
@@ -240,10 +267,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     }
     __syncthreads();
     for (int j = threadIdx.x; j < 512; j += 256) {
-      float a = red[0][0][j] + red[1][0][j] + red[2][0][j] + red[3][0][j];
-      float b = red[0][1][j] + red[1][1][j] + red[2][1][j] + red[3][1][j];
-      if (dgamma) atomicAdd(dgamma + c * 512 + j, a);
-      if (dbeta) atomicAdd(dbeta + c * 512 + j, b);
+      const float a = red[0][0][j] + red[1][0][j] + red[2][0][j] + red[3][0][j];
+      const float b = red[0][1][j] + red[1][1][j] + red[2][1][j] + red[3][1][j];
+      ws[static_cast<size_t>(blockIdx.x) * N + c * 512 + j] = a;
+      ws[static_cast<size_t>(gridDim.x + blockIdx.x) * N + c * 512 + j] = b;
     }
     __syncthreads();
   }
@@ -323,23 +350,28 @@ static void ln_fwd_t(const void* x, const void* res, void* sum_out, const void* 
 
 template <typename T>
 static void ln_bwd_t(const void* dy, const void* s, const float* mean, const float* rstd, const void* gamma,
-                     void* dx, float* dgamma, float* dbeta, int M, int N, hipStream_t st) {
+                     void* dx, float* dgamma, float* dbeta, float* ws, int M, int N, hipStream_t st) {
   auto DY = static_cast<const T*>(dy);
   auto S = static_cast<const T*>(s);
   auto G = static_cast<const T*>(gamma);
   auto DX = static_cast<T*>(dx);
   if (N % 512 == 0 && N <= 4096) {
-    int grid = std::min((M + 3) / 4, 1024);
+    const int grid = layernorm_bwd_grid(M, N);
+    float* W = (dgamma || dbeta) ? ws : nullptr;
+    if ((dgamma || dbeta) && ws == nullptr) throw std::invalid_argument("layernorm_bwd: workspace required");
     switch (N / 512) {
-#define FFK_LNB_CASE(c)                                                                                        \
-  case c:                                                                                                      \
-    hipLaunchKernelGGL((ln_bwd_kernel<T, c>), dim3(grid), dim3(256), 0, st, DY, S, mean, rstd, G, DX, dgamma, \
-                       dbeta, M);                                                                              \
+#define FFK_LNB_CASE(c)                                                                                      \
+  case c:                                                                                                    \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, c>), dim3(grid), dim3(256), 0, st, DY, S, mean, rstd, G, DX, W, M); \
     break;
       FFK_LNB_CASE(1) FFK_LNB_CASE(2) FFK_LNB_CASE(3) FFK_LNB_CASE(4) FFK_LNB_CASE(5) FFK_LNB_CASE(6)
       FFK_LNB_CASE(7) FFK_LNB_CASE(8)
 #undef FFK_LNB_CASE
     }
+    FFK_LAUNCH_CHECK("layernorm_bwd");
+    if (dgamma) colsum_act(kF32, ws, nullptr, nullptr, dgamma, grid, N, 0, 1.f, st);
+    if (dbeta) colsum_act(kF32, ws + static_cast<size_t>(grid) * N, nullptr, nullptr, dbeta, grid, N, 0, 1.f, st);
+    return;
   } else {
     hipLaunchKernelGGL((ln_bwd_generic<T>), dim3(M), dim3(256), 0, st, DY, S, mean, rstd, G, DX, dgamma, dbeta, M,
                        N);
@@ -355,11 +387,17 @@ void layernorm_fwd(int dtype, const void* x, const void* res, void* sum_out, con
   else throw std::invalid_argument("layernorm: unsupported dtype");
 }
 
+int layernorm_bwd_grid(int M, int N) {
+  if (N % 512 == 0 && N <= 4096) return std::max(1, std::min((M + 7) / 8, 512));
+  return 0;
+}
+
 void layernorm_bwd(int dtype, const void* dy, const void* s, const float* mean, const float* rstd,
-                   const void* gamma, void* dx, float* dgamma, float* dbeta, int M, int N, hipStream_t st) {
+                   const void* gamma, void* dx, float* dgamma, float* dbeta, float* ws, int M, int N,
+                   hipStream_t st) {
   if (N % 8 != 0) throw std::invalid_argument("layernorm: N must be a multiple of 8");
-  if (dtype == kBF16) ln_bwd_t<bf16>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, M, N, st);
-  else if (dtype == kF32) ln_bwd_t<float>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, M, N, st);
+  if (dtype == kBF16) ln_bwd_t<bf16>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, ws, M, N, st);
+  else if (dtype == kF32) ln_bwd_t<float>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, ws, M, N, st);
   else throw std::invalid_argument("layernorm: unsupported dtype");
 }
 

@@ -124,8 +124,12 @@ def layernorm_bwd(dy, s, mean, rstd, gamma, dgamma=None, dbeta=None):
     for name, w in (("dgamma", dgamma), ("dbeta", dbeta)):
         if w is not None:
             _check(w, name, torch.float32, N)
+    grid = ext().layernorm_bwd_grid(M, N)
+    ws = None
+    if grid and (dgamma is not None or dbeta is not None):
+        ws = torch.empty(2 * grid * N, device=dy.device, dtype=torch.float32)
     ext().layernorm_bwd(_dt(dy), _p(dy), _p(s), _p(mean), _p(rstd), _p(gamma), _p(dx), _p(dgamma), _p(dbeta),
-                        M, N, _stream())
+                        _p(ws), M, N, _stream())
     STATS["layernorm_bwd"] += 1
     return dx
 
@@ -307,8 +311,15 @@ def embedding_bwd(idx, dout, dweight, aggr: str = "none"):
         B = idx.numel() // max(L, 1)
     if dout.numel() != B * D:
         raise ValueError("embedding_bwd: dout shape mismatch")
+    # privatised accumulation copies for hot (small) tables: aim for <= ~8
+    # contributions per (copy, row) and a workspace of at most 64 MiB
+    rows = B * L
+    copies = 1
+    if rows > 8 * n:
+        copies = int(min(256, rows // (8 * n), max(1, (64 << 20) // max(1, n * D * 4))))
+    ws = torch.zeros(copies * n * D, device=dweight.device, dtype=torch.float32) if copies > 1 else None
     ext().embedding_bwd(_dt(dout), 64 if idx.dtype == torch.int64 else 32, _p(idx), _p(dout), _p(dweight), B, L, D,
-                        _AGGR[aggr], n, _stream())
+                        _AGGR[aggr], n, _p(ws), copies, _stream())
     STATS["embedding_bwd"] += 1
 
 

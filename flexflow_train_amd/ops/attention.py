@@ -128,7 +128,7 @@ class MultiHeadAttentionOp(OpImpl):
         B, Sq, Sk, Hl, kd, vd, Eq, Ek, Ev, E, causal, scale = dims
         dW = weight_grads[0]
         db_in = weight_grads[1] if len(weight_grads) > 1 else None
-        db_out = weight_grads[2] if len(weight_grads) > 2 and ctx.sum_index == 0 else None
+        db_out = weight_grads[2] if len(weight_grads) > 2 else None  # identical on every partial replica
         dout = grad_outputs[0].reshape(B * Sq, E).contiguous()
         o2 = o.reshape(B * Sq, Hl * vd)
         gpu = dout.is_cuda and dout.dtype == torch.bfloat16 and K.available()
@@ -139,9 +139,10 @@ class MultiHeadAttentionOp(OpImpl):
                 K.colsum_act(dout, None, "none", db_out, write_dx=False)
             else:
                 acc_grad(db_out, dout.float().sum(0))
+        wbeta = ctx.extra.get("wgrad_beta", [1.0])[0]
         if dW_views is not None:
             if gpu:
-                matmul(o2, dout, trans_a=True, out=dW_views["o"], beta=1.0)
+                matmul(o2, dout, trans_a=True, out=dW_views["o"], beta=wbeta)
             else:
                 acc_grad(dW_views["o"], o2.float().t() @ dout.float())
         do = matmul(dout, ws["o"], trans_b=True) if gpu else dout @ ws["o"].to(dout.dtype).t()
@@ -179,10 +180,14 @@ class MultiHeadAttentionOp(OpImpl):
                     acc_grad(db_in, d2.float().sum(0))
             if dW_views is not None:
                 if gpu:
-                    matmul(x2, d2, trans_a=True, out=dW_views["qkv"], beta=1.0)
+                    matmul(x2, d2, trans_a=True, out=dW_views["qkv"], beta=wbeta)
                 else:
                     acc_grad(dW_views["qkv"], x2.float().t() @ d2.float())
             if need_input_grad[0]:
+                acc = ctx.extra.get("grad_acc", [None])[0]
+                if gpu and acc is not None and acc.dtype == d2.dtype and acc.is_contiguous():
+                    matmul(d2, ws["qkv"], trans_b=True, out=acc.view(B * Sq, Eq), beta=1.0)
+                    return [acc, None, None]
                 dx_q = (matmul(d2, ws["qkv"], trans_b=True) if gpu else d2 @ ws["qkv"].to(d2.dtype).t()).view(B, Sq, Eq)
             return [dx_q, None, None]
         srcs = ((x2, dq, "q", Eq, Sq, kd), (k_in.reshape(-1, Ek).contiguous(), dk, "k", Ek, Sk, kd),
@@ -195,7 +200,7 @@ class MultiHeadAttentionOp(OpImpl):
                 acc_grad(seg, d2.float().sum(0))
             if dW_views is not None:
                 if gpu:
-                    matmul(xin, d2, trans_a=True, out=dW_views[key], beta=1.0)
+                    matmul(xin, d2, trans_a=True, out=dW_views[key], beta=wbeta)
                 else:
                     acc_grad(dW_views[key], xin.float().t() @ d2.float())
             if need_input_grad[j]:

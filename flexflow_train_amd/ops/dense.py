@@ -57,7 +57,9 @@ class LinearOp(OpImpl):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         has_bias = len(weight_grads) > 1
-        db = weight_grads[1] if has_bias and ctx.sum_index == 0 else None
+        # every partial-sum replica computes the (identical) bias gradient so the
+        # stored copies stay in sync; only replica 0 adds the bias in forward
+        db = weight_grads[1] if has_bias else None
         dW = weight_grads[0]
         if dy2.is_cuda and dy2.dtype == torch.bfloat16 and K.available() and dy2.shape[1] % 8 == 0:
             if act != "none":
@@ -78,11 +80,15 @@ class LinearOp(OpImpl):
                 acc_grad(db, g.float().sum(0))
         if dW is not None:
             if dW.is_cuda and g.dtype == torch.bfloat16:
-                matmul(x2, g, trans_a=True, out=dW, beta=1.0)
+                matmul(x2, g, trans_a=True, out=dW, beta=ctx.extra.get("wgrad_beta", [1.0])[0])
             else:
                 acc_grad(dW, x2.float().t() @ g.float())
         dx = None
         if need_input_grad[0]:
+            acc = ctx.extra.get("grad_acc", [None])[0]
+            if acc is not None and acc.is_cuda and acc.dtype == g.dtype and acc.is_contiguous():
+                matmul(g, W, trans_b=True, out=acc.view(-1, W.shape[0]), beta=1.0)
+                return [acc]
             dx = matmul(g, W, trans_b=True) if g.is_cuda else (g @ W.to(g.dtype).t())
             dx = dx.reshape(*dy.shape[:-1], W.shape[0])
         return [dx]

@@ -56,10 +56,26 @@ def _hip_ok(a, b, trans_a, trans_b) -> bool:
 def _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre):
     A = a.t() if trans_a else a
     B = b.t() if trans_b else b
-    if out is not None and out.dtype == torch.float32:
-        r = torch.mm(A, B, out_dtype=torch.float32) if A.is_cuda else (A.float() @ B.float())
+    if not A.is_cuda:
+        r = A.float() @ B.float() if (out is not None and out.dtype == torch.float32) else A @ B
         if bias is not None:
-            r = r + bias.float()
+            r = r + bias.to(r.dtype)
+        if pre is not None:
+            pre.copy_(r)
+        r = _ACT[act](r)
+        if out is not None:
+            if beta:
+                out.mul_(beta).add_(r.to(out.dtype))
+            else:
+                out.copy_(r)
+            return out
+        return r
+    if out is not None and out.dtype == torch.float32:
+        if not beta and bias is None and act == "none" and pre is None:
+            return torch.mm(A, B, out_dtype=torch.float32, out=out)   # weight grads: written in place
+        r = torch.mm(A, B, out_dtype=torch.float32)
+        if bias is not None:
+            r += bias.float()
         if pre is not None:
             pre.copy_(r)
         r = _ACT[act](r)
@@ -68,20 +84,31 @@ def _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre):
         else:
             out.copy_(r)
         return out
-    if bias is not None:
-        r = torch.addmm(bias, A, B)
-    else:
-        r = A @ B
-    if pre is not None:
-        pre.copy_(r)
-    r = _ACT[act](r)
+    if act != "none":
+        # hipBLASLt GEMM (+ bias epilogue) writes the pre-activation directly,
+        # the activation runs in the HIP element-wise kernel (16 B / lane).
+        u = pre if pre is not None else torch.empty(A.shape[0], B.shape[1], device=A.device, dtype=A.dtype)
+        if bias is not None:
+            torch.addmm(bias, A, B, out=u)
+        else:
+            torch.mm(A, B, out=u)
+        y, _ = K.bias_act_fwd(u, None, act)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
     if out is not None:
+        if beta == 1.0 and bias is None and out.dtype == A.dtype:
+            return out.addmm_(A, B)                                  # in-place gradient accumulation
+        r = torch.addmm(bias, A, B) if bias is not None else A @ B
         if beta:
-            out.mul_(beta).add_(r.to(out.dtype))
+            out.mul_(beta).add_(r)
         else:
             out.copy_(r)
         return out
-    return r
+    if bias is not None:
+        return torch.addmm(bias, A, B)
+    return A @ B
 
 
 def _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre):

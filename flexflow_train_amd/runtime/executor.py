@@ -73,6 +73,7 @@ class ParamPiece:
     numel: int = 0
     flat_id: int = 0
     final_step: int = -1          # forward index of first consumer
+    n_consumers: int = 0
     master: Optional[torch.Tensor] = None
     compute: Optional[torch.Tensor] = None
     grad: Optional[torch.Tensor] = None
@@ -318,6 +319,7 @@ class Executor:
             for o in s.outputs:
                 rg[o] = need
             for p in s.weights:
+                p.n_consumers += 1
                 if p.final_step < 0:
                     p.final_step = idx
         self.requires_grad = rg
@@ -621,6 +623,11 @@ class Executor:
                         gouts[0] = torch.zeros(s.ctx.output_shapes[0], dtype=self.cfg.compute_dtype,
                                                device=self.cfg.device)
                     wgs = [p.grad if p.trainable else None for p in s.weights]
+                    # sole-consumer weights may be overwritten (beta = 0) by their dW GEMM;
+                    # shared ones accumulate.  Existing input grads are offered for in-place
+                    # accumulation (ops return the same tensor when they used it).
+                    s.ctx.extra["wgrad_beta"] = [0.0 if p.n_consumers == 1 else 1.0 for p in s.weights]
+                    s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
                     impl = opbase.get_impl(s.op_type)
                     t0 = self._tick() if prof else None
                     gins = impl.backward(s.ctx, saved, gouts, wgs, need)
@@ -639,6 +646,8 @@ class Executor:
     def _acc(self, grads, v, g):
         if g is None:
             return
+        if v in grads and grads[v] is g:
+            return  # accumulated in place by the op
         if v in grads:
             grads[v] = grads[v] + g
         else:
