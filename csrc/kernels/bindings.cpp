@@ -69,13 +69,14 @@ PYBIND11_MODULE(_ffkernels, m) {
   m.def("softmax_bwd", [](int dt, uintptr_t dy, uintptr_t y, uintptr_t dx, int M, int N, uintptr_t st) {
     softmax_bwd(dt, P(dy), P(y), P(dx), M, N, S(st));
   });
-  m.def("adam_step", [](uintptr_t w, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t wb, int64_t n, float lr,
-                        float b1, float b2, float eps, float wd, int step, float gs, int decoupled, uintptr_t st) {
-    adam_step(F(w), F(g), F(mm), F(v), P(wb), n, lr, b1, b2, eps, wd, step, gs, decoupled, S(st));
+  m.def("adam_step", [](uintptr_t w, uintptr_t g, int gdt, uintptr_t mm, uintptr_t v, uintptr_t wb, int64_t n,
+                        float lr, float b1, float b2, float eps, float wd, int step, float gs, int decoupled,
+                        uintptr_t st) {
+    adam_step(F(w), P(g), gdt, F(mm), F(v), P(wb), n, lr, b1, b2, eps, wd, step, gs, decoupled, S(st));
   });
-  m.def("sgd_step", [](uintptr_t w, uintptr_t g, uintptr_t mom, uintptr_t wb, int64_t n, float lr, float momentum,
-                       float wd, int nesterov, float gs, uintptr_t st) {
-    sgd_step(F(w), F(g), F(mom), P(wb), n, lr, momentum, wd, nesterov, gs, S(st));
+  m.def("sgd_step", [](uintptr_t w, uintptr_t g, int gdt, uintptr_t mom, uintptr_t wb, int64_t n, float lr,
+                       float momentum, float wd, int nesterov, float gs, uintptr_t st) {
+    sgd_step(F(w), P(g), gdt, F(mom), P(wb), n, lr, momentum, wd, nesterov, gs, S(st));
   });
   m.def("sum_squares", [](uintptr_t x, int64_t n, uintptr_t out, uintptr_t st) {
     sum_squares(F(x), n, F(out), S(st));

@@ -254,7 +254,7 @@ void colsum_act(int dtype, const void* dy, const void* pre, void* dx, float* dbi
   need8(N, "colsum_act");
   int gx = static_cast<int>((N + 511) / 512);
   // enough row splits to put ~4 blocks per CU on the chip
-  int gy = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 63) / 64)));
+  int gy = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 15) / 16)));
   if (dtype == kBF16)
     hipLaunchKernelGGL(colsum_act_kernel<bf16>, dim3(gx, gy), dim3(256), 0, st, static_cast<const bf16*>(dy),
                        static_cast<const bf16*>(pre), static_cast<bf16*>(dx), dbias, static_cast<int>(M),

@@ -33,11 +33,11 @@ void softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStream_t st
 void softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int N, hipStream_t st);
 
 // ---- optimizer.hip
-void adam_step(float* w, const float* g, float* m, float* v, void* w_bf16, int64_t n, float lr, float beta1,
-               float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
+void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void* w_bf16, int64_t n, float lr,
+               float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
                hipStream_t st);
-void sgd_step(float* w, const float* g, float* mom, void* w_bf16, int64_t n, float lr, float momentum,
-              float weight_decay, int nesterov, float grad_scale, hipStream_t st);
+void sgd_step(float* w, const void* g, int grad_dtype, float* mom, void* w_bf16, int64_t n, float lr,
+              float momentum, float weight_decay, int nesterov, float grad_scale, hipStream_t st);
 void sum_squares(const float* x, int64_t n, float* out, hipStream_t st);
 
 // ---- embedding.hip  (mode: 0 none, 1 sum, 2 avg)

@@ -14,14 +14,29 @@
 
 namespace ffk {
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const float* __restrict__ g,
+template <typename GT>
+__device__ __forceinline__ f32x4 load_grad4(const GT* g, int64_t i);
+template <>
+__device__ __forceinline__ f32x4 load_grad4<float>(const float* g, int64_t i) {
+  return reinterpret_cast<const f32x4*>(g)[i];
+}
+template <>
+__device__ __forceinline__ f32x4 load_grad4<bf16>(const bf16* g, int64_t i) {
+  u16x4 u = reinterpret_cast<const u16x4*>(g)[i];
+  return f32x4{u2f(u[0]), u2f(u[1]), u2f(u[2]), u2f(u[3])};
+}
+
+// Gradients are fp32 (atomically accumulated parameters) or bf16 (GEMM
+// weight gradients written straight by the dW GEMM epilogue).
+template <typename GT>
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const GT* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16* __restrict__ w_bf16, int64_t n4, float lr, float beta1,
                                                    float beta2, float eps, float weight_decay, float bc1,
                                                    float bc2_sqrt, float grad_scale, int decoupled) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
     f32x4 W = reinterpret_cast<f32x4*>(w)[i];
-    f32x4 G = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 G = load_grad4<GT>(g, i);
     f32x4 Mm = reinterpret_cast<f32x4*>(m)[i];
     f32x4 Vv = reinterpret_cast<f32x4*>(v)[i];
 #pragma unroll
@@ -46,13 +61,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const 
   }
 }
 
-__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const float* __restrict__ g,
+template <typename GT>
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const GT* __restrict__ g,
                                                   float* __restrict__ mom, bf16* __restrict__ w_bf16, int64_t n4,
                                                   float lr, float momentum, float weight_decay, int nesterov,
                                                   float grad_scale) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
     f32x4 W = reinterpret_cast<f32x4*>(w)[i];
-    f32x4 G = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 G = load_grad4<GT>(g, i);
     f32x4 Mo;
     if (mom) Mo = reinterpret_cast<f32x4*>(mom)[i];
 #pragma unroll
@@ -91,24 +107,34 @@ static void need4(int64_t n, const char* w) {
   if (n % 4 != 0) throw std::invalid_argument(std::string(w) + ": flat buffer length must be a multiple of 4");
 }
 
-void adam_step(float* w, const float* g, float* m, float* v, void* w_bf16, int64_t n, float lr, float beta1,
-               float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
+void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void* w_bf16, int64_t n, float lr,
+               float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
                hipStream_t st) {
   need4(n, "adam");
   float bc1 = 1.f - powf(beta1, static_cast<float>(step));
   float bc2s = sqrtf(1.f - powf(beta2, static_cast<float>(step)));
   int grid = grid_for(n / 4, 256, 256 * 8);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, st, w, g, m, v, static_cast<bf16*>(w_bf16), n / 4, lr,
-                     beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale, decoupled);
+  if (grad_dtype == kBF16)
+    hipLaunchKernelGGL(adam_kernel<bf16>, dim3(grid), dim3(256), 0, st, w, static_cast<const bf16*>(g), m, v,
+                       static_cast<bf16*>(w_bf16), n / 4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale,
+                       decoupled);
+  else
+    hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(256), 0, st, w, static_cast<const float*>(g), m, v,
+                       static_cast<bf16*>(w_bf16), n / 4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale,
+                       decoupled);
   FFK_LAUNCH_CHECK("adam");
 }
 
-void sgd_step(float* w, const float* g, float* mom, void* w_bf16, int64_t n, float lr, float momentum,
-              float weight_decay, int nesterov, float grad_scale, hipStream_t st) {
+void sgd_step(float* w, const void* g, int grad_dtype, float* mom, void* w_bf16, int64_t n, float lr,
+              float momentum, float weight_decay, int nesterov, float grad_scale, hipStream_t st) {
   need4(n, "sgd");
   int grid = grid_for(n / 4, 256, 256 * 8);
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, st, w, g, mom, static_cast<bf16*>(w_bf16), n / 4, lr,
-                     momentum, weight_decay, nesterov, grad_scale);
+  if (grad_dtype == kBF16)
+    hipLaunchKernelGGL(sgd_kernel<bf16>, dim3(grid), dim3(256), 0, st, w, static_cast<const bf16*>(g), mom,
+                       static_cast<bf16*>(w_bf16), n / 4, lr, momentum, weight_decay, nesterov, grad_scale);
+  else
+    hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid), dim3(256), 0, st, w, static_cast<const float*>(g), mom,
+                       static_cast<bf16*>(w_bf16), n / 4, lr, momentum, weight_decay, nesterov, grad_scale);
   FFK_LAUNCH_CHECK("sgd");
 }
 

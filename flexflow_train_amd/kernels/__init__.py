@@ -240,29 +240,31 @@ def softmax_bwd(dy, y):
 
 
 def adam_step(w, g, m, v, w_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, decoupled=False):
+    """Fused Adam/AdamW over a flat buffer; g may be fp32 or bf16."""
     n = w.numel()
-    for name, t in (("w", w), ("g", g), ("m", m), ("v", v)):
+    for name, t in (("w", w), ("m", m), ("v", v)):
         _check(t, name, torch.float32, n)
+    _check(g, "g", numel=n)
     if w_bf16 is not None:
         _check(w_bf16, "w_bf16", torch.bfloat16, n)
     if n % 4:
         raise ValueError("adam: flat buffer length must be a multiple of 4")
-    ext().adam_step(_p(w), _p(g), _p(m), _p(v), _p(w_bf16), n, float(lr), float(beta1), float(beta2), float(eps),
-                    float(weight_decay), int(step), float(grad_scale), int(decoupled), _stream())
+    ext().adam_step(_p(w), _p(g), _dt(g), _p(m), _p(v), _p(w_bf16), n, float(lr), float(beta1), float(beta2),
+                    float(eps), float(weight_decay), int(step), float(grad_scale), int(decoupled), _stream())
     STATS["adam_step"] += 1
 
 
 def sgd_step(w, g, mom, w_bf16, lr, momentum, weight_decay, nesterov, grad_scale=1.0):
     n = w.numel()
     _check(w, "w", torch.float32, n)
-    _check(g, "g", torch.float32, n)
+    _check(g, "g", numel=n)
     if mom is not None:
         _check(mom, "mom", torch.float32, n)
     if w_bf16 is not None:
         _check(w_bf16, "w_bf16", torch.bfloat16, n)
     if n % 4:
         raise ValueError("sgd: flat buffer length must be a multiple of 4")
-    ext().sgd_step(_p(w), _p(g), _p(mom), _p(w_bf16), n, float(lr), float(momentum), float(weight_decay),
+    ext().sgd_step(_p(w), _p(g), _dt(g), _p(mom), _p(w_bf16), n, float(lr), float(momentum), float(weight_decay),
                    int(bool(nesterov)), float(grad_scale), _stream())
     STATS["sgd_step"] += 1
 

@@ -98,6 +98,8 @@ def _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre):
             return out
         return y
     if out is not None:
+        if not beta and bias is None and out.dtype == A.dtype:
+            return torch.mm(A, B, out=out)                           # written in place (e.g. bf16 dW)
         if beta == 1.0 and bias is None and out.dtype == A.dtype:
             return out.addmm_(A, B)                                  # in-place gradient accumulation
         r = torch.addmm(bias, A, B) if bias is not None else A @ B
