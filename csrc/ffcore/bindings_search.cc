@@ -1,11 +1,306 @@
-// Bindings for machine mapping / search / simulator (filled in as those land).
+// Bindings for the machine model, cost model, SP decomposition, lowering,
+// simulator, machine mapping, substitutions and strategy search.
+// Structured results cross the boundary as JSON strings (parsed by
+// flexflow_train_amd.search.native); graphs stay native objects.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include "bindings_ext.h"
+#include "ff/mapping.h"
+#include "ff/parallelize.h"
+#include "ff/search.h"
+#include "ff/simulator.h"
+#include "ff/sp.h"
+#include "ff/substitution.h"
 
 namespace py = pybind11;
 
 namespace ff {
-void register_ext_bindings(py::module_& m) { (void)m; }
+
+namespace {
+
+SimConfig sim_config_from_json(const Json& j) {
+  SimConfig c;
+  if (!j.is_object()) return c;
+  auto gi = [&](const char* k, int& v) { if (j.contains(k)) v = static_cast<int>(j.at(k).as_int()); };
+  auto gd = [&](const char* k, double& v) { if (j.contains(k)) v = j.at(k).as_double(); };
+  auto gb = [&](const char* k, bool& v) { if (j.contains(k)) v = j.at(k).as_bool(); };
+  gi("world", c.world);
+  gb("overlap_grad_sync", c.overlap_grad_sync);
+  gd("bucket_bytes", c.bucket_bytes);
+  gb("include_update", c.include_update);
+  gd("update_bytes_per_param", c.update_bytes_per_param);
+  gd("memory_penalty_per_mb", c.memory_penalty_per_mb);
+  gd("comm_compute_slowdown", c.comm_compute_slowdown);
+  gb("bf16_weight_grads", c.bf16_weight_grads);
+  return c;
+}
+
+SearchConfig search_config_from_json(const Json& j) {
+  SearchConfig c;
+  auto gi = [&](const char* k, int& v) { if (j.contains(k)) v = static_cast<int>(j.at(k).as_int()); };
+  auto gd = [&](const char* k, double& v) { if (j.contains(k)) v = j.at(k).as_double(); };
+  auto gb = [&](const char* k, bool& v) { if (j.contains(k)) v = j.at(k).as_bool(); };
+  gi("world", c.world);
+  gi("budget", c.budget);
+  gd("alpha", c.alpha);
+  gd("threshold", c.threshold);
+  gi("max_num_ops", c.max_num_ops);
+  gd("mcmc_beta", c.mcmc_beta);
+  gd("group_move_prob", c.group_move_prob);
+  if (j.contains("seed")) c.seed = static_cast<uint64_t>(j.at("seed").as_int());
+  gd("time_limit", c.time_limit);
+  gb("use_machine_mapping", c.use_machine_mapping);
+  gb("enable_parameter_parallel", c.space.enable_parameter_parallel);
+  gb("enable_attribute_parallel", c.space.enable_attribute_parallel);
+  gb("allow_partial_world", c.space.allow_partial_world);
+  gi("max_model_degree", c.space.max_model_degree);
+  if (j.contains("sim")) c.sim = sim_config_from_json(j.at("sim"));
+  c.sim.world = c.world;
+  return c;
+}
+
+std::map<int, DeviceBlock> views_from_py(const std::map<int, std::pair<int, int>>& v) {
+  std::map<int, DeviceBlock> r;
+  for (auto const& kv : v) r[kv.first] = DeviceBlock{kv.second.first, kv.second.second};
+  return r;
+}
+
+std::map<int, std::pair<int, int>> views_to_py(const std::map<int, DeviceBlock>& v) {
+  std::map<int, std::pair<int, int>> r;
+  for (auto const& kv : v) r[kv.first] = {kv.second.start, kv.second.size};
+  return r;
+}
+
+}  // namespace
+
+void register_ext_bindings(py::module_& m) {
+  // ---- machine
+  py::class_<MachineSpecification>(m, "MachineSpecification")
+      .def(py::init<>())
+      .def_static("mi355x", &MachineSpecification::mi355x, py::arg("num_nodes") = 1, py::arg("gpus_per_node") = 8)
+      .def_readwrite("num_nodes", &MachineSpecification::num_nodes)
+      .def_readwrite("num_cpus_per_node", &MachineSpecification::num_cpus_per_node)
+      .def_readwrite("num_gpus_per_node", &MachineSpecification::num_gpus_per_node)
+      .def_readwrite("inter_node_bandwidth", &MachineSpecification::inter_node_bandwidth)
+      .def_readwrite("intra_node_bandwidth", &MachineSpecification::intra_node_bandwidth)
+      .def_readwrite("peak_bf16_flops", &MachineSpecification::peak_bf16_flops)
+      .def_readwrite("peak_fp32_flops", &MachineSpecification::peak_fp32_flops)
+      .def_readwrite("mfma_efficiency", &MachineSpecification::mfma_efficiency)
+      .def_readwrite("hbm_bandwidth", &MachineSpecification::hbm_bandwidth)
+      .def_readwrite("hbm_capacity", &MachineSpecification::hbm_capacity)
+      .def_readwrite("kernel_launch_overhead", &MachineSpecification::kernel_launch_overhead)
+      .def_readwrite("collective_latency", &MachineSpecification::collective_latency)
+      .def_readwrite("xgmi_links", &MachineSpecification::xgmi_links)
+      .def_readwrite("xgmi_link_bandwidth", &MachineSpecification::xgmi_link_bandwidth)
+      .def("num_devices", &MachineSpecification::num_devices)
+      .def("to_json", [](const MachineSpecification& s) { return s.to_json().dump(); })
+      .def_static("from_json", [](const std::string& s) { return MachineSpecification::from_json(Json::parse(s)); });
+
+  m.def("operator_task_space", &operator_task_space);
+  m.def("get_allowed_machine_views", [](const std::vector<int>& ts, const MachineSpecification& spec) {
+    std::vector<std::string> r;
+    for (auto const& v : get_allowed_machine_views(ts, spec)) r.push_back(v.to_json().dump());
+    return r;
+  });
+  m.def("get_device_ids", [](const std::vector<int>& ts, const std::string& view, const MachineSpecification& spec) {
+    return get_device_ids(ts, MachineView::from_json(Json::parse(view)), spec);
+  });
+  m.def("block_machine_view", [](const std::vector<int>& ts, int start, int size, const MachineSpecification& spec) {
+    return block_machine_view(ts, DeviceBlock{start, size}, spec).to_json().dump();
+  });
+  m.def("get_resource_splits", [](int start, int size) {
+    std::vector<std::pair<std::pair<int, int>, std::pair<int, int>>> r;
+    for (auto const& s : get_resource_splits(DeviceBlock{start, size}))
+      r.push_back({{s.first.start, s.first.size}, {s.second.start, s.second.size}});
+    return r;
+  });
+  m.def("collective_cost", [](const std::string& kind, double bytes, int p, const MachineSpecification& s) {
+    if (kind == "all_reduce") return CollectiveCost::all_reduce(bytes, p, s);
+    if (kind == "all_gather") return CollectiveCost::all_gather(bytes, p, s);
+    if (kind == "reduce_scatter") return CollectiveCost::reduce_scatter(bytes, p, s);
+    if (kind == "all_to_all") return CollectiveCost::all_to_all(bytes, p, s);
+    if (kind == "p2p") return CollectiveCost::p2p(bytes, s);
+    throw FFError("unknown collective " + kind);
+  });
+
+  // ---- cost model
+  py::class_<CostModel>(m, "CostModel")
+      .def(py::init<MachineSpecification>())
+      .def("spec", &CostModel::spec)
+      .def("load_profiles", [](CostModel& c, const std::string& s) { c.profiles().load_json(Json::parse(s)); })
+      .def("put_profile", [](CostModel& c, const std::string& k, double f, double b) { c.profiles().put(k, f, b); })
+      .def("profiles_json", [](CostModel& c) { return c.profiles().to_json().dump(); })
+      .def("num_profiles", [](CostModel& c) { return c.profiles().size(); })
+      .def_static("signature", &CostModel::signature)
+      .def("op_cost",
+           [](const CostModel& c, const OpAttrs& op, const std::vector<ParallelTensorShape>& ins,
+              const std::vector<ParallelTensorShape>& ws, const std::vector<ParallelTensorShape>& outs, int block) {
+             auto r = c.op_cost(op, ins, ws, outs, block);
+             return py::make_tuple(r.forward, r.backward, r.memory, r.sync);
+           })
+      .def("parallel_op_cost",
+           [](const CostModel& c, const OpAttrs& op, const ParallelTensorShape& in, const ParallelTensorShape& out,
+              int block) {
+             auto r = c.parallel_op_cost(op, in, out, block);
+             return py::make_tuple(r.forward, r.backward, r.memory, r.sync);
+           })
+      .def("pcg_node_cost", [](const CostModel& c, const ParallelComputationGraph& p, int node, int block) {
+        auto r = pcg_node_cost(c, p, node, block);
+        return py::make_tuple(r.forward, r.backward, r.memory, r.sync);
+      });
+
+  // ---- SP decomposition
+  m.def("sp_decomposition", [](const ParallelComputationGraph& p, bool strict) -> py::object {
+    auto g = data_path_digraph(p);
+    if (strict) {
+      auto t = get_series_parallel_decomposition(g);
+      if (!t) return py::none();
+      return py::str(t->to_json().dump());
+    }
+    return py::str(get_relaxed_sp_decomposition(g).to_json().dump());
+  }, py::arg("pcg"), py::arg("strict") = false);
+  m.def("cg_sp_decomposition", [](const ComputationGraph& cg, bool strict) -> py::object {
+    // reference CG path: plain SP first; fall back by dropping weights (implicit in leaves)
+    DiGraph g = cg.g.digraph();
+    auto t = get_series_parallel_decomposition(g);
+    if (!t) {
+      std::set<int> keep;
+      for (int id : g.nodes)
+        if (cg.g.node(id).label.op.type != OpType::WEIGHT) keep.insert(id);
+      g = g.induced_subgraph(keep);
+      t = get_series_parallel_decomposition(g);
+    }
+    if (t) return py::str(t->to_json().dump());
+    if (strict) return py::none();
+    return py::str(get_relaxed_sp_decomposition(g).to_json().dump());
+  }, py::arg("cg"), py::arg("strict") = false);
+  m.def("digraph_sp_decomposition", [](const std::vector<std::pair<int, int>>& edges, const std::vector<int>& nodes,
+                                       bool strict) -> py::object {
+    DiGraph g;
+    for (int n : nodes) g.add_node(n);
+    for (auto const& e : edges) g.add_edge(e.first, e.second);
+    if (strict) {
+      auto t = get_series_parallel_decomposition(g);
+      if (!t) return py::none();
+      return py::str(t->to_json().dump());
+    }
+    return py::str(get_relaxed_sp_decomposition(g).to_json().dump());
+  }, py::arg("edges"), py::arg("nodes") = std::vector<int>{}, py::arg("strict") = true);
+
+  // ---- per-layer configs and lowering
+  m.def("candidate_configs", [](const ComputationGraph& cg, int node, int world, bool pp, bool ap, bool partial) {
+    SearchSpaceOptions o;
+    o.enable_parameter_parallel = pp;
+    o.enable_attribute_parallel = ap;
+    o.allow_partial_world = partial;
+    std::vector<std::string> r;
+    for (auto const& c : candidate_configs(cg, node, world, o)) r.push_back(c.to_json().dump());
+    return r;
+  }, py::arg("cg"), py::arg("node"), py::arg("world"), py::arg("enable_parameter_parallel") = true,
+        py::arg("enable_attribute_parallel") = false, py::arg("allow_partial_world") = false);
+  m.def("data_parallel_strategy", [](const ComputationGraph& cg, int world) {
+    return strategy_to_json(cg, data_parallel_strategy(cg, world)).dump();
+  });
+  m.def("lower_strategy", [](const ComputationGraph& cg, const std::string& strategy, int world) {
+    auto L = lower_strategy(cg, strategy_from_json(cg, Json::parse(strategy)), world);
+    return py::make_tuple(L.pcg, L.cg_to_pcg, L.num_parallel_ops);
+  });
+  m.def("convert_parallel_shape", [](ParallelComputationGraph& p, ValueRef v, const ParallelTensorShape& t) {
+    int n = 0;
+    auto r = convert_parallel_shape(p, v, t, &n);
+    return py::make_tuple(r, n);
+  });
+
+  // ---- simulator
+  m.def("simulate", [](const ParallelComputationGraph& p, const CostModel& cm, const std::string& sim_cfg,
+                       const std::map<int, std::pair<int, int>>& views, bool dot) {
+    Simulator S(cm, sim_config_from_json(sim_cfg.empty() ? Json::object() : Json::parse(sim_cfg)));
+    auto r = S.simulate(p, views_from_py(views), dot);
+    return py::make_tuple(r.to_json().dump(), dot ? S.task_graph_dot(r) : std::string());
+  }, py::arg("pcg"), py::arg("cost_model"), py::arg("sim_config") = "",
+        py::arg("views") = std::map<int, std::pair<int, int>>{}, py::arg("dot") = false);
+  m.def("evaluate_strategy", [](const ComputationGraph& cg, const std::string& strategy, const CostModel& cm,
+                                const std::string& sim_cfg, int world) {
+    SimResult r;
+    double t = evaluate_strategy(cg, strategy_from_json(cg, Json::parse(strategy)), cm,
+                                 sim_config_from_json(sim_cfg.empty() ? Json::object() : Json::parse(sim_cfg)),
+                                 world, &r);
+    return py::make_tuple(t, r.to_json().dump());
+  });
+
+  // ---- machine mapping
+  m.def("machine_mapping", [](const ParallelComputationGraph& p, const CostModel& cm, int world, bool sub_blocks) {
+    MachineMappingContext ctx;
+    ctx.cost = &cm;
+    ctx.allow_sub_blocks = sub_blocks;
+    MachineMapper mm(p, ctx);
+    auto r = mm.solve(DeviceBlock{0, world});
+    return py::make_tuple(r.runtime, r.feasible, views_to_py(r.views));
+  }, py::arg("pcg"), py::arg("cost_model"), py::arg("world"), py::arg("allow_sub_blocks") = true);
+
+  // ---- substitutions
+  py::class_<Substitution>(m, "Substitution")
+      .def_readonly("name", &Substitution::name)
+      .def("num_pattern_nodes", [](const Substitution& s) { return s.pattern.nodes.size(); })
+      .def("num_output_nodes", [](const Substitution& s) { return s.out_nodes.size(); })
+      .def("to_json", [](const Substitution& s) { return s.to_json().dump(); });
+  m.def("generate_parallelization_substitutions", &generate_parallelization_substitutions);
+  m.def("find_pattern_matches", [](const Substitution& s, const ParallelComputationGraph& p, size_t max) {
+    std::vector<std::pair<std::vector<int>, std::vector<ValueRef>>> r;
+    for (auto const& mt : find_pattern_matches(s.pattern, p, max)) r.push_back({mt.node_map, mt.input_map});
+    return r;
+  }, py::arg("sub"), py::arg("pcg"), py::arg("max_matches") = 4096);
+  m.def("apply_substitution", [](const ParallelComputationGraph& p, const Substitution& s,
+                                 const std::vector<int>& node_map, const std::vector<ValueRef>& input_map) -> py::object {
+    PCGPatternMatch mt{node_map, input_map};
+    auto r = apply_substitution(p, s, mt);
+    if (!r) return py::none();
+    return py::cast(*r);
+  });
+
+  py::class_<LegacyRuleCollection>(m, "LegacyRuleCollection")
+      .def("__len__", [](const LegacyRuleCollection& c) { return c.rules.size(); })
+      .def("name", [](const LegacyRuleCollection& c, size_t i) { return c.rules.at(i).name; })
+      .def("op_types", [](const LegacyRuleCollection& c, size_t i) {
+        std::vector<std::string> src, dst;
+        for (auto const& o : c.rules.at(i).src) src.push_back(o.type);
+        for (auto const& o : c.rules.at(i).dst) dst.push_back(o.type);
+        return py::make_tuple(src, dst);
+      })
+      .def("to_dot", [](const LegacyRuleCollection& c, size_t i) { return legacy_rule_to_dot(c.rules.at(i)); })
+      .def("to_substitution", [](const LegacyRuleCollection& c, size_t i) -> py::object {
+        auto s = substitution_from_legacy_rule(c.rules.at(i));
+        if (!s) return py::none();
+        return py::cast(*s);
+      });
+  m.def("load_legacy_rules", [](const std::string& s) { return load_legacy_rules(Json::parse(s)); });
+
+  // ---- search
+  m.def("mcmc_search", [](const ComputationGraph& cg, const CostModel& cm, const std::string& cfg) {
+    SearchResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = mcmc_search(cg, cm, search_config_from_json(Json::parse(cfg)));
+    }
+    return py::make_tuple(r.pcg, r.to_json(&cg).dump(), views_to_py(r.views));
+  });
+  m.def("unity_search", [](const ParallelComputationGraph& p, const CostModel& cm, const std::string& cfg) {
+    SearchResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = unity_search(p, cm, search_config_from_json(Json::parse(cfg)));
+    }
+    return py::make_tuple(r.pcg, r.to_json().dump(), views_to_py(r.views));
+  });
+  m.def("graph_optimize", [](const ComputationGraph& cg, const CostModel& cm, const std::string& cfg) {
+    SearchResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = graph_optimize(cg, cm, search_config_from_json(Json::parse(cfg)));
+    }
+    return py::make_tuple(r.pcg, r.to_json(&cg).dump(), views_to_py(r.views));
+  });
+}
+
 }  // namespace ff

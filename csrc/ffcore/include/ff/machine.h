@@ -1,0 +1,156 @@
+// Machine model: specification, machine views, resource splits, and the
+// MI355X cost model (MFMA roofline + HBM3E + xGMI collectives).
+//
+// Parity:
+//  * MachineSpecification{num_nodes, num_cpus_per_node, num_gpus_per_node,
+//    inter/intra_node_bandwidth}: lib/pcg/include/pcg/machine_specification.struct.toml
+//  * MachineView{start, dims[{stride, projection}]} + get_machine_space_coordinate:
+//    lib/pcg/src/pcg/machine_view.cc:45-113
+//  * allowed machine views: lib/compiler/src/compiler/allowed_machine_views.cc:24-120
+//  * resource splits (power-of-two): get_machine_resource_splits.cc:7-29
+//  * machine models (Simple/Enhanced/Networked): lib/runtime/src/machine_model.cc
+//
+// MI355X-first: 8 GPUs per node fully connected by xGMI (7 links each), so
+// placement is topology-symmetric inside a node; candidate views are aligned
+// power-of-two device blocks (start, size), which is what the executor's
+// canonical layouts use.  Collectives are priced with a ring / direct model
+// over the per-GPU xGMI bandwidth, calibratable from measured RCCL numbers.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ff/json.h"
+#include "ff/op_attrs.h"
+#include "ff/types.h"
+
+namespace ff {
+
+struct MachineSpecification {
+  int num_nodes = 1;
+  int num_cpus_per_node = 1;
+  int num_gpus_per_node = 8;
+  double inter_node_bandwidth = 50e9;   // bytes/s per GPU (NIC)
+  double intra_node_bandwidth = 300e9;  // bytes/s per GPU achievable RCCL bus bandwidth over xGMI
+  // ---- MI355X device model
+  double peak_bf16_flops = 2.5e15;      // dense MFMA
+  double peak_fp32_flops = 157e12;
+  double mfma_efficiency = 0.45;        // achieved fraction on large GEMMs (measured ~1.1 PF hipBLASLt)
+  double hbm_bandwidth = 6.0e12;        // achievable (6.3 TB/s float4 copy)
+  double hbm_capacity = 288e9;
+  double kernel_launch_overhead = 4e-6; // s per kernel (graph-replayed ~1.5 us)
+  double collective_latency = 8e-6;     // alpha per collective step
+  int xgmi_links = 7;
+  double xgmi_link_bandwidth = 64e9;    // per direction per link
+
+  int num_devices() const { return num_nodes * num_gpus_per_node; }
+  Json to_json() const;
+  static MachineSpecification from_json(const Json& j);
+  static MachineSpecification mi355x(int num_nodes = 1, int gpus_per_node = 8);
+};
+
+enum class ProjectionType { INTRA_NODE = 0, INTER_NODE = 1 };
+
+struct MachineViewDimension {
+  int stride = 1;
+  ProjectionType projection = ProjectionType::INTRA_NODE;
+  bool operator==(const MachineViewDimension& o) const { return stride == o.stride && projection == o.projection; }
+};
+
+struct MachineSpaceCoordinate {
+  int node_idx = 0;
+  int device_idx = 0;
+  bool operator==(const MachineSpaceCoordinate& o) const {
+    return node_idx == o.node_idx && device_idx == o.device_idx;
+  }
+};
+
+struct MachineView {
+  MachineSpaceCoordinate start;
+  std::vector<MachineViewDimension> dims;
+  bool operator==(const MachineView& o) const { return start == o.start && dims == o.dims; }
+  Json to_json() const;
+  static MachineView from_json(const Json& j);
+};
+
+// Task space of an operator = the degrees of its output [shard..., sum, copy].
+std::vector<int> operator_task_space(const ParallelTensorShape& out);
+
+// Maps a task coordinate to a machine coordinate (mixed radix per projection).
+MachineSpaceCoordinate get_machine_space_coordinate(const std::vector<int>& task_space, const MachineView& view,
+                                                    const std::vector<int>& coord,
+                                                    const MachineSpecification& spec);
+std::vector<int> get_device_ids(const std::vector<int>& task_space, const MachineView& view,
+                                const MachineSpecification& spec);
+// Every strided view (strides up to the machine size, every start, every
+// projection) whose devices fit the machine (allowed_machine_views.cc).
+std::vector<MachineView> get_allowed_machine_views(const std::vector<int>& task_space,
+                                                   const MachineSpecification& spec);
+
+// Aligned device block used by the executor: devices [start, start + size).
+struct DeviceBlock {
+  int start = 0;
+  int size = 1;
+  bool operator==(const DeviceBlock& o) const { return start == o.start && size == o.size; }
+  bool operator<(const DeviceBlock& o) const { return start != o.start ? start < o.start : size < o.size; }
+};
+// Canonical MachineView of an operator with task space `ts` on block `b`
+// (copy axis innermost, implicit replicas innermost of all).
+MachineView block_machine_view(const std::vector<int>& ts, const DeviceBlock& b, const MachineSpecification& spec);
+// Power-of-two splits of a block into two disjoint halves-or-quarters.
+std::vector<std::pair<DeviceBlock, DeviceBlock>> get_resource_splits(const DeviceBlock& b);
+
+// ---------------------------------------------------------------------------
+// Cost model
+struct CollectiveCost {
+  static double all_reduce(double bytes, int p, const MachineSpecification& s);
+  static double all_gather(double bytes_out, int p, const MachineSpecification& s);     // bytes of the gathered result
+  static double reduce_scatter(double bytes_in, int p, const MachineSpecification& s);  // bytes of the full input
+  static double all_to_all(double bytes, int p, const MachineSpecification& s);          // bytes per rank
+  static double p2p(double bytes, const MachineSpecification& s);
+};
+
+struct OpCost {
+  double forward = 0;   // seconds
+  double backward = 0;
+  double memory = 0;    // bytes resident per device (weights + grads + optimizer + activations)
+  double sync = 0;      // weight-gradient all-reduce time
+};
+
+// Optional measured-profile table: op signature -> {fwd_ms, bwd_ms}
+class ProfileTable {
+ public:
+  void load_json(const Json& j);
+  bool lookup(const std::string& key, double& fwd, double& bwd) const;
+  void put(const std::string& key, double fwd, double bwd);
+  Json to_json() const;
+  size_t size() const { return table_.size(); }
+
+ private:
+  std::map<std::string, std::pair<double, double>> table_;
+};
+
+class CostModel {
+ public:
+  explicit CostModel(MachineSpecification spec) : spec_(std::move(spec)) {}
+  const MachineSpecification& spec() const { return spec_; }
+  ProfileTable& profiles() { return profiles_; }
+
+  // Compute cost of one piece (per-device) of an operator.
+  OpCost op_cost(const OpAttrs& op, const std::vector<ParallelTensorShape>& inputs,
+                 const std::vector<ParallelTensorShape>& weights, const std::vector<ParallelTensorShape>& outputs,
+                 int block_size) const;
+  // Cost of a parallel operator (forward / backward communication).
+  OpCost parallel_op_cost(const OpAttrs& op, const ParallelTensorShape& in, const ParallelTensorShape& out,
+                          int block_size) const;
+  // Moving a tensor between two device blocks of the same layout.
+  double movement_cost(const ParallelTensorShape& t, const DeviceBlock& src, const DeviceBlock& dst) const;
+  static std::string signature(const OpAttrs& op, const std::vector<TensorShape>& pieces);
+
+ private:
+  double gemm_time(double flops, double bytes, double eff_hint) const;
+  MachineSpecification spec_;
+  ProfileTable profiles_;
+};
+
+}  // namespace ff

@@ -1,0 +1,69 @@
+// Strategy search: MCMC over per-layer parallel configs (legacy
+// strategy_search_task) and Unity best-first search over PCG substitutions
+// costed by the machine-mapping DP or the simulator (graph_optimize).
+//
+// Parity:
+//  * MCMC: lib/runtime/src/model.cc (legacy strategy_search / optimize with
+//    --budget, --alpha; Metropolis acceptance on simulated runtime)
+//  * Unity: lib/compiler/src/unity_algorithm.cc:27-91 (intended body):
+//    priority queue of GraphOptimizeState{pcg, mapping, runtime}; prune states
+//    worse than best * alpha; expand every substitution at every match;
+//    keep states with runtime <= threshold and #ops <= max_num_ops; `budget`
+//    expansions; state identity = structural graph equality
+//    (graph_optimize_state.cc:10-47).
+#pragma once
+#include <map>
+#include <string>
+
+#include "ff/computation_graph.h"
+#include "ff/machine.h"
+#include "ff/mapping.h"
+#include "ff/parallelize.h"
+#include "ff/simulator.h"
+#include "ff/substitution.h"
+
+namespace ff {
+
+struct SearchConfig {
+  int world = 1;
+  int budget = 1000;            // MCMC proposals / Unity expansions
+  double alpha = 1.05;          // Unity: prune states slower than best * alpha
+  double threshold = 1e30;      // Unity: drop states slower than this (seconds)
+  int max_num_ops = 1 << 20;    // Unity: drop graphs with more operator nodes
+  double mcmc_beta = 200.0;     // Metropolis: accept worse with exp(-beta * rel_delta)
+  double group_move_prob = 0.6; // propose the same config for every layer of the same signature
+  uint64_t seed = 0x5eed;
+  double time_limit = 60.0;     // seconds
+  bool use_machine_mapping = false;  // Unity cost: DP machine mapping (else simulator)
+  SearchSpaceOptions space;
+  SimConfig sim;
+};
+
+struct SearchResult {
+  std::string algorithm;
+  ParallelComputationGraph pcg;
+  StrategyConfig strategy;               // MCMC only
+  std::map<int, DeviceBlock> views;      // PCG node -> block (empty: whole world)
+  double cost = 0;                       // simulated seconds / iteration
+  double data_parallel_cost = 0;
+  int iterations = 0;
+  int evaluated = 0;
+  int accepted = 0;
+  double elapsed = 0;
+  Json trace;                            // [[iteration, best cost], ...]
+  Json to_json(const ComputationGraph* cg = nullptr) const;
+};
+
+// Cost of a lowered strategy with the simulator (inf if invalid).
+double evaluate_strategy(const ComputationGraph& cg, const StrategyConfig& s, const CostModel& cm,
+                         const SimConfig& sim, int world, SimResult* out = nullptr);
+
+SearchResult mcmc_search(const ComputationGraph& cg, const CostModel& cm, const SearchConfig& cfg,
+                         const StrategyConfig* initial = nullptr);
+SearchResult unity_search(const ParallelComputationGraph& initial, const CostModel& cm, const SearchConfig& cfg,
+                          const std::vector<Substitution>& extra_rules = {});
+// MCMC from data parallel, then Unity refinement of the best PCG; returns the
+// best of {data parallel, MCMC, Unity} by simulated iteration time.
+SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, const SearchConfig& cfg);
+
+}  // namespace ff

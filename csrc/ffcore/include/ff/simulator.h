@@ -1,0 +1,86 @@
+// Event-driven simulator of one training iteration of a PCG on a machine.
+//
+// Parity: lib/runtime/src/simulator.cc Simulator::simulate_runtime (:816-1243)
+// — per-op forward/backward tasks (:823-841), transfer tasks for data
+// dependencies between different device sets (:843-901), weight-gradient
+// synchronization overlapped with backward (:914-955), list scheduling with
+// per-device serialization (:1020-1085), the NCCL all-reduce pass
+// (:1087-1215) and the framebuffer memory penalty (:1216-1242); dot export
+// of the task graph (--taskgraph).
+//
+// MI355X model: each device has a compute lane (one HIP stream: kernels and
+// the inline RCCL collectives of parallel ops) and a communication lane (the
+// bucketed gradient all-reduce stream the executor overlaps with backward).
+// Gradient buckets mirror Executor's (grad dtype bf16 for GEMM weights), and
+// the fused Adam/SGD update runs after each device's last bucket.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ff/computation_graph.h"
+#include "ff/machine.h"
+
+namespace ff {
+
+struct SimConfig {
+  int world = 1;                      // devices used by the executor
+  bool overlap_grad_sync = true;
+  double bucket_bytes = 64.0 * (1 << 20);
+  bool include_update = true;
+  double update_bytes_per_param = 30.0;  // fused Adam: w,m,v r/w + grad + bf16 copy
+  double memory_penalty_per_mb = 1e-3;   // seconds per MB over capacity (reference: 1 ms / MB)
+  double comm_compute_slowdown = 0.05;   // compute slowdown while a collective overlaps
+  bool bf16_weight_grads = true;
+};
+
+struct SimTask {
+  enum Type { FORWARD = 0, BACKWARD = 1, COMM = 2, UPDATE = 3, ALLREDUCE = 4 };
+  Type type = FORWARD;
+  int node = -1;
+  std::string name;
+  int dev_start = 0, dev_size = 1;
+  double run_time = 0, ready_time = 0, start_time = 0, end_time = 0;
+  std::vector<int> deps;
+  double xfer = 0;  // extra transfer latency added on the incoming edge
+};
+
+struct SimResult {
+  double iteration_time = 0;   // seconds
+  double forward_time = 0;     // critical-path forward end
+  double backward_end = 0;
+  double sync_time = 0;        // summed all-reduce time
+  double exposed_sync = 0;     // iteration_time - backward_end - update
+  double update_time = 0;
+  double comm_time = 0;        // summed parallel-op communication
+  double peak_memory = 0;      // max bytes on one device
+  double memory_penalty = 0;
+  int num_tasks = 0;
+  std::vector<SimTask> tasks;  // only filled when keep_tasks
+  Json to_json() const;
+};
+
+class Simulator {
+ public:
+  Simulator(const CostModel& cm, SimConfig cfg) : cm_(cm), cfg_(std::move(cfg)) {}
+  const SimConfig& config() const { return cfg_; }
+  // views: PCG node -> device block (defaults to the whole world)
+  SimResult simulate(const ParallelComputationGraph& pcg, const std::map<int, DeviceBlock>& views = {},
+                     bool keep_tasks = false) const;
+  std::string task_graph_dot(const SimResult& r) const;
+
+ private:
+  const CostModel& cm_;
+  SimConfig cfg_;
+};
+
+// Node classification shared by the simulator, the machine-mapping problem
+// and the executor's folding rules.
+enum class NodeRole { COMPUTE = 0, PARALLEL = 1, INPUT_PATH = 2, WEIGHT_PATH = 3 };
+std::map<int, NodeRole> classify_nodes(const ParallelComputationGraph& pcg);
+// Compute cost of a PCG node (op cost + its weights' gradient sync), per device.
+OpCost pcg_node_cost(const CostModel& cm, const ParallelComputationGraph& pcg, int node, int block_size);
+// The PCG data-flow DAG restricted to COMPUTE/PARALLEL/INPUT nodes.
+DiGraph data_path_digraph(const ParallelComputationGraph& pcg);
+
+}  // namespace ff

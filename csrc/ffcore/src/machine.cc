@@ -1,0 +1,376 @@
+#include "ff/machine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <sstream>
+
+namespace ff {
+
+Json MachineSpecification::to_json() const {
+  Json j = Json::object();
+  j["num_nodes"] = num_nodes;
+  j["num_cpus_per_node"] = num_cpus_per_node;
+  j["num_gpus_per_node"] = num_gpus_per_node;
+  j["inter_node_bandwidth"] = inter_node_bandwidth;
+  j["intra_node_bandwidth"] = intra_node_bandwidth;
+  j["peak_bf16_flops"] = peak_bf16_flops;
+  j["peak_fp32_flops"] = peak_fp32_flops;
+  j["mfma_efficiency"] = mfma_efficiency;
+  j["hbm_bandwidth"] = hbm_bandwidth;
+  j["hbm_capacity"] = hbm_capacity;
+  j["kernel_launch_overhead"] = kernel_launch_overhead;
+  j["collective_latency"] = collective_latency;
+  j["xgmi_links"] = xgmi_links;
+  j["xgmi_link_bandwidth"] = xgmi_link_bandwidth;
+  return j;
+}
+
+MachineSpecification MachineSpecification::from_json(const Json& j) {
+  MachineSpecification s;
+  auto gi = [&](const char* k, int& v) {
+    if (j.contains(k)) v = static_cast<int>(j.at(k).as_int());
+  };
+  auto gd = [&](const char* k, double& v) {
+    if (j.contains(k)) v = j.at(k).as_double();
+  };
+  gi("num_nodes", s.num_nodes);
+  gi("num_cpus_per_node", s.num_cpus_per_node);
+  gi("num_gpus_per_node", s.num_gpus_per_node);
+  gd("inter_node_bandwidth", s.inter_node_bandwidth);
+  gd("intra_node_bandwidth", s.intra_node_bandwidth);
+  gd("peak_bf16_flops", s.peak_bf16_flops);
+  gd("peak_fp32_flops", s.peak_fp32_flops);
+  gd("mfma_efficiency", s.mfma_efficiency);
+  gd("hbm_bandwidth", s.hbm_bandwidth);
+  gd("hbm_capacity", s.hbm_capacity);
+  gd("kernel_launch_overhead", s.kernel_launch_overhead);
+  gd("collective_latency", s.collective_latency);
+  gi("xgmi_links", s.xgmi_links);
+  gd("xgmi_link_bandwidth", s.xgmi_link_bandwidth);
+  return s;
+}
+
+MachineSpecification MachineSpecification::mi355x(int num_nodes, int gpus_per_node) {
+  MachineSpecification s;
+  s.num_nodes = num_nodes;
+  s.num_gpus_per_node = gpus_per_node;
+  return s;
+}
+
+Json MachineView::to_json() const {
+  Json j = Json::object();
+  j["start"] = Json(std::vector<int64_t>{start.node_idx, start.device_idx});
+  Json d = Json::array();
+  for (auto const& x : dims) {
+    Json e = Json::object();
+    e["stride"] = x.stride;
+    e["projection"] = x.projection == ProjectionType::INTRA_NODE ? "INTRA_NODE" : "INTER_NODE";
+    d.push_back(e);
+  }
+  j["dimensions"] = d;
+  return j;
+}
+
+MachineView MachineView::from_json(const Json& j) {
+  MachineView v;
+  auto st = j.at("start").as_int_vector();
+  v.start = {static_cast<int>(st.at(0)), static_cast<int>(st.at(1))};
+  for (auto const& e : j.at("dimensions").as_array())
+    v.dims.push_back({static_cast<int>(e.at("stride").as_int()),
+                      e.at("projection").as_string() == "INTER_NODE" ? ProjectionType::INTER_NODE
+                                                                     : ProjectionType::INTRA_NODE});
+  return v;
+}
+
+std::vector<int> operator_task_space(const ParallelTensorShape& out) {
+  std::vector<int> ts = out.shard_degrees();
+  ts.push_back(out.sum_degree);
+  ts.push_back(out.discard_copy_degree);
+  return ts;
+}
+
+// coefficient of task dim i = stride_i * prod_{j>i, same projection} ts[j]
+// (the last task dim varies fastest, matching the executor's row-major
+// canonical placement).
+MachineSpaceCoordinate get_machine_space_coordinate(const std::vector<int>& ts, const MachineView& view,
+                                                    const std::vector<int>& coord,
+                                                    const MachineSpecification& spec) {
+  if (ts.size() != view.dims.size() || coord.size() != ts.size())
+    throw FFError("get_machine_space_coordinate: rank mismatch");
+  MachineSpaceCoordinate r = view.start;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    if (coord[i] < 0 || coord[i] >= ts[i]) throw FFError("task coordinate out of range");
+    int64_t mult = view.dims[i].stride;
+    for (size_t j = i + 1; j < ts.size(); ++j)
+      if (view.dims[j].projection == view.dims[i].projection) mult *= ts[j];
+    if (view.dims[i].projection == ProjectionType::INTRA_NODE) r.device_idx += static_cast<int>(coord[i] * mult);
+    else r.node_idx += static_cast<int>(coord[i] * mult);
+  }
+  (void)spec;
+  return r;
+}
+
+static void for_each_coord(const std::vector<int>& ts, const std::function<void(const std::vector<int>&)>& f) {
+  std::vector<int> c(ts.size(), 0);
+  while (true) {
+    f(c);
+    int i = static_cast<int>(ts.size()) - 1;
+    while (i >= 0) {
+      if (++c[i] < ts[i]) break;
+      c[i] = 0;
+      --i;
+    }
+    if (i < 0) break;
+  }
+}
+
+std::vector<int> get_device_ids(const std::vector<int>& ts, const MachineView& view, const MachineSpecification& spec) {
+  std::vector<int> ids;
+  for_each_coord(ts, [&](const std::vector<int>& c) {
+    auto m = get_machine_space_coordinate(ts, view, c, spec);
+    ids.push_back(m.node_idx * spec.num_gpus_per_node + m.device_idx);
+  });
+  return ids;
+}
+
+std::vector<MachineView> get_allowed_machine_views(const std::vector<int>& ts, const MachineSpecification& spec) {
+  std::vector<MachineView> out;
+  const int n = static_cast<int>(ts.size());
+  std::vector<int> nontrivial;
+  for (int i = 0; i < n; ++i)
+    if (ts[i] > 1) nontrivial.push_back(i);
+  const int max_stride = spec.num_devices();
+  // enumerate strides for the nontrivial dims (trivial dims: stride 1, intra)
+  std::vector<int> strides(nontrivial.size(), 1);
+  std::vector<int> projs(nontrivial.size(), 0);
+  std::function<void(size_t)> rec_proj, rec_stride;
+  auto emit = [&]() {
+    MachineView v;
+    v.dims.assign(n, MachineViewDimension{1, ProjectionType::INTRA_NODE});
+    for (size_t k = 0; k < nontrivial.size(); ++k)
+      v.dims[nontrivial[k]] = {strides[k], projs[k] ? ProjectionType::INTER_NODE : ProjectionType::INTRA_NODE};
+    for (int node = 0; node < spec.num_nodes; ++node)
+      for (int dev = 0; dev < spec.num_gpus_per_node; ++dev) {
+        v.start = {node, dev};
+        bool ok = true;
+        std::vector<int> maxc(ts.size());
+        for (int i = 0; i < n; ++i) maxc[i] = ts[i] - 1;
+        auto m = get_machine_space_coordinate(ts, v, maxc, spec);
+        if (m.node_idx >= spec.num_nodes || m.device_idx >= spec.num_gpus_per_node) ok = false;
+        if (ok) {
+          auto ids = get_device_ids(ts, v, spec);
+          std::sort(ids.begin(), ids.end());
+          if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) ok = false;  // must be injective
+        }
+        if (ok) out.push_back(v);
+      }
+  };
+  rec_stride = [&](size_t k) {
+    if (k == nontrivial.size()) {
+      emit();
+      return;
+    }
+    for (int s = 1; s <= max_stride; ++s) {
+      strides[k] = s;
+      rec_stride(k + 1);
+    }
+  };
+  rec_proj = [&](size_t k) {
+    if (k == nontrivial.size()) {
+      rec_stride(0);
+      return;
+    }
+    for (int p = 0; p < (spec.num_nodes > 1 ? 2 : 1); ++p) {
+      projs[k] = p;
+      rec_proj(k + 1);
+    }
+  };
+  rec_proj(0);
+  return out;
+}
+
+MachineView block_machine_view(const std::vector<int>& ts, const DeviceBlock& b, const MachineSpecification& spec) {
+  int T = 1;
+  for (int d : ts) T *= d;
+  if (T <= 0 || b.size % T != 0) throw FFError("block_machine_view: task space does not divide the block");
+  MachineView v;
+  v.start = {b.start / spec.num_gpus_per_node, b.start % spec.num_gpus_per_node};
+  const int R = b.size / T;
+  for (size_t i = 0; i < ts.size(); ++i) v.dims.push_back({R, ProjectionType::INTRA_NODE});
+  return v;
+}
+
+std::vector<std::pair<DeviceBlock, DeviceBlock>> get_resource_splits(const DeviceBlock& b) {
+  std::vector<std::pair<DeviceBlock, DeviceBlock>> out;
+  for (int k = 1; k < b.size; k *= 2) {
+    out.push_back({{b.start, k}, {b.start + k, b.size - k}});
+    if (b.size - k != k) out.push_back({{b.start, b.size - k}, {b.start + b.size - k, k}});
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+static double eff_bw(int p, const MachineSpecification& s) {
+  if (p <= 1) return 1e30;
+  double links = std::min(p - 1, s.xgmi_links) * s.xgmi_link_bandwidth;
+  double b = std::min(s.intra_node_bandwidth, links);
+  if (p > s.num_gpus_per_node) b = std::min(b, s.inter_node_bandwidth);
+  return b;
+}
+
+double CollectiveCost::all_reduce(double bytes, int p, const MachineSpecification& s) {
+  if (p <= 1 || bytes <= 0) return 0;
+  return 2.0 * (p - 1) / p * bytes / eff_bw(p, s) + 2.0 * (p - 1) * s.collective_latency / 4.0 + s.collective_latency;
+}
+double CollectiveCost::all_gather(double bytes_out, int p, const MachineSpecification& s) {
+  if (p <= 1 || bytes_out <= 0) return 0;
+  return (p - 1.0) / p * bytes_out / eff_bw(p, s) + s.collective_latency;
+}
+double CollectiveCost::reduce_scatter(double bytes_in, int p, const MachineSpecification& s) {
+  return all_gather(bytes_in, p, s);
+}
+double CollectiveCost::all_to_all(double bytes, int p, const MachineSpecification& s) {
+  if (p <= 1 || bytes <= 0) return 0;
+  return (p - 1.0) / p * bytes / eff_bw(p, s) + s.collective_latency;
+}
+double CollectiveCost::p2p(double bytes, const MachineSpecification& s) {
+  return bytes / s.xgmi_link_bandwidth + s.collective_latency;
+}
+
+void ProfileTable::load_json(const Json& j) {
+  for (auto const& kv : j.as_object())
+    table_[kv.first] = {kv.second.at("fwd_ms").as_double(), kv.second.at("bwd_ms").as_double()};
+}
+bool ProfileTable::lookup(const std::string& key, double& fwd, double& bwd) const {
+  auto it = table_.find(key);
+  if (it == table_.end()) return false;
+  fwd = it->second.first * 1e-3;
+  bwd = it->second.second * 1e-3;
+  return true;
+}
+void ProfileTable::put(const std::string& key, double fwd, double bwd) { table_[key] = {fwd, bwd}; }
+Json ProfileTable::to_json() const {
+  Json j = Json::object();
+  for (auto const& kv : table_) {
+    Json e = Json::object();
+    e["fwd_ms"] = kv.second.first;
+    e["bwd_ms"] = kv.second.second;
+    j[kv.first] = e;
+  }
+  return j;
+}
+
+std::string CostModel::signature(const OpAttrs& op, const std::vector<TensorShape>& pieces) {
+  std::ostringstream os;
+  os << op.str();
+  for (auto const& p : pieces) os << "|" << p.str();
+  return os.str();
+}
+
+double CostModel::gemm_time(double flops, double bytes, double eff_hint) const {
+  double eff = spec_.mfma_efficiency * std::max(0.05, std::min(1.0, eff_hint));
+  return std::max(flops / (spec_.peak_bf16_flops * eff), bytes / spec_.hbm_bandwidth);
+}
+
+OpCost CostModel::op_cost(const OpAttrs& op, const std::vector<ParallelTensorShape>& inputs,
+                          const std::vector<ParallelTensorShape>& weights,
+                          const std::vector<ParallelTensorShape>& outputs, int block_size) const {
+  (void)block_size;
+  OpCost c;
+  std::vector<TensorShape> ip, wp, op_;
+  for (auto const& x : inputs) ip.push_back(x.piece_shape());
+  for (auto const& x : weights) wp.push_back(x.piece_shape());
+  for (auto const& x : outputs) op_.push_back(x.piece_shape());
+  std::vector<TensorShape> all = ip;
+  all.insert(all.end(), op_.begin(), op_.end());
+  double f = 0, b = 0;
+  if (profiles_.lookup(signature(op, all), f, b)) {
+    c.forward = f;
+    c.backward = b;
+  } else {
+    OpWork w = estimate_op_work(op, ip, wp, op_);
+    if (w.matmul_like) {
+      c.forward = gemm_time(w.flops, w.bytes, w.mfma_efficiency_hint);
+      c.backward = 2.0 * c.forward;
+    } else {
+      c.forward = std::max(w.flops / spec_.peak_fp32_flops, w.bytes / spec_.hbm_bandwidth);
+      c.backward = 1.8 * c.forward;
+    }
+    int kernels = w.matmul_like ? 2 : 1;
+    if (op.type == OpType::MULTIHEAD_ATTENTION) kernels = 4;
+    if (w.flops > 0 || w.bytes > 0) {
+      c.forward += kernels * spec_.kernel_launch_overhead;
+      c.backward += 2 * kernels * spec_.kernel_launch_overhead;
+    }
+  }
+  // memory: weights (bf16 copy + fp32 master + fp32 m, v + grad) + saved activations
+  double wmem = 0, sync = 0;
+  for (size_t i = 0; i < weights.size(); ++i) {
+    double elems = static_cast<double>(wp[i].num_elements());
+    wmem += elems * 16.0;
+    if (weights[i].discard_copy_degree > 1)
+      sync += CollectiveCost::all_reduce(elems * 2.0, weights[i].discard_copy_degree, spec_);
+  }
+  double amem = 0;
+  for (auto const& t : ip) amem += static_cast<double>(t.size_bytes());
+  for (auto const& t : op_) amem += static_cast<double>(t.size_bytes());
+  c.memory = wmem + amem;
+  c.sync = sync;
+  return c;
+}
+
+OpCost CostModel::parallel_op_cost(const OpAttrs& op, const ParallelTensorShape& in, const ParallelTensorShape& out,
+                                   int block_size) const {
+  (void)block_size;
+  OpCost c;
+  const double in_b = static_cast<double>(in.piece_shape().size_bytes());
+  const double out_b = static_cast<double>(out.piece_shape().size_bytes());
+  switch (op.type) {
+    case OpType::REPARTITION: {
+      int d = static_cast<int>(op.i("degree"));
+      c.forward = out_b / spec_.hbm_bandwidth + spec_.kernel_launch_overhead;  // local slice
+      c.backward = CollectiveCost::all_gather(in_b, d, spec_);                  // gather grads
+      break;
+    }
+    case OpType::COMBINE: {
+      int d = static_cast<int>(op.i("degree"));
+      c.forward = CollectiveCost::all_gather(out_b, d, spec_);
+      c.backward = in_b / spec_.hbm_bandwidth + spec_.kernel_launch_overhead;
+      break;
+    }
+    case OpType::REPLICATE: {
+      int d = static_cast<int>(op.i("degree"));
+      c.forward = 0;
+      c.backward = op.b("partial") ? 0.0 : CollectiveCost::all_reduce(in_b, d, spec_);
+      break;
+    }
+    case OpType::REDUCTION: {
+      int d = static_cast<int>(op.i("degree"));
+      c.forward = CollectiveCost::all_reduce(out_b, d, spec_);
+      c.backward = 0;
+      break;
+    }
+    case OpType::ALLTOALL: {
+      int d = static_cast<int>(op.i("degree"));
+      c.forward = CollectiveCost::all_to_all(in_b, d, spec_);
+      c.backward = c.forward;
+      break;
+    }
+    default:
+      c.forward = c.backward = 0;
+  }
+  c.memory = out_b;
+  return c;
+}
+
+double CostModel::movement_cost(const ParallelTensorShape& t, const DeviceBlock& src, const DeviceBlock& dst) const {
+  if (src == dst) return 0;
+  // an unpartitioned tensor is replicated on every device of its block:
+  // consumers inside that block read their local copy
+  if (t.total_parallel_degree() == 1 && dst.start >= src.start && dst.start + dst.size <= src.start + src.size)
+    return 0;
+  return CollectiveCost::p2p(static_cast<double>(t.piece_shape().size_bytes()), spec_);
+}
+
+}  // namespace ff

@@ -1,0 +1,239 @@
+#include "ff/search.h"
+
+#include <chrono>
+#include <cmath>
+#include <limits>
+#include <queue>
+#include <random>
+#include <unordered_set>
+
+namespace ff {
+
+static constexpr double kInf = std::numeric_limits<double>::infinity();
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+Json SearchResult::to_json(const ComputationGraph* cg) const {
+  Json j = Json::object();
+  j["algorithm"] = algorithm;
+  j["cost"] = cost;
+  j["data_parallel_cost"] = data_parallel_cost;
+  j["predicted_speedup_over_dp"] = cost > 0 ? data_parallel_cost / cost : 0.0;
+  j["iterations"] = iterations;
+  j["evaluated"] = evaluated;
+  j["accepted"] = accepted;
+  j["elapsed"] = elapsed;
+  j["trace"] = trace;
+  if (cg && !strategy.empty()) j["strategy"] = strategy_to_json(*cg, strategy);
+  Json v = Json::object();
+  for (auto const& kv : views) v[std::to_string(kv.first)] = Json(std::vector<int64_t>{kv.second.start, kv.second.size});
+  j["views"] = v;
+  return j;
+}
+
+double evaluate_strategy(const ComputationGraph& cg, const StrategyConfig& s, const CostModel& cm,
+                         const SimConfig& sim, int world, SimResult* out) {
+  try {
+    auto L = lower_strategy(cg, s, world);
+    SimConfig c = sim;
+    c.world = world;
+    Simulator S(cm, c);
+    auto r = S.simulate(L.pcg);
+    if (out) *out = r;
+    return r.iteration_time;
+  } catch (const FFError&) {
+    return kInf;
+  }
+}
+
+static std::string layer_signature(const ComputationGraph& cg, int id) {
+  std::string s = cg.g.node(id).label.op.str();
+  for (auto const& v : cg.layer_data_inputs(id)) s += "|" + cg.shape(v).str();
+  return s;
+}
+
+SearchResult mcmc_search(const ComputationGraph& cg, const CostModel& cm, const SearchConfig& cfg,
+                         const StrategyConfig* initial) {
+  const double t0 = now_s();
+  SearchResult R;
+  R.algorithm = "mcmc";
+  R.trace = Json::array();
+  const int world = cfg.world;
+  std::mt19937_64 rng(cfg.seed);
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+
+  std::vector<int> layers;
+  std::map<int, std::vector<LayerConfig>> cands;
+  std::map<std::string, std::vector<int>> groups;
+  std::map<int, std::string> sig;
+  for (int id : cg.g.topo_order()) {
+    auto t = cg.g.node(id).label.op.type;
+    if (t == OpType::WEIGHT) continue;
+    cands[id] = candidate_configs(cg, id, world, cfg.space);
+    if (cands[id].size() > 1) layers.push_back(id);
+    sig[id] = layer_signature(cg, id);
+    groups[sig[id]].push_back(id);
+  }
+  StrategyConfig dp = data_parallel_strategy(cg, world);
+  SimConfig sim = cfg.sim;
+  sim.world = world;
+  R.data_parallel_cost = evaluate_strategy(cg, dp, cm, sim, world);
+  StrategyConfig cur = initial ? *initial : dp;
+  double cur_cost = initial ? evaluate_strategy(cg, cur, cm, sim, world) : R.data_parallel_cost;
+  StrategyConfig best = cur;
+  double best_cost = cur_cost;
+  R.evaluated = 2;
+  R.trace.push_back(Json(std::vector<double>{0.0, best_cost}));
+  int it = 0;
+  for (; it < cfg.budget && !layers.empty(); ++it) {
+    if (now_s() - t0 > cfg.time_limit) break;
+    int id = layers[rng() % layers.size()];
+    auto const& cs = cands[id];
+    LayerConfig c = cs[rng() % cs.size()];
+    if (c == cur[id]) continue;
+    StrategyConfig next = cur;
+    if (U(rng) < cfg.group_move_prob) {
+      for (int g : groups[sig[id]]) next[g] = c;
+    } else {
+      next[id] = c;
+    }
+    double nc = evaluate_strategy(cg, next, cm, sim, world);
+    ++R.evaluated;
+    if (!std::isfinite(nc)) continue;
+    bool accept = nc < cur_cost || U(rng) < std::exp(-cfg.mcmc_beta * (nc - cur_cost) / cur_cost);
+    if (accept) {
+      cur = std::move(next);
+      cur_cost = nc;
+      ++R.accepted;
+      if (cur_cost < best_cost) {
+        best = cur;
+        best_cost = cur_cost;
+        R.trace.push_back(Json(std::vector<double>{static_cast<double>(it), best_cost}));
+      }
+    }
+  }
+  R.iterations = it;
+  R.strategy = best;
+  R.cost = best_cost;
+  R.pcg = lower_strategy(cg, best, world).pcg;
+  R.elapsed = now_s() - t0;
+  return R;
+}
+
+namespace {
+struct State {
+  double cost;
+  int id;
+  bool operator>(const State& o) const { return cost > o.cost; }
+};
+}  // namespace
+
+SearchResult unity_search(const ParallelComputationGraph& initial, const CostModel& cm, const SearchConfig& cfg,
+                          const std::vector<Substitution>& extra_rules) {
+  const double t0 = now_s();
+  SearchResult R;
+  R.algorithm = "unity";
+  R.trace = Json::array();
+  SimConfig sim = cfg.sim;
+  sim.world = cfg.world;
+  Simulator S(cm, sim);
+  auto cost_of = [&](const ParallelComputationGraph& g, std::map<int, DeviceBlock>* views) -> double {
+    try {
+      if (cfg.use_machine_mapping) {
+        auto m = get_optimal_machine_mapping(g, cm, cfg.world);
+        if (!m.feasible) return kInf;
+        if (views) *views = m.views;
+        return S.simulate(g, m.views).iteration_time;
+      }
+      return S.simulate(g).iteration_time;
+    } catch (const FFError&) {
+      return kInf;
+    }
+  };
+  auto rules = generate_parallelization_substitutions(initial, cfg.world);
+  rules.insert(rules.end(), extra_rules.begin(), extra_rules.end());
+  std::vector<ParallelComputationGraph> states;
+  std::vector<std::map<int, DeviceBlock>> state_views;
+  std::priority_queue<State, std::vector<State>, std::greater<State>> pq;
+  std::unordered_set<size_t> seen;
+  states.push_back(initial);
+  state_views.emplace_back();
+  double c0 = cost_of(initial, &state_views[0]);
+  R.data_parallel_cost = c0;
+  pq.push({c0, 0});
+  seen.insert(initial.structural_hash());
+  int best = 0;
+  double best_cost = c0;
+  R.evaluated = 1;
+  R.trace.push_back(Json(std::vector<double>{0.0, best_cost}));
+  int it = 0;
+  for (; it < cfg.budget && !pq.empty(); ++it) {
+    if (now_s() - t0 > cfg.time_limit) break;
+    State s = pq.top();
+    pq.pop();
+    if (s.cost < best_cost) {
+      best_cost = s.cost;
+      best = s.id;
+      R.trace.push_back(Json(std::vector<double>{static_cast<double>(it), best_cost}));
+    } else if (s.cost > best_cost * cfg.alpha) {
+      continue;
+    }
+    const ParallelComputationGraph cur = states[s.id];
+    for (auto const& rule : rules) {
+      if (now_s() - t0 > cfg.time_limit) break;
+      auto matches = find_pattern_matches(rule.pattern, cur, 4096);
+      for (auto const& m : matches) {
+        auto next = apply_substitution(cur, rule, m);
+        if (!next) continue;
+        if (next->num_operator_nodes() > cfg.max_num_ops) continue;
+        size_t h = next->structural_hash();
+        if (!seen.insert(h).second) continue;
+        std::map<int, DeviceBlock> v;
+        double c = cost_of(*next, &v);
+        ++R.evaluated;
+        if (!std::isfinite(c) || c > cfg.threshold) continue;
+        states.push_back(std::move(*next));
+        state_views.push_back(std::move(v));
+        pq.push({c, static_cast<int>(states.size()) - 1});
+        if (c < best_cost) {
+          best_cost = c;
+          best = static_cast<int>(states.size()) - 1;
+          R.trace.push_back(Json(std::vector<double>{static_cast<double>(it), best_cost}));
+        }
+      }
+    }
+  }
+  R.iterations = it;
+  R.pcg = states[best];
+  R.views = state_views[best];
+  R.cost = best_cost;
+  R.elapsed = now_s() - t0;
+  return R;
+}
+
+SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, const SearchConfig& cfg) {
+  const double t0 = now_s();
+  SearchConfig mc = cfg;
+  mc.time_limit = cfg.time_limit * 0.7;
+  auto m = mcmc_search(cg, cm, mc);
+  SearchConfig uc = cfg;
+  uc.time_limit = std::max(0.0, cfg.time_limit - (now_s() - t0));
+  uc.budget = std::max(1, cfg.budget / 50);
+  SearchResult best = m;
+  if (uc.time_limit > 0.5) {
+    auto u = unity_search(m.pcg, cm, uc);
+    if (u.cost < best.cost * 0.999) {
+      u.data_parallel_cost = m.data_parallel_cost;
+      u.strategy.clear();
+      u.algorithm = "mcmc+unity";
+      u.evaluated += m.evaluated;
+      best = u;
+    }
+  }
+  best.elapsed = now_s() - t0;
+  return best;
+}
+
+}  // namespace ff

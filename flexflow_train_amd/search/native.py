@@ -1,0 +1,90 @@
+"""Python helpers over the native machine/cost/simulator/search bindings.
+
+* ``machine_spec(ffconfig)``: MI355X defaults, overridden by
+  ``--machine-model-file`` (JSON with MachineSpecification fields — the
+  analogue of the reference's EnhancedMachineModel config file,
+  machine_config_example:1-60).
+* ``cost_model(ffconfig)``: analytic MI355X model plus an optional measured
+  profile table (``FF_PROFILE_TABLE`` / ``ffconfig.profile_table_file``,
+  written by tools/profile_ops.py) — the reference's measure_operator_cost
+  cache (simulator.cc:531-571).
+* ``simulate(pcg, ...)`` / ``machine_mapping(...)`` / ``sp_decomposition``
+  return parsed Python structures.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Optional, Tuple
+
+from .. import _ffcore as C
+
+
+def machine_spec(ffconfig=None, world: Optional[int] = None):
+    spec = C.MachineSpecification.mi355x()
+    path = getattr(ffconfig, "machine_model_file", "") if ffconfig is not None else ""
+    if path:
+        with open(path) as f:
+            spec = C.MachineSpecification.from_json(f.read())
+    if ffconfig is not None:
+        nn = getattr(ffconfig, "search_num_nodes", -1)
+        if nn and nn > 0:
+            spec.num_nodes = nn
+        nw = getattr(ffconfig, "search_num_workers", -1)
+        if nw and nw > 0:
+            spec.num_gpus_per_node = nw
+    if world is not None and world > spec.num_devices():
+        spec.num_nodes = (world + spec.num_gpus_per_node - 1) // spec.num_gpus_per_node
+    return spec
+
+
+def cost_model(ffconfig=None, world: Optional[int] = None):
+    cm = C.CostModel(machine_spec(ffconfig, world))
+    path = os.environ.get("FF_PROFILE_TABLE") or (getattr(ffconfig, "profile_table_file", "") if ffconfig else "")
+    if path and os.path.exists(path):
+        with open(path) as f:
+            cm.load_profiles(f.read())
+    return cm
+
+
+def sim_config(ffconfig=None, world: int = 1) -> dict:
+    cfg = {"world": world}
+    if ffconfig is not None:
+        cfg["overlap_grad_sync"] = bool(getattr(ffconfig, "search_overlap_backward_update", True))
+    return cfg
+
+
+def simulate(pcg, cm, world: int, views: Optional[Dict[int, Tuple[int, int]]] = None, dot: bool = False,
+             **sim_kw):
+    cfg = {"world": world, **sim_kw}
+    res, dot_s = C.simulate(pcg, cm, json.dumps(cfg), dict(views or {}), dot)
+    out = json.loads(res)
+    if dot:
+        out["dot"] = dot_s
+    return out
+
+
+def machine_mapping(pcg, cm, world: int, allow_sub_blocks: bool = True):
+    runtime, feasible, views = C.machine_mapping(pcg, cm, world, allow_sub_blocks)
+    return {"runtime": runtime, "feasible": feasible, "views": {int(k): tuple(v) for k, v in views.items()}}
+
+
+def sp_decomposition(graph, strict: bool = False):
+    if isinstance(graph, C.ComputationGraph):
+        s = C.cg_sp_decomposition(graph, strict)
+    else:
+        s = C.sp_decomposition(graph, strict)
+    return None if s is None else json.loads(s)
+
+
+def strategy_speedup_report(cg, world: int, ffconfig=None, strategy_pcg=None, views=None) -> dict:
+    """Simulated iteration time of data parallel vs a given PCG."""
+    cm = cost_model(ffconfig, world)
+    dp = C.data_parallel_pcg(cg, world)
+    t_dp = simulate(dp, cm, world)["iteration_time"]
+    out = {"dp_iteration_time": t_dp}
+    if strategy_pcg is not None:
+        t = simulate(strategy_pcg, cm, world, views)["iteration_time"]
+        out["iteration_time"] = t
+        out["predicted_speedup_over_dp"] = t_dp / t if t > 0 else None
+    return out

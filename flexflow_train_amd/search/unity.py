@@ -1,8 +1,63 @@
-"""Joint substitution + parallelization search entry point (filled in by the
-native search; until the cost model is wired this returns data parallel)."""
+"""Strategy search entry point used by FFModel.compile().
+
+Runs the native search (csrc/ffcore/src/search.cc) on rank 0 and
+broadcasts the chosen PCG + placement to every rank, so all ranks execute
+the same strategy even when the search is time-bounded.
+
+Algorithms (``FFConfig.search_algorithm``):
+  * ``unity``  — MCMC over per-layer parallel configs, then Unity best-first
+    refinement over PCG substitutions (reference: unity_algorithm.cc:27-91,
+    legacy strategy_search_task);
+  * ``mcmc``   — MCMC only;
+  * ``data_parallel`` handled by strategy.build_pcg.
+
+The report carries the simulated data-parallel and searched iteration times
+and their ratio (``predicted_speedup_over_dp``), the reference's headline
+"speedup over DP after search".
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, Tuple
+
 from .. import _ffcore as C
+from . import native
 
 
-def search(cg, ffconfig, world):
-    pcg = C.data_parallel_pcg(cg, world)
-    return pcg, {}, {"source": "data_parallel_fallback"}
+def _search_local(cg, ffconfig, world: int):
+    cm = native.cost_model(ffconfig)
+    budget = ffconfig.search_budget if ffconfig.search_budget and ffconfig.search_budget > 0 else 400
+    cfg = {
+        "world": world,
+        "budget": budget,
+        "alpha": float(ffconfig.search_alpha),
+        "time_limit": float(getattr(ffconfig, "search_time_limit", 60.0)),
+        "enable_parameter_parallel": True,
+        "enable_attribute_parallel": bool(ffconfig.enable_attribute_parallel),
+        "seed": int(ffconfig.seed) & 0x7FFFFFFF,
+        "sim": native.sim_config(ffconfig, world),
+    }
+    algo = ffconfig.search_algorithm
+    if algo == "mcmc":
+        pcg, rep, views = C.mcmc_search(cg, cm, json.dumps(cfg))
+    else:
+        pcg, rep, views = C.graph_optimize(cg, cm, json.dumps(cfg))
+    rep = json.loads(rep)
+    rep["source"] = "search:" + rep.get("algorithm", algo)
+    return pcg, {int(k): tuple(v) for k, v in views.items()}, rep
+
+
+def search(cg, ffconfig, world: int):
+    import torch.distributed as dist
+
+    distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if not distributed or dist.get_rank() == 0:
+        pcg, views, rep = _search_local(cg, ffconfig, world)
+        payload = [pcg.to_json(), {str(k): list(v) for k, v in views.items()}, rep]
+    else:
+        payload = [None, None, None]
+    if distributed:
+        dist.broadcast_object_list(payload, src=0)
+    pcg = C.ParallelComputationGraph.from_json(payload[0])
+    views: Dict[int, Tuple[int, int]] = {int(k): tuple(v) for k, v in payload[1].items()}
+    return pcg, views, payload[2]
