@@ -122,6 +122,15 @@ SearchResult mcmc_search(const ComputationGraph& cg, const CostModel& cm, const 
   return R;
 }
 
+// Every tensor's degrees must fit the devices the executor has.
+static bool fits_world(const ParallelComputationGraph& g, int world) {
+  for (auto const& v : g.g.all_values()) {
+    int t = g.shape(v).total_parallel_degree();
+    if (t > world || world % t != 0) return false;
+  }
+  return true;
+}
+
 namespace {
 struct State {
   double cost;
@@ -188,6 +197,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
         auto next = apply_substitution(cur, rule, m);
         if (!next) continue;
         if (next->num_operator_nodes() > cfg.max_num_ops) continue;
+        if (!fits_world(*next, cfg.world)) continue;
         size_t h = next->structural_hash();
         if (!seen.insert(h).second) continue;
         std::map<int, DeviceBlock> v;

@@ -433,6 +433,42 @@ std::vector<Substitution> generate_parallelization_substitutions(const ParallelC
             [&](PatternValue, int) { return std::vector<OutputOperator>{new_op(OpType::REDUCTION, {}, {{"degree", D}})}; },
             {{AttrConstraint::EQUAL, "activation", std::string("none")}}));
       }
+      // trade d of the sample-dim degree for model parallelism (keeps the
+      // total degree, so they apply on top of a data-parallel PCG)
+      auto trade_pre = [&](OpType rep_kind) {
+        return [&, rep_kind](PatternValue, int) {
+          std::vector<OutputOperator> v{new_op(OpType::COMBINE, {}, {{"dim", int64_t(0)}, {"degree", D}})};
+          if (rep_kind == OpType::REPLICATE) v.push_back(new_op(OpType::REPLICATE, {}, {{"degree", D}}));
+          else v.push_back(new_op(OpType::REPARTITION, {}, {{"dim", int64_t(-1)}, {"degree", D}}));
+          return v;
+        };
+      };
+      if (t == OpType::LINEAR || t == OpType::EMBEDDING) {
+        rules.push_back(wrap_rule(
+            "trade_sample_for_column_" + to_string(t) + "_" + std::to_string(d), t, 1, 1, trade_pre(OpType::REPLICATE),
+            [&](PatternValue, int) {
+              return std::vector<OutputOperator>{new_op(OpType::COMBINE, {}, {{"dim", int64_t(-1)}, {"degree", D}}),
+                                                 new_op(OpType::REPARTITION, {}, {{"dim", int64_t(0)}, {"degree", D}})};
+            }));
+      }
+      if (t == OpType::LINEAR) {
+        rules.push_back(wrap_rule(
+            "trade_sample_for_row_LINEAR_" + std::to_string(d), t, 1, 1, trade_pre(OpType::REPARTITION),
+            [&](PatternValue, int) {
+              return std::vector<OutputOperator>{new_op(OpType::REDUCTION, {}, {{"degree", D}}),
+                                                 new_op(OpType::REPARTITION, {}, {{"dim", int64_t(0)}, {"degree", D}})};
+            },
+            {{AttrConstraint::EQUAL, "activation", std::string("none")}}));
+      }
+      if (t == OpType::MULTIHEAD_ATTENTION) {
+        rules.push_back(wrap_rule(
+            "trade_sample_for_heads_MHA_" + std::to_string(d), t, 3, 1, trade_pre(OpType::REPLICATE),
+            [&](PatternValue, int) {
+              return std::vector<OutputOperator>{new_op(OpType::REDUCTION, {}, {{"degree", D}}),
+                                                 new_op(OpType::REPARTITION, {}, {{"dim", int64_t(0)}, {"degree", D}})};
+            },
+            {{AttrConstraint::DIVISIBLE_BY, "num_heads", D}}));
+      }
       if (t == OpType::MULTIHEAD_ATTENTION) {
         rules.push_back(wrap_rule(
             "head_parallel_MHA_" + std::to_string(d), t, 3, 1,

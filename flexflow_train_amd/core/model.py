@@ -603,4 +603,4 @@ class FFModel:
     def load_checkpoint(self, path: str):
         from ..utils.checkpoint import load_checkpoint
 
-        load_checkpoint(self, path)
+        return load_checkpoint(self, path)

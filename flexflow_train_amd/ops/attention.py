@@ -70,8 +70,72 @@ def _torch_attention(q, k, v, causal, scale):
     return torch.matmul(p, vt.float()).transpose(1, 2).to(q.dtype)
 
 
+def _layout_dims(attrs: dict, Hl: int):
+    E = int(attrs["embed_dim"])
+    H = int(attrs["num_heads"])
+    kd = int(attrs.get("kdim") or 0) or E // H
+    vd = int(attrs.get("vdim") or 0) or E // H
+    Eq, Ek, Ev = (attrs.get("_in_features") or [E, E, E])[:3]
+    return E, kd, vd, int(Eq), int(Ek), int(Ev)
+
+
+def _blocks(E, kd, vd, Eq, Ek, Ev):
+    # per-head logical column: [Wq: Eq x k][Wk: Ek x k][Wv: Ev x v][Wo: v x E]
+    return [(Eq, kd), (Ek, kd), (Ev, vd), (vd, E)]
+
+
 @register("MULTIHEAD_ATTENTION")
 class MultiHeadAttentionOp(OpImpl):
+    def to_physical(self, attrs, index, piece):
+        if index > 1:
+            return piece
+        Hl = piece.shape[-1]
+        E, kd, vd, Eq, Ek, Ev = _layout_dims(attrs, Hl)
+        if index == 1:  # [2k+v, Hl] -> q[Hl, k] | k[Hl, k] | v[Hl, v]
+            return torch.cat([piece[:kd].t().reshape(-1), piece[kd:2 * kd].t().reshape(-1),
+                              piece[2 * kd:].t().reshape(-1)])
+        parts, o = [], 0
+        mats = []
+        for (r, c) in _blocks(E, kd, vd, Eq, Ek, Ev):
+            mats.append(piece[o:o + r * c].view(r, c, Hl))
+            o += r * c
+        q, k, v, wo = mats
+        if Eq == Ek == Ev and kd == vd:
+            qkv = torch.stack([m.permute(0, 2, 1) for m in (q, k, v)], dim=1)  # [E, 3, Hl, k]
+            parts.append(qkv.reshape(-1))
+        else:
+            for m in (q, k, v):
+                parts.append(m.permute(0, 2, 1).reshape(-1))                   # [Ein, Hl, d]
+        parts.append(wo.permute(2, 0, 1).reshape(-1))                           # [Hl, v, E]
+        return torch.cat(parts)
+
+    def to_logical(self, attrs, index, piece):
+        if index > 1:
+            return piece
+        Hl = piece.shape[-1]
+        E, kd, vd, Eq, Ek, Ev = _layout_dims(attrs, Hl)
+        flat = piece.reshape(-1)
+        if index == 1:
+            q = flat[:Hl * kd].view(Hl, kd).t()
+            k = flat[Hl * kd:2 * Hl * kd].view(Hl, kd).t()
+            v = flat[2 * Hl * kd:].view(Hl, vd).t()
+            return torch.cat([q, k, v], dim=0).contiguous()
+        cols = []
+        if Eq == Ek == Ev and kd == vd:
+            n = Eq * 3 * Hl * kd
+            qkv = flat[:n].view(Eq, 3, Hl, kd)
+            for j in range(3):
+                cols.append(qkv[:, j].permute(0, 2, 1).reshape(Eq * kd, Hl))
+            o = n
+        else:
+            o = 0
+            for (r, c) in _blocks(E, kd, vd, Eq, Ek, Ev)[:3]:
+                cols.append(flat[o:o + r * Hl * c].view(r, Hl, c).permute(0, 2, 1).reshape(r * c, Hl))
+                o += r * Hl * c
+        wo = flat[o:o + Hl * vd * E].view(Hl, vd, E).permute(1, 2, 0).reshape(vd * E, Hl)
+        cols.append(wo)
+        return torch.cat(cols, dim=0).contiguous()
+
     def init_weight(self, ctx, index, logical_shape, initializer, gen):
         # glorot per projection block (fan_in=E, fan_out=H*kdim), not on the
         # flattened [P, H] tensor whose fans are meaningless.

@@ -63,6 +63,17 @@ class OpImpl:
     def init_weight(self, ctx: OpContext, index: int, logical_shape, initializer: dict, gen: torch.Generator):
         return None
 
+    # Physical storage of a weight piece.  Ops whose kernels want a fused /
+    # permuted layout (attention: one [E, 3*Hl*k] QKV operand) override these;
+    # the executor stores physical pieces and converts at every logical
+    # boundary (set/get_parameter, checkpoints), so a logical element keeps
+    # its meaning under any sharding.
+    def to_physical(self, attrs: dict, index: int, piece: torch.Tensor) -> torch.Tensor:
+        return piece
+
+    def to_logical(self, attrs: dict, index: int, piece: torch.Tensor) -> torch.Tensor:
+        return piece
+
 
 def register(*op_types: str) -> Callable:
     def deco(cls):

@@ -146,6 +146,10 @@ class PerfMetrics:
     current_time: float = dataclasses.field(default_factory=time.time)
     metrics: tuple = ()
 
+    @property
+    def accuracy(self) -> float:
+        return self.train_correct / self.train_all if self.train_all else 0.0
+
     @classmethod
     def from_buffer(cls, buf: torch.Tensor, metrics, loss_type: str, start_time: float, out_dim: int = 1):
         v = buf.detach().double().cpu().tolist()

@@ -179,10 +179,14 @@ class Executor:
             cnode = consumers[0] if consumers else n
             lay = self._layout(t, node_for_view=cnode)
             init = json.loads(attrs[n].get("initializer") or '{"type":"zero"}')
+            cattrs = dict(attrs[cnode])
+            if cnode != n:  # data-input feature sizes (physical weight layouts depend on them)
+                cattrs["_in_features"] = [int(pcg.shape(C.ValueRef(v.node, v.idx)).shard_dims[-1].size)
+                                          for v in pcg.layer_data_inputs(cnode)]
             piece = ParamPiece(name=names[n] or f"weight_{n}", node=n, terminal=t, layout=lay,
                                logical_shape=tuple(lay.sizes), initializer=init, group=(), trainable=bool(
                                    pcg.create_grad(C.ValueRef(n, 0))),
-                               consumer_op=optype[cnode], consumer_attrs=attrs[cnode])
+                               consumer_op=optype[cnode], consumer_attrs=cattrs)
             self.params.append(piece)
             self.param_of_value[t] = piece
             folded.add(n)
@@ -447,11 +451,29 @@ class Executor:
                     return i
         return 0
 
+    def _impl_of(self, p: ParamPiece):
+        try:
+            return opbase.get_impl(p.consumer_op)
+        except NotImplementedError:
+            return None
+
+    def _to_physical(self, p: ParamPiece, piece: torch.Tensor) -> torch.Tensor:
+        impl = self._impl_of(p)
+        if impl is None:
+            return piece
+        return impl.to_physical(p.consumer_attrs, self._weight_index(p), piece).reshape(piece.shape)
+
+    def _to_logical(self, p: ParamPiece, piece: torch.Tensor) -> torch.Tensor:
+        impl = self._impl_of(p)
+        if impl is None:
+            return piece
+        return impl.to_logical(p.consumer_attrs, self._weight_index(p), piece).reshape(piece.shape)
+
     def _set_piece(self, p: ParamPiece, full: torch.Tensor):
         c = p.layout.coord(self.rank)
         box = p.layout.box(c.shard)
         sl = tuple(slice(lo, hi) for lo, hi in box)
-        p.master.copy_(full.reshape(p.logical_shape)[sl].to(torch.float32))
+        p.master.copy_(self._to_physical(p, full.reshape(p.logical_shape)[sl].to(torch.float32)))
         if p.compute is not p.master:
             p.compute.copy_(p.master)
 
@@ -463,7 +485,7 @@ class Executor:
         owner = c is not None and c.b == 0 and c.rep == 0 and c.a == 0
         if owner:
             box = p.layout.box(c.shard)
-            full[tuple(slice(lo, hi) for lo, hi in box)] = p.master
+            full[tuple(slice(lo, hi) for lo, hi in box)] = self._to_logical(p, p.master)
         if self.dist.distributed:
             import torch.distributed as dist
             dist.all_reduce(full)
@@ -704,9 +726,15 @@ class Executor:
         self.step_num += 1
 
     def grad_norm(self) -> float:
+        # every logical gradient element counted once: only the canonical
+        # owner (copy 0, partial replica 0, implicit replica 0) of each shard
         tot = torch.zeros(1, device=self.cfg.device, dtype=torch.float64)
-        for f in self.flats:
-            tot += f["grad"].double().pow(2).sum()
+        for p in self.params:
+            if not p.group or p.grad is None:
+                continue
+            c = p.layout.coord(self.rank)
+            if c is not None and c.b == 0 and c.a == 0 and c.rep == 0:
+                tot += p.grad.double().pow(2).sum()
         if self.dist.distributed:
             import torch.distributed as dist
             dist.all_reduce(tot)
@@ -753,7 +781,7 @@ class Executor:
         for p in self.params:
             if p.group:
                 c = p.layout.coord(self.rank)
-                st["params"][p.name] = {"tensor": p.master.detach().cpu().clone(),
+                st["params"][p.name] = {"tensor": self._to_logical(p, p.master).detach().cpu().clone(),
                                         "box": p.layout.box(c.shard), "logical_shape": p.logical_shape}
         for f in self.flats:
             st["optimizer"].append({"step": f["opt"].step_num,
@@ -763,7 +791,7 @@ class Executor:
     def load_state_dict(self, st: Dict[str, Any]):
         for p in self.params:
             if p.group and p.name in st["params"]:
-                p.master.copy_(st["params"][p.name]["tensor"].to(p.master.device))
+                p.master.copy_(self._to_physical(p, st["params"][p.name]["tensor"].to(p.master.device)))
                 if p.compute is not p.master:
                     p.compute.copy_(p.master)
         for f, o in zip(self.flats, st.get("optimizer", [])):

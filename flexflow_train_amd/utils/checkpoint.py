@@ -1,0 +1,84 @@
+"""Checkpoint / resume.
+
+Reference: the legacy runtime has no real checkpointing (SURVEY §5.4 —
+only Tensor.get_tensor/set_tensor round-trips and the strategy file); this
+module provides sharded checkpoints for the per-rank executor:
+
+* ``save_checkpoint(model, dir)``: every rank writes ``rank<r>.pt`` holding
+  its LOGICAL weight pieces (with their boxes in the full tensor) and its
+  flat optimizer state; rank 0 writes ``meta.json`` (world, step, strategy
+  fingerprint, parameter shapes).  Files are written with ``torch.save`` of
+  plain tensors/dicts and read back with ``weights_only=True``.
+* ``load_checkpoint(model, dir)``: same world + same strategy -> exact resume
+  (weights + optimizer state + step).  Different world or strategy -> the
+  full logical weights are reassembled from every rank's boxes and
+  re-sliced for the new layout (optimizer state restarts).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict
+
+import torch
+
+
+def _fingerprint(ex) -> str:
+    return str(ex.pcg.structural_hash()) + "@" + str(ex.world) + ":" + json.dumps(
+        sorted((int(k), list(v)) for k, v in ex.views.items()))
+
+
+def save_checkpoint(model, path: str):
+    ex = model.executor if hasattr(model, "executor") else model
+    os.makedirs(path, exist_ok=True)
+    st = ex.state_dict()
+    torch.save(st, os.path.join(path, f"rank{ex.rank}.pt"))
+    if ex.rank == 0:
+        meta = {"format": "ffmi355x.checkpoint.v1", "world": ex.world, "step": ex.step_num,
+                "fingerprint": _fingerprint(ex),
+                "params": {p.name: list(p.logical_shape) for p in ex.params}}
+        with open(os.path.join(path, "meta.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+    ex.dist.barrier()
+
+
+def _assemble_full(path: str, world: int) -> Dict[str, torch.Tensor]:
+    full: Dict[str, torch.Tensor] = {}
+    for r in range(world):
+        f = os.path.join(path, f"rank{r}.pt")
+        if not os.path.exists(f):
+            continue
+        st = torch.load(f, map_location="cpu", weights_only=True)
+        for name, rec in st["params"].items():
+            t = full.get(name)
+            if t is None:
+                t = full[name] = torch.zeros(tuple(rec["logical_shape"]), dtype=torch.float32)
+            box = tuple(slice(lo, hi) for lo, hi in rec["box"])
+            t[box] = rec["tensor"].reshape(t[box].shape)
+    return full
+
+
+def load_checkpoint(model, path: str, strict: bool = True):
+    ex = model.executor if hasattr(model, "executor") else model
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("format") != "ffmi355x.checkpoint.v1":
+        raise ValueError(f"{path}: not a checkpoint")
+    same = meta["world"] == ex.world and meta["fingerprint"] == _fingerprint(ex)
+    if same and os.path.exists(os.path.join(path, f"rank{ex.rank}.pt")):
+        st = torch.load(os.path.join(path, f"rank{ex.rank}.pt"), map_location="cpu", weights_only=True)
+        ex.load_state_dict(st)
+    else:
+        full = _assemble_full(path, meta["world"])
+        names = set(ex.parameter_names())
+        missing = names - set(full)
+        if strict and missing:
+            raise KeyError(f"checkpoint lacks parameters: {sorted(missing)}")
+        for n in names & set(full):
+            ex.set_parameter(n, full[n])
+        for p in ex.params:
+            if p.group and p.compute is not p.master:
+                p.compute.copy_(p.master)
+        ex.step_num = int(meta.get("step", 0))
+    ex.dist.barrier()
+    return meta

@@ -1,0 +1,54 @@
+"""Small models used by the multi-process strategy-equivalence tests.
+Each function builds the model into an FFModel and returns (feeds, labels)
+as GLOBAL tensors (every rank slices its own piece)."""
+import torch
+
+from flexflow_train_amd.core import ActiMode, AggrMode, DataType
+
+
+def mlp(m):
+    x = m.create_tensor([16, 32], DataType.DT_FLOAT, name="x")
+    t = m.dense(x, 64, ActiMode.AC_MODE_RELU, name="fc0")
+    t = m.dense(t, 48, name="fc1")
+    t = m.relu(t, name="act1")
+    t = m.dense(t, 8, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(7)
+    return {"x": torch.randn(16, 32, generator=g)}, torch.randint(0, 8, (16,), generator=g)
+
+
+def attention(m):
+    B, S, E = 4, 8, 32
+    x = m.create_tensor([B, S, E], DataType.DT_FLOAT, name="x")
+    a = m.multihead_attention(x, x, x, E, 4, name="mha")
+    t = m.add(a, x, name="res")
+    t = m.layer_norm(t, [-1], name="ln")
+    t = m.dense(t, 10, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(11)
+    return {"x": torch.randn(B, S, E, generator=g)}, torch.randint(0, 10, (B, S), generator=g)
+
+
+def embedding(m):
+    B, S, V, E = 4, 6, 50, 16
+    ids = m.create_tensor([B, S], DataType.DT_INT32, create_grad=False, name="ids")
+    t = m.embedding(ids, V, E, AggrMode.AGGR_MODE_NONE, name="emb")
+    t = m.dense(t, 12, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(5)
+    return ({"ids": torch.randint(0, V, (B, S), generator=g, dtype=torch.int32)},
+            torch.randint(0, 12, (B, S), generator=g))
+
+
+def bert_tiny(m):
+    from flexflow_train_amd.models.bert import BertConfig, build_bert
+
+    cfg = BertConfig(vocab_size=64, hidden_size=32, num_heads=4, dim_feedforward=64, num_encoder_layers=2,
+                     sequence_length=8, batch_size=4, max_position_embeddings=8, type_vocab_size=2)
+    build_bert(m, cfg)
+    g = torch.Generator().manual_seed(3)
+    B, S = 4, 8
+    feeds = {"input_ids": torch.randint(0, 64, (B, S), generator=g, dtype=torch.int32),
+             "position_ids": torch.arange(S, dtype=torch.int32).expand(B, S).contiguous(),
+             "token_type_ids": torch.randint(0, 2, (B, S), generator=g, dtype=torch.int32)}
+    return feeds, torch.randint(0, 64, (B, S), generator=g)

@@ -1,0 +1,100 @@
+"""Multi-process CPU harness: run the same model under a strategy on W gloo
+ranks and compare against the single-process run (reference: the CI's
+multi_gpu_tests.sh ran examples under DP / searched strategies and checked
+they train; here numerics are compared parameter by parameter)."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import tempfile
+from typing import Callable, Dict, Optional
+
+import torch
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _train(model_fn: Callable, strategy_file: Optional[str], steps: int, seed: int, optimizer: str = "sgd"):
+    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
+
+    cfg = FFConfig()
+    cfg.seed = seed
+    if strategy_file:
+        cfg.import_strategy_file = strategy_file
+    else:
+        cfg.only_data_parallel = True
+    model = FFModel(cfg)
+    feeds, labels = model_fn(model)
+    opt = SGDOptimizer(model, lr=0.05) if optimizer == "sgd" else AdamOptimizer(model, alpha=1e-3)
+    model.compile(optimizer=opt, loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY])
+    ex = model.executor
+    g = torch.Generator().manual_seed(seed)
+    for name in sorted(ex.parameter_names()):
+        full = ex.get_parameter(name)
+        ex.set_parameter(name, torch.randn(full.shape, generator=g) * 0.2)
+    losses = []
+    for _ in range(steps):
+        ex.train_step(feeds, labels)
+        losses.append(float(ex.perf_metrics().loss) if hasattr(ex.perf_metrics(), "loss") else 0.0)
+    params = {n: ex.get_parameter(n).detach().cpu().clone() for n in sorted(ex.parameter_names())}
+    return params, ex
+
+
+def _worker(rank, world, port, model_fn, strategy_file, steps, seed, out_path, optimizer):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    params, ex = _train(model_fn, strategy_file, steps, seed, optimizer)
+    if rank == 0:
+        torch.save({"params": params, "stats": dict(ex.dist.stats)}, out_path)
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_distributed(model_fn: Callable, world: int, strategy_file: Optional[str] = None, steps: int = 2,
+                    seed: int = 0, optimizer: str = "sgd") -> Dict:
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.start_processes(_worker, args=(world, free_port(), model_fn, strategy_file, steps, seed, out, optimizer),
+                           nprocs=world, join=True, start_method="spawn")
+        return torch.load(out, weights_only=True)
+
+
+def run_single(model_fn: Callable, steps: int = 2, seed: int = 0, optimizer: str = "sgd") -> Dict:
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    params, ex = _train(model_fn, None, steps, seed, optimizer)
+    return {"params": params}
+
+
+def write_strategy(model_fn: Callable, world: int, overrides: Dict[str, dict], path: str):
+    """Lower the data-parallel strategy with per-layer overrides and export
+    it as a strategy file the FFModel can --import."""
+    from flexflow_train_amd import _ffcore as C
+    from flexflow_train_amd.core import FFConfig, FFModel
+    from flexflow_train_amd.search.strategy import export_strategy
+
+    m = FFModel(FFConfig())
+    model_fn(m)
+    s = json.loads(C.data_parallel_strategy(m.cg, world))
+    for k, v in overrides.items():
+        assert k in s, f"no layer {k}: {sorted(s)}"
+        s[k] = v
+    pcg, mapping, n = C.lower_strategy(m.cg, json.dumps(s), world)
+    export_strategy(path, pcg, {}, {"world": world, "source": "test"})
+    return pcg
+
+
+def assert_params_close(a: Dict, b: Dict, rtol=2e-4, atol=2e-5):
+    assert sorted(a) == sorted(b), (sorted(a), sorted(b))
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=rtol, atol=atol, msg=lambda m: f"{k}: {m}")

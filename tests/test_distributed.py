@@ -1,0 +1,58 @@
+"""Strategy equivalence on CPU: data parallel, Megatron-style tensor
+parallel, attention-head parallel and embedding channel parallel, run on
+2 gloo ranks, must match the single-process run parameter for parameter."""
+import os
+
+import pytest
+
+import dist_models as M
+from dist_util import assert_params_close, run_distributed, run_single, write_strategy
+
+
+@pytest.fixture(scope="module")
+def ref_mlp():
+    return run_single(M.mlp)
+
+
+def test_mlp_data_parallel(ref_mlp):
+    out = run_distributed(M.mlp, 2)
+    assert_params_close(out["params"], ref_mlp["params"])
+
+
+def test_mlp_tensor_parallel(tmp_path, ref_mlp):
+    path = str(tmp_path / "tp.json")
+    write_strategy(M.mlp, 2, {"fc0": {"batch": 1, "model": 2, "kind": "column"},
+                              "fc1": {"batch": 1, "model": 2, "kind": "row"}}, path)
+    out = run_distributed(M.mlp, 2, path)
+    assert_params_close(out["params"], ref_mlp["params"])
+
+
+def test_mlp_column_then_dp_mix(tmp_path, ref_mlp):
+    path = str(tmp_path / "mix.json")
+    write_strategy(M.mlp, 2, {"out": {"batch": 1, "model": 2, "kind": "column"}}, path)
+    out = run_distributed(M.mlp, 2, path)
+    assert_params_close(out["params"], ref_mlp["params"])
+
+
+def test_attention_head_parallel(tmp_path):
+    ref = run_single(M.attention)
+    path = str(tmp_path / "heads.json")
+    write_strategy(M.attention, 2, {"mha": {"batch": 1, "model": 2, "kind": "heads"}}, path)
+    out = run_distributed(M.attention, 2, path)
+    assert_params_close(out["params"], ref["params"])
+    dp = run_distributed(M.attention, 2)
+    assert_params_close(dp["params"], ref["params"])
+
+
+def test_embedding_channel_parallel(tmp_path):
+    ref = run_single(M.embedding)
+    path = str(tmp_path / "emb.json")
+    write_strategy(M.embedding, 2, {"emb": {"batch": 1, "model": 2, "kind": "column"}}, path)
+    out = run_distributed(M.embedding, 2, path)
+    assert_params_close(out["params"], ref["params"])
+
+
+def test_bert_tiny_data_parallel_adam():
+    ref = run_single(M.bert_tiny, optimizer="adam")
+    out = run_distributed(M.bert_tiny, 2, optimizer="adam")
+    assert_params_close(out["params"], ref["params"], rtol=1e-3, atol=1e-4)
