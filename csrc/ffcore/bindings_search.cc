@@ -7,6 +7,7 @@
 
 #include "bindings_ext.h"
 #include "ff/mapping.h"
+#include "ff/models.h"
 #include "ff/parallelize.h"
 #include "ff/search.h"
 #include "ff/simulator.h"
@@ -275,6 +276,12 @@ void register_ext_bindings(py::module_& m) {
         return py::cast(*s);
       });
   m.def("load_legacy_rules", [](const std::string& s) { return load_legacy_rules(Json::parse(s)); });
+
+  // ---- model zoo (C++ CG builders)
+  m.def("model_names", &model_names);
+  m.def("get_model_computation_graph", [](const std::string& name, const std::string& cfg) {
+    return get_model_computation_graph(name, cfg.empty() ? Json::object() : Json::parse(cfg));
+  }, py::arg("name"), py::arg("config") = "");
 
   // ---- search
   m.def("mcmc_search", [](const ComputationGraph& cg, const CostModel& cm, const std::string& cfg) {

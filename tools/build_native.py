@@ -96,6 +96,21 @@ def write_ninja(targets: list[str]) -> str:
         out = os.path.join(PKG, "_ffkernels" + EXT)
         lines.append(f"build {out}: link_hip {' '.join(objs)}")
         defaults.append(out)
+    if "tools" in targets:
+        # native CLIs (bin/): export-model-arch, substitution-to-dot, protobuf-to-json
+        lines += ["rule link_exe", "  command = $cxx -o $out $in -lpthread", "  description = LINK $out"]
+        core_objs = []
+        for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "ffcore", "src", "*.cc"))):
+            o = os.path.join("obj", "core", os.path.basename(s) + ".o")
+            if "core" not in targets:
+                lines.append(f"build {o}: cxx {s}")
+            core_objs.append(o)
+        for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "tools", "*.cc"))):
+            o = os.path.join("obj", "tools", os.path.basename(s) + ".o")
+            lines.append(f"build {o}: cxx {s}")
+            exe = os.path.join(ROOT, "bin", "ffc-" + os.path.basename(s)[:-3].replace("_", "-"))
+            lines.append(f"build {exe}: link_exe {o} {' '.join(core_objs)}")
+            defaults.append(exe)
     lines.append("default " + " ".join(defaults))
     os.makedirs(BUILD, exist_ok=True)
     path = os.path.join(BUILD, "build.ninja")
@@ -108,7 +123,7 @@ def write_ninja(targets: list[str]) -> str:
 
 
 def build(targets: list[str] | None = None, jobs: int | None = None, verbose: bool = False) -> None:
-    targets = targets or ["core", "kernels"]
+    targets = targets or ["core", "kernels", "tools"]
     write_ninja(targets)
     ninja = shutil.which("ninja")
     if ninja is None:
