@@ -1,0 +1,2 @@
+"""flexflow.torch (reference: python/flexflow/torch)."""
+from flexflow_train_amd.frontends.torch_fx import (PyTorchModel, copy_weights, string_to_ff)  # noqa: F401

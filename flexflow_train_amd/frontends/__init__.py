@@ -1,0 +1,1 @@
+"""User-facing frontends: PyTorch (torch.fx + .ff IR), Keras-style, ONNX."""

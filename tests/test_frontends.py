@@ -1,0 +1,133 @@
+"""Frontends: torch.fx importer (+ .ff round trip, numerics vs torch),
+Keras-style API, ONNX importer (wire-format reader/writer)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from flexflow.core import DataType, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+from flexflow.torch.model import PyTorchModel, copy_weights, file_to_ff
+
+
+class SmallCNN(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 8, 3, 1, 1)
+        self.pool = nn.MaxPool2d(2, 2)
+        self.fc1 = nn.Linear(8 * 4 * 4, 32)
+        self.fc2 = nn.Linear(32, 10)
+
+    def forward(self, x):
+        x = self.pool(torch.relu(self.conv(x)))
+        x = torch.flatten(x, 1)
+        x = torch.relu(self.fc1(x)) * 0.5 + 1.0
+        return torch.softmax(self.fc2(x), dim=-1)
+
+
+class TinyAttn(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.attn = nn.MultiheadAttention(16, 4, batch_first=True)
+        self.ln = nn.LayerNorm(16)
+        self.out = nn.Linear(16, 5)
+
+    def forward(self, x):
+        a = self.attn(x, x, x)[0]
+        return torch.softmax(self.out(self.ln(a + x)), dim=-1)
+
+
+def _compile(m):
+    m.compile(optimizer=SGDOptimizer(m, lr=0.0), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_ACCURACY])
+    return m
+
+
+@pytest.mark.parametrize("mode", ["memory", "file"])
+def test_torch_import_matches_torch(tmp_path, mode):
+    torch.manual_seed(0)
+    net = SmallCNN().eval()
+    pm = PyTorchModel(net)
+    ff = FFModel(FFConfig())
+    x = ff.create_tensor([4, 3, 8, 8], DataType.DT_FLOAT, name="x")
+    if mode == "memory":
+        pm.torch_to_ff(ff, [x])
+    else:
+        path = str(tmp_path / "m.ff")
+        pm.torch_to_file(path)
+        text = open(path).read()
+        assert "; LINEAR; 32; 10; 1" in text and "; CONV2D; 8; 3; 3; 1; 1; 1; 1; 10; 1; 1" in text
+        file_to_ff(path, ff, [x])
+    _compile(ff)
+    copy_weights(ff, pm.weights())
+    inp = torch.randn(4, 3, 8, 8)
+    out = ff.executor.forward({"x": inp}, training=False)
+    torch.testing.assert_close(out.float(), net(inp), rtol=1e-4, atol=1e-5)
+
+
+def test_torch_import_attention_matches_torch():
+    torch.manual_seed(1)
+    net = TinyAttn().eval()
+    ff = FFModel(FFConfig())
+    x = ff.create_tensor([2, 6, 16], DataType.DT_FLOAT, name="x")
+    pm = PyTorchModel(net)
+    pm.torch_to_ff(ff, [x])
+    _compile(ff)
+    copy_weights(ff)
+    inp = torch.randn(2, 6, 16)
+    out = ff.executor.forward({"x": inp}, training=False)
+    torch.testing.assert_close(out.float(), net(inp), rtol=1e-4, atol=1e-5)
+
+
+def test_keras_sequential_learns_synthetic_mnist():
+    from flexflow.keras import Sequential, datasets
+    from flexflow.keras.layers import Dense, Flatten
+    from flexflow.keras.optimizers import SGD
+
+    (xt, yt), _ = datasets.mnist.load_data(num_samples=1024)
+    xt = (xt.astype(np.float32) / 255.0)
+    model = Sequential([Flatten(input_shape=(28, 28)), Dense(64, activation="relu"), Dense(10, activation="softmax")])
+    model.compile(optimizer=SGD(learning_rate=0.1), loss="sparse_categorical_crossentropy", metrics=["accuracy"])
+    hist = model.fit(xt, yt.astype(np.int32), batch_size=64, epochs=3)
+    assert hist["history"][-1]["accuracy"] > 0.9
+
+
+def test_keras_functional_concat_cnn():
+    from flexflow.keras import Input, Model
+    from flexflow.keras.layers import Concatenate, Conv2D, Dense, Flatten, MaxPooling2D
+
+    inp = Input((3, 8, 8))
+    a = MaxPooling2D()(Conv2D(4, 3, padding="same", activation="relu")(inp))
+    b = MaxPooling2D()(Conv2D(4, 1, activation="relu")(inp))
+    t = Dense(5, activation="softmax")(Flatten()(Concatenate(axis=1)([a, b])))
+    model = Model(inp, t)
+    model.compile(optimizer="sgd", loss="sparse_categorical_crossentropy", metrics=["accuracy"])
+    x = np.random.default_rng(0).standard_normal((32, 3, 8, 8)).astype(np.float32)
+    y = np.random.default_rng(1).integers(0, 5, 32).astype(np.int32)
+    model.fit(x, y, batch_size=16, epochs=1)
+    assert "Conv2D" in model.summary()
+
+
+def test_onnx_import_roundtrip():
+    from flexflow.onnx.model import Node, ONNXModel, encode_model
+
+    rng = np.random.default_rng(0)
+    W1 = rng.standard_normal((16, 32)).astype(np.float32)
+    b1 = rng.standard_normal(32).astype(np.float32)
+    W2 = rng.standard_normal((10, 32)).astype(np.float32)   # transB
+    b2 = rng.standard_normal(10).astype(np.float32)
+    nodes = [Node("Gemm", ["x", "W1", "b1"], ["h"], "fc1"), Node("Relu", ["h"], ["r"], "relu"),
+             Node("Gemm", ["r", "W2", "b2"], ["z"], "fc2", {"transB": 1}),
+             Node("Softmax", ["z"], ["y"], "sm", {"axis": -1})]
+    blob = encode_model(nodes, {"W1": W1, "b1": b1, "W2": W2, "b2": b2}, [("x", [8, 16])], [("y", [8, 10])])
+    om = ONNXModel(blob)
+    ff = FFModel(FFConfig())
+    x = ff.create_tensor([8, 16], DataType.DT_FLOAT, name="x")
+    om.apply(ff, [x])
+    _compile(ff)
+    om.copy_weights(ff)
+    xin = rng.standard_normal((8, 16)).astype(np.float32)
+    out = ff.executor.forward({"x": torch.as_tensor(xin)}, training=False).numpy()
+    z = np.maximum(xin @ W1 + b1, 0) @ W2.T + b2
+    ref = np.exp(z - z.max(-1, keepdims=True))
+    ref /= ref.sum(-1, keepdims=True)
+    np.testing.assert_allclose(out, ref, rtol=1e-4, atol=1e-5)
