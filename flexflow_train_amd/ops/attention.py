@@ -46,7 +46,10 @@ def _split_weights(W, E, Hl, kd, vd, Eq, Ek, Ev):
         n_qkv = Eq * 3 * Hl * kd
         Wqkv = flat[:n_qkv].view(Eq, 3 * Hl * kd)
         Wo = flat[n_qkv:n_qkv + Hl * vd * E].view(Hl * vd, E)
-        return {"qkv": Wqkv, "o": Wo}
+        # per-projection strided views of the fused operand, for attention whose
+        # q / k / v are different tensors of the same width (cross-attention)
+        W3 = Wqkv.view(Eq, 3, Hl * kd)
+        return {"qkv": Wqkv, "o": Wo, "q": W3[:, 0], "k": W3[:, 1], "v": W3[:, 2]}
     o0 = 0
     Wq = flat[o0:o0 + Eq * Hl * kd].view(Eq, Hl * kd)
     o0 += Eq * Hl * kd

@@ -38,12 +38,28 @@ def machine_spec(ffconfig=None, world: Optional[int] = None):
     return spec
 
 
-def cost_model(ffconfig=None, world: Optional[int] = None):
+PROFILE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                           "profiles")
+
+
+def cost_model(ffconfig=None, world: Optional[int] = None, use_profiles: bool = True):
+    """Analytic MI355X model + measured op costs.  Tables: ``FF_PROFILE_TABLE``
+    (os.pathsep-separated), ``ffconfig.profile_table_file``, and every
+    committed ``profiles/op_costs_*.json`` (keys are exact op/piece
+    signatures, so tables for different models/worlds merge safely)."""
     cm = C.CostModel(machine_spec(ffconfig, world))
-    path = os.environ.get("FF_PROFILE_TABLE") or (getattr(ffconfig, "profile_table_file", "") if ffconfig else "")
-    if path and os.path.exists(path):
-        with open(path) as f:
-            cm.load_profiles(f.read())
+    if not use_profiles or os.environ.get("FF_NO_PROFILE_TABLES"):
+        return cm
+    paths = [p for p in os.environ.get("FF_PROFILE_TABLE", "").split(os.pathsep) if p]
+    if ffconfig is not None and getattr(ffconfig, "profile_table_file", ""):
+        paths.append(ffconfig.profile_table_file)
+    if os.path.isdir(PROFILE_DIR):
+        paths += sorted(os.path.join(PROFILE_DIR, f) for f in os.listdir(PROFILE_DIR)
+                        if f.startswith("op_costs_") and f.endswith(".json"))
+    for path in paths:
+        if os.path.exists(path):
+            with open(path) as f:
+                cm.load_profiles(f.read())
     return cm
 
 

@@ -78,6 +78,29 @@ def test_torch_import_attention_matches_torch():
     torch.testing.assert_close(out.float(), net(inp), rtol=1e-4, atol=1e-5)
 
 
+class TinyCross(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.attn = nn.MultiheadAttention(16, 2, batch_first=True)
+
+    def forward(self, q, kv):
+        return torch.softmax(self.attn(q, kv, kv)[0], dim=-1)
+
+
+def test_torch_import_cross_attention_matches_torch():
+    torch.manual_seed(2)
+    net = TinyCross().eval()
+    ff = FFModel(FFConfig())
+    q = ff.create_tensor([2, 5, 16], DataType.DT_FLOAT, name="q")
+    kv = ff.create_tensor([2, 7, 16], DataType.DT_FLOAT, name="kv")
+    PyTorchModel(net).torch_to_ff(ff, [q, kv])
+    _compile(ff)
+    copy_weights(ff)
+    a, b = torch.randn(2, 5, 16), torch.randn(2, 7, 16)
+    out = ff.executor.forward({"q": a, "kv": b}, training=False)
+    torch.testing.assert_close(out.float(), net(a, b), rtol=1e-4, atol=1e-5)
+
+
 def test_keras_sequential_learns_synthetic_mnist():
     from flexflow.keras import Sequential, datasets
     from flexflow.keras.layers import Dense, Flatten
