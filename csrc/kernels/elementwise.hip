@@ -9,6 +9,9 @@
 // the bias gradient are one pass (column sums kept in registers across rows,
 // then an LDS reduce over the block and one fp32 atomic per column);
 // dropout regenerates its mask from a counter hash instead of storing it.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -20,7 +23,7 @@ __device__ __forceinline__ float act_apply(int op, float x, float alpha) {
   switch (op) {
     case kRelu: return x > 0.f ? x : 0.f;
     case kSigmoid: return 1.f / (1.f + __expf(-x));
-    case kTanh: return tanhf(x);
+    case kTanh: return fast_tanh(x);
     case kGelu: return gelu_tanh(x);
     case kElu: return x > 0.f ? x : alpha * (__expf(x) - 1.f);
     case kExp: return __expf(x);
@@ -36,7 +39,7 @@ __device__ __forceinline__ float act_grad(int op, float x, float alpha) {
       return s * (1.f - s);
     }
     case kTanh: {
-      float t = tanhf(x);
+      float t = fast_tanh(x);
       return 1.f - t * t;
     }
     case kGelu: return gelu_tanh_grad(x);
@@ -86,10 +89,11 @@ __device__ __forceinline__ void st8<float>(float* p, const float* o) {
 
 // ---------------------------------------------------------------------------
 // y = act(x [+ bias]); optionally pre = x + bias.  x: [M, N] row-major; n8 = M*N/8.
-template <typename T>
+template <typename T, int OP>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__ x, const T* __restrict__ bias,
                                                            T* __restrict__ pre, T* __restrict__ y, int64_t n8,
-                                                           int N, int op, float alpha) {
+                                                           int N, float alpha) {
+  constexpr int op = OP;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
     float v[8];
     ld8<T>(x + i * 8, v);
@@ -107,9 +111,10 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__
 }
 
 // dx = dy * act'(pre).  Element-wise (no bias grad).
-template <typename T>
+template <typename T, int OP>
 __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ pre,
-                                                      T* __restrict__ dx, int64_t n8, int op, float alpha) {
+                                                      T* __restrict__ dx, int64_t n8, float alpha) {
+  constexpr int op = OP;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
     float d[8], p[8];
     ld8<T>(dy + i * 8, d);
@@ -123,10 +128,11 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const T* __restrict__ dy, 
 // Column-sum (bias gradient), optionally fused with the activation backward:
 //   g = dy * act'(pre) (if pre) ; dx = g (if dx) ; dbias += sum_rows g
 // grid = (ceil(N/512), row_splits); block = 4 waves over the same 512 columns.
-template <typename T>
+template <typename T, int OP>
 __global__ __launch_bounds__(256) void colsum_act_kernel(const T* __restrict__ dy, const T* __restrict__ pre,
                                                          T* __restrict__ dx, float* __restrict__ dbias, int M,
-                                                         int N, int op, float alpha) {
+                                                         int N, float alpha) {
+  constexpr int op = OP;  // compile-time activation: no per-element switch
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.x * 512 + lane * 8;
@@ -137,12 +143,12 @@ __global__ __launch_bounds__(256) void colsum_act_kernel(const T* __restrict__ d
   const int rows_per = (M + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(M, r0 + rows_per);
+  constexpr int U = 8;  // rows in flight per wave: 8 x 16 B (x2 with pre) per lane
   if (active) {
-    // 4 rows per wave per iteration: all loads issued before any use
-    for (int r = r0 + wave; r < r1; r += 16) {
-      float d[4][8], p[4][8];
+    for (int r = r0 + wave; r < r1; r += 4 * U) {
+      float d[U][8], p[U][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int rr = r + 4 * u;
         if (rr < r1) {
           const size_t off = static_cast<size_t>(rr) * N + col;
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(256) void colsum_act_kernel(const T* __restrict__ d
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int rr = r + 4 * u;
         if (pre)
 #pragma unroll
@@ -219,33 +225,54 @@ static void need8(int64_t n, const char* what) {
   if (n % 8 != 0) throw std::invalid_argument(std::string(what) + ": element count must be a multiple of 8");
 }
 
+// op code -> compile-time constant (one kernel instantiation per activation)
+template <typename F>
+static void dispatch_act(int op, F&& f) {
+  switch (op) {
+    case kIdentity: f(std::integral_constant<int, kIdentity>{}); break;
+    case kRelu: f(std::integral_constant<int, kRelu>{}); break;
+    case kSigmoid: f(std::integral_constant<int, kSigmoid>{}); break;
+    case kTanh: f(std::integral_constant<int, kTanh>{}); break;
+    case kGelu: f(std::integral_constant<int, kGelu>{}); break;
+    case kElu: f(std::integral_constant<int, kElu>{}); break;
+    case kExp: f(std::integral_constant<int, kExp>{}); break;
+    default: throw std::invalid_argument("unknown activation code");
+  }
+}
+
 void bias_act_fwd(int dtype, const void* x, const void* bias, void* pre, void* y, int64_t M, int64_t N, int op,
                   float alpha, hipStream_t st) {
   need8(N, "bias_act_fwd");
   int64_t n8 = M * N / 8;
   int grid = grid_for(n8, 256, 256 * 8);
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(bias_act_fwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(x),
-                       static_cast<const bf16*>(bias), static_cast<bf16*>(pre), static_cast<bf16*>(y), n8,
-                       static_cast<int>(N), op, alpha);
-  else if (dtype == kF32)
-    hipLaunchKernelGGL(bias_act_fwd_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(x),
-                       static_cast<const float*>(bias), static_cast<float*>(pre), static_cast<float*>(y), n8,
-                       static_cast<int>(N), op, alpha);
-  else throw std::invalid_argument("bias_act_fwd: dtype");
+  dispatch_act(op, [&](auto opc) {
+    constexpr int OPC = decltype(opc)::value;
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((bias_act_fwd_kernel<bf16, OPC>), dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(x),
+                         static_cast<const bf16*>(bias), static_cast<bf16*>(pre), static_cast<bf16*>(y), n8,
+                         static_cast<int>(N), alpha);
+    else if (dtype == kF32)
+      hipLaunchKernelGGL((bias_act_fwd_kernel<float, OPC>), dim3(grid), dim3(256), 0, st,
+                         static_cast<const float*>(x), static_cast<const float*>(bias), static_cast<float*>(pre),
+                         static_cast<float*>(y), n8, static_cast<int>(N), alpha);
+    else throw std::invalid_argument("bias_act_fwd: dtype");
+  });
   FFK_LAUNCH_CHECK("bias_act_fwd");
 }
 
 void act_bwd(int dtype, const void* dy, const void* pre, void* dx, int64_t n, int op, float alpha, hipStream_t st) {
   need8(n, "act_bwd");
   int grid = grid_for(n / 8, 256, 256 * 8);
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(act_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(dy),
-                       static_cast<const bf16*>(pre), static_cast<bf16*>(dx), n / 8, op, alpha);
-  else if (dtype == kF32)
-    hipLaunchKernelGGL(act_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, static_cast<const float*>(dy),
-                       static_cast<const float*>(pre), static_cast<float*>(dx), n / 8, op, alpha);
-  else throw std::invalid_argument("act_bwd: dtype");
+  dispatch_act(op, [&](auto opc) {
+    constexpr int OPC = decltype(opc)::value;
+    if (dtype == kBF16)
+      hipLaunchKernelGGL((act_bwd_kernel<bf16, OPC>), dim3(grid), dim3(256), 0, st, static_cast<const bf16*>(dy),
+                         static_cast<const bf16*>(pre), static_cast<bf16*>(dx), n / 8, alpha);
+    else if (dtype == kF32)
+      hipLaunchKernelGGL((act_bwd_kernel<float, OPC>), dim3(grid), dim3(256), 0, st, static_cast<const float*>(dy),
+                         static_cast<const float*>(pre), static_cast<float*>(dx), n / 8, alpha);
+    else throw std::invalid_argument("act_bwd: dtype");
+  });
   FFK_LAUNCH_CHECK("act_bwd");
 }
 
@@ -253,16 +280,33 @@ void colsum_act(int dtype, const void* dy, const void* pre, void* dx, float* dbi
                 float alpha, hipStream_t st) {
   need8(N, "colsum_act");
   int gx = static_cast<int>((N + 511) / 512);
-  // enough row splits to put ~4 blocks per CU on the chip
-  int gy = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (M + 15) / 16)));
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(colsum_act_kernel<bf16>, dim3(gx, gy), dim3(256), 0, st, static_cast<const bf16*>(dy),
-                       static_cast<const bf16*>(pre), static_cast<bf16*>(dx), dbias, static_cast<int>(M),
-                       static_cast<int>(N), op, alpha);
-  else if (dtype == kF32)
-    hipLaunchKernelGGL(colsum_act_kernel<float>, dim3(gx, gy), dim3(256), 0, st, static_cast<const float*>(dy),
-                       static_cast<const float*>(pre), static_cast<float*>(dx), dbias, static_cast<int>(M),
-                       static_cast<int>(N), op, alpha);
+  // row splits: ~FFK_COLSUM_BLOCKS blocks in total (default 4 per CU) and at
+  // least 64 rows per block, so every wave streams >= 2 pipelined batches
+  static const int64_t target = [] {
+    const char* e = std::getenv("FFK_COLSUM_BLOCKS");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1024);
+  }();
+  int gy = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((target + gx - 1) / gx, (M + 63) / 64)));
+  if (!pre) op = kIdentity;
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(gx, gy), dim3(256), 0, st, static_cast<const T*>(dy), static_cast<const T*>(pre),
+                         static_cast<T*>(dx), dbias, static_cast<int>(M), static_cast<int>(N), alpha);
+    };
+    switch (op) {
+      case kIdentity: go(colsum_act_kernel<T, kIdentity>); break;
+      case kRelu: go(colsum_act_kernel<T, kRelu>); break;
+      case kSigmoid: go(colsum_act_kernel<T, kSigmoid>); break;
+      case kTanh: go(colsum_act_kernel<T, kTanh>); break;
+      case kGelu: go(colsum_act_kernel<T, kGelu>); break;
+      case kElu: go(colsum_act_kernel<T, kElu>); break;
+      case kExp: go(colsum_act_kernel<T, kExp>); break;
+      default: throw std::invalid_argument("colsum_act: activation");
+    }
+  };
+  if (dtype == kBF16) launch(bf16{});
+  else if (dtype == kF32) launch(float{});
   else throw std::invalid_argument("colsum_act: dtype");
   FFK_LAUNCH_CHECK("colsum_act");
 }

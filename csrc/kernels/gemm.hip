@@ -49,7 +49,7 @@ __device__ __forceinline__ float apply_act(int act, float x) {
   switch (act) {
     case 1: return x > 0.f ? x : 0.f;
     case 2: return 1.f / (1.f + __expf(-x));
-    case 3: return tanhf(x);
+    case 3: return fast_tanh(x);
     case 4: return gelu_tanh(x);
     default: return x;
   }

@@ -36,13 +36,25 @@ def main():
         steps = int(sys.argv[sys.argv.index("--steps") + 1])
     agg = {}
     total = 0
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            c = category(row["Name"])
-            d = agg.setdefault(c, {"calls": 0, "ns": 0})
-            d["calls"] += int(row["Calls"])
-            d["ns"] += int(row["TotalDurationNs"])
-            total += int(row["TotalDurationNs"])
+
+    def add(name, calls, ns):
+        nonlocal total
+        d = agg.setdefault(category(name), {"calls": 0, "ns": 0})
+        d["calls"] += int(calls)
+        d["ns"] += int(ns)
+        total += int(ns)
+
+    if path.endswith(".db"):
+        # rocprofv3 rocpd (SQLite) output: per-dispatch durations in ns
+        import sqlite3
+
+        con = sqlite3.connect(path)
+        for name, calls, ns in con.execute("select name, count(*), sum(duration) from kernels group by name"):
+            add(name, calls, ns)
+    else:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                add(row["Name"], row["Calls"], row["TotalDurationNs"])
     rows = sorted(agg.items(), key=lambda kv: -kv[1]["ns"])
     print(f"{'kernel (category)':70s} {'calls/step':>10s} {'ms/step':>9s} {'%':>6s}")
     for k, v in rows:
