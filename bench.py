@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--strategy", default="search", choices=["search", "dp"])
     ap.add_argument("--gemm", default=os.environ.get("FF_GEMM", "auto"))
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="replay the training step from a hipGraph (1) or run eagerly (0); default: graphs on a "
+                         "single GPU, eager across ranks (collective capture is validated on 1 GPU only)")
     args = ap.parse_args()
 
     os.environ["FF_GEMM"] = args.gemm
@@ -87,6 +90,15 @@ def main():
     def step():
         ex.train_step(feeds, labels)
 
+    graphed = False
+    use_graph = args.graph if args.graph >= 0 else int(world == 1)
+    if use_graph and dev.type == "cuda" and not args.profile:
+        try:
+            step = ex.make_graphed_train_step(feeds, labels)
+            graphed = True
+        except Exception as e:  # noqa: BLE001 — fall back to eager execution
+            print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
+
     for _ in range(args.warmup):
         step()
     if dev.type == "cuda":
@@ -134,6 +146,7 @@ def main():
                 "vocab": bcfg.vocab_size,
                 "optimizer": "adamw",
                 "compile_s": round(compile_s, 2),
+                "hipgraph": graphed,
                 "tokens_per_sec": round(sps * args.seq, 1),
                 "final_loss": round(pm.loss, 4),
             },

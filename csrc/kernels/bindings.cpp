@@ -71,8 +71,9 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("adam_step", [](uintptr_t w, uintptr_t g, int gdt, uintptr_t mm, uintptr_t v, uintptr_t wb, int64_t n,
                         float lr, float b1, float b2, float eps, float wd, int step, float gs, int decoupled,
-                        uintptr_t st) {
-    adam_step(F(w), P(g), gdt, F(mm), F(v), P(wb), n, lr, b1, b2, eps, wd, step, gs, decoupled, S(st));
+                        uintptr_t hp, uintptr_t st) {
+    adam_step(F(w), P(g), gdt, F(mm), F(v), P(wb), n, lr, b1, b2, eps, wd, step, gs, decoupled,
+              reinterpret_cast<const float*>(hp), S(st));
   });
   m.def("sgd_step", [](uintptr_t w, uintptr_t g, int gdt, uintptr_t mom, uintptr_t wb, int64_t n, float lr,
                        float momentum, float wd, int nesterov, float gs, uintptr_t st) {

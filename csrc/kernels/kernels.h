@@ -35,7 +35,7 @@ void softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int 
 // ---- optimizer.hip
 void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void* w_bf16, int64_t n, float lr,
                float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
-               hipStream_t st);
+               const float* hp, hipStream_t st);  // hp: optional device {lr, step} (graph replay)
 void sgd_step(float* w, const void* g, int grad_dtype, float* mom, void* w_bf16, int64_t n, float lr,
               float momentum, float weight_decay, int nesterov, float grad_scale, hipStream_t st);
 void sum_squares(const float* x, int64_t n, float* out, hipStream_t st);

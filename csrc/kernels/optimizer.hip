@@ -33,7 +33,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const 
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16* __restrict__ w_bf16, int64_t n4, float lr, float beta1,
                                                    float beta2, float eps, float weight_decay, float bc1,
-                                                   float bc2_sqrt, float grad_scale, int decoupled) {
+                                                   float bc2_sqrt, float grad_scale, int decoupled,
+                                                   const float* __restrict__ hp) {
+  if (hp) {  // device-resident {lr, step}: hipGraph replays see the current values
+    lr = hp[0];
+    bc1 = 1.f - __powf(beta1, hp[1]);
+    bc2_sqrt = sqrtf(1.f - __powf(beta2, hp[1]));
+  }
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
     f32x4 W = reinterpret_cast<f32x4*>(w)[i];
     f32x4 G = load_grad4<GT>(g, i);
@@ -109,7 +115,7 @@ static void need4(int64_t n, const char* w) {
 
 void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void* w_bf16, int64_t n, float lr,
                float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale, int decoupled,
-               hipStream_t st) {
+               const float* hp, hipStream_t st) {
   need4(n, "adam");
   float bc1 = 1.f - powf(beta1, static_cast<float>(step));
   float bc2s = sqrtf(1.f - powf(beta2, static_cast<float>(step)));
@@ -117,11 +123,11 @@ void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void
   if (grad_dtype == kBF16)
     hipLaunchKernelGGL(adam_kernel<bf16>, dim3(grid), dim3(256), 0, st, w, static_cast<const bf16*>(g), m, v,
                        static_cast<bf16*>(w_bf16), n / 4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale,
-                       decoupled);
+                       decoupled, hp);
   else
     hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(256), 0, st, w, static_cast<const float*>(g), m, v,
                        static_cast<bf16*>(w_bf16), n / 4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale,
-                       decoupled);
+                       decoupled, hp);
   FFK_LAUNCH_CHECK("adam");
 }
 

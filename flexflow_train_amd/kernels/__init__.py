@@ -239,8 +239,12 @@ def softmax_bwd(dy, y):
     return dx
 
 
-def adam_step(w, g, m, v, w_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, decoupled=False):
-    """Fused Adam/AdamW over a flat buffer; g may be fp32 or bf16."""
+def adam_step(w, g, m, v, w_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, decoupled=False,
+              hp=None):
+    """Fused Adam/AdamW over a flat buffer; g may be fp32 or bf16.  ``hp``: optional
+    device float32 tensor {lr, step} read by the kernel (hipGraph replay)."""
+    if hp is not None:
+        _check(hp, "hp", torch.float32, 2)
     n = w.numel()
     for name, t in (("w", w), ("m", m), ("v", v)):
         _check(t, name, torch.float32, n)
@@ -250,7 +254,7 @@ def adam_step(w, g, m, v, w_bf16, lr, beta1, beta2, eps, weight_decay, step, gra
     if n % 4:
         raise ValueError("adam: flat buffer length must be a multiple of 4")
     ext().adam_step(_p(w), _p(g), _dt(g), _p(m), _p(v), _p(w_bf16), n, float(lr), float(beta1), float(beta2),
-                    float(eps), float(weight_decay), int(step), float(grad_scale), int(decoupled), _stream())
+                    float(eps), float(weight_decay), int(step), float(grad_scale), int(decoupled), _p(hp), _stream())
     STATS["adam_step"] += 1
 
 

@@ -746,6 +746,55 @@ class Executor:
         self.backward(g)
         self.update(lr)
 
+    def make_graphed_train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, warmup: int = 2):
+        """Capture one whole training iteration (forward, loss, backward with
+        the bucketed RCCL gradient all-reduces, fused optimizer update) into a
+        hipGraph and return ``step(feeds=None, labels=None)`` that replays it.
+
+        Inputs/labels live in static device buffers (pass new batches to
+        ``step`` to copy them in).  Adam's learning rate and step counter are
+        kept on the device, so replays are exact; the GEMM autotuner settles
+        during ``warmup`` (eager) before capture.  This replaces the
+        reference's Legion tracing (begin_trace/end_trace around the loop)."""
+        if self.cfg.device.type != "cuda":
+            raise RuntimeError("graph capture needs a GPU")
+        if self.cfg.grad_clip > 0:
+            raise RuntimeError("gradient clipping syncs with the host; disable it for graph capture")
+        static_feeds = {}
+        for k, v in feeds.items():
+            piece = self._local_piece(k, v)
+            static_feeds[k] = piece.clone() if piece is not None else None
+        static_feeds = {k: v for k, v in static_feeds.items() if v is not None}
+        y = self.local_labels(labels)
+        static_labels = y.clone() if y is not None else None
+        for f in self.flats:
+            f["opt"].enable_device_hparams()
+        side = torch.cuda.Stream(device=self.cfg.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.train_step(static_feeds, static_labels)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize(self.cfg.device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self.train_step(static_feeds, static_labels)
+        self._graph = graph
+
+        def step(new_feeds: Optional[Dict[str, torch.Tensor]] = None, new_labels: Optional[torch.Tensor] = None):
+            if new_feeds:
+                for k, v in new_feeds.items():
+                    if k in static_feeds:
+                        static_feeds[k].copy_(self._local_piece(k, v), non_blocking=True)
+            if new_labels is not None and static_labels is not None:
+                static_labels.copy_(self.local_labels(new_labels), non_blocking=True)
+            graph.replay()
+            self.step_num += 1
+            for f in self.flats:
+                f["opt"].step_num += 1
+
+        return step
+
     def zero_metrics(self):
         self.metrics_buf.zero_()
         self.metrics_start = time.time()

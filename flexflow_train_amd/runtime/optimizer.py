@@ -46,6 +46,7 @@ class FlatOptimizer:
         self.grad = grad
         self.bf16 = bf16_copy
         self.step_num = 0
+        self.hp: Optional[torch.Tensor] = None   # device {lr, step} for hipGraph replay (Adam)
         self.m = self.v = self.mom = None
         if isinstance(cfg, AdamConfig):
             self.m = torch.zeros_like(master)
@@ -56,6 +57,17 @@ class FlatOptimizer:
     def state_tensors(self):
         return {k: t for k, t in (("m", self.m), ("v", self.v), ("mom", self.mom)) if t is not None}
 
+    def enable_device_hparams(self):
+        """Keep {lr, step} in device memory so a captured hipGraph of the
+        training step replays with the current learning rate / bias correction."""
+        if isinstance(self.cfg, AdamConfig) and self.master.is_cuda and self.hp is None:
+            self.hp = torch.tensor([float(self.cfg.lr), float(self.step_num)], device=self.master.device)
+
+    def set_lr(self, lr: float):
+        self.cfg.lr = lr
+        if self.hp is not None:
+            self.hp[0].fill_(float(lr))
+
     def step(self, lr: Optional[float] = None, grad_scale: float = 1.0):
         self.step_num += 1
         c = self.cfg
@@ -65,8 +77,10 @@ class FlatOptimizer:
         use_hip = self.master.is_cuda and K.available() and self.master.numel() % 4 == 0
         if isinstance(c, AdamConfig):
             if use_hip:
+                if self.hp is not None:
+                    self.hp[1:].add_(1.0)   # device-side step counter (captured with the graph)
                 K.adam_step(self.master, self.grad, self.m, self.v, self.bf16, lr, c.beta1, c.beta2, c.epsilon,
-                            c.weight_decay, self.step_num, grad_scale, c.decoupled)
+                            c.weight_decay, self.step_num, grad_scale, c.decoupled, hp=self.hp)
                 return
             g = self.grad * grad_scale
             if not c.decoupled and c.weight_decay:

@@ -105,6 +105,28 @@ def profile_op(op, in_shapes, device: torch.device, dtype=torch.bfloat16, warmup
             fn()
         return (time.perf_counter() - t0) * 1e3 / iters
 
+    def graph_time(fn):
+        """GPU time of ``fn`` replayed from a hipGraph: excludes the host
+        launch overhead that the training loop hides by running ahead."""
+        fn()
+        sync()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fn()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fn()
+        return timeit(graph.replay)
+
+    if device.type == "cuda":
+        try:
+            t_f = graph_time(fwd)
+            t_fb = graph_time(both) if g is not None else t_f
+            return t_f, max(0.0, t_fb - t_f)
+        except Exception:  # noqa: BLE001 — op not capturable: eager timing
+            torch.cuda.synchronize()
     t_f = timeit(fwd)
     t_fb = timeit(both) if g is not None else t_f
     return t_f, max(0.0, t_fb - t_f)
