@@ -150,21 +150,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
           s[kt] = mfma32(kf, qf[ks], s[kt]);
         }
       }
-      // ---- scale, mask, tile max
+      // ---- scale, mask (only tiles that cross the sequence end or the
+      // causal diagonal — a wave-uniform branch), tile max
+      const bool need_mask = (k0 + KV > P.Sk) || (CAUSAL && k0 + KV - 1 > qw);
       float tmax = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float x = s[kt][r] * P.scale_log2;
-          if (key >= P.Sk || (CAUSAL && key > q)) x = -INFINITY;
-          s[kt][r] = x;
-          tmax = fmaxf(tmax, x);
-        }
+        for (int r = 0; r < 16; ++r) s[kt][r] *= P.scale_log2;
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key >= P.Sk || (CAUSAL && key > q)) s[kt][r] = -INFINITY;
+          }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kt][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float m_new = fmaxf(m, tmax);
-      const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+      const float alpha = (m_new == -INFINITY) ? 1.f : fexp2(m - m_new);
       const float msub = (m_new == -INFINITY) ? 0.f : m_new;
       m = m_new;
       float psum = 0.f;
@@ -172,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float pv = exp2f(s[kt][r] - msub);
+          float pv = fexp2(s[kt][r] - msub);
           s[kt][r] = pv;
           psum += pv;
         }
@@ -297,6 +306,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(Att
       vl.load(P.v, b, hh, k0 + KV, P.Sk);
     }
     const bool wave_active = !CAUSAL || (k0 <= qw + 31);
+    const bool need_mask = (k0 + KV > P.Sk) || (CAUSAL && k0 + KV - 1 > qw) || (qw + 31 >= P.Sq);
     if (wave_active) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -307,12 +317,17 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(Att
           s = mfma32(lds_read16(Kt, off), qf[ks], s);
           dp = mfma32(lds_read16(Vt, off), df[ks], dp);
         }
+        if (need_mask) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float pv = exp2f(s[r] * P.scale_log2 - lse);
-          if (key >= P.Sk || (CAUSAL && key > q) || !q_ok) pv = 0.f;
-          s[r] = pv * (dp[r] - dlt);  // dS^T
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float pv = fexp2(s[r] * P.scale_log2 - lse);
+            if (key >= P.Sk || (CAUSAL && key > q) || !q_ok) pv = 0.f;
+            s[r] = pv * (dp[r] - dlt);  // dS^T
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[r] = fexp2(s[r] * P.scale_log2 - lse) * (dp[r] - dlt);
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -410,6 +425,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(A
       dl.load(P.dout, b, hh, q0 + QT, P.Sq);
     }
     const bool wave_active = !CAUSAL || (q0 + QT - 1 >= kw);
+    const bool need_mask = (q0 + QT > P.Sq) || (CAUSAL && q0 < kw + 31) || (kw + 31 >= P.Sk);
     if (wave_active) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
@@ -420,14 +436,24 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(A
           s = mfma32(lds_read16(Qt, off), kf[ks], s);
           dp = mfma32(lds_read16(Dt, off), vf[ks], dp);
         }
+        if (need_mask) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int qq = q0 + ql_;
-          float pv = exp2f(s[r] * P.scale_log2 - ls[ql_]);
-          if (qq >= P.Sq || (CAUSAL && key > qq) || !k_ok) pv = 0.f;
-          s[r] = pv;
-          dp[r] = pv * (dp[r] - ds[ql_]);
+          for (int r = 0; r < 16; ++r) {
+            const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int qq = q0 + ql_;
+            float pv = fexp2(s[r] * P.scale_log2 - ls[ql_]);
+            if (qq >= P.Sq || (CAUSAL && key > qq) || !k_ok) pv = 0.f;
+            s[r] = pv;
+            dp[r] = pv * (dp[r] - ds[ql_]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float pv = fexp2(s[r] * P.scale_log2 - ls[ql_]);
+            s[r] = pv;
+            dp[r] = pv * (dp[r] - ds[ql_]);
+          }
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {

@@ -74,6 +74,10 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
   return r;
 }
 
+// bare v_exp_f32 (2^x): libm exp2f adds a denormal range fix-up (cmp +
+// ldexp + 2 cndmask per element) that dominated the softmax VALU in attention
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // tanh from one v_exp_f32 + one v_rcp_f32 (libm tanhf is ~10x the
 // instructions and made the GELU backward VALU-bound); |err| < 1e-6 abs,
 // saturates correctly at +-inf.
