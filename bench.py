@@ -46,6 +46,8 @@ def main():
 
     from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType)
     from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
+    from flexflow_train_amd.ops.gemm import choices as gemm_choices
+    import collections
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -147,6 +149,7 @@ def main():
                 "optimizer": "adamw",
                 "compile_s": round(compile_s, 2),
                 "hipgraph": graphed,
+                "gemm_choices": dict(collections.Counter(gemm_choices().values())),
                 "tokens_per_sec": round(sps * args.seq, 1),
                 "final_loss": round(pm.loss, 4),
             },

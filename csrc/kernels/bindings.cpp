@@ -121,4 +121,11 @@ PYBIND11_MODULE(_ffkernels, m) {
                    uintptr_t st) {
     gemm_bf16_ex(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32, S(st));
   });
+  m.def("gemm256_supported", &gemm256_supported);
+  m.def("gemm256", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int M, int N, int K,
+                      int lda, int ldb, int ldc, bool ta, bool tb, int act, float alpha, float beta, int out_f32,
+                      int splits, uintptr_t ws, uintptr_t st) {
+    gemm256_bf16(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32,
+                 splits, reinterpret_cast<float*>(ws), S(st));
+  });
 }

@@ -71,4 +71,11 @@ void gemm_bf16_ex(const void* A, const void* B, void* C, const void* bias, void*
                   int ldb, int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
                   hipStream_t st);
 
+// ---- gemm256.hip: 256x256 tiles, LDS-DMA staging, split-K (fp32 partials
+// in `workspace` [splits][M][N] + reduce pass); needs K % 64 == 0.
+bool gemm256_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b);
+void gemm256_bf16(const void* A, const void* B, void* C, const void* bias, void* pre, int M, int N, int K, int lda,
+                  int ldb, int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
+                  int splits, float* workspace, hipStream_t st);
+
 }  // namespace ffk

@@ -404,3 +404,60 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, b
                int(out.dtype == torch.float32), _stream())
     STATS["gemm"] += 1
     return out
+
+
+_WS_CACHE: dict = {}
+
+
+def gemm256_supported(a, b, trans_a=False, trans_b=False) -> bool:
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
+        return False
+    if a.stride(1) != 1 or b.stride(1) != 1 or a.data_ptr() % 16 or b.data_ptr() % 16:
+        return False
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N = b.shape[0] if trans_b else b.shape[1]
+    return bool(ext().gemm256_supported(M, N, K, a.stride(0), b.stride(0), bool(trans_a), bool(trans_b)))
+
+
+def default_splits(M: int, N: int, K: int, target_blocks: int = 512) -> int:
+    """Split-K degree that brings the grid near ``target_blocks`` (2 per CU)
+    while keeping >= 8 K-tiles (512 deep) per split."""
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    s = max(1, min(target_blocks // max(1, tiles), K // 512, 16))
+    return s
+
+
+def gemm256(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, beta=0.0, out=None,
+            out_dtype=None, pre=None, splits=None):
+    """256x256-tile MFMA GEMM with LDS-DMA staging and optional split-K
+    (split-K: fp32 partial slabs + reduce; no bias/activation epilogue)."""
+    if not gemm256_supported(a, b, trans_a, trans_b):
+        raise ValueError("gemm256: unsupported operands (bf16, 16-B aligned, K % 64, dims % 8)")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm256: inner dims differ ({K} vs {Kb})")
+    dt = out_dtype or (out.dtype if out is not None else torch.bfloat16)
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=dt)
+    if out.shape != (M, N) or out.stride(1) != 1:
+        raise ValueError("gemm256: bad output")
+    if bias is not None:
+        _check(bias, "bias", torch.bfloat16, N)
+    if pre is not None:
+        _check(pre, "pre", torch.bfloat16, M * N)
+    s = default_splits(M, N, K) if splits is None else int(splits)
+    if bias is not None or pre is not None or act != "none":
+        s = 1
+    ws = None
+    if s > 1:
+        key = (a.device, s * M * N)
+        ws = _WS_CACHE.get(key)
+        if ws is None:
+            ws = torch.empty(s * M * N, device=a.device, dtype=torch.float32)
+            _WS_CACHE[key] = ws
+    ext().gemm256(a.data_ptr(), b.data_ptr(), out.data_ptr(), _p(bias), _p(pre), M, N, K, a.stride(0), b.stride(0),
+                  out.stride(0), bool(trans_a), bool(trans_b), ACT_CODES[act], float(alpha), float(beta),
+                  int(out.dtype == torch.float32), s, _p(ws), _stream())
+    STATS["gemm256"] += 1
+    return out

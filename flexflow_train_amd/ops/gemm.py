@@ -4,8 +4,11 @@ The MFMA kernel (csrc/kernels/gemm.hip) fuses bias / activation /
 pre-activation store / fp32-accumulate epilogues; hipBLASLt (through
 torch.mm / addmm) is the plain library GEMM.  ``FF_GEMM`` selects:
 
-* ``auto`` (default): time both once per (shape, layout, epilogue) signature
-  outside graph capture and keep the faster — "measure, don't guess";
+* ``auto`` (default): time every candidate once per (shape, layout,
+  epilogue) signature outside graph capture and keep the fastest — "measure,
+  don't guess".  Candidates: hipBLASLt, the 128² register-staged MFMA kernel,
+  and the 256² LDS-DMA kernel (csrc/kernels/gemm256.hip) at several split-K
+  degrees (the long-K weight-gradient GEMMs are where split-K wins);
 * ``hip``: always the MFMA kernel; ``blas``: always hipBLASLt.
 
 On CPU everything is a torch matmul in the compute dtype.
@@ -117,16 +120,41 @@ def _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre):
     return K.gemm(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre)
 
 
-def _time(fn, iters=3) -> float:
+def _hip256(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
+    return K.gemm256(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
+                     splits=splits)
+
+
+def _candidates(a, b, trans_a, trans_b, bias, act, pre):
+    """name -> callable(a, b, ta, tb, bias, act, out, beta, pre) tried by the autotuner."""
+    c = {"hip": _hip, "blas": _blas}
+    if os.environ.get("FF_GEMM256", "1") != "0" and K.gemm256_supported(a, b, trans_a, trans_b):
+        M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+        N = b.shape[0] if trans_b else b.shape[1]
+        plain = bias is None and act == "none" and pre is None
+        splits = {1}
+        if plain:
+            d = K.default_splits(M, N, Kd)
+            splits |= {s for s in (d // 2, d, d * 2) if 1 <= s <= max(1, Kd // 512)}
+        for s in sorted(splits):
+            c[f"hip256:{s}"] = (lambda s_: (lambda *args: _hip256(*args, splits=s_)))(s)
+    return c
+
+
+def _time(fn, iters=5, rounds=2) -> float:
+    """min over rounds of the mean time of ``iters`` back-to-back calls."""
     fn()
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / iters
+    best = float("inf")
+    for _ in range(rounds):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / iters)
+    return best
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias: Optional[torch.Tensor] = None,
@@ -142,6 +170,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         return _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre)
     key = (tuple(a.shape), tuple(b.shape), trans_a, trans_b, bias is not None, act,
            None if out is None else out.dtype, bool(beta), pre is not None)
+    cands = _candidates(a, b, trans_a, trans_b, bias, act, pre)
     choice = _CHOICE.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
@@ -149,10 +178,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         else:
             scratch = None if out is None else out.clone()
             pscratch = None if pre is None else pre.clone()
-            t_hip = _time(lambda: _hip(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))
-            t_blas = _time(lambda: _blas(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))
-            choice = "hip" if t_hip <= t_blas else "blas"
+            times = {name: _time(lambda fn=fn: fn(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))
+                     for name, fn in cands.items()}
+            choice = min(times, key=times.get)
         _CHOICE[key] = choice
-    if choice == "hip":
-        return _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre)
-    return _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre)
+    return cands[choice](a, b, trans_a, trans_b, bias, act, out, beta, pre)

@@ -209,6 +209,32 @@ def test_gemm(ta, tb, M, N, Kd):
     assert _rel(c3, ref + 1) < 1e-2
 
 
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
+                                            (296, 136, 1024, 3)])
+def test_gemm256(ta, tb, M, N, Kd, splits):
+    torch.manual_seed(11)
+    a = torch.randn(Kd, M, device=DEV, dtype=torch.bfloat16) if ta else torch.randn(M, Kd, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    b = torch.randn(N, Kd, device=DEV, dtype=torch.bfloat16) if tb else torch.randn(Kd, N, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    af = a.float().t() if ta else a.float()
+    bf = b.float().t() if tb else b.float()
+    ref = af @ bf
+    c = K.gemm256(a, b, trans_a=ta, trans_b=tb, splits=splits)
+    assert _rel(c, ref) < 1e-2
+    c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
+    K.gemm256(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
+    assert _rel(c3, ref + 1) < 1e-2
+    if splits == 1:
+        bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        c2 = K.gemm256(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
+        u = ref + bias.float()
+        assert _rel(pre, u) < 1e-2
+        assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
+
+
 def test_dropout_and_cast():
     x = torch.randn(1 << 16, device=DEV, dtype=torch.bfloat16)
     y = K.dropout(x, 0.25, 1234)
