@@ -121,6 +121,65 @@ PYBIND11_MODULE(_ffkernels, m) {
                    uintptr_t st) {
     gemm_bf16_ex(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32, S(st));
   });
+  // ---- tensorops
+  auto shape = [](const std::vector<int64_t>& v) {
+    if (v.size() > 6) throw std::invalid_argument("tensorops: at most 6 dims");
+    NdShape s;
+    s.nd = static_cast<int>(v.size());
+    for (size_t i = 0; i < v.size(); ++i) s.size[i] = v[i];
+    return s;
+  };
+  auto strides = [](const std::vector<int64_t>& v) {
+    if (v.size() > 6) throw std::invalid_argument("tensorops: at most 6 dims");
+    NdStrides s;
+    for (size_t i = 0; i < v.size(); ++i) s.s[i] = v[i];
+    return s;
+  };
+  m.def("binary_nd", [=](int dt, uintptr_t a, uintptr_t b, uintptr_t y, std::vector<int64_t> s,
+                         std::vector<int64_t> sa, std::vector<int64_t> sb, int op, uintptr_t st) {
+    binary_nd(dt, P(a), P(b), P(y), shape(s), strides(sa), strides(sb), op, S(st));
+  });
+  m.def("binary_grad_nd", [=](int dt, uintptr_t dy, uintptr_t a, uintptr_t b, uintptr_t g, std::vector<int64_t> s,
+                              std::vector<int64_t> sa, std::vector<int64_t> sb, int op, int which, uintptr_t st) {
+    binary_grad_nd(dt, P(dy), P(a), P(b), F(g), shape(s), strides(sa), strides(sb), op, which, S(st));
+  });
+  m.def("sum_to", [=](int dt, uintptr_t full, uintptr_t out, std::vector<int64_t> s, std::vector<int64_t> t,
+                      float beta, uintptr_t st) {
+    sum_to(dt, F(full), P(out), shape(s), shape(t), beta, S(st));
+  });
+  m.def("permute_nd", [=](int dt, uintptr_t x, uintptr_t y, std::vector<int64_t> out_shape,
+                          std::vector<int64_t> in_strides, uintptr_t st) {
+    permute_nd(dt, P(x), P(y), shape(out_shape), strides(in_strides), S(st));
+  });
+  m.def("slice_copy", [](int dt, uintptr_t x, uintptr_t y, int64_t outer, int64_t len, int64_t inner, int64_t total,
+                         int64_t off, int to_slice, int acc, uintptr_t st) {
+    slice_copy(dt, P(x), P(y), outer, len, inner, total, off, to_slice, acc, S(st));
+  });
+  m.def("reverse_axis", [](int dt, uintptr_t x, uintptr_t y, int64_t outer, int64_t len, int64_t inner,
+                           uintptr_t st) { reverse_axis(dt, P(x), P(y), outer, len, inner, S(st)); });
+  m.def("gather_axis", [](int dt, int ib, uintptr_t x, uintptr_t idx, uintptr_t y, int64_t outer, int64_t lx,
+                          int64_t li, int64_t inner, uintptr_t st) {
+    gather_axis(dt, ib, P(x), P(idx), P(y), outer, lx, li, inner, S(st));
+  });
+  m.def("scatter_add_axis", [](int dt, int ib, uintptr_t dy, uintptr_t idx, uintptr_t dx, int64_t outer, int64_t lx,
+                               int64_t li, int64_t inner, uintptr_t st) {
+    scatter_add_axis(dt, ib, P(dy), P(idx), F(dx), outer, lx, li, inner, S(st));
+  });
+  m.def("reduce_axis", [](int dt, uintptr_t x, uintptr_t y, int64_t outer, int64_t red, int64_t inner, int op,
+                          uintptr_t st) { reduce_axis(dt, P(x), P(y), outer, red, inner, op, S(st)); });
+  m.def("topk_rows", [](int dt, uintptr_t x, uintptr_t vals, uintptr_t idx, int64_t rows, int n, int k,
+                        uintptr_t st) {
+    topk_rows(dt, P(x), P(vals), reinterpret_cast<int64_t*>(idx), rows, n, k, S(st));
+  });
+  m.def("unary_op", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, int64_t n, int op, float s, int bwd,
+                       uintptr_t st) { unary_op(dt, P(x), P(dy), P(y), n, op, s, bwd, S(st)); });
+  m.def("mse_loss", [](int dt, uintptr_t p, uintptr_t y, uintptr_t g, uintptr_t metrics, int64_t n, float scale,
+                       uintptr_t st) { mse_loss(dt, P(p), P(y), P(g), F(metrics), n, scale, S(st)); });
+  m.def("init_tensor", [=](int dt, uintptr_t out, std::vector<int64_t> piece, std::vector<int64_t> full,
+                           std::vector<int64_t> lo, int kind, uint64_t seed, float a, float b, float c, float d,
+                           uintptr_t st) {
+    init_tensor(dt, P(out), shape(piece), shape(full), strides(lo), kind, seed, a, b, c, d, S(st));
+  });
   m.def("gemm256_supported", &gemm256_supported);
   m.def("gemm256", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int M, int N, int K,
                       int lda, int ldb, int ldc, bool ta, bool tb, int act, float alpha, float beta, int out_f32,

@@ -78,4 +78,43 @@ void gemm256_bf16(const void* A, const void* B, void* C, const void* bias, void*
                   int ldb, int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
                   int splits, float* workspace, hipStream_t st);
 
+// ---- tensorops.hip: general tensor operators (N-d, <= 6 dims)
+struct NdShape {
+  int nd = 0;
+  int64_t size[6] = {1, 1, 1, 1, 1, 1};
+};
+struct NdStrides {
+  int64_t s[6] = {0, 0, 0, 0, 0, 0};
+};
+// op: 0 add 1 sub 2 mul 3 div 4 max 5 min 6 eq 7 gt 8 lt; strides 0 on broadcast dims
+void binary_nd(int dtype, const void* a, const void* b, void* y, const NdShape& s, const NdStrides& sa,
+               const NdStrides& sb, int op, hipStream_t st);
+// fp32 full-shape gradient w.r.t. a (which = 0) or b (which = 1)
+void binary_grad_nd(int dtype, const void* dy, const void* a, const void* b, float* g, const NdShape& s,
+                    const NdStrides& sa, const NdStrides& sb, int op, int which, hipStream_t st);
+// out (shape `target`, same rank as s, 1 on broadcast dims) = sum_broadcast(full) + beta*out
+void sum_to(int dtype, const float* full, void* out, const NdShape& s, const NdShape& target, float beta,
+            hipStream_t st);
+void permute_nd(int dtype, const void* x, void* y, const NdShape& out_shape, const NdStrides& in_strides_permuted,
+                hipStream_t st);
+void slice_copy(int dtype, const void* x, void* y, int64_t outer, int64_t len, int64_t inner, int64_t total,
+                int64_t off, int to_slice, int accumulate, hipStream_t st);
+void reverse_axis(int dtype, const void* x, void* y, int64_t outer, int64_t len, int64_t inner, hipStream_t st);
+void gather_axis(int dtype, int index_bits, const void* x, const void* idx, void* y, int64_t outer, int64_t len_x,
+                 int64_t len_i, int64_t inner, hipStream_t st);
+void scatter_add_axis(int dtype, int index_bits, const void* dy, const void* idx, float* dx, int64_t outer,
+                      int64_t len_x, int64_t len_i, int64_t inner, hipStream_t st);
+// op: 0 sum 1 mean 2 max 3 min 4 prod over the middle dim of [outer, red, inner]
+void reduce_axis(int dtype, const void* x, void* y, int64_t outer, int64_t red, int64_t inner, int op,
+                 hipStream_t st);
+void topk_rows(int dtype, const void* x, void* vals, int64_t* idx, int64_t rows, int n, int k, hipStream_t st);
+// op: 0 +s 1 -s 2 *s 3 /s 4 pow 5 log 6 sqrt 7 rsqrt 8 sin 9 cos 10 leaky_relu 11 ceil 12 round 13 identity
+void unary_op(int dtype, const void* x, const void* dy, void* y, int64_t n, int op, float scalar, int backward,
+              hipStream_t st);
+void mse_loss(int dtype, const void* pred, const void* label, void* grad, float* metrics, int64_t n, float scale,
+              hipStream_t st);
+// kind: 0 uniform[a,b) 1 normal(a,b) 2 truncated normal(a,b) in [c,d] 3 constant a
+void init_tensor(int dtype, void* out, const NdShape& piece, const NdShape& full, const NdStrides& box_lo, int kind,
+                 uint64_t seed, float a, float b, float c, float d, hipStream_t st);
+
 }  // namespace ffk

@@ -461,3 +461,204 @@ def gemm256(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0
                   int(out.dtype == torch.float32), s, _p(ws), _stream())
     STATS["gemm256"] += 1
     return out
+
+
+# ---------------------------------------------------------------------------
+# General tensor operators (csrc/kernels/tensorops.hip).  Inputs: contiguous
+# GPU tensors in bf16 or fp32; _check's 16-byte alignment is not required.
+def tensorop_ok(*ts) -> bool:
+    return available() and all(t is not None and t.is_cuda and t.is_contiguous() and
+                               t.dtype in (torch.bfloat16, torch.float32) for t in ts)
+
+
+def _cstrides(shape):
+    st, acc = [0] * len(shape), 1
+    for i in range(len(shape) - 1, -1, -1):
+        st[i] = acc
+        acc *= shape[i]
+    return st
+
+
+def _bcast_strides(shape, out_shape):
+    shape = [1] * (len(out_shape) - len(shape)) + list(shape)
+    st = _cstrides(shape)
+    return [0 if (s == 1 and o != 1) else t for s, o, t in zip(shape, out_shape, st)]
+
+
+BINARY_CODES = {"EW_ADD": 0, "EW_SUB": 1, "EW_MUL": 2, "EW_DIV": 3, "EW_MAX": 4, "EW_MIN": 5}
+CMP_CODES = {"EW_EQUAL": 6, "EW_GREATER": 7, "EW_LESS": 8}   # 0/1 in the operand dtype
+
+
+def binary(a, b, op: str):
+    """Broadcasting element-wise binary op (same dtype)."""
+    out_shape = list(torch.broadcast_shapes(a.shape, b.shape))
+    y = torch.empty(out_shape, device=a.device, dtype=a.dtype)
+    ext().binary_nd(_dt(a), a.data_ptr(), b.data_ptr(), y.data_ptr(), out_shape or [1],
+                    _bcast_strides(a.shape, out_shape) or [0], _bcast_strides(b.shape, out_shape) or [0],
+                    BINARY_CODES[op] if op in BINARY_CODES else CMP_CODES[op], _stream())
+    STATS["binary"] += 1
+    return y
+
+
+def binary_grad(dy, a, b, op: str, which: int, a_shape=None, b_shape=None):
+    """Gradient of ``op`` w.r.t. a (0) or b (1), reduced to that operand's
+    shape.  For add / sub the operand values are not read: a / b may be None
+    (then ``a_shape`` / ``b_shape`` give the shapes)."""
+    out_shape = list(dy.shape)
+    a_shape = list(a.shape) if a is not None else list(a_shape)
+    b_shape = list(b.shape) if b is not None else list(b_shape)
+    tgt0 = a_shape if which == 0 else b_shape
+    if op in ("EW_ADD", "EW_SUB") and tgt0 == out_shape:   # no broadcast: dy (or -dy) itself
+        return dy if (op == "EW_ADD" or which == 0) else unary(dy, "SCALAR_MULTIPLY", -1.0)
+    pa = a.data_ptr() if a is not None else dy.data_ptr()
+    pb = b.data_ptr() if b is not None else dy.data_ptr()
+    g = torch.empty(out_shape, device=dy.device, dtype=torch.float32)
+    ext().binary_grad_nd(_dt(dy), dy.data_ptr(), pa, pb, g.data_ptr(), out_shape,
+                         _bcast_strides(a_shape, out_shape), _bcast_strides(b_shape, out_shape),
+                         BINARY_CODES[op], int(which), _stream())
+    STATS["binary_grad"] += 1
+    tgt = a_shape if which == 0 else b_shape
+    if list(tgt) == out_shape:
+        return g.to(dy.dtype)
+    padded = [1] * (len(out_shape) - len(tgt)) + list(tgt)
+    r = torch.empty(padded, device=dy.device, dtype=dy.dtype)
+    ext().sum_to(_dt(r), g.data_ptr(), r.data_ptr(), out_shape, padded, 0.0, _stream())
+    return r.reshape(tgt)
+
+
+def permute(x, perm):
+    out_shape = [x.shape[p] for p in perm]
+    st = _cstrides(list(x.shape))
+    y = torch.empty(out_shape, device=x.device, dtype=x.dtype)
+    ext().permute_nd(_dt(x), x.data_ptr(), y.data_ptr(), out_shape, [st[p] for p in perm], _stream())
+    STATS["permute"] += 1
+    return y
+
+
+def _oli(shape, axis):
+    axis = axis % len(shape)
+    outer = 1
+    for s in shape[:axis]:
+        outer *= s
+    inner = 1
+    for s in shape[axis + 1:]:
+        inner *= s
+    return outer, shape[axis], inner, axis
+
+
+def concat(xs, axis):
+    shape = list(xs[0].shape)
+    outer, _, inner, axis = _oli(shape, axis)
+    total = sum(int(x.shape[axis]) for x in xs)
+    shape[axis] = total
+    y = torch.empty(shape, device=xs[0].device, dtype=xs[0].dtype)
+    off = 0
+    for x in xs:
+        ln = int(x.shape[axis])
+        ext().slice_copy(_dt(x), x.data_ptr(), y.data_ptr(), outer, ln, inner, total, off, 0, 0, _stream())
+        off += ln
+    STATS["concat"] += 1
+    return y
+
+
+def split(x, sizes, axis):
+    outer, total, inner, axis = _oli(list(x.shape), axis)
+    outs, off = [], 0
+    for ln in sizes:
+        shape = list(x.shape)
+        shape[axis] = ln
+        y = torch.empty(shape, device=x.device, dtype=x.dtype)
+        ext().slice_copy(_dt(x), x.data_ptr(), y.data_ptr(), outer, ln, inner, total, off, 1, 0, _stream())
+        outs.append(y)
+        off += ln
+    STATS["split"] += 1
+    return outs
+
+
+def reverse(x, axis):
+    outer, ln, inner, _ = _oli(list(x.shape), axis)
+    y = torch.empty_like(x)
+    ext().reverse_axis(_dt(x), x.data_ptr(), y.data_ptr(), outer, ln, inner, _stream())
+    return y
+
+
+def gather(x, idx, dim):
+    outer, lx, inner, dim = _oli(list(x.shape), dim)
+    li = idx.shape[dim]
+    y = torch.empty(idx.shape, device=x.device, dtype=x.dtype)
+    ext().gather_axis(_dt(x), 64 if idx.dtype == torch.int64 else 32, x.data_ptr(), idx.contiguous().data_ptr(),
+                      y.data_ptr(), outer, lx, li, inner, _stream())
+    return y
+
+
+def scatter_add(dy, idx, dim, x_shape):
+    outer, lx, inner, dim = _oli(list(x_shape), dim)
+    dx = torch.zeros(x_shape, device=dy.device, dtype=torch.float32)
+    ext().scatter_add_axis(_dt(dy), 64 if idx.dtype == torch.int64 else 32, dy.data_ptr(),
+                           idx.contiguous().data_ptr(), dx.data_ptr(), outer, lx, idx.shape[dim], inner, _stream())
+    return dx
+
+
+REDUCE_CODES = {"sum": 0, "mean": 1, "max": 2, "min": 3, "prod": 4}
+
+
+def reduce_contig(x, first: int, last: int, op: str):
+    """Reduce the contiguous dim range [first, last] of x; returns the
+    tensor with those dims removed."""
+    shape = list(x.shape)
+    outer = 1
+    for s in shape[:first]:
+        outer *= s
+    red = 1
+    for s in shape[first:last + 1]:
+        red *= s
+    inner = 1
+    for s in shape[last + 1:]:
+        inner *= s
+    out = torch.empty(shape[:first] + shape[last + 1:], device=x.device, dtype=x.dtype)
+    ext().reduce_axis(_dt(x), x.data_ptr(), out.data_ptr(), outer, red, inner, REDUCE_CODES[op], _stream())
+    return out
+
+
+def topk(x, k: int):
+    n = x.shape[-1]
+    rows = x.numel() // n
+    vals = torch.empty(list(x.shape[:-1]) + [k], device=x.device, dtype=x.dtype)
+    idx = torch.empty(list(x.shape[:-1]) + [k], device=x.device, dtype=torch.int64)
+    ext().topk_rows(_dt(x), x.data_ptr(), vals.data_ptr(), idx.data_ptr(), rows, n, int(k), _stream())
+    return vals, idx
+
+
+UNARY_CODES = {"SCALAR_ADD": 0, "SCALAR_SUB": 1, "SCALAR_MULTIPLY": 2, "SCALAR_TRUE_DIV": 3, "POW": 4, "LOG": 5,
+               "SQRT": 6, "RSQRT": 7, "SIN": 8, "COS": 9, "LEAKYRELU": 10, "CEIL": 11, "ROUND": 12,
+               "IDENTITY": 13, "NOOP": 13}
+
+
+def unary(x, op: str, scalar: float = 0.0, dy=None):
+    """Forward (dy None) or backward (returns dy * op'(x)) of a unary / scalar op."""
+    y = torch.empty_like(x if dy is None else dy)
+    ext().unary_op(_dt(x), x.data_ptr(), _p(dy), y.data_ptr(), x.numel(), UNARY_CODES[op], float(scalar),
+                   int(dy is not None), _stream())
+    STATS["unary"] += 1
+    return y
+
+
+def mse(pred, label, grad=None, metrics=None, scale: float = 1.0):
+    """grad = scale * (pred - label); metrics[0] += sum sq err, metrics[1] += sum abs err."""
+    ext().mse_loss(_dt(pred), pred.data_ptr(), label.data_ptr(), _p(grad), _p(metrics), pred.numel(), float(scale),
+                   _stream())
+    STATS["mse"] += 1
+    return grad
+
+
+INIT_KINDS = {"uniform": 0, "normal": 1, "truncated_normal": 2, "constant": 3}
+
+
+def init_piece(out, full_shape, box_lo, kind: str, seed: int, a=0.0, b=1.0, c=-2.0, d=2.0):
+    """Fill ``out`` (a box of the logical tensor ``full_shape`` starting at
+    ``box_lo``) from a counter-based RNG keyed by (seed, global index)."""
+    ext().init_tensor(_dt(out), out.data_ptr(), list(out.shape) or [1], list(full_shape) or [1],
+                      list(box_lo) or [0], INIT_KINDS[kind], int(seed) & ((1 << 64) - 1), float(a), float(b),
+                      float(c), float(d), _stream())
+    STATS["init"] += 1
+    return out

@@ -152,6 +152,17 @@ class MultiHeadAttentionOp(OpImpl):
             return (torch.rand(P, H, generator=gen) * 2 - 1) * bound
         return torch.randn(P, H, generator=gen) * math.sqrt(2.0 / (E + H * kd))
 
+    def init_spec(self, ctx, index, logical_shape, initializer):
+        if index != 0 or initializer.get("type") not in ("glorot_uniform", "glorot_normal"):
+            return None
+        P, H = logical_shape
+        E = int(ctx.a("embed_dim"))
+        kd = int(ctx.a("kdim") or 0) or E // int(ctx.a("num_heads"))
+        if initializer["type"] == "glorot_uniform":
+            bound = math.sqrt(6.0 / (E + H * kd))
+            return (0, -bound, bound, 0.0, 0.0)
+        return (1, 0.0, math.sqrt(2.0 / (E + H * kd)), 0.0, 0.0)
+
     def forward(self, ctx: OpContext, inputs, weights):
         q_in, k_in, v_in = inputs
         W = weights[0]

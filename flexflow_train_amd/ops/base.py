@@ -63,6 +63,11 @@ class OpImpl:
     def init_weight(self, ctx: OpContext, index: int, logical_shape, initializer: dict, gen: torch.Generator):
         return None
 
+    # Counter-based (sharded) initialisation: (kind, a, b, c, d) for
+    # runtime.initializers.counter_init_piece, or None for the generic mapping.
+    def init_spec(self, ctx: OpContext, index: int, logical_shape, initializer: dict):
+        return None
+
     # Physical storage of a weight piece.  Ops whose kernels want a fused /
     # permuted layout (attention: one [E, 3*Hl*k] QKV operand) override these;
     # the executor stores physical pieces and converts at every logical

@@ -100,8 +100,34 @@ class ActivationOp(OpImpl):
 @register("LEAKYRELU", "LOG", "SQRT", "RSQRT", "SIN", "COS", "POW", "CEIL", "ROUND", "LOGICAL_NOT", "IDENTITY",
           "NOOP", "SCALAR_MULTIPLY", "SCALAR_ADD", "SCALAR_SUB", "SCALAR_TRUE_DIV", "SCALAR_FLOOR_DIV")
 class UnaryOp(AutogradOp):
+    """Scalar / math unary ops: HIP unary kernel on GPU (tensorops.hip),
+    autograd recompute elsewhere (CPU, LOGICAL_NOT, FLOOR_DIV)."""
+
+    @staticmethod
+    def _scalar(ctx):
+        op = ctx.op_type
+        if op == "POW":
+            return float(ctx.a("exponent"))
+        if op == "LEAKYRELU":
+            return float(ctx.a("alpha", 0.01))
+        return float(ctx.a("scalar", 0.0))
+
     def compute(self, ctx, inputs, weights):
         return [_torch_unary(ctx.op_type, ctx, inputs[0])]
+
+    def forward(self, ctx, inputs, weights):
+        x = inputs[0]
+        if ctx.op_type in K.UNARY_CODES and K.tensorop_ok(x):
+            s = self._scalar(ctx)
+            return [K.unary(x, ctx.op_type, s)], ("hip", x, s)
+        return super().forward(ctx, inputs, weights)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        if saved[0] == "hip":
+            _, x, s = saved
+            g = grad_outputs[0]
+            return [K.unary(x, ctx.op_type, s, dy=g.contiguous().to(x.dtype)) if need_input_grad[0] else None]
+        return super().backward(ctx, saved, grad_outputs, weight_grads, need_input_grad)
 
 
 def _unbroadcast(g, shape):
@@ -118,6 +144,10 @@ class BinaryOp(OpImpl):
     def forward(self, ctx, inputs, weights):
         a, b = inputs
         op = ctx.op_type
+        if op in K.BINARY_CODES and a.dtype == b.dtype and K.tensorop_ok(a, b) and a.dim() <= 6 and b.dim() <= 6:
+            y = K.binary(a, b, op)
+            keep = (a, b) if op in ("EW_MUL", "EW_DIV", "EW_MAX", "EW_MIN") else (None, None)
+            return [y], ("hip", keep, tuple(a.shape), tuple(b.shape))
         with torch.no_grad():
             if op == "EW_ADD":
                 y = a + b
@@ -141,6 +171,13 @@ class BinaryOp(OpImpl):
         return [y], (keep, a.shape, b.shape)
 
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        if saved[0] == "hip":
+            _, (a, b), sa, sb = saved
+            g = grad_outputs[0].contiguous()
+            if a is not None and g.dtype != a.dtype:
+                g = g.to(a.dtype)
+            return [K.binary_grad(g, a, b, ctx.op_type, 0, sa, sb) if need_input_grad[0] else None,
+                    K.binary_grad(g, a, b, ctx.op_type, 1, sa, sb) if need_input_grad[1] else None]
         (a, b), sa, sb = saved
         g = grad_outputs[0]
         op = ctx.op_type

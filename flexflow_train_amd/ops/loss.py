@@ -96,6 +96,18 @@ class LossFunction:
             metrics[M_COUNT] += rows
             return ((torch.softmax(lf, -1) - y) * scale).to(logits.dtype).view(logits.shape)
         if lt in ("mean_squared_error", "mean_squared_error_sum"):
+            s = (2.0 / (self.global_rows * C)) if lt == "mean_squared_error" else 2.0
+            y = labels.reshape(logits.shape)
+            if (K.tensorop_ok(logits) and metrics.dtype == torch.float32 and metrics.is_cuda
+                    and logits.numel() > 0):
+                # fused HIP pass: grad + squared/absolute error sums (slots 3,4 adjacent)
+                y = y.to(logits.dtype).contiguous()
+                g = torch.empty_like(logits)
+                before = metrics[M_SQERR].clone()
+                K.mse(logits.contiguous(), y, g, metrics[M_SQERR:], s)
+                metrics[M_LOSS] += (metrics[M_SQERR] - before) / C
+                metrics[M_COUNT] += rows
+                return g
             p = logits.float()
             y = labels.reshape(p.shape).float()
             d = p - y
@@ -103,7 +115,6 @@ class LossFunction:
             metrics[M_ABSERR] += d.abs().sum()
             metrics[M_LOSS] += (d * d).sum() / C
             metrics[M_COUNT] += rows
-            s = (2.0 / (self.global_rows * C)) if lt == "mean_squared_error" else 2.0
             return (d * s).to(logits.dtype)
         # identity: the output itself is the loss
         metrics[M_LOSS] += logits.float().sum()

@@ -56,6 +56,10 @@ class ExecConfig:
     grad_clip: float = 0.0
     overlap_grad_sync: bool = True
     bf16_weight_grads: bool = True
+    # "counter": every rank generates only its own piece from a counter-based
+    # RNG keyed by the global element index (on-device on GPU);
+    # "host": full weight from a torch.Generator on every rank, then sliced.
+    init_mode: str = "counter"
 
 
 @dataclasses.dataclass
@@ -423,6 +427,9 @@ class Executor:
         """Deterministic initialisation: every rank generates the full logical
         weight from a seed derived from the weight name, then keeps its piece
         (identical across replicas without any broadcast)."""
+        if self.cfg.init_mode == "counter":
+            self._init_counter()
+            return
         for p in self.params:
             if not p.group:
                 continue
@@ -440,6 +447,28 @@ class Executor:
             if full is None:
                 full = make_initializer_tensor(p.initializer, p.logical_shape, gen)
             self._set_piece(p, full)
+        for f in self.flats:
+            if f["compute"] is not None:
+                f["compute"].copy_(f["master"])
+
+    def _init_counter(self):
+        from .initializers import counter_init_piece, counter_spec
+        for p in self.params:
+            if not p.group:
+                continue
+            impl = self._impl_of(p)
+            spec = None
+            if impl is not None:
+                ctx = opbase.OpContext(op_type=p.consumer_op, attrs=p.consumer_attrs, name=p.name)
+                spec = impl.init_spec(ctx, self._weight_index(p), p.logical_shape, p.initializer or {})
+            if spec is None:
+                spec = counter_spec(p.initializer, p.logical_shape)
+            box = p.layout.box(p.layout.coord(self.rank).shard)
+            piece = counter_init_piece(spec, p.logical_shape, box, _stable_seed(self.cfg.seed, p.name),
+                                       p.master.device)
+            p.master.copy_(self._to_physical(p, piece))
+            if p.compute is not p.master:
+                p.compute.copy_(p.master)
         for f in self.flats:
             if f["compute"] is not None:
                 f["compute"].copy_(f["master"])
