@@ -304,6 +304,34 @@ OpCost CostModel::op_cost(const OpAttrs& op, const std::vector<ParallelTensorSha
       c.backward += 2 * kernels * spec_.kernel_launch_overhead;
     }
   }
+  // Sequence-parallel attention (flexflow_train_amd/parallel/sequence.py):
+  // the piece costs above see S/s keys, the real core attends to all S, and
+  // the lowering moves data.  Ulysses (local heads divisible by s): 4
+  // all-to-alls of a q-sized piece each way.  Ring: s-1 K/V block hops
+  // forward (overlapped with the block compute), s hops of K/V/dK/dV back.
+  if (op.type == OpType::MULTIHEAD_ATTENTION && !inputs.empty() && inputs[0].num_dims() == 3 &&
+      inputs[0].dim(1).degree > 1 && !wp.empty()) {
+    const int s = inputs[0].dim(1).degree;
+    const double b = static_cast<double>(ip[0].dims[0]), sl = static_cast<double>(ip[0].dims[1]);
+    const double h = static_cast<double>(wp[0].dims[1]);
+    const double kd = op.i("kdim") > 0 ? static_cast<double>(op.i("kdim"))
+                                       : static_cast<double>(op.i("embed_dim")) / static_cast<double>(op.i("num_heads"));
+    double core = 4.0 * b * h * sl * sl * kd * (s - 1);
+    if (op.b("causal")) core *= 0.5;
+    const double core_t = gemm_time(core, 0.0, 0.8);
+    const double piece = b * sl * h * kd * 2.0;  // bf16 [B, S/s, H, d]
+    const bool ulysses = static_cast<int64_t>(h) % s == 0 && op.s("seq_parallel_mode") != "ring";
+    if (ulysses) {
+      const double a2a = CollectiveCost::all_to_all(piece, s, spec_);
+      c.forward += core_t + 4 * a2a;
+      c.backward += 2.5 * core_t + 4 * a2a;
+    } else {
+      const double hop_f = CollectiveCost::p2p(2 * piece, spec_);
+      const double hop_b = CollectiveCost::p2p(2 * piece + 4 * piece, spec_);
+      c.forward += std::max(core_t, (s - 1) * hop_f);
+      c.backward += std::max(2.5 * core_t, s * hop_b);
+    }
+  }
   // memory: weights (bf16 copy + fp32 master + fp32 m, v + grad) + saved activations
   double wmem = 0, sync = 0;
   for (size_t i = 0; i < weights.size(); ++i) {

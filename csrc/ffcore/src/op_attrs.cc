@@ -545,7 +545,8 @@ OpSpec mha_spec() {
   s.num_inputs = 3;
   s.required = {"embed_dim", "num_heads"};
   s.defaults = {{"kdim", int64_t(0)}, {"vdim", int64_t(0)}, {"dropout", 0.0}, {"bias", true},
-                {"add_bias_kv", false}, {"add_zero_attn", false}, {"causal", false}};
+                {"add_bias_kv", false}, {"add_zero_attn", false}, {"causal", false},
+                {"seq_parallel_mode", std::string("auto")}};  // auto | ulysses | ring
   s.weights = [](const OpAttrs& a) {
     std::vector<std::string> w{"weight"};
     if (a.b("bias")) {

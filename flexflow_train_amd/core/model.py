@@ -413,10 +413,14 @@ class FFModel:
         return self._add("DROPOUT", [input], name, rate=float(rate), seed=int(seed))
 
     def multihead_attention(self, query, key, value, embed_dim, num_heads, kdim=0, vdim=0, dropout=0.0, bias=True,
-                            add_bias_kv=False, add_zero_attn=False, kernel_initializer=None, causal=False, name=None):
+                            add_bias_kv=False, add_zero_attn=False, kernel_initializer=None, causal=False, name=None,
+                            seq_parallel_mode="auto"):
+        """``seq_parallel_mode`` selects the lowering when a strategy shards
+        the sequence dim: "ulysses" (all-to-all), "ring" or "auto"."""
         return self._add("MULTIHEAD_ATTENTION", [query, key, value], name, (kernel_initializer,),
                          embed_dim=embed_dim, num_heads=num_heads, kdim=kdim, vdim=vdim, dropout=float(dropout),
-                         bias=bias, add_bias_kv=add_bias_kv, add_zero_attn=add_zero_attn, causal=causal)
+                         bias=bias, add_bias_kv=add_bias_kv, add_zero_attn=add_zero_attn, causal=causal,
+                         seq_parallel_mode=seq_parallel_mode)
 
     def cast(self, input, dtype, name=None):
         return self._add("CAST", [input], name, dtype=_dt_str(dtype))

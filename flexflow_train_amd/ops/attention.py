@@ -24,6 +24,7 @@ import math
 import torch
 
 from .. import kernels as K
+from ..parallel import sequence as SP
 from .base import OpContext, OpImpl, acc_grad, register
 from .gemm import matmul
 
@@ -190,8 +191,13 @@ class MultiHeadAttentionOp(OpImpl):
             k = matmul(k_in.reshape(-1, Ek).contiguous(), ws["k"], bias=bk).view(B, Sk, Hl, kd)
             v = matmul(v_in.reshape(-1, Ev).contiguous(), ws["v"], bias=bv).view(B, Sk, Hl, vd)
             proj = (q, k, v)
+        grp = ctx.extra.get("seq_group")
         use_flash = (q.is_cuda and q.dtype == torch.bfloat16 and kd == vd and kd in (64, 128) and K.available())
-        if use_flash:
+        if grp is not None and grp.size > 1:
+            # sequence-sharded q/k/v: Ulysses all-to-all or ring attention
+            o, lse = SP.sp_attention_fwd(q, k, v, causal, scale, grp, SP.choose_mode(ctx.attrs, Hl, grp))
+            lse = ("sp", lse)
+        elif use_flash:
             o, lse = K.attention_fwd(q, k, v, causal=causal, scale=scale)
         else:
             o, lse = _torch_attention(q, k, v, causal, scale), None
@@ -232,7 +238,13 @@ class MultiHeadAttentionOp(OpImpl):
             q, k, v = qkv5[:, :, 0], qkv5[:, :, 1], qkv5[:, :, 2]
         else:
             q, k, v = proj
-        if lse is not None:
+        if isinstance(lse, tuple):
+            dq_, dk_, dv_ = SP.sp_attention_bwd(do4, lse[1], causal, scale, ctx.extra["seq_group"])
+            if self_attn:
+                dproj = torch.stack([dq_, dk_, dv_], dim=2).reshape(B * Sq, 3 * Hl * kd)
+            else:
+                dq, dk, dv = dq_, dk_, dv_
+        elif lse is not None:
             if self_attn:
                 dproj = torch.empty_like(qkv)
                 d5 = dproj.view(B, Sq, 3, Hl, kd)

@@ -36,6 +36,7 @@ from ..ops import base as opbase
 from ..ops.loss import N_SLOTS, LossFunction, PerfMetrics
 from ..parallel.comm import DistContext, Redistributor
 from ..parallel.layout import Layout, layout_from_pshape
+from ..parallel.sequence import SeqGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig
 from .initializers import make_initializer_tensor
 
@@ -219,6 +220,7 @@ class Executor:
 
         # ---- steps
         self.steps: List[Step] = []
+        self._sp_groups: set = set()
         self.value_layout: Dict[Value, Layout] = {}
         for nm, (t, lay, _) in self.inputs.items():
             self.value_layout[t] = lay
@@ -273,6 +275,18 @@ class Executor:
                 compute_dtype=self.cfg.compute_dtype, device=self.cfg.device,
                 seed=_stable_seed(self.cfg.seed, names[n], self.rank // max(1, olay.reps) if coord else 0),
                 output_shapes=[self.value_layout[o].piece_shape for o in outs])
+            if t == "MULTIHEAD_ATTENTION" and len(olay.degrees) >= 2 and olay.degrees[1] > 1:
+                # sequence-parallel attention: the ranks holding the other
+                # sequence chunks of the same (batch, head) slice
+                def _seq_ranks(c, lay=olay):
+                    return [lay.rank_of(dataclasses.replace(c, shard=(c.shard[0], j) + tuple(c.shard[2:])))
+                            for j in range(lay.degrees[1])]
+                for r in range(self.world):
+                    cr = olay.coord(r)
+                    if cr is not None:
+                        self._sp_groups.add(tuple(sorted(_seq_ranks(cr))))
+                if coord is not None:
+                    ctx.extra["seq_group"] = SeqGroup(self.dist, _seq_ranks(coord), coord.shard[1])
             if t in ("REDUCE_MEAN", "MEAN") and in0 is not None:
                 axes = [int(a) % len(in0.shard_dims) for a in attrs[n].get("axes", [])]
                 deg = math.prod(int(in0.shard_dims[a].degree) for a in axes)
@@ -414,6 +428,7 @@ class Executor:
                     if c is None:
                         continue
                     all_groups.add(tuple(sorted(lay.rank_of(dataclasses.replace(c, b=b)) for b in range(lay.b_deg))))
+            all_groups |= self._sp_groups
             for g in sorted(all_groups):
                 if len(g) > 1:
                     self.dist.group(g)

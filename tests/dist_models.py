@@ -52,3 +52,30 @@ def bert_tiny(m):
              "position_ids": torch.arange(S, dtype=torch.int32).expand(B, S).contiguous(),
              "token_type_ids": torch.randint(0, 2, (B, S), generator=g, dtype=torch.int32)}
     return feeds, torch.randint(0, 64, (B, S), generator=g)
+
+
+def _seq_attention(m, mode, causal, heads=4):
+    B, S, E = 2, 8, 32
+    x = m.create_tensor([B, S, E], DataType.DT_FLOAT, name="x")
+    a = m.multihead_attention(x, x, x, E, heads, causal=causal, seq_parallel_mode=mode, name="mha")
+    t = m.add(a, x, name="res")
+    t = m.dense(t, 10, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(13)
+    return {"x": torch.randn(B, S, E, generator=g)}, torch.randint(0, 10, (B, S), generator=g)
+
+
+def attention_ulysses(m):
+    return _seq_attention(m, "ulysses", False)
+
+
+def attention_ring(m):
+    return _seq_attention(m, "ring", False)
+
+
+def attention_ring_causal(m):
+    return _seq_attention(m, "ring", True)
+
+
+def attention_ulysses_causal(m):
+    return _seq_attention(m, "ulysses", True)

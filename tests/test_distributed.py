@@ -56,3 +56,28 @@ def test_bert_tiny_data_parallel_adam():
     ref = run_single(M.bert_tiny, optimizer="adam")
     out = run_distributed(M.bert_tiny, 2, optimizer="adam")
     assert_params_close(out["params"], ref["params"], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("fn", ["attention_ulysses", "attention_ring", "attention_ring_causal",
+                                "attention_ulysses_causal"])
+def test_attention_sequence_parallel(tmp_path, fn):
+    """Sequence-sharded attention (Ulysses all-to-all / ring attention)
+    matches the single-process run."""
+    model_fn = getattr(M, fn)
+    ref = run_single(model_fn)
+    path = str(tmp_path / "seq.json")
+    write_strategy(model_fn, 2, {"mha": {"batch": 1, "seq": 2}}, path)
+    out = run_distributed(model_fn, 2, path)
+    assert_params_close(out["params"], ref["params"])
+    kind = "sp_all_to_all" if "ulysses" in fn else "ring_p2p"
+    assert out["stats"].get(kind, 0) > 0, out["stats"]
+
+
+@pytest.mark.parametrize("fn", ["attention_ring_causal", "attention_ulysses"])
+def test_attention_sequence_parallel_4way(tmp_path, fn):
+    model_fn = getattr(M, fn)
+    ref = run_single(model_fn)
+    path = str(tmp_path / "seq4.json")
+    write_strategy(model_fn, 4, {"mha": {"batch": 1, "seq": 4}}, path)
+    out = run_distributed(model_fn, 4, path)
+    assert_params_close(out["params"], ref["params"])
