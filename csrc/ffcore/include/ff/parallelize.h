@@ -22,7 +22,7 @@
 
 namespace ff {
 
-enum class MPKind { NONE = 0, COLUMN = 1, ROW = 2, HEADS = 3 };
+enum class MPKind { NONE = 0, COLUMN = 1, ROW = 2, HEADS = 3, EXPERTS = 4 };
 std::string mp_kind_to_string(MPKind k);
 MPKind mp_kind_from_string(const std::string& s);
 
@@ -62,6 +62,9 @@ StrategyConfig data_parallel_strategy(const ComputationGraph& cg, int world);
 // cannot be parallelized that way).
 std::optional<std::vector<ParallelTensorShape>> required_input_shapes(const ComputationGraph& cg, int node,
                                                                       const LayerConfig& cfg);
+// The layer's attrs as lowered under `cfg` (all-to-all expert parallelism
+// records its expert degree on the op).
+OpAttrs configured_op(const OpAttrs& op, const LayerConfig& cfg);
 
 struct Lowering {
   ParallelComputationGraph pcg;

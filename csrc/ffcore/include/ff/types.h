@@ -52,7 +52,7 @@ DataType datatype_from_string(const std::string& s);
   X(SLICE) X(RESIZE) X(PRELU) X(GELU) X(MULTIHEAD_ATTENTION) X(FUSED) X(RSQRT) \
   X(POW) X(MEAN) X(LAYERNORM) X(GATHER) X(BROADCAST) X(REPARTITION) X(COMBINE) \
   X(REPLICATE) X(REDUCTION) X(BATCH) X(PIPELINE) X(FUSED_PARALLEL)             \
-  X(ALLTOALL)
+  X(ALLTOALL) X(EXPERTS)
 
 enum class OpType : int {
 #define FF_ENUM_ITEM(n) n,

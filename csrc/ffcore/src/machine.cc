@@ -332,6 +332,18 @@ OpCost CostModel::op_cost(const OpAttrs& op, const std::vector<ParallelTensorSha
       c.backward += std::max(2.5 * core_t, s * hop_b);
     }
   }
+  // All-to-all expert parallelism: dispatch + combine all-to-alls forward,
+  // their transposes backward (token pairs of this piece, bf16 rows).
+  if (op.type == OpType::EXPERTS && op.s("expert_parallel_mode") == "alltoall" && op.i("expert_degree") > 1 &&
+      ip.size() == 3) {
+    const int ed = static_cast<int>(op.i("expert_degree"));
+    const double pairs = static_cast<double>(ip[1].dims[0]) * static_cast<double>(ip[1].dims[1]);
+    const double disp = pairs * static_cast<double>(ip[0].dims[1]) * 2.0;
+    const double comb = pairs * static_cast<double>(op.i("out_dim")) * 2.0;
+    const double t = CollectiveCost::all_to_all(disp, ed, spec_) + CollectiveCost::all_to_all(comb, ed, spec_);
+    c.forward += t;
+    c.backward += t;
+  }
   // memory: weights (bf16 copy + fp32 master + fp32 m, v + grad) + saved activations
   double wmem = 0, sync = 0;
   for (size_t i = 0; i < weights.size(); ++i) {

@@ -1181,6 +1181,88 @@ OpSpec fused_parallel_spec() {
   return s;
 }
 
+// Mixture-of-experts FFN block (the reference's MoE example builds it from
+// top-k + group_by + dense experts + aggregate, examples/cpp/
+// mixture_of_experts/moe.cc:159-164, with operators its vocabulary lacks).
+// Inputs: x [B, D], expert ids [B, k] (int), gate weights [B, k].
+// Weights: w1 [E, D, H], b1 [E, H], w2 [E, H, O], b2 [E, O].
+// out[b] = sum_j gate[b, j] * expert_{id[b, j]}(x[b]).
+// Expert parallelism, two lowerings:
+//  * "replicated": token inputs carry discard_copy c; experts are sharded c
+//    ways; each rank applies only its experts -> output sum_degree c
+//    (resolved by a Reduction);
+//  * "alltoall": token inputs are batch-sharded; experts are sharded
+//    `expert_degree` ways across consecutive batch shards and tokens are
+//    dispatched / combined with all-to-alls inside the op.
+OpSpec experts_spec() {
+  OpSpec s;
+  s.num_inputs = 3;
+  s.required = {"num_experts", "hidden_size", "out_dim"};
+  s.defaults = {{"activation", std::string("relu")}, {"use_bias", true}, {"expert_degree", int64_t(1)},
+                {"expert_parallel_mode", std::string("replicated")}};
+  s.weights = [](const OpAttrs& a) {
+    if (a.b("use_bias")) return std::vector<std::string>{"w1", "b1", "w2", "b2"};
+    return std::vector<std::string>{"w1", "w2"};
+  };
+  s.out = [](const OpAttrs& a, const Shapes& in) {
+    require(nd(in[0]) == 2, a, "x must be [batch, features]");
+    require(nd(in[1]) == 2 && nd(in[2]) == 2, a, "expert ids / gates must be [batch, k]");
+    require(in[1].dims == in[2].dims && in[1].dims[0] == in[0].dims[0], a, "ids / gates / x batch mismatch");
+    require(in[1].dims[1] <= a.i("num_experts"), a, "k exceeds the number of experts");
+    return Shapes{TensorShape{{in[0].dims[0], a.i("out_dim")}, in[0].dtype}};
+  };
+  s.wts = [](const OpAttrs& a, const Shapes& in) {
+    const int64_t E = a.i("num_experts"), D = in[0].dims[1], H = a.i("hidden_size"), O = a.i("out_dim");
+    Shapes w{TensorShape{{E, D, H}, in[0].dtype}};
+    if (a.b("use_bias")) w.push_back(TensorShape{{E, H}, in[0].dtype});
+    w.push_back(TensorShape{{E, H, O}, in[0].dtype});
+    if (a.b("use_bias")) w.push_back(TensorShape{{E, O}, in[0].dtype});
+    return w;
+  };
+  auto parse = [](const OpAttrs& a, const PShapes& in) {
+    for (auto const& t : in) {
+      require(t.num_dims() == 2, a, "rank-2 inputs");
+      require(t.sum_degree == 1, a, "inputs cannot be partial sums");
+      require(t.dim(1).degree == 1, a, "feature / k dims must be unpartitioned");
+      require(t.dim(0).degree == in[0].dim(0).degree, a, "batch degrees differ");
+      require(t.discard_copy_degree == in[0].discard_copy_degree, a, "replica degrees differ");
+    }
+    const int c = in[0].discard_copy_degree;
+    require(a.i("num_experts") % c == 0, a, "experts not divisible by the expert degree");
+    if (a.s("expert_parallel_mode") == "alltoall") {
+      const int ed = static_cast<int>(a.i("expert_degree"));
+      require(c == 1, a, "all-to-all expert parallelism takes batch-sharded (not replicated) tokens");
+      require(ed >= 1 && in[0].dim(0).degree % ed == 0, a, "expert degree must divide the batch degree");
+      require(a.i("num_experts") % ed == 0, a, "experts not divisible by the expert degree");
+    }
+  };
+  s.pout = [parse](const OpAttrs& a, const PShapes& in) {
+    parse(a, in);
+    auto o = registry()[static_cast<int>(OpType::EXPERTS)].out(
+        a, {in[0].reduced_shape(), in[1].reduced_shape(), in[2].reduced_shape()})[0];
+    return PShapes{lift_to_parallel_with_degrees(o, in[0].discard_copy_degree, 1, {in[0].dim(0).degree, 1})};
+  };
+  s.pwts = [parse](const OpAttrs& a, const PShapes& in) {
+    parse(a, in);
+    auto ws = registry()[static_cast<int>(OpType::EXPERTS)].wts(
+        a, {in[0].reduced_shape(), in[1].reduced_shape(), in[2].reduced_shape()});
+    const int bx = in[0].dim(0).degree;
+    int ed = in[0].discard_copy_degree, copies = bx;
+    if (a.s("expert_parallel_mode") == "alltoall") {
+      ed = static_cast<int>(a.i("expert_degree"));
+      copies = bx / ed;
+    }
+    PShapes r;
+    for (auto const& w : ws) {
+      std::vector<int> deg(w.num_dims(), 1);
+      deg[0] = ed;
+      r.push_back(lift_to_parallel_with_degrees(w, 1, copies, deg));
+    }
+    return r;
+  };
+  return s;
+}
+
 OpSpec noop_spec() { return unary_spec(); }
 
 std::unordered_map<int, OpSpec> build_registry() {
@@ -1236,6 +1318,7 @@ std::unordered_map<int, OpSpec> build_registry() {
   put(OpType::REDUCTION, reduction_spec());
   put(OpType::ALLTOALL, alltoall_spec());
   put(OpType::FUSED_PARALLEL, fused_parallel_spec());
+  put(OpType::EXPERTS, experts_spec());
   return r;
 }
 
@@ -1357,6 +1440,19 @@ OpWork estimate_op_work(const OpAttrs& a, const std::vector<TensorShape>& in,
       if (a.b("causal")) r.flops -= 2 * b * h * sq * sk * kd;
       r.matmul_like = true;
       r.mfma_efficiency_hint = 0.8;
+      break;
+    }
+    case OpType::EXPERTS: {
+      // dropless routing: B*k token-expert pairs through two GEMMs, spread
+      // evenly over the expert shards of this piece
+      const double pairs = static_cast<double>(in[1].dims[0]) * static_cast<double>(in[1].dims[1]);
+      const double E = static_cast<double>(a.i("num_experts")), El = static_cast<double>(w[0].dims[0]);
+      const double D = static_cast<double>(in[0].dims[1]), H = static_cast<double>(a.i("hidden_size"));
+      const double O = static_cast<double>(a.i("out_dim"));
+      r.flops = 2 * pairs * (El / E) * (D * H + H * O);
+      r.bytes = static_cast<double>(w[0].size_bytes()) * (1 + (O / D)) + 4 * pairs * (D + O);
+      r.matmul_like = true;
+      r.mfma_efficiency_hint = std::min(1.0, pairs * (El / E) / El / 512.0 + 0.2);
       break;
     }
     case OpType::EMBEDDING:

@@ -12,6 +12,7 @@ std::string mp_kind_to_string(MPKind k) {
     case MPKind::COLUMN: return "column";
     case MPKind::ROW: return "row";
     case MPKind::HEADS: return "heads";
+    case MPKind::EXPERTS: return "experts";
   }
   return "none";
 }
@@ -20,6 +21,7 @@ MPKind mp_kind_from_string(const std::string& s) {
   if (s == "column") return MPKind::COLUMN;
   if (s == "row") return MPKind::ROW;
   if (s == "heads") return MPKind::HEADS;
+  if (s == "experts") return MPKind::EXPERTS;
   if (s == "none" || s.empty()) return MPKind::NONE;
   throw FFError("unknown model-parallel kind '" + s + "'");
 }
@@ -71,6 +73,7 @@ bool is_mp_capable(const OpAttrs& op, MPKind k) {
       if (k == MPKind::ROW) return activation_from_string(op.s("activation")) == Activation::NONE;
       return false;
     case OpType::MULTIHEAD_ATTENTION: return k == MPKind::HEADS;
+    case OpType::EXPERTS: return k == MPKind::EXPERTS;
     case OpType::EMBEDDING: return k == MPKind::COLUMN && op.s("aggr") == "none";
     default: return false;
   }
@@ -91,10 +94,19 @@ ParallelTensorShape batch_seq_shape(const TensorShape& s, const TensorShape& ref
 
 }  // namespace
 
+OpAttrs configured_op(const OpAttrs& op, const LayerConfig& cfg) {
+  if (op.type == OpType::EXPERTS && cfg.kind == MPKind::EXPERTS && op.s("expert_parallel_mode") == "alltoall") {
+    OpAttrs o = op;
+    o.set("expert_degree", static_cast<int64_t>(cfg.model));
+    return o;
+  }
+  return op;
+}
+
 std::optional<std::vector<ParallelTensorShape>> required_input_shapes(const ComputationGraph& cg, int node,
                                                                       const LayerConfig& cfg) {
   auto const& n = cg.g.node(node);
-  auto const& op = n.label.op;
+  const OpAttrs op = configured_op(n.label.op, cfg);
   auto data = cg.layer_data_inputs(node);
   if (data.empty()) return std::vector<ParallelTensorShape>{};
   std::vector<TensorShape> ss;
@@ -125,6 +137,18 @@ std::optional<std::vector<ParallelTensorShape>> required_input_shapes(const Comp
       case MPKind::HEADS: {
         if (op.i("num_heads") % cfg.model) return std::nullopt;
         for (auto& p : ps) p.discard_copy_degree = cfg.model;
+        break;
+      }
+      case MPKind::EXPERTS: {
+        if (op.i("num_experts") % cfg.model) return std::nullopt;
+        if (op.s("expert_parallel_mode") == "alltoall") {
+          // tokens spread over batch x expert ranks, dispatched in the op
+          const int64_t B = ref.dims[0];
+          if (B % (static_cast<int64_t>(cfg.batch) * cfg.model)) return std::nullopt;
+          for (auto& p : ps) p.shard_dims[0].degree = cfg.batch * cfg.model;
+        } else {
+          for (auto& p : ps) p.discard_copy_degree = cfg.model;
+        }
         break;
       }
       default: return std::nullopt;
@@ -283,14 +307,15 @@ Lowering lower_strategy(const ComputationGraph& cg, const StrategyConfig& cfg, i
     for (size_t i = 0; i < data.size(); ++i) din.push_back(convert(vm.at(data[i]), (*req)[i]));
     std::vector<ParallelTensorShape> ps;
     for (auto const& v : din) ps.push_back(p.shape(v));
-    auto wshapes = infer_parallel_weight_shapes(n.label.op, ps);
+    const OpAttrs op = configured_op(n.label.op, c);
+    auto wshapes = infer_parallel_weight_shapes(op, ps);
     std::vector<ValueRef> all = din;
     for (size_t i = 0; i < wts.size(); ++i) {
       auto const& wn = cg.g.node(wts[i].node);
       all.push_back(p.add_weight(wn.outputs[0].shape, wshapes[i], wn.outputs[0].initializer,
                                  wn.outputs[0].create_grad, wn.label.name));
     }
-    auto outs = p.add_layer(n.label.op, all, n.label.name);
+    auto outs = p.add_layer(op, all, n.label.name);
     L.cg_to_pcg[id] = outs.empty() ? -1 : outs[0].node;
     for (size_t i = 0; i < outs.size(); ++i) vm[{id, static_cast<int>(i)}] = outs[i];
   }

@@ -50,6 +50,12 @@ class Layout:
     block: int = 1          # number of ranks in the device block
     start: int = 0          # first rank of the block
     summed: str = "a"       # which of a / b is summed ("a": forward, "b": gradient)
+    # Parameters place their copy axis OUTERMOST: a weight's copies follow
+    # the consumer's outer (batch / sequence) task dims while its shards
+    # follow the consumer's inner copy / last-dim axes, so DP x TP puts a
+    # TP group's weight shards on consecutive ranks, exactly where the
+    # matching activation pieces live.
+    copy_outer: bool = False
 
     def __post_init__(self):
         if len(self.sizes) != len(self.degrees):
@@ -93,17 +99,27 @@ class Layout:
         if idx < 0 or idx >= self.block:
             return None
         lin, rep = divmod(idx, self.reps)
-        dims = list(self.degrees) + [self.a_deg, self.b_deg]
+        dims = self._dims()
         c = []
         for d in reversed(dims):
             lin, r = divmod(lin, d)
             c.append(r)
         c.reverse()
+        if self.copy_outer:
+            return Coord(tuple(c[1:-1]), c[-1], c[0], rep)
         return Coord(tuple(c[:-2]), c[-2], c[-1], rep)
 
+    def _dims(self) -> List[int]:
+        if self.copy_outer:
+            return [self.b_deg] + list(self.degrees) + [self.a_deg]
+        return list(self.degrees) + [self.a_deg, self.b_deg]
+
     def rank_of(self, coord: Coord) -> int:
-        dims = list(self.degrees) + [self.a_deg, self.b_deg]
-        vals = list(coord.shard) + [coord.a, coord.b]
+        dims = self._dims()
+        if self.copy_outer:
+            vals = [coord.b] + list(coord.shard) + [coord.a]
+        else:
+            vals = list(coord.shard) + [coord.a, coord.b]
         lin = 0
         for d, v in zip(dims, vals):
             lin = lin * d + v

@@ -182,7 +182,7 @@ class Executor:
                 cur = inputs_of[cur[0]][0]
             consumers = [c for (c, _) in uses.get(t, [])]
             cnode = consumers[0] if consumers else n
-            lay = self._layout(t, node_for_view=cnode)
+            lay = dataclasses.replace(self._layout(t, node_for_view=cnode), copy_outer=True)
             init = json.loads(attrs[n].get("initializer") or '{"type":"zero"}')
             cattrs = dict(attrs[cnode])
             if cnode != n:  # data-input feature sizes (physical weight layouts depend on them)

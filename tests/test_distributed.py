@@ -81,3 +81,19 @@ def test_attention_sequence_parallel_4way(tmp_path, fn):
     write_strategy(model_fn, 4, {"mha": {"batch": 1, "seq": 4}}, path)
     out = run_distributed(model_fn, 4, path)
     assert_params_close(out["params"], ref["params"])
+
+
+def test_dp_x_tp_4way(tmp_path):
+    """Data parallel x tensor parallel on 4 ranks (2 x 2): column/row
+    Linear pairs and head-parallel attention inside DP replicas."""
+    ref = run_single(M.mlp)
+    path = str(tmp_path / "m.json")
+    write_strategy(M.mlp, 4, {"fc0": {"batch": 2, "model": 2, "kind": "column"},
+                              "fc1": {"batch": 2, "model": 2, "kind": "row"}}, path)
+    out = run_distributed(M.mlp, 4, path)
+    assert_params_close(out["params"], ref["params"])
+    ref = run_single(M.attention)
+    path = str(tmp_path / "h.json")
+    write_strategy(M.attention, 4, {"mha": {"batch": 2, "model": 2, "kind": "heads"}}, path)
+    out = run_distributed(M.attention, 4, path)
+    assert_params_close(out["params"], ref["params"])
