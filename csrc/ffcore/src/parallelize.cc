@@ -177,7 +177,7 @@ std::vector<LayerConfig> candidate_configs(const ComputationGraph& cg, int node,
   if (op.type == OpType::WEIGHT) return {LayerConfig{}};
   std::vector<MPKind> kinds{MPKind::NONE};
   if (opt.enable_parameter_parallel)
-    for (MPKind k : {MPKind::COLUMN, MPKind::ROW, MPKind::HEADS})
+    for (MPKind k : {MPKind::COLUMN, MPKind::ROW, MPKind::HEADS, MPKind::EXPERTS})
       if (is_mp_capable(op, k)) kinds.push_back(k);
   for (int b : divisors(world))
     for (int q : divisors(world / b)) {

@@ -422,6 +422,27 @@ class FFModel:
                          bias=bias, add_bias_kv=add_bias_kv, add_zero_attn=add_zero_attn, causal=causal,
                          seq_parallel_mode=seq_parallel_mode)
 
+    def experts(self, input, expert_ids, gate_weights, num_experts, hidden_size, out_dim=None,
+                activation=ActiMode.AC_MODE_RELU, use_bias=True, expert_parallel_mode="replicated", name=None):
+        """Routed expert FFN block: ``input`` [B, D], ``expert_ids`` /
+        ``gate_weights`` [B, k] (e.g. the indices / values of ``top_k``)."""
+        out_dim = out_dim or input.dims[-1]
+        return self._add("EXPERTS", [input, expert_ids, gate_weights], name, num_experts=num_experts,
+                         hidden_size=hidden_size, out_dim=out_dim, activation=_act(activation), use_bias=use_bias,
+                         expert_parallel_mode=expert_parallel_mode)
+
+    def moe(self, input, num_exp, num_select, expert_hidden_size, alpha=2.0, lambda_bal=0.04, out_dim=None,
+            expert_parallel_mode="replicated", name=None):
+        """Mixture of experts (reference: examples/cpp/mixture_of_experts/
+        moe.cc:159-164): softmax gate -> top-k -> routed experts.  ``alpha``
+        (capacity factor) and ``lambda_bal`` (balance loss) are accepted for
+        API parity; routing here is dropless."""
+        nm = name or self._uname(None, "moe")
+        gate = self.softmax(self.dense(input, num_exp, name=f"{nm}.gate"), name=f"{nm}.gate_softmax")
+        vals, idx = self.top_k(gate, num_select, True, name=f"{nm}.topk")
+        return self.experts(input, idx, vals, num_exp, expert_hidden_size, out_dim=out_dim,
+                            expert_parallel_mode=expert_parallel_mode, name=f"{nm}.experts")
+
     def cast(self, input, dtype, name=None):
         return self._add("CAST", [input], name, dtype=_dt_str(dtype))
 

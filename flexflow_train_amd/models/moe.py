@@ -2,13 +2,12 @@
 input -> gate (Dense + softmax + top-k) -> experts -> aggregate -> softmax).
 
 The reference's ``ff.moe`` relies on GROUP_BY / AGGREGATE operators that do
-not exist in its operator vocabulary.  Here the gating is
-expressed with existing operators: the top-k of the gate's softmax selects
-the experts, every expert is a Dense applied to the whole batch, and the
-output is the gate-weighted sum of the experts restricted to the top-k
-(probabilities below the k-th largest are zeroed with a comparison mask).
-Experts are independent branches of the PCG, so the machine-mapping search
-can place them on disjoint device blocks (expert parallelism by placement).
+not exist in its operator vocabulary.  Here ``FFModel.moe``
+builds the softmax gate and top-k selection from ordinary operators and
+routes tokens through the EXPERTS operator (ops/moe.py), which the search can
+shard expert-parallel (replicated tokens + partial sums, or all-to-all
+dispatch).  ``build_moe_dense_gating`` keeps the original formulation in
+which every expert is its own Dense branch (expert parallelism by placement).
 """
 from __future__ import annotations
 
@@ -27,9 +26,17 @@ class MoEConfig:
     num_select: int = 2
     expert_hidden: int = 512
     num_classes: int = 10
+    expert_parallel_mode: str = "replicated"
 
 
 def build_moe(model: FFModel, cfg: MoEConfig):
+    x = model.create_tensor([cfg.batch_size, cfg.input_dim], DataType.DT_FLOAT, name="input")
+    h = model.moe(x, cfg.num_experts, cfg.num_select, cfg.expert_hidden, out_dim=cfg.num_classes,
+                  expert_parallel_mode=cfg.expert_parallel_mode, name="moe")
+    return {"input": x}, model.softmax(h, name="softmax")
+
+
+def build_moe_dense_gating(model: FFModel, cfg: MoEConfig):
     x = model.create_tensor([cfg.batch_size, cfg.input_dim], DataType.DT_FLOAT, name="input")
     gate = model.softmax(model.dense(x, cfg.num_experts, name="gate"), name="gate_softmax")
     vals, _ = model.top_k(gate, cfg.num_select, True, name="gate_topk")

@@ -37,6 +37,7 @@ from ..ops.loss import N_SLOTS, LossFunction, PerfMetrics
 from ..parallel.comm import DistContext, Redistributor
 from ..parallel.layout import Layout, layout_from_pshape
 from ..parallel.sequence import SeqGroup
+from ..ops.moe import ExpertGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig
 from .initializers import make_initializer_tensor
 
@@ -287,6 +288,22 @@ class Executor:
                         self._sp_groups.add(tuple(sorted(_seq_ranks(cr))))
                 if coord is not None:
                     ctx.extra["seq_group"] = SeqGroup(self.dist, _seq_ranks(coord), coord.shard[1])
+            if (t == "EXPERTS" and attrs[n].get("expert_parallel_mode") == "alltoall"
+                    and int(attrs[n].get("expert_degree", 1)) > 1 and wpieces):
+                # all-to-all expert parallelism: ranks holding the other expert
+                # shards of the same weight replica exchange tokens
+                wl = wpieces[0].layout
+
+                def _ep_ranks(c, lay=wl):
+                    return [lay.rank_of(dataclasses.replace(c, shard=(e,) + tuple(c.shard[1:])))
+                            for e in range(lay.degrees[0])]
+                for r in range(self.world):
+                    cr = wl.coord(r)
+                    if cr is not None:
+                        self._sp_groups.add(tuple(sorted(_ep_ranks(cr))))
+                cw = wl.coord(self.rank)
+                if cw is not None:
+                    ctx.extra["ep_group"] = ExpertGroup(self.dist, _ep_ranks(cw), cw.shard[0])
             if t in ("REDUCE_MEAN", "MEAN") and in0 is not None:
                 axes = [int(a) % len(in0.shard_dims) for a in attrs[n].get("axes", [])]
                 deg = math.prod(int(in0.shard_dims[a].degree) for a in axes)

@@ -79,3 +79,20 @@ def attention_ring_causal(m):
 
 def attention_ulysses_causal(m):
     return _seq_attention(m, "ulysses", True)
+
+
+def _moe(m, mode):
+    B, D, E, k = 8, 12, 4, 2
+    x = m.create_tensor([B, D], DataType.DT_FLOAT, name="x")
+    h = m.moe(x, E, k, 16, out_dim=6, expert_parallel_mode=mode, name="moe")
+    m.softmax(h, name="sm")
+    g = torch.Generator().manual_seed(17)
+    return {"x": torch.randn(B, D, generator=g)}, torch.randint(0, 6, (B,), generator=g)
+
+
+def moe_replicated(m):
+    return _moe(m, "replicated")
+
+
+def moe_alltoall(m):
+    return _moe(m, "alltoall")

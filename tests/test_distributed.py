@@ -97,3 +97,23 @@ def test_dp_x_tp_4way(tmp_path):
     write_strategy(M.attention, 4, {"mha": {"batch": 2, "model": 2, "kind": "heads"}}, path)
     out = run_distributed(M.attention, 4, path)
     assert_params_close(out["params"], ref["params"])
+
+
+@pytest.mark.parametrize("fn,world,cfg", [
+    ("moe_replicated", 2, {"batch": 1, "model": 2, "kind": "experts"}),
+    ("moe_alltoall", 2, {"batch": 1, "model": 2, "kind": "experts"}),
+    ("moe_alltoall", 4, {"batch": 1, "model": 4, "kind": "experts"}),
+    ("moe_alltoall", 4, {"batch": 2, "model": 2, "kind": "experts"}),
+    ("moe_replicated", 4, {"batch": 2, "model": 2, "kind": "experts"}),
+])
+def test_moe_expert_parallel(tmp_path, fn, world, cfg):
+    """Expert parallelism (replicated tokens + reduction, or all-to-all
+    dispatch) matches the single-process MoE."""
+    model_fn = getattr(M, fn)
+    ref = run_single(model_fn)
+    path = str(tmp_path / "ep.json")
+    write_strategy(model_fn, world, {"moe.experts": cfg}, path)
+    out = run_distributed(model_fn, world, path)
+    assert_params_close(out["params"], ref["params"])
+    if "alltoall" in fn:
+        assert out["stats"].get("ep_all_to_all", 0) > 0, out["stats"]
