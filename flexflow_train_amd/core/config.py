@@ -57,6 +57,8 @@ class FFConfig:
     search_algorithm: str = "unity"    # unity | mcmc | data_parallel
     compute_dtype: str = "bfloat16"    # bfloat16 on GPU; CPU runs float unless asked
     seed: int = 0
+    shard_optimizer: bool = False      # ZeRO-style sharded optimizer state (reduce-scatter + all-gather)
+    bucket_mb: int = 64                # gradient all-reduce bucket size
     _start_time: float = dataclasses.field(default_factory=time.time)
 
     def __post_init__(self):
@@ -138,6 +140,8 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--substitution-json", dest="substitution_json_path", type=str)
     a("--search-algorithm", dest="search_algorithm", type=str)
     a("--compute-dtype", dest="compute_dtype", type=str)
+    a("--shard-optimizer", "--zero", dest="shard_optimizer", action="store_const", const=True)
+    a("--bucket-mb", dest="bucket_mb", type=int)
     a("--seed", dest="seed", type=int)
     # Legion / Realm flags: accepted, ignored
     for f in ("-ll:fsize", "-ll:zsize", "-ll:util", "-ll:bgwork", "-ll:csize", "-lg:prof", "-lg:prof_logfile"):

@@ -489,7 +489,9 @@ class FFModel:
         cdt = {"bfloat16": torch.bfloat16, "float": torch.float32, "float32": torch.float32,
                "half": torch.float16}[dt]
         cfg = ExecConfig(compute_dtype=cdt, device=device, seed=self.ffconfig.seed,
-                         profiling=self.ffconfig.profiling, fuse_add_layernorm=self.ffconfig.perform_fusion)
+                         profiling=self.ffconfig.profiling, fuse_add_layernorm=self.ffconfig.perform_fusion,
+                         shard_optimizer=bool(self.ffconfig.shard_optimizer),
+                         bucket_bytes=int(self.ffconfig.bucket_mb) << 20)
         out_v = None
         if output is not None:
             out_v = self._pcg_value_of(output)

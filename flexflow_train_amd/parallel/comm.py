@@ -83,6 +83,38 @@ class DistContext:
         self.stats["bytes"] += t.numel() * t.element_size()
         return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
 
+    def reduce_scatter_(self, t: torch.Tensor, ranks: Sequence[int], async_op: bool = False):
+        """In-place reduce-scatter of the 1-D ``t``: afterwards chunk i (of
+        len(ranks) equal chunks) on the i-th rank of sorted(ranks) holds the
+        sum.  RCCL runs it in place (output = input + rank * chunk); gloo has
+        no reduce-scatter, so the CPU path all-reduces (a superset)."""
+        if len(ranks) <= 1 or not self.distributed:
+            return None
+        self.stats["reduce_scatter"] = self.stats.get("reduce_scatter", 0) + 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+        if t.is_cuda:
+            n = len(ranks)
+            i = sorted(ranks).index(self.rank)
+            chunk = t.numel() // n
+            return dist.reduce_scatter_tensor(t[i * chunk:(i + 1) * chunk], t, group=self.group(ranks),
+                                              async_op=async_op)
+        return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
+
+    def all_gather_(self, t: torch.Tensor, ranks: Sequence[int]):
+        """In-place all-gather of the equal chunks of the 1-D ``t`` (chunk i
+        comes from the i-th rank of sorted(ranks))."""
+        if len(ranks) <= 1 or not self.distributed:
+            return
+        n = len(ranks)
+        i = sorted(ranks).index(self.rank)
+        chunk = t.numel() // n
+        self.stats["all_gather"] += 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+        if t.is_cuda:
+            dist.all_gather_into_tensor(t, t[i * chunk:(i + 1) * chunk], group=self.group(ranks))
+        else:
+            dist.all_gather(list(t.split(chunk)), t[i * chunk:(i + 1) * chunk].clone(), group=self.group(ranks))
+
     def max_scalar(self, v: float) -> float:
         if not self.distributed:
             return v

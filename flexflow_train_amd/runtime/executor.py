@@ -38,7 +38,7 @@ from ..parallel.comm import DistContext, Redistributor
 from ..parallel.layout import Layout, layout_from_pshape
 from ..parallel.sequence import SeqGroup
 from ..ops.moe import ExpertGroup
-from .optimizer import AdamConfig, FlatOptimizer, SGDConfig
+from .optimizer import AdamConfig, FlatOptimizer, SGDConfig, ShardedOptimizer
 from .initializers import make_initializer_tensor
 
 Value = Tuple[int, int]
@@ -62,6 +62,10 @@ class ExecConfig:
     # RNG keyed by the global element index (on-device on GPU);
     # "host": full weight from a torch.Generator on every rank, then sliced.
     init_mode: str = "counter"
+    # ZeRO-style sharded optimizer: gradients are reduce-scattered, each rank
+    # of a data-parallel group updates (and keeps Adam state for) one shard
+    # of every bucket, and the updated weights are all-gathered.
+    shard_optimizer: bool = False
 
 
 @dataclasses.dataclass
@@ -398,12 +402,36 @@ class Executor:
             groups.setdefault((p.group, str(p.grad_dtype)), []).append(p)
         self.flats = []
         for fid, ((g, gdt), plist) in enumerate(sorted(groups.items(), key=lambda kv: kv[0])):
-            off = 0
+            zero = self.cfg.shard_optimizer and len(g) > 1
+            esize = torch.tensor([], dtype=plist[0].grad_dtype).element_size()
+            # buckets: contiguous param ranges, finalised in backward order
+            buckets, cur, cur_bytes = [], [], 0
             for p in plist:
                 p.numel = int(math.prod(p.layout.piece_shape))
-                p.offset = off
-                p.flat_id = fid
-                off += (p.numel + 63) // 64 * 64
+                cur.append(p)
+                cur_bytes += p.numel * esize
+                if cur_bytes >= self.cfg.bucket_bytes:
+                    buckets.append(cur)
+                    cur, cur_bytes = [], 0
+            if cur:
+                buckets.append(cur)
+            # sharded optimizer: every bucket splits evenly over the group
+            unit = 64 * (len(g) if zero else 1)
+            off = 0
+            binfo = []
+            for b in buckets:
+                lo = off
+                for p in b:
+                    p.offset = off
+                    p.flat_id = fid
+                    off += (p.numel + 63) // 64 * 64
+                off = (off + unit - 1) // unit * unit
+                info = {"params": b, "lo": lo, "hi": off, "pending": 0}
+                if zero:
+                    S = (off - lo) // len(g)
+                    gi = g.index(self.rank)
+                    info["shard"] = (lo + gi * S, lo + (gi + 1) * S)
+                binfo.append(info)
             master = torch.zeros(off, dtype=torch.float32, device=dev)
             grad = torch.zeros(off, dtype=plist[0].grad_dtype, device=dev)
             compute = torch.zeros(off, dtype=cd, device=dev) if cd != torch.float32 else None
@@ -412,24 +440,12 @@ class Executor:
                 p.master = master[p.offset:p.offset + p.numel].view(shp)
                 p.grad = grad[p.offset:p.offset + p.numel].view(shp)
                 p.compute = (compute[p.offset:p.offset + p.numel].view(shp) if compute is not None else p.master)
-            # buckets: contiguous param ranges, finalised in backward order
-            buckets, cur, cur_bytes = [], [], 0
-            for p in plist:
-                cur.append(p)
-                cur_bytes += p.numel * grad.element_size()
-                if cur_bytes >= self.cfg.bucket_bytes:
-                    buckets.append(cur)
-                    cur, cur_bytes = [], 0
-            if cur:
-                buckets.append(cur)
-            binfo = []
-            for b in buckets:
-                lo = b[0].offset
-                hi = b[-1].offset + (b[-1].numel + 63) // 64 * 64
-                binfo.append({"params": b, "lo": lo, "hi": hi, "pending": 0})
-            opt = FlatOptimizer(self.optimizer_cfg, master, grad, compute)
+            if zero:
+                opt = ShardedOptimizer(self.optimizer_cfg, master, grad, compute, [b["shard"] for b in binfo])
+            else:
+                opt = FlatOptimizer(self.optimizer_cfg, master, grad, compute)
             self.flats.append({"group": g, "params": plist, "master": master, "grad": grad, "compute": compute,
-                               "buckets": binfo, "opt": opt})
+                               "buckets": binfo, "opt": opt, "zero": zero})
         self._param_bucket = {}
         for f in self.flats:
             for bi, b in enumerate(f["buckets"]):
@@ -540,6 +556,7 @@ class Executor:
 
     def get_parameter(self, name: str) -> torch.Tensor:
         """Full logical weight (gathered across ranks)."""
+        self._gather_masters()
         p = next(pp for pp in self.params if pp.name == name)
         full = torch.zeros(p.logical_shape, dtype=torch.float32, device=self.cfg.device)
         c = p.layout.coord(self.rank)
@@ -759,10 +776,32 @@ class Executor:
 
     def _launch_bucket(self, f, b):
         if len(f["group"]) > 1 and self.dist.distributed and not b.get("launched"):
-            w = self.dist.all_reduce_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
+            if f["zero"]:
+                # sharded optimizer: each rank only needs the sum of its shard
+                w = self.dist.reduce_scatter_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
+            else:
+                w = self.dist.all_reduce_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
             b["launched"] = True
             if w is not None:
                 self._works.append(w)
+
+    def _gather_updated(self):
+        """Sharded optimizer: all-gather every bucket's updated compute copy
+        (the bf16 weights, or the fp32 master when computing in fp32)."""
+        for f in self.flats:
+            if not f["zero"] or not self.dist.distributed:
+                continue
+            tgt = f["compute"] if f["compute"] is not None else f["master"]
+            for b in f["buckets"]:
+                self.dist.all_gather_(tgt[b["lo"]:b["hi"]], f["group"])
+
+    def _gather_masters(self):
+        """Make the fp32 masters whole again (checkpoints, get_parameter)."""
+        for f in self.flats:
+            if not f["zero"] or not self.dist.distributed or f["compute"] is None:
+                continue
+            for b in f["buckets"]:
+                self.dist.all_gather_(f["master"][b["lo"]:b["hi"]], f["group"])
 
     def _finish_grad_sync(self):
         for f in self.flats:
@@ -784,14 +823,23 @@ class Executor:
                 scale = self.cfg.grad_clip / (norm + 1e-6)
         for f in self.flats:
             f["opt"].step(lr=lr, grad_scale=scale)
+        self._gather_updated()
         self.step_num += 1
 
     def grad_norm(self) -> float:
         # every logical gradient element counted once: only the canonical
         # owner (copy 0, partial replica 0, implicit replica 0) of each shard
         tot = torch.zeros(1, device=self.cfg.device, dtype=torch.float64)
+        for f in self.flats:
+            if f["zero"]:
+                # reduce-scattered: every rank of the group owns one shard of the sum
+                c = f["params"][0].layout.coord(self.rank)
+                if c is not None and c.a == 0 and c.rep == 0:
+                    for b in f["buckets"]:
+                        s0, s1 = b["shard"]
+                        tot += f["grad"][s0:s1].double().pow(2).sum()
         for p in self.params:
-            if not p.group or p.grad is None:
+            if not p.group or p.grad is None or self.flats[p.flat_id]["zero"]:
                 continue
             c = p.layout.coord(self.rank)
             if c is not None and c.b == 0 and c.a == 0 and c.rep == 0:
@@ -887,6 +935,7 @@ class Executor:
     # ------------------------------------------------------------ checkpoint
     def state_dict(self) -> Dict[str, Any]:
         """Local (this rank's) shards + optimizer state + shard metadata."""
+        self._gather_masters()
         st = {"step": self.step_num, "rank": self.rank, "world": self.world, "params": {}, "optimizer": []}
         for p in self.params:
             if p.group:

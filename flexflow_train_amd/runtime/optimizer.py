@@ -107,3 +107,53 @@ class FlatOptimizer:
             self.master.add_(g, alpha=-lr)
         if self.bf16 is not None:
             self.bf16.copy_(self.master)
+
+
+class ShardedOptimizer:
+    """ZeRO-style sharded optimizer over one flat buffer: this rank updates
+    (and keeps optimizer state for) only its shard of every gradient bucket;
+    the executor reduce-scatters gradients into those shards and all-gathers
+    the updated weights.  Optimizer memory and update traffic drop by the
+    data-parallel degree; the collective volume equals one all-reduce.
+    (The reference has no sharded optimizer)"""
+
+    def __init__(self, cfg, master: torch.Tensor, grad: torch.Tensor, bf16_copy: Optional[torch.Tensor],
+                 shards):
+        self.cfg = cfg
+        self.master = master
+        self.shards = list(shards)
+        self.parts = [FlatOptimizer(cfg, master[a:b], grad[a:b], bf16_copy[a:b] if bf16_copy is not None else None)
+                      for a, b in self.shards]
+
+    @property
+    def step_num(self) -> int:
+        return self.parts[0].step_num if self.parts else 0
+
+    @step_num.setter
+    def step_num(self, v: int):
+        for p in self.parts:
+            p.step_num = v
+
+    @property
+    def hp(self):
+        return self.parts[0].hp if self.parts else None
+
+    def state_tensors(self):
+        out = {}
+        for i, p in enumerate(self.parts):
+            for k, t in p.state_tensors().items():
+                out[f"{k}.{i}"] = t
+        return out
+
+    def enable_device_hparams(self):
+        for p in self.parts:
+            p.enable_device_hparams()
+
+    def set_lr(self, lr: float):
+        self.cfg.lr = lr
+        for p in self.parts:
+            p.set_lr(lr)
+
+    def step(self, lr: Optional[float] = None, grad_scale: float = 1.0):
+        for p in self.parts:
+            p.step(lr=lr, grad_scale=grad_scale)

@@ -20,11 +20,14 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _train(model_fn: Callable, strategy_file: Optional[str], steps: int, seed: int, optimizer: str = "sgd"):
+def _train(model_fn: Callable, strategy_file: Optional[str], steps: int, seed: int, optimizer: str = "sgd",
+           cfg_over: Optional[Dict] = None):
     from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
 
     cfg = FFConfig()
     cfg.seed = seed
+    for k, v in (cfg_over or {}).items():
+        setattr(cfg, k, v)
     if strategy_file:
         cfg.import_strategy_file = strategy_file
     else:
@@ -47,11 +50,11 @@ def _train(model_fn: Callable, strategy_file: Optional[str], steps: int, seed: i
     return params, ex
 
 
-def _worker(rank, world, port, model_fn, strategy_file, steps, seed, out_path, optimizer):
+def _worker(rank, world, port, model_fn, strategy_file, steps, seed, out_path, optimizer, cfg_over=None):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(1)
-    params, ex = _train(model_fn, strategy_file, steps, seed, optimizer)
+    params, ex = _train(model_fn, strategy_file, steps, seed, optimizer, cfg_over)
     if rank == 0:
         torch.save({"params": params, "stats": dict(ex.dist.stats)}, out_path)
     import torch.distributed as dist
@@ -61,10 +64,10 @@ def _worker(rank, world, port, model_fn, strategy_file, steps, seed, out_path, o
 
 
 def run_distributed(model_fn: Callable, world: int, strategy_file: Optional[str] = None, steps: int = 2,
-                    seed: int = 0, optimizer: str = "sgd") -> Dict:
+                    seed: int = 0, optimizer: str = "sgd", cfg_over: Optional[Dict] = None) -> Dict:
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(world, free_port(), model_fn, strategy_file, steps, seed, out, optimizer),
+        mp.start_processes(_worker, args=(world, free_port(), model_fn, strategy_file, steps, seed, out, optimizer, cfg_over),
                            nprocs=world, join=True, start_method="spawn")
         return torch.load(out, weights_only=True)
 

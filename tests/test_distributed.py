@@ -117,3 +117,14 @@ def test_moe_expert_parallel(tmp_path, fn, world, cfg):
     assert_params_close(out["params"], ref["params"])
     if "alltoall" in fn:
         assert out["stats"].get("ep_all_to_all", 0) > 0, out["stats"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_optimizer_matches(world):
+    """ZeRO-style sharded Adam (reduce-scatter + shard update + all-gather)
+    matches the single-process run."""
+    ref = run_single(M.bert_tiny, steps=3, optimizer="adam")
+    out = run_distributed(M.bert_tiny, world, steps=3, optimizer="adam",
+                          cfg_over={"shard_optimizer": True, "bucket_mb": 0})
+    assert_params_close(out["params"], ref["params"], rtol=1e-3, atol=1e-4)
+    assert out["stats"].get("reduce_scatter", 0) > 0
