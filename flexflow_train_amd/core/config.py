@@ -59,7 +59,9 @@ class FFConfig:
     seed: int = 0
     shard_optimizer: bool = False      # ZeRO-style sharded optimizer state (reduce-scatter + all-gather)
     bucket_mb: int = 64                # gradient all-reduce bucket size
+    enable_hipgraph: bool = True       # fit(): capture the training iteration as a hipGraph (1 GPU)
     _start_time: float = dataclasses.field(default_factory=time.time)
+    _models: list = dataclasses.field(default_factory=list, repr=False, compare=False)
 
     def __post_init__(self):
         pass
@@ -92,10 +94,15 @@ class FFConfig:
         return (time.time() - self._start_time) * 1e6   # microseconds, like Legion's timer
 
     def begin_trace(self, trace_id: int):
-        """Legion trace capture; the MI355X executor captures hipGraphs itself."""
+        """Reference: Legion trace memoisation around one iteration.  Here the
+        FFModels built on this config capture the traced iteration as a
+        hipGraph (second occurrence) and replay it afterwards."""
+        for m in self._models:
+            m._trace_begin(trace_id)
 
     def end_trace(self, trace_id: int):
-        pass
+        for m in self._models:
+            m._trace_end(trace_id)
 
 
 def build_arg_parser() -> argparse.ArgumentParser:
@@ -142,6 +149,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--compute-dtype", dest="compute_dtype", type=str)
     a("--shard-optimizer", "--zero", dest="shard_optimizer", action="store_const", const=True)
     a("--bucket-mb", dest="bucket_mb", type=int)
+    a("--disable-hipgraph", dest="enable_hipgraph", action="store_const", const=False)
     a("--seed", dest="seed", type=int)
     # Legion / Realm flags: accepted, ignored
     for f in ("-ll:fsize", "-ll:zsize", "-ll:util", "-ll:bgwork", "-ll:csize", "-lg:prof", "-lg:prof_logfile"):

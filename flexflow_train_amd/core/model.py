@@ -186,11 +186,15 @@ class SingleDataLoader:
         self.idx = 0
 
     def next_batch(self, ffmodel=None):
+        """Next global batch; also attached to the loader's tensor so a
+        following ``ffmodel.forward()`` consumes it (reference semantics)."""
         b = self.batch_size
         if self.idx + b > self._num_samples:
             self.idx = 0
         out = self.full[self.idx:self.idx + b]
         self.idx += b
+        if self.tensor is not None:
+            (ffmodel or self.model)._pending_feeds[self.tensor.name or f"input_{self.tensor.vref.node}"] = out
         return out
 
 
@@ -206,6 +210,9 @@ class FFModel:
         self.loss_type = None
         self.metrics: List[str] = []
         self._pending_feeds: Dict[str, np.ndarray] = {}
+        self._traces: Dict[int, dict] = {}
+        self._active_trace: Optional[dict] = None
+        self.ffconfig._models.append(self)
         self._label_tensor: Optional[Tensor] = None
         self._last_labels = None
         self._name_counter = 0
@@ -533,19 +540,63 @@ class FFModel:
     def _feeds_from(self, batch_inputs: Dict[str, np.ndarray]):
         return {k: torch.as_tensor(v) for k, v in batch_inputs.items()}
 
+    # ---- Legion-trace equivalent: hipGraph capture of a traced iteration.
+    # ``ffconfig.begin_trace(id) ... forward/zero_gradients/backward/update
+    # ... ffconfig.end_trace(id)`` (flexflow_cffi.py:562-566, used around
+    # every iteration of the reference's training loops) runs the first
+    # traced iteration eagerly (autotuning, allocator warm-up), captures the
+    # second one into a hipGraph and replays it from then on: forward() feeds
+    # the batch into the graph's static buffers and replays the whole
+    # iteration; backward()/update()/zero_gradients() inside the trace are
+    # then already done.
+    def _trace_begin(self, trace_id: int):
+        st = self._traces.setdefault(trace_id, {"count": 0, "step": None})
+        st["count"] += 1
+        st["done"] = False
+        self._active_trace = st
+
+    def _trace_end(self, trace_id: int):
+        self._active_trace = None
+
+    def _traced(self) -> bool:
+        st = self._active_trace
+        return bool(st and st.get("done"))
+
+    def _graph_capable(self) -> bool:
+        ex = self.executor
+        return (ex is not None and ex.cfg.device.type == "cuda" and ex.cfg.grad_clip <= 0
+                and self.dist.world == 1)
+
     def forward(self, seq_length=None):
         feeds = dict(self._pending_feeds)
+        st = self._active_trace
+        if st is not None and self._graph_capable() and "label" in feeds:
+            lab = torch.as_tensor(feeds.pop("label"))
+            tfeeds = self._feeds_from({k: v for k, v in feeds.items() if k in self.executor.inputs})
+            if st["step"] is None and st["count"] >= 2:
+                st["step"] = self.executor.make_graphed_train_step(tfeeds, lab, warmup=0)
+            if st["step"] is not None:
+                st["step"](tfeeds, lab)
+                st["done"] = True
+                return
+        feeds = {k: v for k, v in feeds.items() if k in self.executor.inputs}
         self.executor.forward(self._feeds_from(feeds), training=True)
 
     def backward(self, seq_length=None):
+        if self._traced():
+            return
         lab = self._pending_feeds.get("label")
         g = self.executor.compute_loss(torch.as_tensor(lab) if lab is not None else None)
         self.executor.backward(g)
 
     def update(self):
+        if self._traced():
+            return
         self.executor.update(lr=self._optimizer.cfg.lr)
 
     def zero_gradients(self):
+        if self._traced():
+            return
         for f in self.executor.flats:
             f["grad"].zero_()
 
@@ -565,6 +616,8 @@ class FFModel:
             l.batch_size = bs
         num_samples = ylo.num_samples
         iters = num_samples // bs
+        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
+        graphed = None
         ex.zero_metrics()
         if ex.cfg.device.type == "cuda":
             torch.cuda.synchronize()
@@ -576,7 +629,14 @@ class FFModel:
             for it in range(iters):
                 feeds = {self._inputs[i].name: torch.as_tensor(l.next_batch()) for i, l in enumerate(loaders)}
                 labels = torch.as_tensor(ylo.next_batch())
-                ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
+                if use_graph and (epoch > 0 or it >= 1):
+                    # iteration 0 ran eagerly (autotune / allocator warm-up);
+                    # capture the next one and replay it from then on
+                    if graphed is None:
+                        graphed = ex.make_graphed_train_step(feeds, labels, warmup=0)
+                    graphed(feeds, labels)
+                else:
+                    ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
                 if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0 and self.dist.rank == 0:
                     print(f"epoch {epoch} iter {it + 1}/{iters}: {ex.perf_metrics()}", flush=True)
             if self.dist.rank == 0 and iters:

@@ -43,7 +43,11 @@ def _run(dev, dtype, tol):
     assert gins[1] is None
     torch.testing.assert_close(gins[2].float().cpu(), leaves[1].grad, rtol=tol, atol=tol)
     for got, leaf in zip(grads, leaves[2:]):
-        torch.testing.assert_close(got.cpu(), leaf.grad, rtol=tol, atol=tol * 4)
+        if dtype == torch.float32:
+            torch.testing.assert_close(got.cpu(), leaf.grad, rtol=tol, atol=tol * 4)
+        else:  # bf16 inputs can flip a ReLU near 0: compare in norm
+            err = (got.cpu() - leaf.grad).norm() / leaf.grad.norm()
+            assert err < 3e-2, err
 
 
 def test_experts_cpu_fp32():
