@@ -6,3 +6,4 @@ from .initializers import (ConstantInitializer, GlorotNormalInitializer, GlorotU
 from .model import (AdamOptimizer, FFModel, Layer, Parameter, SGDOptimizer, SingleDataLoader,  # noqa: F401
                     Tensor)
 from .types import *  # noqa: F401,F403
+from .recompile import RecompileState  # noqa: F401

@@ -681,6 +681,44 @@ class FFModel:
     def _get_gradient(self, t: Tensor):
         raise NotImplementedError
 
+    # ------------------------------------------------------------ recompile
+    def recompile_on_condition(self, r) -> bool:
+        """Reference: FFModel::recompile_on_condition (model.h:107)."""
+        if r.ff is None:
+            r.ff = self
+        if not r.trigger():
+            return False
+        r.alter()
+        self.recompile()
+        return True
+
+    def recompile(self):
+        """Re-plan the parallelisation (search / import / DP per the current
+        FFConfig) and move the training state onto the new executor."""
+        old = self.executor
+        if old is None:
+            raise RuntimeError("call compile() first")
+        names = old.parameter_names()
+        params = {n: old.get_parameter(n).cpu() for n in names}
+        ostate = {n: {k: t.cpu() for k, t in old.get_optimizer_state(n).items()} for n in names}
+        step = old.step_num
+        opt_steps = max([f["opt"].step_num for f in old.flats] or [0])
+        if old.dist.distributed:
+            opt_steps = int(old.dist.max_scalar(float(opt_steps)))
+        self.executor = None
+        self.compile(optimizer=self._optimizer, loss_type=self.loss_type, metrics=self.metrics)
+        ex = self.executor
+        for n in ex.parameter_names():
+            if n in params:
+                ex.set_parameter(n, params[n])
+                if ostate.get(n):
+                    ex.set_optimizer_state(n, ostate[n])
+        ex.step_num = step
+        for f in ex.flats:
+            f["opt"].step_num = opt_steps
+        self.recompilations = getattr(self, "recompilations", 0) + 1
+        return self
+
     # ------------------------------------------------------------ checkpoint
     def save_checkpoint(self, path: str):
         from ..utils.checkpoint import save_checkpoint

@@ -569,6 +569,46 @@ class Executor:
             dist.all_reduce(full)
         return full
 
+    def _opt_state_keys(self) -> List[str]:
+        if isinstance(self.optimizer_cfg, AdamConfig):
+            return ["m", "v"]
+        return ["mom"] if getattr(self.optimizer_cfg, "momentum", 0.0) else []
+
+    def get_optimizer_state(self, name: str) -> Dict[str, torch.Tensor]:
+        """Full logical optimizer state of one weight ({"m", "v"} for Adam,
+        {"mom"} for momentum SGD), gathered across ranks; {} when the
+        optimizer is sharded (ZeRO) — its state stays rank-local."""
+        if self.cfg.shard_optimizer:
+            return {}
+        p = next(pp for pp in self.params if pp.name == name)
+        out = {}
+        for key in self._opt_state_keys():
+            full = torch.zeros(p.logical_shape, dtype=torch.float32, device=self.cfg.device)
+            c = p.layout.coord(self.rank)
+            if c is not None and c.b == 0 and c.rep == 0 and c.a == 0 and p.group:
+                flat = getattr(self.flats[p.flat_id]["opt"], key)
+                piece = flat[p.offset:p.offset + p.numel].view(p.layout.piece_shape)
+                box = p.layout.box(c.shard)
+                full[tuple(slice(lo, hi) for lo, hi in box)] = self._to_logical(p, piece)
+            if self.dist.distributed:
+                import torch.distributed as dist
+                dist.all_reduce(full)
+            out[key] = full
+        return out
+
+    def set_optimizer_state(self, name: str, state: Dict[str, torch.Tensor]):
+        p = next(pp for pp in self.params if pp.name == name)
+        if not p.group or self.cfg.shard_optimizer:
+            return
+        c = p.layout.coord(self.rank)
+        box = p.layout.box(c.shard)
+        for key, full in state.items():
+            flat = getattr(self.flats[p.flat_id]["opt"], key, None)
+            if flat is None:
+                continue
+            piece = full.to(self.cfg.device).float().reshape(p.logical_shape)[tuple(slice(lo, hi) for lo, hi in box)]
+            flat[p.offset:p.offset + p.numel].view(p.layout.piece_shape).copy_(self._to_physical(p, piece))
+
     def set_parameter(self, name: str, value: torch.Tensor):
         p = next(pp for pp in self.params if pp.name == name)
         if p.group:

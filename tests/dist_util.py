@@ -101,3 +101,50 @@ def assert_params_close(a: Dict, b: Dict, rtol=2e-4, atol=2e-5):
     assert sorted(a) == sorted(b), (sorted(a), sorted(b))
     for k in a:
         torch.testing.assert_close(a[k], b[k], rtol=rtol, atol=atol, msg=lambda m: f"{k}: {m}")
+
+
+def _recompile_worker(rank, world, port, model_fn, strategy_file, before, after, out_path):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, RecompileState)
+
+    cfg = FFConfig()
+    cfg.seed = 0
+    cfg.only_data_parallel = True
+    model = FFModel(cfg)
+    feeds, labels = model_fn(model)
+    model.compile(optimizer=AdamOptimizer(model, alpha=1e-3), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY])
+    ex = model.executor
+    g = torch.Generator().manual_seed(0)
+    for name in sorted(ex.parameter_names()):
+        full = ex.get_parameter(name)
+        ex.set_parameter(name, torch.randn(full.shape, generator=g) * 0.2)
+    state = {"it": 0}
+
+    def alter(ff):
+        ff.ffconfig.only_data_parallel = False
+        ff.ffconfig.import_strategy_file = strategy_file
+
+    r = RecompileState(lambda ff: state["it"] == before, alter, model)
+    for it in range(before + after):
+        state["it"] = it
+        model.recompile_on_condition(r)
+        model.executor.train_step(feeds, labels)
+    ex = model.executor
+    params = {n: ex.get_parameter(n).detach().cpu().clone() for n in sorted(ex.parameter_names())}
+    if rank == 0:
+        torch.save({"params": params, "recompilations": r.recompilations}, out_path)
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_recompile(model_fn, world, strategy_file, steps_before=2, steps_after=2):
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.start_processes(_recompile_worker, args=(world, free_port(), model_fn, strategy_file, steps_before,
+                                                    steps_after, out), nprocs=world, join=True, start_method="spawn")
+        return torch.load(out, weights_only=True)

@@ -128,3 +128,17 @@ def test_sharded_optimizer_matches(world):
                           cfg_over={"shard_optimizer": True, "bucket_mb": 0})
     assert_params_close(out["params"], ref["params"], rtol=1e-3, atol=1e-4)
     assert out["stats"].get("reduce_scatter", 0) > 0
+
+
+def test_recompile_switches_strategy(tmp_path):
+    """RecompileState: after 2 DP steps switch to a tensor-parallel strategy
+    (alter = import a strategy file) and continue; the result matches 4
+    single-process steps exactly (weights + Adam moments carried over)."""
+    from dist_util import run_recompile
+    ref = run_single(M.mlp, steps=4, optimizer="adam")
+    path = str(tmp_path / "tp.json")
+    write_strategy(M.mlp, 2, {"fc0": {"batch": 1, "model": 2, "kind": "column"},
+                              "fc1": {"batch": 1, "model": 2, "kind": "row"}}, path)
+    out = run_recompile(M.mlp, 2, path, steps_before=2, steps_after=2)
+    assert out["recompilations"] == 1
+    assert_params_close(out["params"], ref["params"], rtol=1e-3, atol=1e-4)
