@@ -66,4 +66,8 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
 // best of {data parallel, MCMC, Unity} by simulated iteration time.
 SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, const SearchConfig& cfg);
 
+// JSON forms of the configs (keys as in SearchConfig / SimConfig; "sim" nests).
+SimConfig sim_config_from_json(const Json& j);
+SearchConfig search_config_from_json(const Json& j);
+
 }  // namespace ff

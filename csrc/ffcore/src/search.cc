@@ -246,4 +246,46 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
   return best;
 }
 
+// JSON configuration (Python bindings, C FFI, CLIs)
+SimConfig sim_config_from_json(const Json& j) {
+  SimConfig c;
+  if (!j.is_object()) return c;
+  auto gi = [&](const char* k, int& v) { if (j.contains(k)) v = static_cast<int>(j.at(k).as_int()); };
+  auto gd = [&](const char* k, double& v) { if (j.contains(k)) v = j.at(k).as_double(); };
+  auto gb = [&](const char* k, bool& v) { if (j.contains(k)) v = j.at(k).as_bool(); };
+  gi("world", c.world);
+  gb("overlap_grad_sync", c.overlap_grad_sync);
+  gd("bucket_bytes", c.bucket_bytes);
+  gb("include_update", c.include_update);
+  gd("update_bytes_per_param", c.update_bytes_per_param);
+  gd("memory_penalty_per_mb", c.memory_penalty_per_mb);
+  gd("comm_compute_slowdown", c.comm_compute_slowdown);
+  gb("bf16_weight_grads", c.bf16_weight_grads);
+  return c;
+}
+
+SearchConfig search_config_from_json(const Json& j) {
+  SearchConfig c;
+  auto gi = [&](const char* k, int& v) { if (j.contains(k)) v = static_cast<int>(j.at(k).as_int()); };
+  auto gd = [&](const char* k, double& v) { if (j.contains(k)) v = j.at(k).as_double(); };
+  auto gb = [&](const char* k, bool& v) { if (j.contains(k)) v = j.at(k).as_bool(); };
+  gi("world", c.world);
+  gi("budget", c.budget);
+  gd("alpha", c.alpha);
+  gd("threshold", c.threshold);
+  gi("max_num_ops", c.max_num_ops);
+  gd("mcmc_beta", c.mcmc_beta);
+  gd("group_move_prob", c.group_move_prob);
+  if (j.contains("seed")) c.seed = static_cast<uint64_t>(j.at("seed").as_int());
+  gd("time_limit", c.time_limit);
+  gb("use_machine_mapping", c.use_machine_mapping);
+  gb("enable_parameter_parallel", c.space.enable_parameter_parallel);
+  gb("enable_attribute_parallel", c.space.enable_attribute_parallel);
+  gb("allow_partial_world", c.space.allow_partial_world);
+  gi("max_model_degree", c.space.max_model_degree);
+  if (j.contains("sim")) c.sim = sim_config_from_json(j.at("sim"));
+  c.sim.world = c.world;
+  return c;
+}
+
 }  // namespace ff

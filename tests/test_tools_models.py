@@ -16,10 +16,10 @@ REF_SUBST = "/root/reference/substitutions"
 @pytest.fixture(scope="module", autouse=True)
 def _tools_built():
     if not all(os.path.exists(os.path.join(BIN, b)) for b in
-               ("ffc-export-model-arch", "ffc-substitution-to-dot", "ffc-protobuf-to-json")):
+               ("ffc-export-model-arch", "ffc-substitution-to-dot", "ffc-protobuf-to-json", "ffc-ffi-test")):
         from tools.build_native import build
 
-        build(["core", "tools"])
+        build(["core", "tools", "ffi"])
 
 
 def _run(*args):
@@ -67,3 +67,13 @@ def test_substitution_to_dot():
     assert "cluster_src" in dot and "cluster_dst" in dot
     lst = _run("ffc-substitution-to-dot", path, "--list").stdout.strip().splitlines()
     assert len(lst) == 640
+
+
+def test_c_ffi(tmp_path):
+    """C ABI (csrc/ffi/flexflow_c.h): build, serialise, search, query from C."""
+    r = _run("ffc-ffi-test", str(tmp_path / "cg.json"))
+    assert "FFI OK" in r.stdout
+    cg = C.ComputationGraph.from_json(open(tmp_path / "cg.json").read()) if hasattr(C.ComputationGraph, "from_json") \
+        else None
+    if cg is not None:
+        assert len(list(cg.topo_order())) >= 5

@@ -51,7 +51,8 @@ def write_ninja(targets: list[str]) -> str:
         "ninja_required_version = 1.5",
         f"cxx = {cxx}",
         f"hipcc = {HIPCC}",
-        f"core_flags = -O2 -g0 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function {core_inc} {inc}",
+        f"core_flags = -O2 -g0 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function {core_inc} "
+        f"-I{os.path.join(ROOT, 'csrc', 'ffi')} {inc}",
         # -mcode-object-version=5 keeps the code object loadable by the HIP
         # runtime bundled with the PyTorch wheel (ROCm 7.0) as well as 7.2.
         f"hip_flags = -O3 -std=c++17 -fPIC --offload-arch={ARCH} -mcode-object-version=5 "
@@ -111,6 +112,26 @@ def write_ninja(targets: list[str]) -> str:
             exe = os.path.join(ROOT, "bin", "ffc-" + os.path.basename(s)[:-3].replace("_", "-"))
             lines.append(f"build {exe}: link_exe {o} {' '.join(core_objs)}")
             defaults.append(exe)
+    if "ffi" in targets:
+        # C ABI (csrc/ffi/flexflow_c.h): libflexflow_c.so + a C smoke program
+        lines += ["rule link_so", "  command = $cxx -shared -o $out $in -lpthread", "  description = LINK $out",
+                  "rule cc_exe",
+                  f"  command = gcc -O2 -std=c11 -I{os.path.join(ROOT, 'csrc', 'ffi')} -o $out $in "
+                  f"-L{os.path.join(PKG, 'lib')} -lflexflow_c -Wl,-rpath,{os.path.join(PKG, 'lib')}",
+                  "  description = CC $out"]
+        core_objs = []
+        for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "ffcore", "src", "*.cc"))):
+            o = os.path.join("obj", "core", os.path.basename(s) + ".o")
+            if "core" not in targets and "tools" not in targets:
+                lines.append(f"build {o}: cxx {s}")
+            core_objs.append(o)
+        fo = os.path.join("obj", "ffi", "flexflow_c.cc.o")
+        lines.append(f"build {fo}: cxx {os.path.join(ROOT, 'csrc', 'ffi', 'flexflow_c.cc')}")
+        lib = os.path.join(PKG, "lib", "libflexflow_c.so")
+        lines.append(f"build {lib}: link_so {fo} {' '.join(core_objs)}")
+        exe = os.path.join(ROOT, "bin", "ffc-ffi-test")
+        lines.append(f"build {exe}: cc_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_ffi.c')} | {lib}")
+        defaults += [lib, exe]
     lines.append("default " + " ".join(defaults))
     os.makedirs(BUILD, exist_ok=True)
     path = os.path.join(BUILD, "build.ninja")
@@ -123,7 +144,7 @@ def write_ninja(targets: list[str]) -> str:
 
 
 def build(targets: list[str] | None = None, jobs: int | None = None, verbose: bool = False) -> None:
-    targets = targets or ["core", "kernels", "tools"]
+    targets = targets or ["core", "kernels", "tools", "ffi"]
     write_ninja(targets)
     ninja = shutil.which("ninja")
     if ninja is None:

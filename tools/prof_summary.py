@@ -2,6 +2,11 @@
 """Summarise a rocprofv3 kernel_stats.csv into categories (short names).
 
     python tools/prof_summary.py gpurun_out/prof/bert_kernel_stats.csv [--steps N]
+    python tools/prof_summary.py gpurun_out/prof/bert_results.db --steps 10 --window-ms 540
+
+``--window-ms W`` (rocpd .db only) keeps the dispatches that START within
+the last W ms of the trace: the timed steps of a bench run, excluding
+autotuning / warm-up kernels.
 """
 import csv
 import json
@@ -49,7 +54,12 @@ def main():
         import sqlite3
 
         con = sqlite3.connect(path)
-        for name, calls, ns in con.execute("select name, count(*), sum(duration) from kernels group by name"):
+        where = ""
+        if "--window-ms" in sys.argv:
+            w = float(sys.argv[sys.argv.index("--window-ms") + 1])
+            (end,) = con.execute("select max(end) from kernels").fetchone()
+            where = f" where start >= {int(end - w * 1e6)}"
+        for name, calls, ns in con.execute(f"select name, count(*), sum(duration) from kernels{where} group by name"):
             add(name, calls, ns)
     else:
         with open(path) as f:
