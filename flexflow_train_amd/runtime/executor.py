@@ -40,6 +40,7 @@ from ..parallel.sequence import SeqGroup
 from ..ops.moe import ExpertGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig, ShardedOptimizer
 from .initializers import make_initializer_tensor
+from ..utils.tracing import Tracer
 
 Value = Tuple[int, int]
 _PAR_OPS = {"REPARTITION", "COMBINE", "REPLICATE", "REDUCTION", "ALLTOALL", "FUSED_PARALLEL"}
@@ -126,7 +127,7 @@ class Executor:
         self.optimizer_cfg = optimizer or SGDConfig()
         self.valid_classes = valid_classes
         self.step_num = 0
-        self._profile: Dict[str, float] = {}
+        self.tracer = Tracer(self.cfg.device, self.rank, enabled=self.cfg.profiling)
         self._build(output)
         self.loss = LossFunction(loss_type, self._global_rows(), valid_cols=valid_classes) if loss_type else None
         self.metrics_buf = torch.zeros(N_SLOTS, device=cfg.device, dtype=torch.float32)
@@ -684,13 +685,15 @@ class Executor:
             if p.group:
                 env[p.terminal] = p.compute
         self._saved = {}
-        prof = self.cfg.profiling and self.cfg.device.type == "cuda"
+        prof = self.cfg.profiling
         for i, s in enumerate(self.steps):
             if training and s is self.softmax_fused_step and self.loss is not None and self.loss.fuses_softmax:
                 continue
             if s.kind == "comm":
                 x = env.get(s.inputs[0])
+                t0 = self.tracer.begin(f"{s.name}:fwd", "comm", self.step_num) if prof else None
                 env[s.outputs[0]] = self.redist(x, s.src, s.dst, self._dtype_of(s.inputs[0], x), self.cfg.device)
+                self.tracer.end(t0)
                 continue
             if not s.active:
                 continue
@@ -699,10 +702,9 @@ class Executor:
             ins = [env[v] for v in s.inputs]
             ws = [p.compute for p in s.weights]
             impl = opbase.get_impl(s.op_type)
-            t0 = self._tick() if prof else None
+            t0 = self.tracer.begin(f"{s.name}:fwd", "compute", self.step_num) if prof else None
             outs, saved = impl.forward(s.ctx, ins, ws)
-            if prof:
-                self._tock(t0, f"{s.name}:fwd")
+            self.tracer.end(t0)
             for o, t in zip(s.outputs, outs):
                 env[o] = t
             if training:
@@ -749,7 +751,7 @@ class Executor:
             for b in f["buckets"]:
                 b["pending"] = sum(1 for p in b["params"] if p.trainable)
         self._works = []
-        prof = self.cfg.profiling and self.cfg.device.type == "cuda"
+        prof = self.cfg.profiling
         n = len(self.steps)
         for i in range(n - 1, -1, -1):
             s = self.steps[i]
@@ -761,8 +763,10 @@ class Executor:
                     continue
                 if g is None and s.dst.coord(self.rank) is not None:
                     g = torch.zeros(s.dst.piece_shape, dtype=self.cfg.compute_dtype, device=self.cfg.device)
+                t0 = self.tracer.begin(f"{s.name}:bwd", "comm", self.step_num) if prof else None
                 gi = self.redist(g, s.dst.dual(), s.src.dual(), g.dtype if g is not None else self.cfg.compute_dtype,
                                  self.cfg.device)
+                self.tracer.end(t0)
                 self._acc(grads, s.inputs[0], gi)
                 continue
             saved = self._saved.pop(i, None)
@@ -781,10 +785,9 @@ class Executor:
                     s.ctx.extra["wgrad_beta"] = [0.0 if p.n_consumers == 1 else 1.0 for p in s.weights]
                     s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
                     impl = opbase.get_impl(s.op_type)
-                    t0 = self._tick() if prof else None
+                    t0 = self.tracer.begin(f"{s.name}:bwd", "compute", self.step_num) if prof else None
                     gins = impl.backward(s.ctx, saved, gouts, wgs, need)
-                    if prof:
-                        self._tock(t0, f"{s.name}:bwd")
+                    self.tracer.end(t0)
                     for v, g, nd in zip(s.inputs, gins, need):
                         if g is not None and nd:
                             self._acc(grads, v, g)
@@ -958,19 +961,13 @@ class Executor:
                                        self.metrics_start, out_dim)
 
     # --------------------------------------------------------------- profiling
-    def _tick(self):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
-
-    def _tock(self, start, key):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        e.synchronize()
-        self._profile[key] = self._profile.get(key, 0.0) + start.elapsed_time(e)
-
     def profile_report(self) -> Dict[str, float]:
-        return dict(sorted(self._profile.items(), key=lambda kv: -kv[1]))
+        """Milliseconds per ``op:fwd`` / ``op:bwd`` / redistribution since the
+        last ``tracer.clear()`` (needs ExecConfig.profiling)."""
+        return self.tracer.report()
+
+    def export_chrome_trace(self, path: str) -> str:
+        return self.tracer.export_chrome_trace(path, {"world": self.world, "rank": self.rank})
 
     # ------------------------------------------------------------ checkpoint
     def state_dict(self) -> Dict[str, Any]:

@@ -21,6 +21,7 @@ import os
 from typing import Dict, Tuple
 
 from .. import _ffcore as C
+from ..utils.logging import get_logger
 
 
 def _cg_to_pcg_map_by_name(cg, pcg) -> Dict[int, int]:
@@ -56,6 +57,8 @@ def build_pcg(cg, ffconfig, world: int):
         pcg, views, rep = unity.search(cg, ffconfig, world)
         report.update(rep)
     report["cg_to_pcg"] = _cg_to_pcg_map_by_name(cg, pcg)
+    get_logger("search").info("strategy for %d ranks: %s", world,
+                              {k: v for k, v in report.items() if k not in ("cg_to_pcg", "trace", "strategy")})
     return pcg, views, report
 
 

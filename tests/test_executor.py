@@ -132,3 +132,30 @@ def test_strategy_export_import_roundtrip(tmp_path):
     assert doc["ops"] and all("device_ids" in o for o in doc["ops"])
     with pytest.raises(ValueError):
         import_strategy(path, 2)
+
+
+def test_tracing_chrome_export(tmp_path):
+    """ExecConfig.profiling: per-op spans, aggregate report and a chrome
+    trace (reference: profiling wrapper + --taskgraph export)."""
+    import json as _json
+    import dist_models as M
+    from flexflow_train_amd.core import FFConfig, FFModel, LossType, SGDOptimizer
+
+    cfg = FFConfig()
+    cfg.profiling = True
+    m = FFModel(cfg)
+    feeds, labels = M.mlp(m)
+    m.compile(optimizer=SGDOptimizer(m, lr=0.01), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY)
+    m.executor.train_step(feeds, labels)
+    rep = m.executor.profile_report()
+    assert any(k.endswith(":fwd") for k in rep) and any(k.endswith(":bwd") for k in rep)
+    path = m.executor.export_chrome_trace(str(tmp_path / "trace.json"))
+    doc = _json.load(open(path))
+    xs = [e for e in doc["traceEvents"] if e["ph"] == "X"]
+    assert len(xs) >= 6 and all(e["dur"] >= 0 for e in xs)
+
+
+def test_logging_categories(monkeypatch):
+    from flexflow_train_amd.utils.logging import get_logger
+    lg = get_logger("search")
+    assert lg.name == "flexflow.search"
