@@ -7,6 +7,7 @@
 
 #include "bindings_ext.h"
 #include "ff/mapping.h"
+#include "ff/network.h"
 #include "ff/models.h"
 #include "ff/parallelize.h"
 #include "ff/search.h"
@@ -53,9 +54,49 @@ void register_ext_bindings(py::module_& m) {
       .def_readwrite("collective_latency", &MachineSpecification::collective_latency)
       .def_readwrite("xgmi_links", &MachineSpecification::xgmi_links)
       .def_readwrite("xgmi_link_bandwidth", &MachineSpecification::xgmi_link_bandwidth)
+      .def_readwrite("collective_bw", &MachineSpecification::collective_bw)
+      .def_readwrite("all_to_all_bw", &MachineSpecification::all_to_all_bw)
       .def("num_devices", &MachineSpecification::num_devices)
       .def("to_json", [](const MachineSpecification& s) { return s.to_json().dump(); })
       .def_static("from_json", [](const std::string& s) { return MachineSpecification::from_json(Json::parse(s)); });
+
+  py::class_<NetworkTopology>(m, "NetworkTopology")
+      .def_readonly("num_devices", &NetworkTopology::num_devices)
+      .def_readonly("num_vertices", &NetworkTopology::num_vertices)
+      .def_readonly("name", &NetworkTopology::name)
+      .def("num_links", [](const NetworkTopology& t) { return t.links.size(); })
+      .def_static("fully_connected", &NetworkTopology::fully_connected)
+      .def_static("big_switch", &NetworkTopology::big_switch)
+      .def_static("flat_deg_constraint", &NetworkTopology::flat_deg_constraint)
+      .def_static("mi355x_cluster", &NetworkTopology::mi355x_cluster, py::arg("nodes"), py::arg("gpus_per_node") = 8,
+                  py::arg("xgmi_bw") = 64e9, py::arg("xgmi_lat") = 1e-6, py::arg("nic_bw") = 50e9,
+                  py::arg("nic_lat") = 5e-6)
+      .def_static("from_config_text", [](const std::string& t) {
+        MachineSpecification spec;
+        auto topo = NetworkTopology::from_config_text(t, &spec);
+        return py::make_tuple(topo, spec);
+      })
+      .def_static("from_config_file", [](const std::string& p) {
+        MachineSpecification spec;
+        auto topo = NetworkTopology::from_config_file(p, &spec);
+        return py::make_tuple(topo, spec);
+      })
+      .def("to_json", [](const NetworkTopology& t) { return t.to_json().dump(); });
+  py::class_<NetworkModel>(m, "NetworkModel")
+      .def(py::init([](const NetworkTopology& t, const std::string& routing, int max_rings) {
+             return NetworkModel(t, routing == "weighted" ? RoutingStrategy::WEIGHTED_SHORTEST_PATH
+                                                          : RoutingStrategy::SHORTEST_PATH_ECMP, max_rings);
+           }),
+           py::arg("topology"), py::arg("routing") = "ecmp", py::arg("max_rings") = 4)
+      .def("routes", &NetworkModel::routes)
+      .def("p2p_time", &NetworkModel::p2p_time)
+      .def("all_reduce_time", &NetworkModel::all_reduce_time)
+      .def("all_gather_time", &NetworkModel::all_gather_time)
+      .def("all_to_all_time", &NetworkModel::all_to_all_time)
+      .def("calibrate", [](const NetworkModel& nm, MachineSpecification spec, double probe) {
+        nm.calibrate(spec, probe);
+        return spec;
+      }, py::arg("spec"), py::arg("probe_bytes") = 256.0 * (1 << 20));
 
   m.def("operator_task_space", &operator_task_space);
   m.def("get_allowed_machine_views", [](const std::vector<int>& ts, const MachineSpecification& spec) {

@@ -42,6 +42,11 @@ struct MachineSpecification {
   double collective_latency = 8e-6;     // alpha per collective step
   int xgmi_links = 7;
   double xgmi_link_bandwidth = 64e9;    // per direction per link
+  // Optional effective bus bandwidths (bytes/s) per group size p, from the
+  // topology model (network.h NetworkModel::calibrate) or RCCL measurements;
+  // override the analytic link model when present.
+  std::map<int, double> collective_bw;
+  std::map<int, double> all_to_all_bw;
 
   int num_devices() const { return num_nodes * num_gpus_per_node; }
   Json to_json() const;

@@ -23,6 +23,13 @@ Json MachineSpecification::to_json() const {
   j["collective_latency"] = collective_latency;
   j["xgmi_links"] = xgmi_links;
   j["xgmi_link_bandwidth"] = xgmi_link_bandwidth;
+  auto bwmap = [](const std::map<int, double>& m) {
+    Json o = Json::object();
+    for (auto const& kv : m) o[std::to_string(kv.first)] = kv.second;
+    return o;
+  };
+  if (!collective_bw.empty()) j["collective_bw"] = bwmap(collective_bw);
+  if (!all_to_all_bw.empty()) j["all_to_all_bw"] = bwmap(all_to_all_bw);
   return j;
 }
 
@@ -48,6 +55,11 @@ MachineSpecification MachineSpecification::from_json(const Json& j) {
   gd("collective_latency", s.collective_latency);
   gi("xgmi_links", s.xgmi_links);
   gd("xgmi_link_bandwidth", s.xgmi_link_bandwidth);
+  for (const char* key : {"collective_bw", "all_to_all_bw"}) {
+    if (!j.contains(key)) continue;
+    auto& m = std::string(key) == "collective_bw" ? s.collective_bw : s.all_to_all_bw;
+    for (auto const& kv : j.at(key).as_object()) m[std::stoi(kv.first)] = kv.second.as_double();
+  }
   return s;
 }
 
@@ -213,6 +225,8 @@ std::vector<std::pair<DeviceBlock, DeviceBlock>> get_resource_splits(const Devic
 // ---------------------------------------------------------------------------
 static double eff_bw(int p, const MachineSpecification& s) {
   if (p <= 1) return 1e30;
+  auto it = s.collective_bw.find(p);
+  if (it != s.collective_bw.end()) return it->second;
   double links = std::min(p - 1, s.xgmi_links) * s.xgmi_link_bandwidth;
   double b = std::min(s.intra_node_bandwidth, links);
   if (p > s.num_gpus_per_node) b = std::min(b, s.inter_node_bandwidth);
@@ -232,7 +246,9 @@ double CollectiveCost::reduce_scatter(double bytes_in, int p, const MachineSpeci
 }
 double CollectiveCost::all_to_all(double bytes, int p, const MachineSpecification& s) {
   if (p <= 1 || bytes <= 0) return 0;
-  return (p - 1.0) / p * bytes / eff_bw(p, s) + s.collective_latency;
+  auto it = s.all_to_all_bw.find(p);
+  const double bw = it != s.all_to_all_bw.end() ? it->second : eff_bw(p, s);
+  return (p - 1.0) / p * bytes / bw + s.collective_latency;
 }
 double CollectiveCost::p2p(double bytes, const MachineSpecification& s) {
   return bytes / s.xgmi_link_bandwidth + s.collective_latency;

@@ -21,11 +21,23 @@ from .. import _ffcore as C
 
 
 def machine_spec(ffconfig=None, world: Optional[int] = None):
+    """MachineSpecification for the search.  ``--machine-model-file``: JSON
+    with MachineSpecification fields, or a reference-style ``key = value``
+    machine config (machine_config_example).  ``--machine-model-version 1``
+    (or any key=value file) runs the topology-aware network model
+    (csrc/ffcore/src/network.cc) and calibrates the per-group-size
+    collective bandwidths from its routed ring / all-to-all link loads."""
     spec = C.MachineSpecification.mi355x()
     path = getattr(ffconfig, "machine_model_file", "") if ffconfig is not None else ""
+    version = int(getattr(ffconfig, "machine_model_version", 0) or 0) if ffconfig is not None else 0
+    topo = None
     if path:
         with open(path) as f:
-            spec = C.MachineSpecification.from_json(f.read())
+            text = f.read()
+        if text.lstrip().startswith("{"):
+            spec = C.MachineSpecification.from_json(text)
+        else:
+            topo, spec = C.NetworkTopology.from_config_text(text)
     if ffconfig is not None:
         nn = getattr(ffconfig, "search_num_nodes", -1)
         if nn and nn > 0:
@@ -35,6 +47,11 @@ def machine_spec(ffconfig=None, world: Optional[int] = None):
             spec.num_gpus_per_node = nw
     if world is not None and world > spec.num_devices():
         spec.num_nodes = (world + spec.num_gpus_per_node - 1) // spec.num_gpus_per_node
+    if topo is None and version >= 1:
+        topo = C.NetworkTopology.mi355x_cluster(spec.num_nodes, spec.num_gpus_per_node, spec.xgmi_link_bandwidth,
+                                                1e-6, spec.inter_node_bandwidth, 5e-6)
+    if topo is not None:
+        spec = C.NetworkModel(topo).calibrate(spec)
     return spec
 
 

@@ -269,3 +269,43 @@ def test_search_prefers_tensor_parallel_for_huge_weights_small_batch():
     assert rep["predicted_speedup_over_dp"] > 1.5
     kinds = {v["kind"] for v in rep["strategy"].values()}
     assert kinds & {"column", "row"}
+
+
+def test_network_model_topologies():
+    """Topology-aware network model (reference NetworkedMachineModel +
+    routing + ring all-reduce expansion)."""
+    from flexflow_train_amd import _ffcore as C
+    t = C.NetworkTopology.mi355x_cluster(1)
+    assert t.num_devices == 8 and t.num_links() == 56
+    nm = C.NetworkModel(t)
+    assert nm.routes(0, 5) and len(nm.routes(0, 5)[0]) == 1          # direct xGMI link
+    ar = [nm.all_reduce_time(list(range(p)), 256e6) for p in (2, 4, 8)]
+    assert ar[0] > ar[1] > ar[2] > 0                                   # more rings over more links
+    two = C.NetworkModel(C.NetworkTopology.mi355x_cluster(2))
+    assert len(two.routes(0, 9)[0]) == 2                               # via the NIC switch
+    assert two.all_reduce_time(list(range(16)), 256e6) > ar[2]          # NIC-bound
+    bs = C.NetworkModel(C.NetworkTopology.big_switch(8, 64e9, 1e-6))
+    assert len(bs.routes(1, 2)[0]) == 2
+    fd = C.NetworkModel(C.NetworkTopology.flat_deg_constraint(8, 3, 64e9, 1e-6, 7))
+    assert fd.p2p_time(0, 4, 1e6) > 0
+    spec = nm.calibrate(C.MachineSpecification.mi355x(1, 8))
+    assert spec.collective_bw[8] > spec.collective_bw[2]
+    cm = C.CostModel(spec)
+    assert cm is not None
+    topo, sp = C.NetworkTopology.from_config_text("num_nodes = 2\nnum_sockets_per_node = 2\nnum_gpus_per_socket = 2\n"
+                                                  "nvlink_bandwidth = 18.5\nnic_bandwidth = 10.9\n")
+    assert sp.num_nodes == 2 and sp.num_gpus_per_node == 4 and topo.num_devices == 8
+
+
+def test_machine_spec_from_reference_config(tmp_path):
+    from flexflow_train_amd.core import FFConfig
+    from flexflow_train_amd.search.native import machine_spec
+    p = tmp_path / "machine.cfg"
+    p.write_text("num_nodes = 1\nnum_gpus_per_node = 8\nxgmi_bandwidth = 64\n")
+    cfg = FFConfig()
+    cfg.machine_model_file = str(p)
+    spec = machine_spec(cfg, 8)
+    assert 8 in spec.collective_bw and spec.collective_bw[8] > 1e11
+    cfg2 = FFConfig()
+    cfg2.machine_model_version = 1
+    assert 4 in machine_spec(cfg2, 8).collective_bw
