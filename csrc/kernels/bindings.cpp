@@ -187,4 +187,50 @@ PYBIND11_MODULE(_ffkernels, m) {
     gemm256_bf16(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32,
                  splits, reinterpret_cast<float*>(ws), S(st));
   });
+
+  // conv geometry crosses as a list [N,H,W,C,K,R,S,sh,sw,ph,pw,dh,dw]
+  auto cshape = [](const std::vector<int>& v) {
+    if (v.size() != 13) throw std::invalid_argument("conv shape must have 13 entries");
+    ConvShape c;
+    c.N = v[0]; c.H = v[1]; c.W = v[2]; c.C = v[3]; c.K = v[4]; c.R = v[5]; c.S = v[6];
+    c.sh = v[7]; c.sw = v[8]; c.ph = v[9]; c.pw = v[10]; c.dh = v[11]; c.dw = v[12];
+    return c;
+  };
+  m.def("conv2d_fwd", [=](std::vector<int> shp, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y,
+                          uintptr_t stats, int act, uintptr_t st) {
+    conv2d_fwd(cshape(shp), P(x), P(w), P(bias), P(y), F(stats), act, S(st));
+  });
+  m.def("conv2d_dgrad", [=](std::vector<int> shp, uintptr_t dy, uintptr_t w, uintptr_t dx, float beta,
+                            uintptr_t st) { conv2d_dgrad(cshape(shp), P(dy), P(w), P(dx), beta, S(st)); });
+  m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, int splits,
+                            uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), splits, S(st)); });
+  m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st) {
+    bn_stats(P(x), F(stats), M, C, S(st));
+  });
+  m.def("bn_finalize", [](uintptr_t stats, uintptr_t g, uintptr_t b, int pdt, uintptr_t rm, uintptr_t rv,
+                          uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t rstd, int C, double count,
+                          float momentum, float eps, uintptr_t st) {
+    bn_finalize(F(stats), P(g), P(b), pdt, F(rm), F(rv), F(scale), F(shift), F(mean), F(rstd), C, count, momentum,
+                eps, S(st));
+  });
+  m.def("bn_apply", [](uintptr_t x, uintptr_t res, uintptr_t scale, uintptr_t shift, uintptr_t y, int64_t M, int C,
+                       int relu, uintptr_t st) { bn_apply(P(x), P(res), F(scale), F(shift), P(y), M, C, relu, S(st)); });
+  m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t g, int pdt,
+                     uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, uintptr_t ws, int64_t M, int C,
+                     int relu, uintptr_t st) {
+    bn_bwd(P(dy), P(x), P(y), F(mean), F(rstd), P(g), pdt, P(dx), P(dres), F(dg), F(db), F(ws), M, C, relu, S(st));
+  });
+  // pool geometry: [N,H,W,C,R,S,sh,sw,ph,pw,avg,count_pad]
+  auto pshape = [](const std::vector<int>& v) {
+    if (v.size() != 12) throw std::invalid_argument("pool shape must have 12 entries");
+    PoolShape p;
+    p.N = v[0]; p.H = v[1]; p.W = v[2]; p.C = v[3]; p.R = v[4]; p.S = v[5];
+    p.sh = v[6]; p.sw = v[7]; p.ph = v[8]; p.pw = v[9]; p.avg = v[10]; p.count_pad = v[11];
+    return p;
+  };
+  m.def("pool2d_fwd", [=](std::vector<int> shp, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {
+    pool2d_fwd(pshape(shp), P(x), P(y), P(arg), S(st));
+  });
+  m.def("pool2d_bwd", [=](std::vector<int> shp, uintptr_t dy, uintptr_t arg, uintptr_t dx, float beta,
+                          uintptr_t st) { pool2d_bwd(pshape(shp), P(dy), P(arg), P(dx), beta, S(st)); });
 }

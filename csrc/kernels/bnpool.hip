@@ -1,0 +1,421 @@
+// BatchNorm (training mode) and 2-D pooling for NHWC bf16 activations (gfx950).
+//
+// Parity: lib/kernels/src/cuda/ops/batch_norm_kernels.cu
+// (cudnnBatchNormalizationForwardTraining :35 with running statistics,
+// fused ReLU, cudnnBatchNormalizationBackward :71 + reluBackward :68) and
+// pool_2d_kernels.cu (cudnnPoolingForward :103 / Backward :123, max and
+// average).
+//
+// Layout: activations are [M = N*H*W][C] (channels innermost, torch
+// channels_last), so every thread moves 8 channels as one 16-byte vector and
+// the per-channel parameters a thread needs are fixed for its whole life.
+//   * statistics: per-channel (sum, sum of squares) — either produced by the
+//     convolution epilogue (conv.hip) or by bn_stats here — then bn_finalize
+//     turns them into scale/shift (+ running-stat update, + saved mean/rstd);
+//   * bn_apply: y = x*scale + shift [+ residual] [ReLU] in one pass;
+//   * backward: bn_bwd_reduce accumulates sum(g), sum(g*xhat) with g = dy
+//     masked by the ReLU (recomputed from y), bn_bwd_apply writes
+//     dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) and dgamma/dbeta.
+// Reductions: a block is RL row-lanes x GL channel-group lanes; each thread
+// strides over rows with 8 fp32 accumulators per quantity, the block reduces
+// its row-lanes through LDS and issues one fp32 atomic per channel.
+// Pooling: forward one thread per (output pixel, 8 channels), max pooling
+// records the winning tap as a byte; backward is a gather over the windows
+// that cover an input pixel (no atomics, deterministic).
+#include "common.h"
+#include "kernels.h"
+
+namespace ffk {
+
+namespace {
+
+__device__ __forceinline__ void load8(const bf16* p, float (&v)[8]) {
+  const bf16x8 t = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = bf2f(t[i]);
+}
+__device__ __forceinline__ void store8(bf16* p, const float (&v)[8]) {
+  bf16x8 t;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = f2bf(v[i]);
+  *reinterpret_cast<bf16x8*>(p) = t;
+}
+__device__ __forceinline__ float ldp(const void* p, int dt, int i) {
+  return dt == 1 ? bf2f(static_cast<const bf16*>(p)[i]) : static_cast<const float*>(p)[i];
+}
+
+struct RedGeom {
+  int GL, RL, G;  // group lanes, row lanes, channel groups
+};
+RedGeom red_geom(int C) {
+  RedGeom r;
+  r.G = C / 8;
+  r.GL = 1;
+  while (r.GL < r.G && r.GL < 64) r.GL <<= 1;
+  r.RL = 256 / r.GL;
+  return r;
+}
+dim3 red_grid(const RedGeom& r, int64_t M) {
+  const int gy = (r.G + r.GL - 1) / r.GL;
+  int64_t gx = (M + r.RL - 1) / r.RL;
+  const int64_t want = std::max<int64_t>(1, 2048 / gy);
+  gx = std::min(gx, want);
+  return dim3(static_cast<unsigned>(std::max<int64_t>(gx, 1)), gy);
+}
+
+// MODE 0: stats of x  -> out[0:C] += sum x, out[C:2C] += sum x^2
+// MODE 1: bwd reduce  -> out[0:C] += sum g,  out[C:2C] += sum g*xhat
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        const bf16* __restrict__ y, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, float* __restrict__ out,
+                                                        int64_t M, int C, int GL, int relu) {
+  __shared__ float red[2][256 * 8 + 8];
+  const int RL = 256 / GL;
+  const int gl = threadIdx.x % GL, rl = threadIdx.x / GL;
+  const int grp = blockIdx.y * GL + gl;
+  const bool gok = grp * 8 < C;
+  const int c0 = grp * 8;
+  float a[8], b[8], mu[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = b[i] = 0.f;
+  if (MODE == 1 && gok) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      mu[i] = mean[c0 + i];
+      rs[i] = rstd[c0 + i];
+    }
+  }
+  if (gok) {
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RL + rl; r < M; r += static_cast<int64_t>(gridDim.x) * RL) {
+      const int64_t off = r * C + c0;
+      float xv[8];
+      load8(x + off, xv);
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a[i] += xv[i];
+          b[i] += xv[i] * xv[i];
+        }
+      } else {
+        float g[8];
+        load8(dy + off, g);
+        if (relu) {
+          float yv[8];
+          load8(y + off, yv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a[i] += g[i];
+          b[i] += g[i] * (xv[i] - mu[i]) * rs[i];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[0][threadIdx.x * 8 + i] = a[i];
+    red[1][threadIdx.x * 8 + i] = b[i];
+  }
+  __syncthreads();
+  // column j of the block tile (GL*8 channels) reduced over RL row lanes
+  for (int j = threadIdx.x; j < GL * 8 * 2; j += 256) {
+    const int q = j / (GL * 8), col = j % (GL * 8);
+    const int lg = col / 8, e = col % 8;
+    float s = 0.f;
+    for (int l = 0; l < RL; ++l) s += red[q][(l * GL + lg) * 8 + e];
+    const int ch = blockIdx.y * GL * 8 + col;
+    if (ch < C) atomicAdd(out + q * C + ch, s);
+  }
+}
+
+// scale/shift from accumulated stats; running stats; saved mean / rstd.
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, const void* gamma, const void* beta, int pdt,
+                                   float* running_mean, float* running_var, float* scale, float* shift, float* mean_o,
+                                   float* rstd_o, int C, double count, float momentum, float eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = stats[c] / count;
+  double var = stats[C + c] / count - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = static_cast<float>(1.0 / sqrt(var + eps));
+  const float g = gamma ? ldp(gamma, pdt, c) : 1.f;
+  const float b = beta ? ldp(beta, pdt, c) : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = b - static_cast<float>(mean) * g * rstd;
+  if (mean_o) mean_o[c] = static_cast<float>(mean);
+  if (rstd_o) rstd_o[c] = rstd;
+  if (running_mean && momentum > 0.f) {
+    const double unbiased = count > 1.0 ? var * count / (count - 1.0) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * static_cast<float>(mean);
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * static_cast<float>(unbiased);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, bf16* __restrict__ y,
+                                                       int64_t nvec, int C, int relu) {
+  for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t off = v * 8;
+    const int c0 = static_cast<int>(off % C);
+    float xv[8];
+    load8(x + off, xv);
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c0), s1 = *reinterpret_cast<const f32x4*>(scale + c0 + 4);
+    const f32x4 h0 = *reinterpret_cast<const f32x4*>(shift + c0), h1 = *reinterpret_cast<const f32x4*>(shift + c0 + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xv[i] = xv[i] * s0[i] + h0[i];
+      xv[i + 4] = xv[i + 4] * s1[i] + h1[i];
+    }
+    if (res) {
+      float rv[8];
+      load8(res + off, rv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[i] += rv[i];
+    }
+    if (relu) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[i] = xv[i] > 0.f ? xv[i] : 0.f;
+    }
+    store8(y + off, xv);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                           const bf16* __restrict__ y, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, const void* gamma,
+                                                           int pdt, const float* __restrict__ sums,
+                                                           bf16* __restrict__ dx, bf16* __restrict__ dres,
+                                                           float* dgamma, float* dbeta,
+                                                           int64_t nvec, int C, int relu, float inv_count) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (dbeta) dbeta[c] += sums[c];
+      if (dgamma) dgamma[c] += sums[C + c];
+    }
+  }
+  for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t off = v * 8;
+    const int c0 = static_cast<int>(off % C);
+    float g[8], xv[8];
+    load8(dy + off, g);
+    load8(x + off, xv);
+    if (relu) {
+      float yv[8];
+      load8(y + off, yv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+    }
+    if (dres) store8(dres + off, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      const float rs = rstd[c];
+      const float xh = (xv[i] - mean[c]) * rs;
+      const float gm = gamma ? ldp(gamma, pdt, c) : 1.f;
+      g[i] = gm * rs * (g[i] - sums[c] * inv_count - xh * sums[C + c] * inv_count);
+    }
+    store8(dx + off, g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct PoolArgs {
+  int N, H, W, C, P, Q, R, S, sh, sw, ph, pw;
+  int avg, count_pad;
+};
+
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                       unsigned char* __restrict__ arg, PoolArgs a, int64_t nthreads) {
+  const int G = a.C / 8;
+  for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < nthreads;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(t % G);
+    int64_t pix = t / G;
+    const int q = static_cast<int>(pix % a.Q);
+    pix /= a.Q;
+    const int p = static_cast<int>(pix % a.P);
+    const int n = static_cast<int>(pix / a.P);
+    const int h0 = p * a.sh - a.ph, w0 = q * a.sw - a.pw;
+    float acc[8];
+    unsigned char best[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      acc[i] = a.avg ? 0.f : -__builtin_inff();
+      best[i] = 0;
+    }
+    int cnt = 0;
+    for (int r = 0; r < a.R; ++r) {
+      const int ih = h0 + r;
+      if (ih < 0 || ih >= a.H) continue;
+      for (int s = 0; s < a.S; ++s) {
+        const int iw = w0 + s;
+        if (iw < 0 || iw >= a.W) continue;
+        float v[8];
+        load8(x + ((static_cast<int64_t>(n) * a.H + ih) * a.W + iw) * a.C + g * 8, v);
+        ++cnt;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (a.avg) {
+            acc[i] += v[i];
+          } else if (v[i] > acc[i]) {
+            acc[i] = v[i];
+            best[i] = static_cast<unsigned char>(r * a.S + s);
+          }
+        }
+      }
+    }
+    const int64_t off = t * 8;
+    if (a.avg) {
+      const float div = a.count_pad ? static_cast<float>(a.R * a.S) : static_cast<float>(cnt > 0 ? cnt : 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] /= div;
+    } else if (arg) {
+      uint64_t packed = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) packed |= static_cast<uint64_t>(best[i]) << (8 * i);
+      *reinterpret_cast<uint64_t*>(arg + off) = packed;
+    }
+    store8(y + off, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ dy,
+                                                       const unsigned char* __restrict__ arg,
+                                                       bf16* __restrict__ dx, PoolArgs a, int64_t nthreads,
+                                                       float beta) {
+  const int G = a.C / 8;
+  for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < nthreads;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(t % G);
+    int64_t pix = t / G;
+    const int w = static_cast<int>(pix % a.W);
+    pix /= a.W;
+    const int h = static_cast<int>(pix % a.H);
+    const int n = static_cast<int>(pix / a.H);
+    // windows p with p*sh - ph <= h < p*sh - ph + R
+    const int pl = max(0, (h + a.ph - a.R + a.sh) / a.sh), ph_ = min(a.P - 1, (h + a.ph) / a.sh);
+    const int ql = max(0, (w + a.pw - a.S + a.sw) / a.sw), qh = min(a.Q - 1, (w + a.pw) / a.sw);
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int p = pl; p <= ph_; ++p) {
+      const int r = h - (p * a.sh - a.ph);
+      if (r < 0 || r >= a.R) continue;
+      for (int q = ql; q <= qh; ++q) {
+        const int s = w - (q * a.sw - a.pw);
+        if (s < 0 || s >= a.S) continue;
+        const int64_t o = ((static_cast<int64_t>(n) * a.P + p) * a.Q + q) * a.C + g * 8;
+        float d[8];
+        load8(dy + o, d);
+        if (a.avg) {
+          float div;
+          if (a.count_pad) {
+            div = static_cast<float>(a.R * a.S);
+          } else {
+            const int h0 = p * a.sh - a.ph, w0 = q * a.sw - a.pw;
+            const int nh = min(h0 + a.R, a.H) - max(h0, 0), nw = min(w0 + a.S, a.W) - max(w0, 0);
+            div = static_cast<float>(max(nh * nw, 1));
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[i] += d[i] / div;
+        } else {
+          const uint64_t packed = *reinterpret_cast<const uint64_t*>(arg + o);
+          const unsigned tap = static_cast<unsigned>(r * a.S + s);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (((packed >> (8 * i)) & 0xff) == tap) acc[i] += d[i];
+        }
+      }
+    }
+    const int64_t off = t * 8;
+    if (beta != 0.f) {
+      float old[8];
+      load8(dx + off, old);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += beta * old[i];
+    }
+    store8(dx + off, acc);
+  }
+}
+
+int ew_blocks(int64_t n) { return static_cast<int>(std::min<int64_t>((n + 255) / 256, 8192)); }
+
+}  // namespace
+
+void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st) {
+  if (C % 8) throw std::invalid_argument("bn_stats: C must be a multiple of 8");
+  if (M <= 0) return;
+  const RedGeom r = red_geom(C);
+  hipLaunchKernelGGL((bn_reduce_kernel<0>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x), nullptr,
+                     nullptr, nullptr, nullptr, stats, M, C, r.GL, 0);
+  FFK_LAUNCH_CHECK("bn_stats");
+}
+
+void bn_finalize(const float* stats, const void* gamma, const void* beta, int param_dtype, float* running_mean,
+                 float* running_var, float* scale, float* shift, float* mean, float* rstd, int C, double count,
+                 float momentum, float eps, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, gamma, beta, param_dtype,
+                     running_mean, running_var, scale, shift, mean, rstd, C, count, momentum, eps);
+  FFK_LAUNCH_CHECK("bn_finalize");
+}
+
+void bn_apply(const void* x, const void* residual, const float* scale, const float* shift, void* y, int64_t M, int C,
+              int relu, hipStream_t st) {
+  if (C % 8) throw std::invalid_argument("bn_apply: C must be a multiple of 8");
+  const int64_t nvec = M * C / 8;
+  if (nvec <= 0) return;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, st, static_cast<const bf16*>(x),
+                     static_cast<const bf16*>(residual), scale, shift, static_cast<bf16*>(y), nvec, C, relu);
+  FFK_LAUNCH_CHECK("bn_apply");
+}
+
+void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
+            int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
+            int relu, hipStream_t st) {
+  if (C % 8) throw std::invalid_argument("bn_bwd: C must be a multiple of 8");
+  if (M <= 0) return;
+  const RedGeom r = red_geom(C);
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C, st);
+  hipLaunchKernelGGL((bn_reduce_kernel<1>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x),
+                     static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean, rstd, ws, M, C, r.GL, relu);
+  const int64_t nvec = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, st, static_cast<const bf16*>(dy),
+                     static_cast<const bf16*>(x), static_cast<const bf16*>(y), mean, rstd, gamma, param_dtype, ws,
+                     static_cast<bf16*>(dx), static_cast<bf16*>(dres), dgamma, dbeta, nvec, C, relu, static_cast<float>(1.0 / M));
+  FFK_LAUNCH_CHECK("bn_bwd");
+}
+
+static PoolArgs pool_args(const PoolShape& s) {
+  if (s.C % 8) throw std::invalid_argument("pool2d: C must be a multiple of 8");
+  if (s.R * s.S > 256) throw std::invalid_argument("pool2d: window larger than 256 taps");
+  PoolArgs a{s.N, s.H, s.W, s.C, 0, 0, s.R, s.S, s.sh, s.sw, s.ph, s.pw, s.avg, s.count_pad};
+  a.P = (s.H + 2 * s.ph - s.R) / s.sh + 1;
+  a.Q = (s.W + 2 * s.pw - s.S) / s.sw + 1;
+  if (a.P <= 0 || a.Q <= 0 || s.sh <= 0 || s.sw <= 0) throw std::invalid_argument("pool2d: bad geometry");
+  return a;
+}
+
+void pool2d_fwd(const PoolShape& s, const void* x, void* y, void* argmax, hipStream_t st) {
+  const PoolArgs a = pool_args(s);
+  const int64_t n = static_cast<int64_t>(a.N) * a.P * a.Q * (a.C / 8);
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(ew_blocks(n)), dim3(256), 0, st, static_cast<const bf16*>(x),
+                     static_cast<bf16*>(y), static_cast<unsigned char*>(argmax), a, n);
+  FFK_LAUNCH_CHECK("pool2d_fwd");
+}
+
+void pool2d_bwd(const PoolShape& s, const void* dy, const void* argmax, void* dx, float beta, hipStream_t st) {
+  const PoolArgs a = pool_args(s);
+  if (!a.avg && !argmax) throw std::invalid_argument("pool2d_bwd: max pooling needs the argmax bytes");
+  const int64_t n = static_cast<int64_t>(a.N) * a.H * a.W * (a.C / 8);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(ew_blocks(n)), dim3(256), 0, st, static_cast<const bf16*>(dy),
+                     static_cast<const unsigned char*>(argmax), static_cast<bf16*>(dx), a, n, beta);
+  FFK_LAUNCH_CHECK("pool2d_bwd");
+}
+
+}  // namespace ffk

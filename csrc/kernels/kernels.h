@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 namespace ffk {
@@ -116,5 +117,40 @@ void mse_loss(int dtype, const void* pred, const void* label, void* grad, float*
 // kind: 0 uniform[a,b) 1 normal(a,b) 2 truncated normal(a,b) in [c,d] 3 constant a
 void init_tensor(int dtype, void* out, const NdShape& piece, const NdShape& full, const NdStrides& box_lo, int kind,
                  uint64_t seed, float a, float b, float c, float d, hipStream_t st);
+
+// ---- conv.hip: implicit-GEMM convolution, NHWC bf16 activations, weight
+// physically [K][R][S][C]; C % 8 == 0 and K % 8 == 0.
+struct ConvShape {
+  int N = 0, H = 0, W = 0, C = 0, K = 0, R = 1, S = 1;
+  int sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
+};
+// y = act(conv(x, w) + bias); stats (optional, [2][K] fp32, accumulated):
+// per-channel sum / sum of squares of y for a following BatchNorm.
+void conv2d_fwd(const ConvShape& s, const void* x, const void* w, const void* bias, void* y, float* stats, int act,
+                hipStream_t st);
+// dx = conv_transpose(dy, w) + beta * dx
+void conv2d_dgrad(const ConvShape& s, const void* dy, const void* w, void* dx, float beta, hipStream_t st);
+// dw (fp32, [K][R][S][C]) += x^T-conv dy  (split-K, fp32 atomics; splits <= 0: auto)
+void conv2d_wgrad(const ConvShape& s, const void* x, const void* dy, float* dw, int splits, hipStream_t st);
+
+// ---- bnpool.hip: BatchNorm (training) + pooling over NHWC bf16 [M][C]
+void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st);
+void bn_finalize(const float* stats, const void* gamma, const void* beta, int param_dtype, float* running_mean,
+                 float* running_var, float* scale, float* shift, float* mean, float* rstd, int C, double count,
+                 float momentum, float eps, hipStream_t st);
+void bn_apply(const void* x, const void* residual, const float* scale, const float* shift, void* y, int64_t M, int C,
+              int relu, hipStream_t st);
+// ws: 2*C floats; dgamma / dbeta (fp32) accumulate; dres (optional) = dy
+// masked by the ReLU (the residual branch's gradient of relu(bn(x) + res))
+void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
+            int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
+            int relu, hipStream_t st);
+struct PoolShape {
+  int N = 0, H = 0, W = 0, C = 0, R = 1, S = 1, sh = 1, sw = 1, ph = 0, pw = 0;
+  int avg = 0, count_pad = 0;
+};
+// argmax: one byte per output element (max pooling; may be null when no backward)
+void pool2d_fwd(const PoolShape& s, const void* x, void* y, void* argmax, hipStream_t st);
+void pool2d_bwd(const PoolShape& s, const void* dy, const void* argmax, void* dx, float beta, hipStream_t st);
 
 }  // namespace ffk

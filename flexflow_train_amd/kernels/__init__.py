@@ -662,3 +662,188 @@ def init_piece(out, full_shape, box_lo, kind: str, seed: int, a=0.0, b=1.0, c=-2
                       float(c), float(d), _stream())
     STATS["init"] += 1
     return out
+
+
+# ---------------------------------------------------------------------------
+# Convolution / BatchNorm / pooling over NHWC (torch channels_last) bf16
+# activations.  Activation tensors keep their logical NCHW shape; the kernels
+# read the channels_last storage.  Conv weights are physically [K][R][S][C].
+def _check_nhwc(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a GPU tensor")
+    if t.dtype != torch.bfloat16:
+        raise ValueError(f"{name}: expected bfloat16, got {t.dtype}")
+    if t.dim() != 4 or not t.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError(f"{name}: expected a 4-d channels_last tensor")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name}: data pointer must be 16-byte aligned")
+
+
+def nhwc(t: torch.Tensor) -> torch.Tensor:
+    """channels_last bf16 view/copy of a 4-d activation."""
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def conv_out_hw(H, W, R, S, sh, sw, ph, pw, dh=1, dw=1):
+    return (H + 2 * ph - dh * (R - 1) - 1) // sh + 1, (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+
+
+def _conv_geom(x_shape, K, R, S, stride, pad, dil):
+    N, C, H, W = x_shape
+    if C % 8 or K % 8:
+        raise ValueError("conv2d: input and output channels must be multiples of 8")
+    return [int(N), int(H), int(W), int(C), int(K), int(R), int(S), int(stride[0]), int(stride[1]),
+            int(pad[0]), int(pad[1]), int(dil[0]), int(dil[1])]
+
+
+def conv2d_fwd(x, w, bias=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), act: str = "none", stats=None):
+    """x [N,C,H,W] channels_last bf16; w [K,R,S,C] contiguous bf16 -> y [N,K,P,Q]
+    channels_last.  ``stats`` (fp32 [2,K]) accumulates per-channel sum / sumsq of y."""
+    _check_nhwc(x, "x")
+    K_, R, S, C = w.shape
+    _check(w, "w", torch.bfloat16)
+    if C != x.shape[1]:
+        raise ValueError(f"conv2d: weight has {C} input channels, input has {x.shape[1]}")
+    g = _conv_geom(x.shape, K_, R, S, stride, pad, dil)
+    P, Q = conv_out_hw(x.shape[2], x.shape[3], R, S, *stride, *pad, *dil)
+    if bias is not None:
+        _check(bias, "bias", torch.bfloat16, K_)
+    if stats is not None:
+        _check(stats, "stats", torch.float32, 2 * K_)
+    y = torch.empty((x.shape[0], K_, P, Q), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    ext().conv2d_fwd(g, _p(x), _p(w), _p(bias), _p(y), _p(stats), ACT_CODES[act], _stream())
+    STATS["conv2d_fwd"] += 1
+    return y
+
+
+def conv2d_dgrad(dy, w, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), out=None, beta: float = 0.0):
+    _check_nhwc(dy, "dy")
+    K_, R, S, C = w.shape
+    _check(w, "w", torch.bfloat16)
+    g = _conv_geom(x_shape, K_, R, S, stride, pad, dil)
+    P, Q = conv_out_hw(x_shape[2], x_shape[3], R, S, *stride, *pad, *dil)
+    if tuple(dy.shape) != (x_shape[0], K_, P, Q):
+        raise ValueError(f"conv2d_dgrad: dy shape {tuple(dy.shape)} != {(x_shape[0], K_, P, Q)}")
+    if out is None:
+        out = torch.empty(tuple(x_shape), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        beta = 0.0
+    else:
+        _check_nhwc(out, "dx")
+        if tuple(out.shape) != tuple(x_shape):
+            raise ValueError("conv2d_dgrad: out has the wrong shape")
+    ext().conv2d_dgrad(g, _p(dy), _p(w), _p(out), float(beta), _stream())
+    STATS["conv2d_dgrad"] += 1
+    return out
+
+
+def conv2d_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), splits: int = 0):
+    """dw (fp32, K*R*S*C elements, layout [K][R][S][C]) += wgrad."""
+    _check_nhwc(x, "x")
+    _check_nhwc(dy, "dy")
+    K_ = dy.shape[1]
+    g = _conv_geom(x.shape, K_, R, S, stride, pad, dil)
+    P, Q = conv_out_hw(x.shape[2], x.shape[3], R, S, *stride, *pad, *dil)
+    if tuple(dy.shape) != (x.shape[0], K_, P, Q):
+        raise ValueError("conv2d_wgrad: dy shape mismatch")
+    if not dw.is_cuda or dw.dtype != torch.float32 or not dw.is_contiguous() or dw.numel() != K_ * R * S * x.shape[1]:
+        raise ValueError("conv2d_wgrad: dw must be a contiguous fp32 [K,R,S,C] buffer")
+    ext().conv2d_wgrad(g, _p(x), _p(dy), _p(dw), int(splits), _stream())
+    STATS["conv2d_wgrad"] += 1
+
+
+def bn_stats(x, stats):
+    _check_nhwc(x, "x")
+    C = x.shape[1]
+    _check(stats, "stats", torch.float32, 2 * C)
+    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream())
+    STATS["bn_stats"] += 1
+
+
+def bn_finalize(stats, gamma, beta, count, eps, momentum=0.0, running_mean=None, running_var=None):
+    """-> (scale, shift, mean, rstd) fp32 [C]."""
+    C = stats.numel() // 2
+    f = torch.empty(4, C, device=stats.device, dtype=torch.float32)
+    pdt = DT_BF16
+    for name, t in (("gamma", gamma), ("beta", beta)):
+        if t is not None:
+            if t.numel() != C or not t.is_contiguous():
+                raise ValueError(f"bn_finalize: {name} must have {C} contiguous elements")
+            pdt = _dt(t)
+    if gamma is not None and beta is not None and gamma.dtype != beta.dtype:
+        raise ValueError("bn_finalize: gamma/beta dtype mismatch")
+    for t in (running_mean, running_var):
+        if t is not None:
+            _check(t, "running stat", torch.float32, C)
+    ext().bn_finalize(_p(stats), _p(gamma), _p(beta), pdt, _p(running_mean), _p(running_var), _p(f[0]), _p(f[1]),
+                      _p(f[2]), _p(f[3]), C, float(count), float(momentum), float(eps), _stream())
+    STATS["bn_finalize"] += 1
+    return f[0], f[1], f[2], f[3]
+
+
+def bn_apply(x, scale, shift, relu: bool, residual=None):
+    _check_nhwc(x, "x")
+    C = x.shape[1]
+    if residual is not None:
+        _check_nhwc(residual, "residual")
+        if residual.shape != x.shape:
+            raise ValueError("bn_apply: residual shape mismatch")
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    ext().bn_apply(_p(x), _p(residual), _p(scale), _p(shift), _p(y), x.numel() // C, C, int(relu), _stream())
+    STATS["bn_apply"] += 1
+    return y
+
+
+def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, want_masked: bool = False):
+    """-> (dx, masked dy or None)."""
+    _check_nhwc(dy, "dy")
+    _check_nhwc(x, "x")
+    if relu:
+        _check_nhwc(y, "y")
+    C = x.shape[1]
+    for name, t in (("dgamma", dgamma), ("dbeta", dbeta)):
+        if t is not None and (t.dtype != torch.float32 or t.numel() != C or not t.is_contiguous()):
+            raise ValueError(f"bn_bwd: {name} must be fp32 [{C}]")
+    pdt = _dt(gamma) if gamma is not None else DT_BF16
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    dres = torch.empty_like(x, memory_format=torch.channels_last) if want_masked else None
+    ws = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+    ext().bn_bwd(_p(dy), _p(x), _p(y if relu else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx), _p(dres),
+                 _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, int(relu), _stream())
+    STATS["bn_bwd"] += 1
+    return dx, dres
+
+
+def _pool_geom(x_shape, k, s, p, avg, count_pad):
+    N, C, H, W = x_shape
+    if C % 8:
+        raise ValueError("pool2d: channels must be a multiple of 8")
+    if k[0] * k[1] > 256:
+        raise ValueError("pool2d: window larger than 256 taps")
+    return [int(N), int(H), int(W), int(C), int(k[0]), int(k[1]), int(s[0]), int(s[1]), int(p[0]), int(p[1]),
+            int(avg), int(count_pad)]
+
+
+def pool2d_fwd(x, k, s, p, avg: bool, count_pad: bool = False, need_argmax: bool = True):
+    _check_nhwc(x, "x")
+    g = _pool_geom(x.shape, k, s, p, avg, count_pad)
+    P = (x.shape[2] + 2 * p[0] - k[0]) // s[0] + 1
+    Q = (x.shape[3] + 2 * p[1] - k[1]) // s[1] + 1
+    y = torch.empty((x.shape[0], x.shape[1], P, Q), device=x.device, dtype=x.dtype,
+                    memory_format=torch.channels_last)
+    arg = None
+    if not avg and need_argmax:
+        arg = torch.empty(y.numel(), device=x.device, dtype=torch.uint8)
+    ext().pool2d_fwd(g, _p(x), _p(y), _p(arg), _stream())
+    STATS["pool2d_fwd"] += 1
+    return y, arg
+
+
+def pool2d_bwd(dy, arg, x_shape, k, s, p, avg: bool, count_pad: bool = False):
+    _check_nhwc(dy, "dy")
+    g = _pool_geom(x_shape, k, s, p, avg, count_pad)
+    if not avg and (arg is None or arg.numel() != dy.numel()):
+        raise ValueError("pool2d_bwd: max pooling needs the forward's argmax")
+    dx = torch.empty(tuple(x_shape), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+    ext().pool2d_bwd(g, _p(dy), _p(arg), _p(dx), 0.0, _stream())
+    STATS["pool2d_bwd"] += 1
+    return dx

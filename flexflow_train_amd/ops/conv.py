@@ -2,51 +2,191 @@
 
 Parity: lib/kernels/src/cuda/ops/conv_2d_kernels.cu (cuDNN conv with
 autotuned algorithms, fused bias + activation, :8-391) and
-pool_2d_kernels.cu.  Channel parallelism follows op-attrs conv_2d.cc: an
-input-channel shard produces partial sums (bias on replica 0 only), an
-output-channel shard is expressed by the weight piece.
+pool_2d_kernels.cu (:103 forward, :123 backward).  Channel parallelism
+follows op-attrs conv_2d.cc: an input-channel shard produces partial sums
+(bias on replica 0 only), an output-channel shard is expressed by the weight
+piece.
 
-MI355X path: bf16 convolution through PyTorch-ROCm (MIOpen, channels-last
-NHWC so MIOpen picks its implicit-GEMM MFMA solvers), bias + activation
-applied in the same expression so MIOpen's fusion can take them.  A
-hand-written implicit-GEMM MFMA convolution is future work.
+MI355X path (csrc/kernels/conv.hip, bnpool.hip): activations stay NHWC
+(torch channels_last, logical shape NCHW) end to end; the weight is stored
+physically as [K][R][S][C] (``to_physical``) so the implicit-GEMM kernels
+read both operands in 16-byte channel chunks.  Forward fuses bias +
+activation and, when the executor pairs the conv with a following
+BatchNorm (``emit_bn_stats``), the per-channel statistics that BN needs.
+Backward = dgrad implicit GEMM + split-K wgrad accumulating in fp32 straight
+into the flat gradient buffer.  Inputs with fewer than 8 channels (the RGB
+stem) are zero-padded to 8.  Grouped convolutions and CPU tensors run
+through PyTorch (the weight is viewed back to OIHW).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
-from .base import register
-from .generic import AutogradOp
+from .. import kernels as K
+from .base import OpImpl, acc_grad, register
 
 _ACTS = {"none": lambda t: t, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
          "gelu": lambda t: F.gelu(t, approximate="tanh")}
 
 
+def _geom(ctx):
+    return ((int(ctx.a("stride_h", 1)), int(ctx.a("stride_w", 1))),
+            (int(ctx.a("padding_h", 0)), int(ctx.a("padding_w", 0))),
+            int(ctx.a("groups", 1)), ctx.a("activation", "none"))
+
+
+def _oihw(W: torch.Tensor) -> torch.Tensor:
+    """Logical-shaped [K, C, R, S] piece holding physical [K, R, S, C] data -> OIHW view."""
+    Kc, C, R, S = W.shape
+    return W.reshape(Kc, R, S, C).permute(0, 3, 1, 2)
+
+
 @register("CONV2D")
-class Conv2DOp(AutogradOp):
-    def compute(self, ctx, inputs, weights):
+class Conv2DOp(OpImpl):
+    def to_physical(self, attrs, index, piece):
+        if index != 0:
+            return piece
+        return piece.permute(0, 2, 3, 1).contiguous()
+
+    def to_logical(self, attrs, index, piece):
+        if index != 0:
+            return piece
+        return _oihw(piece).contiguous()
+
+    @staticmethod
+    def _native(x, W, groups, act):
+        return (x.is_cuda and x.dtype == torch.bfloat16 and groups == 1 and W.shape[0] % 8 == 0
+                and (x.shape[1] % 8 == 0 or x.shape[1] < 8) and act in ("none", "relu", "sigmoid", "tanh")
+                and K.use_hip(x))
+
+    def forward(self, ctx, inputs, weights):
         x = inputs[0]
         W = weights[0]
         b = weights[1] if len(weights) > 1 and ctx.sum_index == 0 else None
-        if x.is_cuda:
-            x = x.contiguous(memory_format=torch.channels_last)
-        y = F.conv2d(x, W.to(x.dtype), b.to(x.dtype) if b is not None else None,
-                     stride=(int(ctx.a("stride_h", 1)), int(ctx.a("stride_w", 1))),
-                     padding=(int(ctx.a("padding_h", 0)), int(ctx.a("padding_w", 0))),
-                     groups=int(ctx.a("groups", 1)))
-        return [_ACTS[ctx.a("activation", "none")](y)]
+        stride, pad, groups, act = _geom(ctx)
+        Kc, C, R, S = W.shape
+        if self._native(x, W, groups, act):
+            wp = W.reshape(Kc, R, S, C)
+            if wp.dtype != torch.bfloat16:
+                wp = wp.to(torch.bfloat16)
+            xin = K.nhwc(x)
+            if C % 8:  # RGB stem: zero-pad channels to 8 (input and weight)
+                xp = torch.zeros((x.shape[0], 8, x.shape[2], x.shape[3]), device=x.device, dtype=x.dtype,
+                                 memory_format=torch.channels_last)
+                xp[:, :C].copy_(xin)
+                xin = xp
+                wpad = torch.zeros((Kc, R, S, 8), device=x.device, dtype=wp.dtype)
+                wpad[..., :C].copy_(wp)
+                wp = wpad
+            stats = None
+            if ctx.extra.get("emit_bn_stats"):
+                stats = torch.zeros(2 * Kc, device=x.device, dtype=torch.float32)
+            bias = None if b is None else b.to(torch.bfloat16).contiguous()
+            y = K.conv2d_fwd(xin, wp, bias, stride, pad, act=act, stats=stats)
+            if stats is not None:
+                y._ff_bn_stats = stats
+            return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape))
+        xw = x.contiguous(memory_format=torch.channels_last) if x.is_cuda else x
+        with torch.no_grad():
+            y = _ACTS[act](F.conv2d(xw, _oihw(W).to(x.dtype), b.to(x.dtype) if b is not None else None,
+                                    stride=stride, padding=pad, groups=groups))
+        return [y], ("torch", x, W, b)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        stride, pad, groups, act = _geom(ctx)
+        if saved[0] == "torch":
+            _, x, W, b = saved
+            xi = x.detach().requires_grad_(bool(need_input_grad[0]))
+            Wr = W.detach().requires_grad_(weight_grads[0] is not None)
+            with torch.enable_grad():
+                xw = xi.contiguous(memory_format=torch.channels_last) if xi.is_cuda else xi
+                u = F.conv2d(xw, _oihw(Wr).to(x.dtype), None, stride=stride, padding=pad, groups=groups)
+                u.retain_grad()
+                y = _ACTS[act](u + b.to(u.dtype).view(1, -1, 1, 1) if b is not None else u)
+            torch.autograd.backward([y], [grad_outputs[0].to(y.dtype)])
+            if weight_grads[0] is not None and Wr.grad is not None:
+                acc_grad(weight_grads[0], Wr.grad)
+            if len(weight_grads) > 1 and weight_grads[1] is not None:
+                # every partial-sum replica computes the (identical) bias gradient
+                acc_grad(weight_grads[1], u.grad.float().sum((0, 2, 3)))
+            return [xi.grad if xi.requires_grad else None]
+
+        _, xin, wp, y, xshape = saved
+        Kc, R, S, Cp = wp.shape
+        dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))
+        if act != "none":
+            if act == "relu":
+                dy = torch.where(y > 0, dy, torch.zeros((), device=dy.device, dtype=dy.dtype))
+            else:
+                yf = y.float().detach()
+                if act == "sigmoid":
+                    d = yf * (1 - yf)
+                elif act == "tanh":
+                    d = 1 - yf * yf
+                else:
+                    raise NotImplementedError("conv2d: gelu backward needs the pre-activation")
+                dy = (dy.float() * d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if len(weight_grads) > 1 and weight_grads[1] is not None:
+            d2 = dy.permute(0, 2, 3, 1).reshape(-1, Kc)  # channels_last -> [pixels, K] view
+            K.colsum_act(d2, None, "none", weight_grads[1], write_dx=False)
+        dW = weight_grads[0]
+        if dW is not None:
+            if Cp == xshape[1]:
+                K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
+            else:  # padded stem: wgrad into a padded buffer, keep the real channels
+                tmp = torch.zeros(Kc * R * S * Cp, device=dy.device, dtype=torch.float32)
+                K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad)
+                dW.view(Kc, R, S, xshape[1]).add_(tmp.view(Kc, R, S, Cp)[..., :xshape[1]])
+        if not need_input_grad[0]:
+            return [None]
+        if Cp != xshape[1]:
+            dx = K.conv2d_dgrad(dy, wp, (xshape[0], Cp, xshape[2], xshape[3]), stride, pad)
+            return [dx[:, :xshape[1]]]
+        acc = ctx.extra.get("grad_acc", [None])[0]
+        if (acc is not None and acc.is_cuda and acc.dtype == torch.bfloat16 and tuple(acc.shape) == tuple(xshape)
+                and acc.is_contiguous(memory_format=torch.channels_last)):
+            K.conv2d_dgrad(dy, wp, xshape, stride, pad, out=acc, beta=1.0)
+            return [acc]
+        return [K.conv2d_dgrad(dy, wp, xshape, stride, pad)]
 
 
 @register("POOL2D")
-class Pool2DOp(AutogradOp):
-    def compute(self, ctx, inputs, weights):
-        x = inputs[0]
+class Pool2DOp(OpImpl):
+    @staticmethod
+    def _geom(ctx):
         k = (int(ctx.a("kernel_h")), int(ctx.a("kernel_w")))
         s = (int(ctx.a("stride_h", 1)), int(ctx.a("stride_w", 1)))
         p = (int(ctx.a("padding_h", 0)), int(ctx.a("padding_w", 0)))
-        if ctx.a("pool_type", "max") == "max":
-            y = F.max_pool2d(x, k, s, p)
-        else:
-            y = F.avg_pool2d(x, k, s, p, count_include_pad=False)
-        return [_ACTS[ctx.a("activation", "none")](y)]
+        return k, s, p, ctx.a("pool_type", "max") != "max", ctx.a("activation", "none")
+
+    def forward(self, ctx, inputs, weights):
+        x = inputs[0]
+        k, s, p, avg, act = self._geom(ctx)
+        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and act == "none"
+                and k[0] * k[1] <= 256 and K.use_hip(x)):
+            xin = K.nhwc(x)
+            y, arg = K.pool2d_fwd(xin, k, s, p, avg, count_pad=False, need_argmax=ctx.training)
+            return [y], ("hip", tuple(x.shape), arg)
+        with torch.no_grad():
+            y = self._torch(x, k, s, p, avg, act)
+        return [y], ("torch", x)
+
+    @staticmethod
+    def _torch(x, k, s, p, avg, act):
+        y = F.avg_pool2d(x, k, s, p, count_include_pad=False) if avg else F.max_pool2d(x, k, s, p)
+        return _ACTS[act](y)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        if not need_input_grad[0]:
+            return [None]
+        k, s, p, avg, act = self._geom(ctx)
+        if saved[0] == "hip":
+            _, xshape, arg = saved
+            dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))
+            return [K.pool2d_bwd(dy, arg, xshape, k, s, p, avg, count_pad=False)]
+        x = saved[1].detach().requires_grad_(True)
+        with torch.enable_grad():
+            y = self._torch(x, k, s, p, avg, act)
+        y.backward(grad_outputs[0].to(y.dtype))
+        return [x.grad]

@@ -95,7 +95,10 @@ def _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre):
             torch.addmm(bias, A, B, out=u)
         else:
             torch.mm(A, B, out=u)
-        y, _ = K.bias_act_fwd(u, None, act)
+        if u.shape[-1] % 8 == 0:
+            y, _ = K.bias_act_fwd(u, None, act)
+        else:  # narrow heads (e.g. DLRM's 1-wide output) miss the 16-byte vector path
+            y = _ACT[act](u)
         if out is not None:
             out.copy_(y)
             return out

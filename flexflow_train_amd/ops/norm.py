@@ -15,7 +15,6 @@ import torch
 
 from .. import kernels as K
 from .base import OpImpl, acc_grad, register
-from .generic import AutogradOp
 
 
 def _ln_axes_are_trailing(ctx, x):
@@ -90,25 +89,97 @@ class FusedAddLayerNormOp(_LayerNormBase):
 
 
 @register("BATCHNORM")
-class BatchNormOp(AutogradOp):
+class BatchNormOp(OpImpl):
     """Training-mode batch norm over the sample + spatial dims, running stats
-    kept in the op's persistent state (ctx.extra['state'])."""
+    kept in the op's persistent state (ctx.extra['state']).
 
-    def compute(self, ctx, inputs, weights):
-        x = inputs[0]
+    GPU (bnpool.hip): per-channel statistics come from the producing
+    convolution's epilogue when the executor paired them (``_ff_bn_stats`` on
+    the input tensor) or from one reduction pass; apply = one fused pass
+    (scale/shift [+ residual] [ReLU]); backward = one reduction + one apply
+    pass.  ``ctx.extra['residual_relu']`` (set by the executor's
+    BATCHNORM -> EW_ADD -> RELU fusion) makes the op compute
+    relu(bn(x) + residual) and return the residual's gradient too.
+    """
+
+    @staticmethod
+    def _state(ctx, C, dev):
         state = ctx.extra.setdefault("state", {})
+        if "running_mean" not in state or state["running_mean"].device != dev:
+            state["running_mean"] = torch.zeros(C, device=dev, dtype=torch.float32)
+            state["running_var"] = torch.ones(C, device=dev, dtype=torch.float32)
+        return state
+
+    def forward(self, ctx, inputs, weights):
+        x = inputs[0]
+        fused = bool(ctx.extra.get("residual_relu"))
+        res = inputs[1] if fused else None
+        relu = True if fused else bool(ctx.a("relu", False))
         C = x.shape[1]
-        if "running_mean" not in state:
-            state["running_mean"] = torch.zeros(C, device=x.device, dtype=torch.float32)
-            state["running_var"] = torch.ones(C, device=x.device, dtype=torch.float32)
+        state = self._state(ctx, C, x.device)
         g = weights[0] if weights else None
         b = weights[1] if len(weights) > 1 else None
-        train = ctx.training and not torch.is_grad_enabled()  # update stats only in the real forward
+        eps = float(ctx.a("eps", 1e-5))
+        mom = float(ctx.a("momentum", 0.1))
+        if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and C % 8 == 0 and K.use_hip(x)
+                and (res is None or (res.dtype == x.dtype and res.shape == x.shape))):
+            stats_in = getattr(x, "_ff_bn_stats", None)
+            xin = K.nhwc(x)
+            if ctx.training:
+                stats = stats_in
+                if stats is None:
+                    stats = torch.zeros(2 * C, device=x.device, dtype=torch.float32)
+                    K.bn_stats(xin, stats)
+                scale, shift, mean, rstd = K.bn_finalize(stats, g, b, xin.numel() // C, eps, mom,
+                                                         state["running_mean"], state["running_var"])
+            else:
+                rstd = torch.rsqrt(state["running_var"] + eps)
+                mean = state["running_mean"]
+                gf = g.float() if g is not None else torch.ones_like(rstd)
+                bf = b.float() if b is not None else torch.zeros_like(rstd)
+                scale = (gf * rstd).contiguous()
+                shift = (bf - mean * gf * rstd).contiguous()
+            y = K.bn_apply(xin, scale, shift, relu, residual=None if res is None else K.nhwc(res))
+            return [y], ("hip", xin, y if relu else None, mean, rstd, g, relu, fused)
+        train = ctx.training
+        xf = x.float()
         y = torch.nn.functional.batch_norm(
-            x.float(), state["running_mean"], state["running_var"],
+            xf, state["running_mean"], state["running_var"],
             g.float() if g is not None else None, b.float() if b is not None else None,
-            training=ctx.training, momentum=float(ctx.a("momentum", 0.1)) if train else 0.0,
-            eps=float(ctx.a("eps", 1e-5)))
-        if ctx.a("relu", False):
+            training=train, momentum=mom if train else 0.0, eps=eps)
+        if res is not None:
+            y = y + res.float()
+        if relu:
             y = torch.relu(y)
-        return [y.to(x.dtype)]
+        return [y.to(x.dtype)], ("torch", x, res, g, b, relu)
+
+    def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        dy = grad_outputs[0]
+        dg = weight_grads[0] if weight_grads else None
+        db = weight_grads[1] if len(weight_grads) > 1 else None
+        if saved[0] == "hip":
+            _, xin, y, mean, rstd, g, relu, fused = saved
+            dyn = K.nhwc(dy.to(torch.bfloat16))
+            dx, dres = K.bn_bwd(dyn, xin, y, mean, rstd, g, relu, dgamma=dg, dbeta=db, want_masked=fused)
+            return [dx, dres] if fused else [dx]
+        _, x, res, g, b, relu = saved
+        eps = float(ctx.a("eps", 1e-5))
+        xi = x.detach().float().requires_grad_(True)
+        gr = g.detach().float().requires_grad_(True) if g is not None else None
+        br = b.detach().float().requires_grad_(True) if b is not None else None
+        rr = res.detach().float().requires_grad_(True) if res is not None else None
+        with torch.enable_grad():
+            y = torch.nn.functional.batch_norm(xi, None, None, gr, br, training=True, eps=eps)
+            if rr is not None:
+                y = y + rr
+            if relu:
+                y = torch.relu(y)
+        y.backward(dy.float())
+        if dg is not None and gr is not None:
+            acc_grad(dg, gr.grad)
+        if db is not None and br is not None:
+            acc_grad(db, br.grad)
+        outs = [xi.grad.to(x.dtype)]
+        if rr is not None:
+            outs.append(rr.grad.to(res.dtype))
+        return outs

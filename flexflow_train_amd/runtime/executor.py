@@ -330,6 +330,7 @@ class Executor:
             self.loss_value = prod_step.inputs[0]
         if self.cfg.fuse_add_layernorm:
             self._fuse_add_layernorm()
+            self._fuse_conv_bn()
         self._mark_requires_grad()
         self._assign_params_to_buffers()
 
@@ -351,6 +352,67 @@ class Executor:
                     drop.add(id(prod))
         for s in self.steps:
             if id(s) not in drop:
+                keep.append(s)
+        self.steps = keep
+
+    def _fuse_conv_bn(self):
+        """CNN fusions (the reference's FusedOp grouping, lib/runtime/src/ops/fused.cc,
+        done as real kernel fusion):
+        * CONV2D whose only consumer is a BATCHNORM on the same layout emits the
+          per-channel statistics from its epilogue (``emit_bn_stats``);
+        * BATCHNORM(relu=False) -> EW_ADD -> RELU (the residual block tail) becomes
+          one BATCHNORM step computing relu(bn(x) + residual), placed where the add
+          was (both operands are available there)."""
+        by_out = {o: s for s in self.steps for o in s.outputs}
+        uses: Dict[Value, List[Step]] = {}
+        for s in self.steps:
+            for v in s.inputs:
+                uses.setdefault(v, []).append(s)
+        lay = self.value_layout
+        for s in self.steps:
+            if s.kind != "compute" or s.op_type != "BATCHNORM" or len(s.inputs) != 1:
+                continue
+            prod = by_out.get(s.inputs[0])
+            if (prod is not None and prod.kind == "compute" and prod.op_type == "CONV2D"
+                    and len(uses.get(s.inputs[0], [])) == 1 and s.inputs[0] != self.loss_value
+                    and prod.ctx.sum_degree == 1 and s.ctx.sum_degree == 1):
+                prod.ctx.extra["emit_bn_stats"] = True
+        drop = set()
+        moves = {}
+        for s in self.steps:
+            if (s.kind != "compute" or s.op_type != "BATCHNORM" or len(s.inputs) != 1 or s.ctx.a("relu", False)
+                    or len(s.outputs) != 1):
+                continue
+            v = s.outputs[0]
+            u = uses.get(v, [])
+            if len(u) != 1 or u[0].kind != "compute" or u[0].op_type != "EW_ADD" or v == self.loss_value:
+                continue
+            add = u[0]
+            if id(add) in moves:  # both add operands are BN outputs: fuse one of them
+                continue
+            a = add.outputs[0]
+            ua = uses.get(a, [])
+            if len(ua) != 1 or ua[0].kind != "compute" or ua[0].op_type != "RELU" or a == self.loss_value:
+                continue
+            relu = ua[0]
+            other = add.inputs[1] if add.inputs[0] == v else add.inputs[0]
+            if other == v or not (lay[other] == lay[v] == lay[a] == lay[relu.outputs[0]]):
+                continue
+            if tuple(lay[other].piece_shape) != tuple(lay[v].piece_shape):
+                continue
+            s.inputs = [s.inputs[0], other]
+            s.outputs = list(relu.outputs)
+            s.ctx.extra["residual_relu"] = True
+            drop.add(id(relu))
+            moves[id(add)] = s
+        keep = []
+        moved = {id(s) for s in moves.values()}
+        for s in self.steps:
+            if id(s) in moves:
+                keep.append(moves[id(s)])
+            elif id(s) in drop or id(s) in moved:
+                continue
+            else:
                 keep.append(s)
         self.steps = keep
 
