@@ -196,14 +196,17 @@ PYBIND11_MODULE(_ffkernels, m) {
     c.sh = v[7]; c.sw = v[8]; c.ph = v[9]; c.pw = v[10]; c.dh = v[11]; c.dw = v[12];
     return c;
   };
+  m.def("conv2d_stats_ws_floats", [=](std::vector<int> shp) { return conv2d_stats_ws_floats(cshape(shp)); });
+  m.def("conv2d_wgrad_ws_floats",
+        [=](std::vector<int> shp, int splits) { return conv2d_wgrad_ws_floats(cshape(shp), splits); });
   m.def("conv2d_fwd", [=](std::vector<int> shp, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y,
-                          uintptr_t stats, int act, uintptr_t st) {
-    conv2d_fwd(cshape(shp), P(x), P(w), P(bias), P(y), F(stats), act, S(st));
+                          uintptr_t stats, uintptr_t ws, int act, uintptr_t st) {
+    conv2d_fwd(cshape(shp), P(x), P(w), P(bias), P(y), F(stats), F(ws), act, S(st));
   });
   m.def("conv2d_dgrad", [=](std::vector<int> shp, uintptr_t dy, uintptr_t w, uintptr_t dx, float beta,
                             uintptr_t st) { conv2d_dgrad(cshape(shp), P(dy), P(w), P(dx), beta, S(st)); });
-  m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, int splits,
-                            uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), splits, S(st)); });
+  m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws, int splits,
+                            uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), F(ws), splits, S(st)); });
   m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st) {
     bn_stats(P(x), F(stats), M, C, S(st));
   });

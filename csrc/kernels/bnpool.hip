@@ -14,8 +14,9 @@
 //     turns them into scale/shift (+ running-stat update, + saved mean/rstd);
 //   * bn_apply: y = x*scale + shift [+ residual] [ReLU] in one pass;
 //   * backward: bn_bwd_reduce accumulates sum(g), sum(g*xhat) with g = dy
-//     masked by the ReLU (recomputed from y), bn_bwd_apply writes
-//     dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) and dgamma/dbeta.
+//     masked by the ReLU (recomputed from y), bn_bwd_coef folds them into
+//     per-channel (A, B, D) and dgamma/dbeta, bn_bwd_apply writes
+//     dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) = A*g + B*x + D.
 // Reductions: a block is RL row-lanes x GL channel-group lanes; each thread
 // strides over rows with 8 fp32 accumulators per quantity, the block reduces
 // its row-lanes through LDS and issues one fp32 atomic per channel.
@@ -185,19 +186,28 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
   }
 }
 
+// per-channel backward coefficients: dx = A*g + B*x + D with
+// A = gamma*rstd, B = -A*rstd*mean(g*xhat), D = -A*mean(g) - B*mean;
+// also dgamma += sum(g*xhat), dbeta += sum(g).
+__global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* __restrict__ mean,
+                                   const float* __restrict__ rstd, const void* gamma, int pdt, float* __restrict__ coef,
+                                   float* dgamma, float* dbeta, int C, float inv_count) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float s1 = sums[c], s2 = sums[C + c];
+  const float A = (gamma ? ldp(gamma, pdt, c) : 1.f) * rstd[c];
+  const float B = -A * rstd[c] * s2 * inv_count;
+  coef[c] = A;
+  coef[C + c] = B;
+  coef[2 * C + c] = -A * s1 * inv_count - B * mean[c];
+  if (dbeta) dbeta[c] += s1;
+  if (dgamma) dgamma[c] += s2;
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                           const bf16* __restrict__ y, const float* __restrict__ mean,
-                                                           const float* __restrict__ rstd, const void* gamma,
-                                                           int pdt, const float* __restrict__ sums,
+                                                           const bf16* __restrict__ y, const float* __restrict__ coef,
                                                            bf16* __restrict__ dx, bf16* __restrict__ dres,
-                                                           float* dgamma, float* dbeta,
-                                                           int64_t nvec, int C, int relu, float inv_count) {
-  if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      if (dbeta) dbeta[c] += sums[c];
-      if (dgamma) dgamma[c] += sums[C + c];
-    }
-  }
+                                                           int64_t nvec, int C, int relu) {
   for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvec;
        v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t off = v * 8;
@@ -213,12 +223,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     }
     if (dres) store8(dres + off, g);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      const float rs = rstd[c];
-      const float xh = (xv[i] - mean[c]) * rs;
-      const float gm = gamma ? ldp(gamma, pdt, c) : 1.f;
-      g[i] = gm * rs * (g[i] - sums[c] * inv_count - xh * sums[C + c] * inv_count);
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 A = *reinterpret_cast<const f32x4*>(coef + c0 + 4 * h);
+      const f32x4 B = *reinterpret_cast<const f32x4*>(coef + C + c0 + 4 * h);
+      const f32x4 D = *reinterpret_cast<const f32x4*>(coef + 2 * C + c0 + 4 * h);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g[4 * h + i] = A[i] * g[4 * h + i] + B[i] * xv[4 * h + i] + D[i];
     }
     store8(dx + off, g);
   }
@@ -384,10 +394,13 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C, st);
   hipLaunchKernelGGL((bn_reduce_kernel<1>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x),
                      static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean, rstd, ws, M, C, r.GL, relu);
+  float* coef = ws + 2 * C;
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, mean, rstd, gamma,
+                     param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M));
   const int64_t nvec = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, st, static_cast<const bf16*>(dy),
-                     static_cast<const bf16*>(x), static_cast<const bf16*>(y), mean, rstd, gamma, param_dtype, ws,
-                     static_cast<bf16*>(dx), static_cast<bf16*>(dres), dgamma, dbeta, nvec, C, relu, static_cast<float>(1.0 / M));
+                     static_cast<const bf16*>(x), static_cast<const bf16*>(y), coef, static_cast<bf16*>(dx),
+                     static_cast<bf16*>(dres), nvec, C, relu);
   FFK_LAUNCH_CHECK("bn_bwd");
 }
 

@@ -22,10 +22,11 @@
 // (out-of-image taps and tile tails load zeros).  BN = 64 serves the
 // 64-channel layers without wasting half the MFMAs.  Epilogues: FWD fuses
 // bias + activation and (optionally) the per-channel sum / sum-of-squares a
-// following training-mode BatchNorm needs (one wave-reduce + one fp32 atomic
-// per column per wave), so BN never re-reads Y for its statistics; WGRAD is
-// split-K over the pixel axis with fp32 atomic accumulation straight into the
-// flat gradient buffer (which already has += semantics).
+// following training-mode BatchNorm needs (a wave-reduce per column into a
+// per-tile partial slot, folded by reduce_rows — no same-address atomic
+// storms), so BN never re-reads Y for its statistics; WGRAD is split-K over
+// the pixel axis with per-split fp32 slabs summed by reduce_rows into the
+// flat gradient buffer (+=); a single-split launch accumulates in place.
 #include "kernels.h"
 #include "mfma.h"
 
@@ -42,7 +43,8 @@ struct ConvArgs {
   const bf16* dy;   // DGRAD/WGRAD      [N][P][Q][K]
   void* out;        // FWD y [N][P][Q][K] bf16 | DGRAD dx [N][H][W][C] bf16 | WGRAD dw [K][R][S][C] f32
   const bf16* bias; // FWD only
-  float* stats;     // FWD only: [2][K] (sum, sum of squares), accumulated
+  float* stats;     // FWD only: per-wave partials [gm*2][2][K] (sum, sum of squares)
+  float* wpart;     // WGRAD split-K partial slabs [splits][K][R*S*C] (null: splits == 1)
   int N, H, W, C, K, R, S, P, Q;
   int sh, sw, ph, pw, dh, dw;
   int M, NG, KG;    // GEMM sizes
@@ -319,7 +321,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   // ---- epilogue: acc[nt][mt] holds C^T; lane&31 = m row, registers = 4 n columns
   const int h = lane >> 5;
   if (MODE == MODE_WGRAD) {
-    float* out = static_cast<float*>(g.out);
+    // one writer per element: split 0 of a single-split launch accumulates into
+    // dW directly; otherwise this split's slab (summed by reduce_rows)
+    float* out = g.wpart ? g.wpart + static_cast<int64_t>(split) * g.M * g.NG : static_cast<float*>(g.out);
+    const bool accumulate = g.wpart == nullptr;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const int m = m0 + wm * 64 + mt * 32 + (lane & 31);
@@ -330,9 +335,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
         for (int g4 = 0; g4 < 4; ++g4) {
           const int n = n0 + wn * (BN / 2) + nt * 32 + 8 * g4 + 4 * h;
           if (n >= g.NG) continue;
-          float* dst = out + static_cast<int64_t>(m) * g.NG + n;
+          f32x4* dst = reinterpret_cast<f32x4*>(out + static_cast<int64_t>(m) * g.NG + n);
+          f32x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) atomicAdd(dst + e, acc[nt][mt][4 * g4 + e]);
+          for (int e = 0; e < 4; ++e) v[e] = acc[nt][mt][4 * g4 + e];
+          if (accumulate) v += *dst;
+          *dst = v;
         }
     }
     return;
@@ -387,6 +395,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
       }
   }
   if (MODE == MODE_FWD && g.stats) {
+    // per-wave column partials (no atomics: a slot per (m tile, wave row));
+    // reduce_rows folds them into the [2][K] statistics
+    float* part = g.stats + static_cast<int64_t>(tm * 2 + wm) * 2 * g.NG;
 #pragma unroll
     for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
@@ -401,11 +412,48 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
           }
           const int n = n0 + wn * (BN / 2) + nt * 32 + 8 * g4 + 4 * h + e;
           if ((lane & 31) == 0 && n < g.NG) {
-            atomicAdd(g.stats + n, s);
-            atomicAdd(g.stats + g.NG + n, q);
+            part[n] = s;
+            part[g.NG + n] = q;
           }
         }
   }
+}
+
+// out[j] (+)= sum_r ws[r][j]; grid (column blocks of 1024, row chunks) —
+// row chunks > 1 combine with fp32 atomics (few per address).
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                          int rows, int64_t W, int rows_per_chunk, int accumulate) {
+  const int64_t j = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (j >= W) return;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (j + 3 < W) {
+    for (int r = r0; r < r1; ++r) s += *reinterpret_cast<const f32x4*>(ws + static_cast<int64_t>(r) * W + j);
+    if (gridDim.y == 1) {
+      f32x4* d = reinterpret_cast<f32x4*>(out + j);
+      *d = accumulate ? *d + s : s;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(out + j + e, s[e]);
+    }
+  } else {
+    for (int e = 0; j + e < W; ++e) {
+      float t = 0.f;
+      for (int r = r0; r < r1; ++r) t += ws[static_cast<int64_t>(r) * W + j + e];
+      if (gridDim.y == 1) out[j + e] = accumulate ? out[j + e] + t : t;
+      else atomicAdd(out + j + e, t);
+    }
+  }
+}
+
+void reduce_rows(const float* ws, float* out, int rows, int64_t W, int accumulate, hipStream_t st) {
+  const int64_t cols = (W + 1023) / 1024;
+  int chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(rows / 16, 1024 / std::max<int64_t>(cols, 1))));
+  if (chunks > 1 && !accumulate) throw std::logic_error("reduce_rows: chunked reduce needs accumulate");
+  const int per = (rows + chunks - 1) / chunks;
+  chunks = (rows + per - 1) / per;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(static_cast<unsigned>(cols), chunks), dim3(256), 0, st, ws, out, rows,
+                     W, per, accumulate);
 }
 
 ConvArgs make_args(const ConvShape& cs) {
@@ -439,23 +487,36 @@ void launch(const ConvArgs& g, int bn, int blocks, hipStream_t st) {
 
 }  // namespace
 
-void conv2d_fwd(const ConvShape& cs, const void* x, const void* w, const void* bias, void* y, float* stats, int act,
-                hipStream_t st) {
+int conv2d_stats_ws_floats(const ConvShape& cs) {
+  ConvArgs g = make_args(cs);
+  const int64_t M = static_cast<int64_t>(g.N) * g.P * g.Q;
+  return static_cast<int>(((M + BM - 1) / BM) * 2 * 2 * cs.K);
+}
+
+void conv2d_fwd(const ConvShape& cs, const void* x, const void* w, const void* bias, void* y, float* stats,
+                float* stats_ws, int act, hipStream_t st) {
   check_shape(cs, "conv2d_fwd");
+  if (stats && !stats_ws) throw std::invalid_argument("conv2d_fwd: statistics need a workspace");
   ConvArgs g = make_args(cs);
   g.x = static_cast<const bf16*>(x);
   g.w = static_cast<const bf16*>(w);
   g.bias = static_cast<const bf16*>(bias);
   g.out = y;
-  g.stats = stats;
+  g.stats = stats ? stats_ws : nullptr;
   g.act = act;
   g.M = g.N * g.P * g.Q;
   g.NG = g.K;
   g.KG = g.R * g.S * g.C;
   const int bn = g.NG <= 64 ? 64 : 128;
-  const int blocks = ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn);
+  const int gm = (g.M + BM - 1) / BM;
+  const int blocks = gm * ((g.NG + bn - 1) / bn);
   launch<MODE_FWD>(g, bn, blocks, st);
   FFK_LAUNCH_CHECK("conv2d_fwd");
+  if (stats) {
+    (void)hipMemsetAsync(stats, 0, sizeof(float) * 2 * g.NG, st);
+    reduce_rows(stats_ws, stats, gm * 2, 2 * static_cast<int64_t>(g.NG), 1, st);
+    FFK_LAUNCH_CHECK("conv2d_fwd stats");
+  }
 }
 
 void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, float beta, hipStream_t st) {
@@ -474,28 +535,57 @@ void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, 
   FFK_LAUNCH_CHECK("conv2d_dgrad");
 }
 
-void conv2d_wgrad(const ConvShape& cs, const void* x, const void* dy, float* dw, int splits, hipStream_t st) {
+namespace {
+struct WgradPlan {
+  int bn, tiles, splits, kt_per_split;
+};
+WgradPlan wgrad_plan(const ConvShape& cs, int splits) {
+  ConvArgs g = make_args(cs);
+  const int M = cs.K, NG = cs.R * cs.S * cs.C;
+  const int64_t KG = static_cast<int64_t>(g.N) * g.P * g.Q;
+  WgradPlan p;
+  p.bn = NG <= 64 ? 64 : 128;
+  p.tiles = ((M + BM - 1) / BM) * ((NG + p.bn - 1) / p.bn);
+  const int nk = static_cast<int>((KG + BK - 1) / BK);
+  if (splits <= 0) {
+    // ~2048 blocks (8 per CU), >= 8 K-tiles per split, slabs <= 256 MiB
+    splits = (2048 + p.tiles - 1) / p.tiles;
+    splits = std::min(splits, std::max(1, nk / 8));
+    const int64_t slab = static_cast<int64_t>(M) * NG * 4;
+    splits = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(splits, (int64_t(256) << 20) / slab)));
+  }
+  splits = std::max(1, std::min(splits, nk));
+  p.kt_per_split = (nk + splits - 1) / splits;
+  p.splits = (nk + p.kt_per_split - 1) / p.kt_per_split;
+  return p;
+}
+}  // namespace
+
+int64_t conv2d_wgrad_ws_floats(const ConvShape& cs, int splits) {
+  const WgradPlan p = wgrad_plan(cs, splits);
+  return p.splits > 1 ? static_cast<int64_t>(p.splits) * cs.K * cs.R * cs.S * cs.C : 0;
+}
+
+void conv2d_wgrad(const ConvShape& cs, const void* x, const void* dy, float* dw, float* ws, int splits,
+                  hipStream_t st) {
   check_shape(cs, "conv2d_wgrad");
+  const WgradPlan p = wgrad_plan(cs, splits);
+  if (p.splits > 1 && !ws) throw std::invalid_argument("conv2d_wgrad: split-K needs a workspace");
   ConvArgs g = make_args(cs);
   g.x = static_cast<const bf16*>(x);
   g.dy = static_cast<const bf16*>(dy);
   g.out = dw;
+  g.wpart = p.splits > 1 ? ws : nullptr;
   g.M = g.K;
   g.NG = g.R * g.S * g.C;
   g.KG = g.N * g.P * g.Q;
-  const int bn = g.NG <= 64 ? 64 : 128;
-  const int tiles = ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn);
-  const int nk = (g.KG + BK - 1) / BK;
-  if (splits <= 0) {
-    // aim for ~4 waves of blocks over 256 CUs, at least 4 K-tiles per split
-    splits = (2048 + tiles - 1) / tiles;
-    splits = std::max(1, std::min(splits, nk / 4));
-  }
-  splits = std::max(1, std::min(splits, nk));
-  g.kt_per_split = (nk + splits - 1) / splits;
-  splits = (nk + g.kt_per_split - 1) / g.kt_per_split;
-  launch<MODE_WGRAD>(g, bn, tiles * splits, st);
+  g.kt_per_split = p.kt_per_split;
+  launch<MODE_WGRAD>(g, p.bn, p.tiles * p.splits, st);
   FFK_LAUNCH_CHECK("conv2d_wgrad");
+  if (p.splits > 1) {
+    reduce_rows(ws, dw, p.splits, static_cast<int64_t>(g.M) * g.NG, 1, st);
+    FFK_LAUNCH_CHECK("conv2d_wgrad reduce");
+  }
 }
 
 }  // namespace ffk

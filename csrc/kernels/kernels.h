@@ -124,14 +124,19 @@ struct ConvShape {
   int N = 0, H = 0, W = 0, C = 0, K = 0, R = 1, S = 1;
   int sh = 1, sw = 1, ph = 0, pw = 0, dh = 1, dw = 1;
 };
-// y = act(conv(x, w) + bias); stats (optional, [2][K] fp32, accumulated):
-// per-channel sum / sum of squares of y for a following BatchNorm.
-void conv2d_fwd(const ConvShape& s, const void* x, const void* w, const void* bias, void* y, float* stats, int act,
-                hipStream_t st);
+// y = act(conv(x, w) + bias); stats (optional, [2][K] fp32, overwritten):
+// per-channel sum / sum of squares of y for a following BatchNorm, reduced
+// from per-tile partials in stats_ws (conv2d_stats_ws_floats(s) floats).
+int conv2d_stats_ws_floats(const ConvShape& s);
+void conv2d_fwd(const ConvShape& s, const void* x, const void* w, const void* bias, void* y, float* stats,
+                float* stats_ws, int act, hipStream_t st);
 // dx = conv_transpose(dy, w) + beta * dx
 void conv2d_dgrad(const ConvShape& s, const void* dy, const void* w, void* dx, float beta, hipStream_t st);
-// dw (fp32, [K][R][S][C]) += x^T-conv dy  (split-K, fp32 atomics; splits <= 0: auto)
-void conv2d_wgrad(const ConvShape& s, const void* x, const void* dy, float* dw, int splits, hipStream_t st);
+// dw (fp32, [K][R][S][C]) += wgrad; split-K partial slabs in ws
+// (conv2d_wgrad_ws_floats(s, splits) floats; splits <= 0: auto)
+int64_t conv2d_wgrad_ws_floats(const ConvShape& s, int splits);
+void conv2d_wgrad(const ConvShape& s, const void* x, const void* dy, float* dw, float* ws, int splits,
+                  hipStream_t st);
 
 // ---- bnpool.hip: BatchNorm (training) + pooling over NHWC bf16 [M][C]
 void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st);
@@ -140,7 +145,7 @@ void bn_finalize(const float* stats, const void* gamma, const void* beta, int pa
                  float momentum, float eps, hipStream_t st);
 void bn_apply(const void* x, const void* residual, const float* scale, const float* shift, void* y, int64_t M, int C,
               int relu, hipStream_t st);
-// ws: 2*C floats; dgamma / dbeta (fp32) accumulate; dres (optional) = dy
+// ws: 5*C floats; dgamma / dbeta (fp32) accumulate; dres (optional) = dy
 // masked by the ReLU (the residual branch's gradient of relu(bn(x) + res))
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,

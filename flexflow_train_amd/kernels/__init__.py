@@ -698,7 +698,7 @@ def _conv_geom(x_shape, K, R, S, stride, pad, dil):
 
 def conv2d_fwd(x, w, bias=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), act: str = "none", stats=None):
     """x [N,C,H,W] channels_last bf16; w [K,R,S,C] contiguous bf16 -> y [N,K,P,Q]
-    channels_last.  ``stats`` (fp32 [2,K]) accumulates per-channel sum / sumsq of y."""
+    channels_last.  ``stats`` (fp32 [2,K]) receives the per-channel sum / sumsq of y."""
     _check_nhwc(x, "x")
     K_, R, S, C = w.shape
     _check(w, "w", torch.bfloat16)
@@ -711,7 +711,10 @@ def conv2d_fwd(x, w, bias=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), act: str 
     if stats is not None:
         _check(stats, "stats", torch.float32, 2 * K_)
     y = torch.empty((x.shape[0], K_, P, Q), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
-    ext().conv2d_fwd(g, _p(x), _p(w), _p(bias), _p(y), _p(stats), ACT_CODES[act], _stream())
+    ws = None
+    if stats is not None:
+        ws = torch.empty(ext().conv2d_stats_ws_floats(g), device=x.device, dtype=torch.float32)
+    ext().conv2d_fwd(g, _p(x), _p(w), _p(bias), _p(y), _p(stats), _p(ws), ACT_CODES[act], _stream())
     STATS["conv2d_fwd"] += 1
     return y
 
@@ -747,7 +750,9 @@ def conv2d_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), splits:
         raise ValueError("conv2d_wgrad: dy shape mismatch")
     if not dw.is_cuda or dw.dtype != torch.float32 or not dw.is_contiguous() or dw.numel() != K_ * R * S * x.shape[1]:
         raise ValueError("conv2d_wgrad: dw must be a contiguous fp32 [K,R,S,C] buffer")
-    ext().conv2d_wgrad(g, _p(x), _p(dy), _p(dw), int(splits), _stream())
+    nws = ext().conv2d_wgrad_ws_floats(g, int(splits))
+    ws = torch.empty(nws, device=x.device, dtype=torch.float32) if nws else None
+    ext().conv2d_wgrad(g, _p(x), _p(dy), _p(dw), _p(ws), int(splits), _stream())
     STATS["conv2d_wgrad"] += 1
 
 
@@ -806,7 +811,7 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, wan
     pdt = _dt(gamma) if gamma is not None else DT_BF16
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     dres = torch.empty_like(x, memory_format=torch.channels_last) if want_masked else None
-    ws = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+    ws = torch.empty(5 * C, device=x.device, dtype=torch.float32)
     ext().bn_bwd(_p(dy), _p(x), _p(y if relu else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx), _p(dres),
                  _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, int(relu), _stream())
     STATS["bn_bwd"] += 1

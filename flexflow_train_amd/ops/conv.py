@@ -72,8 +72,8 @@ class Conv2DOp(OpImpl):
                 wp = wp.to(torch.bfloat16)
             xin = K.nhwc(x)
             if C % 8:  # RGB stem: zero-pad channels to 8 (input and weight)
-                xp = torch.zeros((x.shape[0], 8, x.shape[2], x.shape[3]), device=x.device, dtype=x.dtype,
-                                 memory_format=torch.channels_last)
+                xp = torch.zeros((x.shape[0], 8, x.shape[2], x.shape[3]), device=x.device,
+                                 dtype=x.dtype).contiguous(memory_format=torch.channels_last)
                 xp[:, :C].copy_(xin)
                 xin = xp
                 wpad = torch.zeros((Kc, R, S, 8), device=x.device, dtype=wp.dtype)
@@ -81,7 +81,7 @@ class Conv2DOp(OpImpl):
                 wp = wpad
             stats = None
             if ctx.extra.get("emit_bn_stats"):
-                stats = torch.zeros(2 * Kc, device=x.device, dtype=torch.float32)
+                stats = torch.empty(2 * Kc, device=x.device, dtype=torch.float32)
             bias = None if b is None else b.to(torch.bfloat16).contiguous()
             y = K.conv2d_fwd(xin, wp, bias, stride, pad, act=act, stats=stats)
             if stats is not None:

@@ -117,13 +117,13 @@ def test_pool2d(k, s, p, avg):
     torch.manual_seed(3)
     x = _rand_nhwc((2, 24, 14, 14))
     y, arg = K.pool2d_fwd(x, k, s, p, avg)
-    xr = x.float().requires_grad_(True)
+    xr = x.float().cpu().contiguous().requires_grad_(True)  # fp32 CPU reference
     yr = F.avg_pool2d(xr, k, s, p, count_include_pad=False) if avg else F.max_pool2d(xr, k, s, p)
-    torch.testing.assert_close(y.float(), yr.detach(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=1e-2, atol=1e-2)
     dy = _rand_nhwc(yr.shape)
-    yr.backward(dy.float())
+    yr.backward(dy.float().cpu())
     dx = K.pool2d_bwd(dy, arg, tuple(x.shape), k, s, p, avg)
-    torch.testing.assert_close(dx.float(), xr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dx.float().cpu(), xr.grad, rtol=2e-2, atol=2e-2)
 
 
 def test_resnet_gpu_step_matches_cpu_fp32():
