@@ -13,6 +13,14 @@ batch is fixed (weak scaling); the strategy comes from the framework's
 compile() (searched, or --strategy dp for the data-parallel baseline).
 Each timed step = forward + loss + backward + gradient all-reduce + Adam
 update over all parameters.  Rank 0 prints ONE JSON line.
+
+Other BASELINE.json configs run through the same contract with --model:
+  resnet50     ResNet-50, synthetic 224x224 ImageNet batches (1000 classes),
+               per-GPU batch 256, SGD momentum 0.9
+  dlrm         DLRM (8 tables x 1M rows, sparse 64, bot 64-512-512-64,
+               top 576-1024-1024-1024-1), per-GPU batch 1024, SGD
+  gpt3-medium  GPT-3 medium (24 layers, hidden 1024, 16 heads, seq 2048,
+               vocab 50257), per-GPU batch 8, AdamW
 """
 import argparse
 import json
@@ -29,9 +37,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-per-gpu", type=int, default=32)
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: 32 (BERT), 256 (ResNet-50), "
+                                                                   "1024 (DLRM), 8 (GPT-3 medium)")
     ap.add_argument("--seq", type=int, default=512)
-    ap.add_argument("--model", default="bert-large")
+    ap.add_argument("--model", default="bert-large",
+                    choices=["bert-large", "bert-base", "resnet50", "dlrm", "gpt3-medium"])
     ap.add_argument("--layers", type=int, default=None, help="override (debug only; invalidates the metric)")
     ap.add_argument("--strategy", default="search", choices=["search", "dp"])
     ap.add_argument("--gemm", default=os.environ.get("FF_GEMM", "auto"))
@@ -53,6 +63,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.model not in ("bert-large", "bert-base"):
+        return bench_zoo(args, world, rank)
+    args.batch_per_gpu = args.batch_per_gpu or 32
     global_batch = args.batch_per_gpu * world
     mk = bert_large if args.model == "bert-large" else bert_base
     kw = dict(batch_size=global_batch, sequence_length=args.seq)
@@ -159,6 +172,109 @@ def main():
             rep = ex.profile_report()
             print(json.dumps({"profile_ms_total": {k: round(v, 3) for k, v in list(rep.items())[:40]}}),
                   file=sys.stderr)
+
+
+_ZOO = {
+    # bench name -> (zoo name, per-GPU batch, config overrides, optimizer, extra config for the JSON line)
+    "resnet50": ("resnet50", 256, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
+    "dlrm": ("dlrm", 1024, dict(embedding_size=[1000000] * 8, sparse_feature_size=64, mlp_bot=[64, 512, 512, 64],
+                                mlp_top=[576, 1024, 1024, 1024, 1]), "sgd", {"tables": "8x1M", "sparse": 64}),
+    "gpt3-medium": ("gpt", 8, dict(hidden_size=1024, num_layers=24, num_heads=16, sequence_length=2048),
+                    "adamw", {"seq_len": 2048, "layers": 24, "hidden": 1024}),
+}
+
+
+def bench_zoo(args, world, rank):
+    """The other BASELINE configs: model-zoo network + synthetic data of its
+    shape, same timing contract as the BERT path."""
+    import dataclasses
+    import numpy as np
+    import torch
+
+    from flexflow_train_amd import models as Z
+    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
+
+    zname, bpg, over, opt, extra = _ZOO[args.model]
+    bpg = args.batch_per_gpu or bpg
+    global_batch = bpg * world
+    cfg = FFConfig()
+    cfg.batch_size = global_batch
+    cfg.print_freq = 0
+    cfg.profiling = args.profile
+    cfg.only_data_parallel = args.strategy == "dp"
+    model = FFModel(cfg)
+    inputs, out, mcfg = Z.build(zname, model, batch_size=global_batch, **over)
+    ce = Z.loss_of(zname) == Z.LOSS_CE
+    optimizer = (SGDOptimizer(model, lr=0.01, momentum=0.9) if opt == "sgd"
+                 else AdamOptimizer(model, alpha=1e-4, weight_decay=0.01, decoupled=True))
+    t0 = time.time()
+    model.compile(optimizer=optimizer,
+                  loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY if ce
+                  else LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE,
+                  metrics=[MetricsType.METRICS_ACCURACY] if ce else [MetricsType.METRICS_MEAN_SQUARED_ERROR])
+    compile_s = time.time() - t0
+    ex = model.executor
+    dev = ex.cfg.device
+
+    # synthetic data of the model's shape, generated at this rank's batch
+    first = next(iter(ex.inputs))
+    lb = ex.local_input_shape(first)[0]
+    rng = np.random.default_rng(1234 + rank)
+    feeds_np, labels_np = Z.synthetic(zname, dataclasses.replace(mcfg, batch_size=lb), inputs, rng)
+    try:
+        feeds = {k: ex._local_piece(k, torch.as_tensor(v)) for k, v in feeds_np.items()}
+        labels = ex.local_labels(torch.as_tensor(labels_np))
+    except ValueError:  # inputs not batch-sharded under this strategy: global batch, then slice
+        feeds_np, labels_np = Z.synthetic(zname, mcfg, inputs, np.random.default_rng(1234))
+        feeds = {k: ex._local_piece(k, torch.as_tensor(v)) for k, v in feeds_np.items()}
+        labels = ex.local_labels(torch.as_tensor(labels_np))
+    del feeds_np, labels_np
+
+    def step():
+        ex.train_step(feeds, labels)
+
+    graphed = False
+    use_graph = args.graph if args.graph >= 0 else int(world == 1)
+    if use_graph and dev.type == "cuda" and not args.profile:
+        try:
+            step = ex.make_graphed_train_step(feeds, labels)
+            graphed = True
+        except Exception as e:  # noqa: BLE001
+            print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
+    for _ in range(args.warmup):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ex.dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ex.dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = ex.dist.max_scalar(time.perf_counter() - t0)
+    ms = elapsed / args.steps * 1000.0
+    sps = global_batch * args.steps / elapsed
+    pm = ex.perf_metrics()
+    if rank == 0:
+        par = model.search_report.get("source", "")
+        conf = {"model": args.model, "global_batch": global_batch,
+                "parallelism": ("dp%d" % world) if par in ("data_parallel", "single_device",
+                                                            "data_parallel_fallback") else par,
+                "strategy_source": par, "optimizer": opt, "compile_s": round(compile_s, 2), "hipgraph": graphed,
+                "final_loss": round(pm.loss, 4)}
+        conf.update(extra)
+        if zname == "gpt":
+            conf["tokens_per_sec"] = round(sps * mcfg.sequence_length, 1)
+        print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(sps, 2), "unit": "samples/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                          "data": "synthetic inputs of the model's shape, random-init weights", "config": conf}),
+              flush=True)
 
 
 if __name__ == "__main__":
