@@ -11,6 +11,7 @@
 #include "ff/graph.h"
 #include "ff/json.h"
 #include "ff/op_attrs.h"
+#include "ff/sp.h"
 #include "ff/types.h"
 #include "bindings_ext.h"
 
@@ -243,6 +244,95 @@ PYBIND11_MODULE(_ffcore, m) {
   m.def("data_parallel_pcg", &data_parallel_pcg);
 
   m.def("json_roundtrip", [](const std::string& s) { return Json::parse(s).dump(); });
+
+  // ---- graph library (lib/utils/graph parity), DiGraph given as (nodes, edges)
+  auto mkg = [](const std::vector<int>& nodes, const std::vector<std::pair<int, int>>& edges) {
+    DiGraph g;
+    for (int n : nodes) g.add_node(n);
+    for (auto const& e : edges) g.add_edge(e.first, e.second);
+    return g;
+  };
+  auto edges_of = [](const DiGraph& g) {
+    std::vector<std::pair<int, int>> r;
+    for (auto const& kv : g.succ)
+      for (int s : kv.second) r.emplace_back(kv.first, s);
+    return r;
+  };
+  auto g = m.def_submodule("graph", "DiGraph algorithms over (nodes, edges)");
+  g.def("topological_order", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) {
+    return topological_order(mkg(n, e));
+  });
+  g.def("is_acyclic", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) { return is_acyclic(mkg(n, e)); });
+  g.def("transitive_closure", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) {
+    return edges_of([&] {
+      DiGraph r;
+      for (auto const& kv : transitive_closure(mkg(n, e))) {
+        r.add_node(kv.first);
+        for (int s : kv.second) r.add_edge(kv.first, s);
+      }
+      return r;
+    }());
+  });
+  g.def("transitive_reduction", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) {
+    return edges_of(transitive_reduction(mkg(n, e)));
+  });
+  g.def("dominators", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) { return dominators(mkg(n, e)); });
+  g.def("post_dominators",
+        [=](std::vector<int> n, std::vector<std::pair<int, int>> e) { return post_dominators(mkg(n, e)); });
+  g.def("immediate_dominators",
+        [=](std::vector<int> n, std::vector<std::pair<int, int>> e) { return immediate_dominators(mkg(n, e)); });
+  g.def("immediate_post_dominators", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) {
+    return immediate_post_dominators(mkg(n, e));
+  });
+  g.def("weakly_connected_components", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) {
+    return weakly_connected_components(mkg(n, e));
+  });
+  g.def("longest_path", [=](std::vector<int> n, std::vector<std::pair<int, int>> e, std::map<int, double> w) {
+    return longest_path(mkg(n, e), [&](int x) { auto it = w.find(x); return it == w.end() ? 1.0 : it->second; });
+  });
+  g.def("find_isomorphism", [=](std::vector<int> na, std::vector<std::pair<int, int>> ea, std::vector<int> nb,
+                                std::vector<std::pair<int, int>> eb, std::map<int, std::string> la,
+                                std::map<int, std::string> lb) -> py::object {
+    auto A = mkg(na, ea), B = mkg(nb, eb);
+    auto r = find_isomorphism(A, B, [&](int x) { auto it = la.find(x); return it == la.end() ? std::string() : it->second; },
+                              [&](int x) { auto it = lb.find(x); return it == lb.end() ? std::string() : it->second; });
+    if (!r) return py::none();
+    return py::cast(*r);
+  }, py::arg("nodes_a"), py::arg("edges_a"), py::arg("nodes_b"), py::arg("edges_b"),
+     py::arg("labels_a") = std::map<int, std::string>{}, py::arg("labels_b") = std::map<int, std::string>{});
+  g.def("inverse_line_graph", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) -> py::object {
+    auto r = inverse_line_graph(mkg(n, e));
+    if (!r) return py::none();
+    return py::make_tuple(std::vector<int>(r->h.nodes.begin(), r->h.nodes.end()), edges_of(r->h), r->edge);
+  });
+  g.def("as_dot", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) {
+    return digraph_as_dot(mkg(n, e), [](int x) { return std::to_string(x); });
+  });
+  // SP tree utilities on the decomposition of a DiGraph
+  auto sp_of = [=](const std::vector<int>& n, const std::vector<std::pair<int, int>>& e) {
+    return get_relaxed_sp_decomposition(mkg(n, e));
+  };
+  g.def("sp_paths_to_leaf", [=](std::vector<int> n, std::vector<std::pair<int, int>> e, int node) {
+    return find_paths_to_leaf(sp_of(n, e), node);
+  });
+  g.def("sp_subtree_leaves_at_path", [=](std::vector<int> n, std::vector<std::pair<int, int>> e,
+                                         std::vector<int> path) -> py::object {
+    auto t = sp_of(n, e);
+    const int i = get_subtree_at_path(t, path);
+    if (i < 0) return py::none();
+    return py::cast(t.leaves(i));
+  });
+  g.def("sp_associative", [=](std::vector<int> n, std::vector<std::pair<int, int>> e, bool left) {
+    auto t = sp_of(n, e);
+    auto r = left ? left_associative(t) : right_associative(t);
+    // binary nested tuples: leaf = node id, split = ("S"|"P", left, right)
+    std::function<py::object(int)> conv = [&](int i) -> py::object {
+      const auto& x = r.e[i];
+      if (x.kind == SPTree::LEAF) return py::int_(x.node);
+      return py::make_tuple(x.kind == SPTree::SERIES ? "S" : "P", conv(x.left), conv(x.right));
+    };
+    return r.root < 0 ? py::object(py::none()) : conv(r.root);
+  });
 
   register_ext_bindings(m);
 }

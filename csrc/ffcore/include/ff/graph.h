@@ -61,6 +61,26 @@ std::map<int, std::set<int>> dominators(const DiGraph& g);
 std::map<int, std::set<int>> post_dominators(const DiGraph& g);
 std::vector<std::set<int>> weakly_connected_components(const DiGraph& g);
 std::string digraph_as_dot(const DiGraph& g, const std::function<std::string(int)>& label);
+// idom[n] = immediate dominator of n (-1 for sources / nodes dominated only by themselves)
+std::map<int, int> immediate_dominators(const DiGraph& g);
+std::map<int, int> immediate_post_dominators(const DiGraph& g);
+// Critical path with node weights: (length, nodes on one longest path).
+std::pair<double, std::vector<int>> longest_path(const DiGraph& g, const std::function<double(int)>& weight);
+// Graph isomorphism a -> b (node map) respecting node labels (equal strings),
+// or nullopt.  Backtracking over a topological order of `a` with degree /
+// label / neighbourhood-consistency pruning (DAGs of a few thousand nodes).
+std::optional<std::map<int, int>> find_isomorphism(const DiGraph& a, const DiGraph& b,
+                                                   const std::function<std::string(int)>& label_a,
+                                                   const std::function<std::string(int)>& label_b);
+bool is_isomorphic(const DiGraph& a, const DiGraph& b);
+// Line digraph L(H): one node per edge of H, e1 -> e2 when head(e1) == tail(e2).
+// inverse_line_graph(G) recovers H (nodes = endpoint classes, edge id = node of
+// G) if G is a line digraph; nullopt otherwise.
+struct InverseLineGraph {
+  DiGraph h;                                // endpoint classes as nodes
+  std::map<int, std::pair<int, int>> edge;  // node of G -> (tail, head) in h
+};
+std::optional<InverseLineGraph> inverse_line_graph(const DiGraph& g);
 
 // ---------------------------------------------------------------------------
 struct ValueRef {

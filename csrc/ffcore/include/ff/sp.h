@@ -49,6 +49,16 @@ struct SPTree {
   Json to_json(int idx) const;
 };
 
+// Paths in the binary tree (parity: utils/full_binary_tree/binary_tree_path,
+// find_paths_to_leaf, get_subtree_at_path — machine-mapping results are keyed
+// by path).  A path is a sequence of 0 (left) / 1 (right) from the root.
+using BinaryTreePath = std::vector<int>;
+std::vector<BinaryTreePath> find_paths_to_leaf(const SPTree& t, int node);
+int get_subtree_at_path(const SPTree& t, const BinaryTreePath& path);  // entry index, -1 if invalid
+// Re-associate maximal same-kind chains left-deep (((a b) c) d) or right-deep.
+SPTree left_associative(const SPTree& t);
+SPTree right_associative(const SPTree& t);
+
 std::optional<SPTree> get_series_parallel_decomposition(const DiGraph& g);
 SPTree get_relaxed_sp_decomposition(const DiGraph& g);
 bool is_series_parallel(const DiGraph& g);

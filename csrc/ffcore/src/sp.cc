@@ -1,6 +1,7 @@
 #include "ff/sp.h"
 
 #include <algorithm>
+#include <functional>
 #include <cstdint>
 #include <map>
 
@@ -215,5 +216,72 @@ SPTree get_relaxed_sp_decomposition(const DiGraph& g) {
 }
 
 bool is_series_parallel(const DiGraph& g) { return get_series_parallel_decomposition(g).has_value(); }
+
+// ---------------------------------------------------------------------------
+std::vector<BinaryTreePath> find_paths_to_leaf(const SPTree& t, int node) {
+  std::vector<BinaryTreePath> out;
+  BinaryTreePath cur;
+  std::function<void(int)> rec = [&](int i) {
+    if (i < 0) return;
+    const auto& e = t.e[i];
+    if (e.kind == SPTree::LEAF) {
+      if (e.node == node) out.push_back(cur);
+      return;
+    }
+    cur.push_back(0);
+    rec(e.left);
+    cur.back() = 1;
+    rec(e.right);
+    cur.pop_back();
+  };
+  rec(t.root);
+  return out;
+}
+
+int get_subtree_at_path(const SPTree& t, const BinaryTreePath& path) {
+  int i = t.root;
+  for (int step : path) {
+    if (i < 0 || t.e[i].kind == SPTree::LEAF) return -1;
+    i = step == 0 ? t.e[i].left : t.e[i].right;
+  }
+  return i;
+}
+
+static SPTree reassociate(const SPTree& t, bool left) {
+  SPTree r;
+  // flatten maximal chains of the same split kind (relaxed series cuts are kept
+  // as chain boundaries: they carry their own cost semantics)
+  std::function<void(int, SPTree::Kind, std::vector<int>&)> flatten = [&](int i, SPTree::Kind k,
+                                                                          std::vector<int>& items) {
+    const auto& e = t.e[i];
+    if (e.kind == k && !e.relaxed) {
+      flatten(e.left, k, items);
+      flatten(e.right, k, items);
+    } else {
+      items.push_back(i);
+    }
+  };
+  std::function<int(int)> build = [&](int i) -> int {
+    const auto& e = t.e[i];
+    if (e.kind == SPTree::LEAF) return r.add_leaf(e.node);
+    if (e.relaxed) return r.add_split(e.kind, build(e.left), build(e.right), true);
+    std::vector<int> items;
+    flatten(i, e.kind, items);
+    std::vector<int> built;
+    for (int it : items) built.push_back(build(it));
+    if (left) {
+      int acc = built[0];
+      for (size_t j = 1; j < built.size(); ++j) acc = r.add_split(e.kind, acc, built[j]);
+      return acc;
+    }
+    int acc = built.back();
+    for (size_t j = built.size() - 1; j-- > 0;) acc = r.add_split(e.kind, built[j], acc);
+    return acc;
+  };
+  if (t.root >= 0) r.root = build(t.root);
+  return r;
+}
+SPTree left_associative(const SPTree& t) { return reassociate(t, true); }
+SPTree right_associative(const SPTree& t) { return reassociate(t, false); }
 
 }  // namespace ff
