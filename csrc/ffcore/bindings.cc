@@ -335,4 +335,5 @@ PYBIND11_MODULE(_ffcore, m) {
   });
 
   register_ext_bindings(m);
+  register_data_bindings(m);
 }

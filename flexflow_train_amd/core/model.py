@@ -608,10 +608,13 @@ class FFModel:
         reference's ``ELAPSED TIME = ..., THROUGHPUT = ... samples/s``."""
         ex = self.executor
         xs = x if isinstance(x, (list, tuple)) else [x]
+        bs = batch_size or self.ffconfig.batch_size
+        native = self._native_loader(xs, y, bs)
+        if native is not None:
+            return self._fit_native(native, epochs)
         loaders = [d if isinstance(d, SingleDataLoader) else SingleDataLoader(self, self._inputs[i], d)
                    for i, d in enumerate(xs)]
         ylo = y if isinstance(y, SingleDataLoader) else SingleDataLoader(self, self._label_tensor, y)
-        bs = batch_size or self.ffconfig.batch_size
         for l in loaders + [ylo]:
             l.batch_size = bs
         num_samples = ylo.num_samples
@@ -641,6 +644,60 @@ class FFModel:
                     print(f"epoch {epoch} iter {it + 1}/{iters}: {ex.perf_metrics()}", flush=True)
             if self.dist.rank == 0 and iters:
                 print(f"epoch {epoch}: {ex.perf_metrics()}", flush=True)
+        if ex.cfg.device.type == "cuda":
+            torch.cuda.synchronize()
+        elapsed = time.time() - t0
+        thr = num_samples * epochs / max(elapsed, 1e-9)
+        if self.dist.rank == 0:
+            print(f"ELAPSED TIME = {elapsed:.4f}s, THROUGHPUT = {thr:.2f} samples/s", flush=True)
+        self.last_throughput = thr
+        return thr
+
+    def _native_loader(self, xs, y, bs):
+        """Arrays (not loader objects) on a batch-split layout -> the native
+        prefetching loader (runtime/dataloader.py); None -> host loaders."""
+        if not self.ffconfig.native_data_loader:
+            return None
+        if any(isinstance(d, SingleDataLoader) for d in list(xs) + [y]) or y is None:
+            return None
+        if bs != self.ffconfig.batch_size or len(xs) != len(self._inputs):
+            return None
+        from ..runtime.dataloader import NativeDataLoader
+        arrays = {self._inputs[i].name: np.asarray(d) for i, d in enumerate(xs)}
+        arrays["__label__"] = np.asarray(y)
+        try:
+            return NativeDataLoader(self.executor, arrays, "__label__", bs,
+                                    shuffle=bool(self.ffconfig.shuffle_data), seed=self.ffconfig.seed)
+        except (ValueError, KeyError):
+            return None
+
+    def _fit_native(self, loader, epochs):
+        ex = self.executor
+        iters = loader.iters_per_epoch
+        num_samples = iters * loader.batch
+        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
+        graphed = None
+        if ex.cfg.device.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.time()
+        try:
+            for epoch in range(epochs):
+                ex.zero_metrics()
+                for it in range(iters):
+                    feeds, labels, _ = loader.next()
+                    if use_graph and (epoch > 0 or it >= 1):
+                        if graphed is None:
+                            graphed = ex.make_graphed_train_step(feeds, labels, warmup=0)
+                        graphed(feeds, labels)
+                    else:
+                        ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
+                    if (self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0
+                            and self.dist.rank == 0):
+                        print(f"epoch {epoch} iter {it + 1}/{iters}: {ex.perf_metrics()}", flush=True)
+                if self.dist.rank == 0 and iters:
+                    print(f"epoch {epoch}: {ex.perf_metrics()}", flush=True)
+        finally:
+            loader.close()
         if ex.cfg.device.type == "cuda":
             torch.cuda.synchronize()
         elapsed = time.time() - t0
