@@ -87,6 +87,39 @@ class Tensor:
     def get_model_output_tensor(self, ffmodel):
         return ffmodel._get_value(self)
 
+    def get_model_output_gradients(self, ffmodel, comm_type=None):
+        return ffmodel._get_gradient(self)
+
+    # ---- Legion region access (flexflow_cffi.py Tensor.inline_map /
+    # attach_numpy_array / get_array ...).  There are no regions here: a
+    # "mapped" tensor is a host numpy view of the current value (inputs: the
+    # pending feed, others: the last computed value), and attaching an array
+    # makes it the next fed batch.
+    def inline_map(self, ffmodel, ffconfig=None):
+        self._mapped = self.get_tensor(ffmodel)
+        return self._mapped
+
+    def inline_unmap(self, ffmodel, ffconfig=None):
+        self._mapped = None
+
+    def is_mapped(self):
+        return getattr(self, "_mapped", None) is not None
+
+    def get_array(self, ffmodel, ffconfig=None, data_type=None):
+        a = self._mapped if self.is_mapped() else self.get_tensor(ffmodel)
+        return None if a is None else np.asarray(a)
+
+    def get_flat_array(self, ffmodel, ffconfig=None, data_type=None):
+        a = self.get_array(ffmodel, ffconfig, data_type)
+        return None if a is None else a.reshape(-1)
+
+    def attach_numpy_array(self, ffmodel, ffconfig, np_array):
+        self.set_tensor(ffmodel, np_array)
+
+    def detach_numpy_array(self, ffmodel=None, ffconfig=None):
+        m = ffmodel or self.model
+        m._pending_feeds.pop(self.name or f"input_{self.vref.node}", None)
+
     def __repr__(self):
         return f"Tensor({self.name}, dims={self.dims})"
 
@@ -521,6 +554,19 @@ class FFModel:
             return (mapping[t.vref.node], t.vref.idx)
         return None
 
+    def prefetch(self):
+        """Reference: Legion prefetch of the next batch's regions.  The native
+        loader (runtime/dataloader.py) already stages batches ahead; no-op."""
+        return None
+
+    def add_layer(self, op_type, name=None, inputs=(), **attrs):
+        """Generic layer constructor (reference: FFModel.add_layer / _add_to_model):
+        any operator of the IR by type name with attributes."""
+        t = op_type if isinstance(op_type, str) else getattr(op_type, "name", str(op_type))
+        if t.startswith("OP_"):
+            t = t[3:]
+        return self._add(t, list(inputs), name, **attrs)
+
     def init_layers(self):
         if self.executor is None:
             raise RuntimeError("call compile() first")
@@ -732,11 +778,39 @@ class FFModel:
             print(f"eval: {pm}", flush=True)
         return pm
 
+    def _value_key(self, t: Tensor):
+        if self.executor is None or t.vref is None:
+            return None
+        v = self._pcg_value_of(t)
+        if v is None:
+            return None
+        return v
+
     def _get_value(self, t: Tensor):
-        raise NotImplementedError("get_tensor of activations is available through Executor.forward outputs")
+        """Latest value of a tensor as numpy (this rank's piece): a pending
+        feed for inputs, else the last forward's activation.  Asking for an
+        activation registers it for retention, so the next forward keeps it."""
+        key = t.name or (f"input_{t.vref.node}" if t.vref is not None else None)
+        if key in self._pending_feeds:
+            return np.asarray(self._pending_feeds[key])
+        v = self._value_key(t)
+        if v is None:
+            return None
+        ex = self.executor
+        ex.retain.add(v)
+        x = ex._env.get(v, ex.retained.get(v))
+        return None if x is None else x.detach().float().cpu().numpy()
 
     def _get_gradient(self, t: Tensor):
-        raise NotImplementedError
+        """Gradient of the loss w.r.t. an activation from the last backward
+        (registered for retention on first request)."""
+        v = self._value_key(t)
+        if v is None:
+            return None
+        ex = self.executor
+        ex.retain.add(v)
+        g = ex.retained_grads.get(v)
+        return None if g is None else g.float().cpu().numpy()
 
     # ------------------------------------------------------------ recompile
     def recompile_on_condition(self, r) -> bool:

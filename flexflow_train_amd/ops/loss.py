@@ -161,6 +161,10 @@ class PerfMetrics:
     def accuracy(self) -> float:
         return self.train_correct / self.train_all if self.train_all else 0.0
 
+    def get_accuracy(self) -> float:
+        """Percent, as the reference's PerfMetrics.get_accuracy (flexflow_cffi.py)."""
+        return 100.0 * self.accuracy
+
     @classmethod
     def from_buffer(cls, buf: torch.Tensor, metrics, loss_type: str, start_time: float, out_dim: int = 1):
         v = buf.detach().double().cpu().tolist()

@@ -133,6 +133,11 @@ class Executor:
         self.metrics_buf = torch.zeros(N_SLOTS, device=cfg.device, dtype=torch.float32)
         self.metrics_start = time.time()
         self._saved: Dict[int, Any] = {}
+        # values whose latest forward value / gradient the API asked to keep
+        # (Tensor.get_tensor / get_gradients on activations)
+        self.retain: set = set()
+        self.retained: Dict[Value, torch.Tensor] = {}
+        self.retained_grads: Dict[Value, torch.Tensor] = {}
         self._env: Dict[Value, torch.Tensor] = {}
         self._works = []
 
@@ -769,6 +774,8 @@ class Executor:
             self.tracer.end(t0)
             for o, t in zip(s.outputs, outs):
                 env[o] = t
+                if o in self.retain:
+                    self.retained[o] = t
             if training:
                 self._saved[i] = saved
         self._env = env
@@ -834,6 +841,9 @@ class Executor:
             saved = self._saved.pop(i, None)
             if s.active:
                 gouts = [grads.pop(o, None) for o in s.outputs]
+                for o, g in zip(s.outputs, gouts):
+                    if g is not None and o in self.retain:
+                        self.retained_grads[o] = g.detach().clone()
                 need = [self.requires_grad.get(v, False) for v in s.inputs]
                 if any(g is not None for g in gouts) and (any(need) or any(p.trainable for p in s.weights)):
                     gouts = [g if g is not None else None for g in gouts]

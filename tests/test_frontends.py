@@ -154,3 +154,57 @@ def test_onnx_import_roundtrip():
     ref = np.exp(z - z.max(-1, keepdims=True))
     ref /= ref.sum(-1, keepdims=True)
     np.testing.assert_allclose(out, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_reference_tensor_access_api():
+    """Legion-era Tensor/FFModel calls (inline_map, attach_numpy_array,
+    get_array, add_layer, prefetch, PerfMetrics.get_accuracy) keep working."""
+    import numpy as np
+    from flexflow_train_amd.core import DataType, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+
+    cfg = FFConfig()
+    cfg.batch_size = 8
+    m = FFModel(cfg)
+    x = m.create_tensor([8, 16], DataType.DT_FLOAT, name="x")
+    t = m.add_layer("LINEAR", name="lin", inputs=[x], out_channels=4, activation="none", use_bias=True)
+    m.softmax(t)
+    m.compile(optimizer=SGDOptimizer(m, lr=0.05), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_ACCURACY])
+    data = np.arange(128, dtype=np.float32).reshape(8, 16) / 128
+    x.attach_numpy_array(m, cfg, data)
+    x.inline_map(m, cfg)
+    assert x.is_mapped()
+    np.testing.assert_allclose(x.get_array(m, cfg), data)
+    assert x.get_flat_array(m, cfg).shape == (128,)
+    x.inline_unmap(m, cfg)
+    assert not x.is_mapped()
+    assert m.prefetch() is None
+    assert m.get_perf_metrics().get_accuracy() == 0.0
+    x.detach_numpy_array(m, cfg)
+
+
+def test_activation_value_and_gradient_access():
+    import numpy as np
+    import torch
+    from flexflow_train_amd.core import ActiMode, DataType, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+
+    cfg = FFConfig()
+    cfg.batch_size = 4
+    m = FFModel(cfg)
+    x = m.create_tensor([4, 8], DataType.DT_FLOAT, name="x")
+    h = m.dense(x, 6, ActiMode.AC_MODE_RELU, name="h")
+    m.softmax(m.dense(h, 3, name="o"))
+    m.compile(optimizer=SGDOptimizer(m, lr=0.0), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_ACCURACY])
+    assert h.get_tensor(m) is None          # registers retention
+    assert h.get_gradients(m) is None
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((4, 8)).astype(np.float32)
+    Y = np.array([[0], [1], [2], [1]], np.int32)
+    m.fit(x=X, y=Y, epochs=1)
+    hv = h.get_tensor(m)
+    W = m.get_layer_by_name("h").get_weight_tensor().get_weights(m)
+    b = m.get_layer_by_name("h").get_bias_tensor().get_weights(m)
+    np.testing.assert_allclose(hv, np.maximum(X @ W + b, 0), rtol=1e-4, atol=1e-5)
+    g = h.get_gradients(m)
+    assert g.shape == (4, 6) and np.isfinite(g).all() and np.abs(g).sum() > 0
