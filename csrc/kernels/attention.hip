@@ -28,6 +28,8 @@
 // Tensor addressing: every tensor is [B, S, H, D] with arbitrary strides for
 // b / s / h and contiguous d, so the fused QKV projection output
 // [B, S, 3, H, D] is consumed in place.  LSE is [B, H, S] fp32, log2 domain.
+#include <cstdlib>
+
 #include "kernels.h"
 #include "mfma.h"
 
@@ -359,36 +361,48 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(Att
 }
 
 // ===========================================================================
-// dK / dV: key block resident (4 waves x 32 keys), loop over 64-query tiles.
+// dK / dV: key block resident (4 waves x NKT*32 keys), loop over 64-query tiles.
 //   S = Q K^T (key on lane) ; P = exp2(S*c - lse[q]) ; dP = dO V^T ;
 //   dS = P (dP - delta[q]) ; dV^T += dO^T P ; dK^T += Q^T dS ; dK = scale*dK
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(AttnParams P) {
-  constexpr int KS = D / 16, DT = D / 32, QT = 64;
+// NKT = 2 (64 keys per wave): every Q / dO fragment read from LDS feeds two
+// key subtiles, halving LDS traffic per MFMA; slower in practice (register
+// pressure -> 1 wave/SIMD), kept behind FFK_ATTN_BWD_NKT=2 for experiments.
+template <int D, bool CAUSAL, int NKT>
+__global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_dkdv_kernel(AttnParams P) {
+  constexpr int KS = D / 16, DT = D / 32, QT = 64, KW = 32 * NKT;
   constexpr int TILE_BYTES = QT * D * 2;
   constexpr int STAGE = 2 * TILE_BYTES + 2 * QT * 4;  // Q, dO, lse, delta
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / P.H, hh = bh % P.H;
-  const int k_blk = blockIdx.x * 128;
-  const int kw = k_blk + wave * 32;
-  const int key = kw + (lane & 31);
-  const bool k_ok = key < P.Sk;
+  const int k_blk = blockIdx.x * (4 * KW);
+  const int kw = k_blk + wave * KW;
 
   // K, V rows as B operands (lane holds row `key`, d = 16ks + 8h ..)
-  bf16x8 kf[KS], vf[KS];
+  bf16x8 kf[NKT][KS], vf[NKT][KS];
+  int key[NKT];
+  bool k_ok[NKT];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    kf[ks] = k_ok ? *reinterpret_cast<const bf16x8*>(P.k.p + b * P.k.sb + static_cast<int64_t>(key) * P.k.ss +
-                                                     hh * P.k.sh + ks * 16 + 8 * h)
-                  : bf16x8{};
-    vf[ks] = k_ok ? *reinterpret_cast<const bf16x8*>(P.v.p + b * P.v.sb + static_cast<int64_t>(key) * P.v.ss +
-                                                     hh * P.v.sh + ks * 16 + 8 * h)
-                  : bf16x8{};
+  for (int j = 0; j < NKT; ++j) {
+    key[j] = kw + 32 * j + (lane & 31);
+    k_ok[j] = key[j] < P.Sk;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[j][ks] = k_ok[j] ? *reinterpret_cast<const bf16x8*>(P.k.p + b * P.k.sb +
+                                                             static_cast<int64_t>(key[j]) * P.k.ss + hh * P.k.sh +
+                                                             ks * 16 + 8 * h)
+                          : bf16x8{};
+      vf[j][ks] = k_ok[j] ? *reinterpret_cast<const bf16x8*>(P.v.p + b * P.v.sb +
+                                                             static_cast<int64_t>(key[j]) * P.v.ss + hh * P.v.sh +
+                                                             ks * 16 + 8 * h)
+                          : bf16x8{};
+    }
   }
-  f32x16 dk[DT], dv[DT];
+  f32x16 dk[NKT][DT], dv[NKT][DT];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x16{};
+  for (int j = 0; j < NKT; ++j)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dk[j][dt] = dv[j][dt] = f32x16{};
 
   const int n_q_tiles = (P.Sq + QT - 1) / QT;
   const int t0 = CAUSAL ? (k_blk / QT) : 0;
@@ -425,44 +439,62 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(A
       dl.load(P.dout, b, hh, q0 + QT, P.Sq);
     }
     const bool wave_active = !CAUSAL || (q0 + QT - 1 >= kw);
-    const bool need_mask = (q0 + QT > P.Sq) || (CAUSAL && q0 < kw + 31) || (kw + 31 >= P.Sk);
+    const bool need_mask = (q0 + QT > P.Sq) || (CAUSAL && q0 < kw + KW - 1) || (kw + KW - 1 >= P.Sk);
     if (wave_active) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        f32x16 s = f32x16{}, dp = f32x16{};
+        f32x16 s[NKT], dp[NKT];
+#pragma unroll
+        for (int j = 0; j < NKT; ++j) s[j] = dp[j] = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int off = lds_off<D>(qt * 32 + (lane & 31), 2 * ks + h);
-          s = mfma32(lds_read16(Qt, off), kf[ks], s);
-          dp = mfma32(lds_read16(Dt, off), vf[ks], dp);
-        }
-        if (need_mask) {
+          const bf16x8 qa = lds_read16(Qt, off), da = lds_read16(Dt, off);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int qq = q0 + ql_;
-            float pv = fexp2(s[r] * P.scale_log2 - ls[ql_]);
-            if (qq >= P.Sq || (CAUSAL && key > qq) || !k_ok) pv = 0.f;
-            s[r] = pv;
-            dp[r] = pv * (dp[r] - ds[ql_]);
+          for (int j = 0; j < NKT; ++j) {
+            s[j] = mfma32(qa, kf[j][ks], s[j]);
+            dp[j] = mfma32(da, vf[j][ks], dp[j]);
           }
-        } else {
+        }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float pv = fexp2(s[r] * P.scale_log2 - ls[ql_]);
-            s[r] = pv;
-            dp[r] = pv * (dp[r] - ds[ql_]);
+        for (int j = 0; j < NKT; ++j) {
+          if (need_mask) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              const int qq = q0 + ql_;
+              float pv = fexp2(s[j][r] * P.scale_log2 - ls[ql_]);
+              if (qq >= P.Sq || (CAUSAL && key[j] > qq) || !k_ok[j]) pv = 0.f;
+              s[j][r] = pv;
+              dp[j][r] = pv * (dp[j][r] - ds[ql_]);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              const float pv = fexp2(s[j][r] * P.scale_log2 - ls[ql_]);
+              s[j][r] = pv;
+              dp[j][r] = pv * (dp[j][r] - ds[ql_]);
+            }
           }
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          bf16x8 pf = acc_to_frag(s, st);
-          bf16x8 sf = acc_to_frag(dp, st);
+          bf16x8 pf[NKT], sf[NKT];
+#pragma unroll
+          for (int j = 0; j < NKT; ++j) {
+            pf[j] = acc_to_frag(s[j], st);
+            sf[j] = acc_to_frag(dp[j], st);
+          }
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
-            dv[dt] = mfma32(tr_frag<D>(Dt, qt * 32 + 16 * st, dt, lane), pf, dv[dt]);
-            dk[dt] = mfma32(tr_frag<D>(Qt, qt * 32 + 16 * st, dt, lane), sf, dk[dt]);
+            const bf16x8 da = tr_frag<D>(Dt, qt * 32 + 16 * st, dt, lane);
+            const bf16x8 qa = tr_frag<D>(Qt, qt * 32 + 16 * st, dt, lane);
+#pragma unroll
+            for (int j = 0; j < NKT; ++j) {
+              dv[j][dt] = mfma32(da, pf[j], dv[j][dt]);
+              dk[j][dt] = mfma32(qa, sf[j], dk[j][dt]);
+            }
           }
         }
       }
@@ -475,9 +507,11 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(A
     }
     __syncthreads();
   }
-  if (k_ok) {
-    bf16* krow = P.dk + b * P.dk_sb + static_cast<int64_t>(key) * P.dk_ss + hh * P.dk_sh;
-    bf16* vrow = P.dv + b * P.dv_sb + static_cast<int64_t>(key) * P.dv_ss + hh * P.dv_sh;
+#pragma unroll
+  for (int j = 0; j < NKT; ++j) {
+    if (!k_ok[j]) continue;
+    bf16* krow = P.dk + b * P.dk_sb + static_cast<int64_t>(key[j]) * P.dk_ss + hh * P.dk_sh;
+    bf16* vrow = P.dv + b * P.dv_sb + static_cast<int64_t>(key[j]) * P.dv_ss + hh * P.dv_sh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -485,8 +519,8 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dkdv_kernel(A
         bf16x4 a, c;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          a[e] = f2bf(dk[dt][4 * g4 + e] * P.scale);
-          c[e] = f2bf(dv[dt][4 * g4 + e]);
+          a[e] = f2bf(dk[j][dt][4 * g4 + e] * P.scale);
+          c[e] = f2bf(dv[j][dt][4 * g4 + e]);
         }
         *reinterpret_cast<bf16x4*>(krow + dt * 32 + 8 * g4 + 4 * h) = a;
         *reinterpret_cast<bf16x4*>(vrow + dt * 32 + 8 * g4 + 4 * h) = c;
@@ -538,16 +572,35 @@ void attention_fwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, fl
   FFK_LAUNCH_CHECK("attention_fwd");
 }
 
+template <int D, bool CAUSAL>
+static void launch_dkdv(int nkt, dim3 grid, dim3 block, hipStream_t st, const AttnParams& P) {
+  if constexpr (D == 64) {
+    if (nkt == 2) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 2>), grid, block, 0, st, P);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 1>), grid, block, 0, st, P);
+}
+
 void attention_bwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, float scale, bool causal,
                    hipStream_t st) {
   AttnParams P = make_params(t, B, H, Sq, Sk, D, scale);
   const int64_t rows = static_cast<int64_t>(B) * H * Sq;
   const int tpr = D / 8;
   dim3 gd(static_cast<unsigned>((rows * tpr + 255) / 256));
-  dim3 gq((Sq + 127) / 128, B * H), gk((Sk + 127) / 128, B * H), block(256);
+  static const int nkt_env = [] {
+    const char* e = getenv("FFK_ATTN_BWD_NKT");
+    return e ? atoi(e) : 0;
+  }();
+  // NKT = 2 (64 keys per wave) halves LDS reads per MFMA but needs ~500
+  // registers (1 wave/SIMD, spills when causal): measured 0.24 vs 0.21 ms
+  // (BERT shape) and 0.92 vs 0.56 ms (GPT causal) — opt-in only.
+  const int nkt = D == 64 && nkt_env == 2 ? 2 : 1;
+  dim3 gq((Sq + 127) / 128, B * H), gk((Sk + 128 * nkt - 1) / (128 * nkt), B * H), block(256);
 #define FFK_ATTN_BWD(DD, CC)                                                          \
   hipLaunchKernelGGL((attn_bwd_delta_kernel<DD>), gd, block, 0, st, P);               \
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, CC>), gk, block, 0, st, P);            \
+  launch_dkdv<DD, CC>(nkt, gk, block, st, P);                                         \
   hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, CC>), gq, block, 0, st, P)
   if (D == 64) {
     if (causal) { FFK_ATTN_BWD(64, true); }
