@@ -51,7 +51,29 @@ struct ConvArgs {
   int act;
   float beta;       // DGRAD: dx = result + beta * dx
   int kt_per_split; // WGRAD split-K
+  // DGRAD parity class (strided convs): rows are the input pixels with
+  // h % sh == pch, w % sw == pcw (Hc x Wc per image); the K axis runs only over
+  // the taps r = rf + i*sh (i < nr), s = sf + j*sw (j < ns) that reach them.
+  int par, pch, pcw, Hc, Wc, rf, sf, nr, ns;
 };
+
+// DGRAD output row of local row m (parity classes scatter to the full image)
+__device__ __forceinline__ int64_t dgrad_row(const ConvArgs& g, int m) {
+  if (!g.par) return m;
+  const int ww = m % g.Wc, t = m / g.Wc, hh = t % g.Hc, n = t / g.Hc;
+  return (static_cast<int64_t>(n) * g.H + hh * g.sh + g.pch) * g.W + ww * g.sw + g.pcw;
+}
+// (r, s) of tap index rs of the K axis
+__device__ __forceinline__ void tap_of(const ConvArgs& g, int rs, int& r, int& s) {
+  if (g.par) {
+    const int j = rs % g.ns, i = rs / g.ns;
+    r = g.rf + i * g.sh;
+    s = g.sf + j * g.sw;
+  } else {
+    s = rs % g.S;
+    r = rs / g.S;
+  }
+}
 
 __device__ __forceinline__ float conv_act(int act, float x) {
   switch (act) {
@@ -93,7 +115,18 @@ struct AGather {
         xa[i] = q * g.sw - g.pw;
         base[i] = static_cast<int64_t>(n) * g.H * g.W * g.C;
       } else {
-        const int w = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
+        int w, h, n;
+        if (g.par) {
+          const int ww = m % g.Wc, t = m / g.Wc, hh = t % g.Hc;
+          n = t / g.Hc;
+          h = hh * g.sh + g.pch;
+          w = ww * g.sw + g.pcw;
+        } else {
+          const int t = m / g.W;
+          w = m % g.W;
+          h = t % g.H;
+          n = t / g.H;
+        }
         ya[i] = h + g.ph;
         xa[i] = w + g.pw;
         base[i] = static_cast<int64_t>(n) * g.P * g.Q * g.K;
@@ -104,7 +137,14 @@ struct AGather {
     const int k = k0 + (threadIdx.x & 7) * 8;
     const bool kok = k < g.KG;
     const int CC = MODE == MODE_FWD ? g.C : g.K;
-    const int cc = k % CC, rs = k / CC, s = rs % g.S, r = rs / g.S;
+    const int cc = k % CC, rs = k / CC;
+    int r, s;
+    if (MODE == MODE_FWD) {
+      s = rs % g.S;
+      r = rs / g.S;
+    } else {
+      tap_of(g, rs, r, s);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       bool ok = kok;
@@ -188,7 +228,9 @@ struct ColStager {
       if (KIND == 0) {
         src = P + static_cast<int64_t>(k) * ld + o;
       } else if (KIND == 1) {
-        const int kout = k % g.K, rs = k / g.K, s = rs % g.S, rr = rs / g.S;
+        const int kout = k % g.K, rs = k / g.K;
+        int rr, s;
+        tap_of(g, rs, rr, s);
         src = g.w + ((static_cast<int64_t>(kout) * g.R + rr) * g.S + s) * g.C + o;
       } else {
         const int q = k % g.Q, t = k / g.Q, p = t % g.P, n = t / g.P;
@@ -355,22 +397,27 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) csum[nt][g4][e] = csq[nt][g4][e] = 0.f;
 
+  // Epilogue through LDS: lanes own one row x 4 columns of the accumulator
+  // (8-byte pieces of many rows), so the tile is first written to an LDS
+  // image and then stored row-contiguously, 16 B per lane (full 128-B lines).
+  constexpr int ROWB = BN * 2 + 16;  // padded row: conflict-free 8-B writes
+  unsigned char* ctile = smem;       // 128 x ROWB <= the staging buffers (free after the K loop)
+  static_assert(BM * ROWB <= 2 * (IMG + IMGB), "epilogue tile exceeds LDS");
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
-    const int m = m0 + wm * 64 + mt * 32 + (lane & 31);
-    const bool mok = m < g.M;
+    const int ml = wm * 64 + mt * 32 + (lane & 31);
+    const bool mok = m0 + ml < g.M;
 #pragma unroll
     for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int n = n0 + wn * (BN / 2) + nt * 32 + 8 * g4 + 4 * h;
-        if (!mok || n >= g.NG) continue;  // NG % 8 == 0: a 4-group is all in or all out
+        const int nl = wn * (BN / 2) + nt * 32 + 8 * g4 + 4 * h;
+        const int n = n0 + nl;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[nt][mt][4 * g4 + e];
-        bf16* dst = out + static_cast<int64_t>(m) * g.NG + n;
         if (MODE == MODE_FWD) {
-          if (g.bias) {
+          if (g.bias && n < g.NG) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] += bf2f(g.bias[n + e]);
           }
@@ -378,21 +425,39 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = conv_act(g.act, v[e]);
           }
-        } else if (g.beta != 0.f) {
-          const bf16x4 old = *reinterpret_cast<const bf16x4*>(dst);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += g.beta * bf2f(old[e]);
         }
         bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = f2bf(v[e]);
-          const float r = bf2f(o[e]);  // statistics of the stored (rounded) value
-          csum[nt][g4][e] += r;
-          csq[nt][g4][e] += r * r;
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        if (mok && n < g.NG) {  // NG % 8 == 0: a 4-group is all in or all out
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float r = bf2f(o[e]);  // statistics of the stored (rounded) value
+            csum[nt][g4][e] += r;
+            csq[nt][g4][e] += r * r;
+          }
         }
-        *reinterpret_cast<bf16x4*>(dst) = o;
+        *reinterpret_cast<bf16x4*>(ctile + ml * ROWB + nl * 2) = o;
       }
+  }
+  __syncthreads();
+  {
+    constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+#pragma unroll
+    for (int i = 0; i < BM * CPR / 256; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int ml = c / CPR, ch = c % CPR;
+      const int m = m0 + ml, n = n0 + ch * 8;
+      if (m >= g.M || n >= g.NG) continue;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(ctile + ml * ROWB + ch * 16);
+      bf16* dst = out + (MODE == MODE_DGRAD ? dgrad_row(g, m) : static_cast<int64_t>(m)) * g.NG + n;
+      if (MODE == MODE_DGRAD && g.beta != 0.f) {
+        const bf16x8 old = *reinterpret_cast<const bf16x8*>(dst);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + g.beta * bf2f(old[e]));
+      }
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    }
   }
   if (MODE == MODE_FWD && g.stats) {
     // per-wave column partials (no atomics: a slot per (m tile, wave row));
@@ -419,42 +484,53 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   }
 }
 
-// out[j] (+)= sum_r ws[r][j]; grid (column blocks of 1024, row chunks) —
-// row chunks > 1 combine with fp32 atomics (few per address).
+// out[j] (+)= sum_r ws[r][j] over rows [blockIdx.y*per, +per); with several
+// row chunks each writes its partial row of `out` (a [chunks][W] scratch),
+// summed by a second single-chunk pass — no atomics anywhere.
 __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                           int rows, int64_t W, int rows_per_chunk, int accumulate) {
   const int64_t j = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
   if (j >= W) return;
   const int r0 = blockIdx.y * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  float* o = out + static_cast<int64_t>(blockIdx.y) * W;
   if (j + 3 < W) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
     for (int r = r0; r < r1; ++r) s += *reinterpret_cast<const f32x4*>(ws + static_cast<int64_t>(r) * W + j);
-    if (gridDim.y == 1) {
-      f32x4* d = reinterpret_cast<f32x4*>(out + j);
-      *d = accumulate ? *d + s : s;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(out + j + e, s[e]);
-    }
+    f32x4* d = reinterpret_cast<f32x4*>(o + j);
+    *d = accumulate ? *d + s : s;
   } else {
     for (int e = 0; j + e < W; ++e) {
       float t = 0.f;
       for (int r = r0; r < r1; ++r) t += ws[static_cast<int64_t>(r) * W + j + e];
-      if (gridDim.y == 1) out[j + e] = accumulate ? out[j + e] + t : t;
-      else atomicAdd(out + j + e, t);
+      o[j + e] = accumulate ? o[j + e] + t : t;
     }
   }
 }
 
-void reduce_rows(const float* ws, float* out, int rows, int64_t W, int accumulate, hipStream_t st) {
+constexpr int kMaxChunks = 256;
+
+// tmp: kMaxChunks * W floats (null: single pass)
+void reduce_rows(const float* ws, float* out, int rows, int64_t W, int accumulate, float* tmp, hipStream_t st) {
   const int64_t cols = (W + 1023) / 1024;
-  int chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(rows / 16, 1024 / std::max<int64_t>(cols, 1))));
-  if (chunks > 1 && !accumulate) throw std::logic_error("reduce_rows: chunked reduce needs accumulate");
+  int chunks = 1;
+  if (tmp && rows >= 64)
+    chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({rows / 32, kMaxChunks, 2048 / cols})));
   const int per = (rows + chunks - 1) / chunks;
   chunks = (rows + per - 1) / per;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(static_cast<unsigned>(cols), chunks), dim3(256), 0, st, ws, out, rows,
-                     W, per, accumulate);
+  if (chunks == 1) {
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3(static_cast<unsigned>(cols), 1), dim3(256), 0, st, ws, out, rows, W,
+                       rows, accumulate);
+    return;
+  }
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(static_cast<unsigned>(cols), chunks), dim3(256), 0, st, ws, tmp, rows,
+                     W, per, 0);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(static_cast<unsigned>(cols), 1), dim3(256), 0, st,
+                     static_cast<const float*>(tmp), out, chunks, W, chunks, accumulate);
 }
+
+}  // namespace
+
+namespace {
 
 ConvArgs make_args(const ConvShape& cs) {
   ConvArgs g{};
@@ -490,7 +566,7 @@ void launch(const ConvArgs& g, int bn, int blocks, hipStream_t st) {
 int conv2d_stats_ws_floats(const ConvShape& cs) {
   ConvArgs g = make_args(cs);
   const int64_t M = static_cast<int64_t>(g.N) * g.P * g.Q;
-  return static_cast<int>(((M + BM - 1) / BM) * 2 * 2 * cs.K);
+  return static_cast<int>((((M + BM - 1) / BM) * 2 + kMaxChunks) * 2 * cs.K);
 }
 
 void conv2d_fwd(const ConvShape& cs, const void* x, const void* w, const void* bias, void* y, float* stats,
@@ -513,8 +589,8 @@ void conv2d_fwd(const ConvShape& cs, const void* x, const void* w, const void* b
   launch<MODE_FWD>(g, bn, blocks, st);
   FFK_LAUNCH_CHECK("conv2d_fwd");
   if (stats) {
-    (void)hipMemsetAsync(stats, 0, sizeof(float) * 2 * g.NG, st);
-    reduce_rows(stats_ws, stats, gm * 2, 2 * static_cast<int64_t>(g.NG), 1, st);
+    const int64_t W = 2 * static_cast<int64_t>(g.NG);
+    reduce_rows(stats_ws, stats, gm * 2, W, 0, stats_ws + static_cast<int64_t>(gm) * 2 * W, st);
     FFK_LAUNCH_CHECK("conv2d_fwd stats");
   }
 }
@@ -526,10 +602,33 @@ void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, 
   g.w = static_cast<const bf16*>(w);
   g.out = dx;
   g.beta = beta;
-  g.M = g.N * g.H * g.W;
   g.NG = g.C;
-  g.KG = g.R * g.S * g.K;
   const int bn = g.NG <= 64 ? 64 : 128;
+  if ((g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1) {
+    // strided: one launch per output-parity class, each a dense implicit GEMM
+    // over only the taps that reach it (no MFMA work on structural zeros)
+    g.par = 1;
+    for (int pch = 0; pch < g.sh; ++pch)
+      for (int pcw = 0; pcw < g.sw; ++pcw) {
+        g.pch = pch;
+        g.pcw = pcw;
+        g.Hc = (g.H - pch + g.sh - 1) / g.sh;
+        g.Wc = (g.W - pcw + g.sw - 1) / g.sw;
+        if (g.Hc <= 0 || g.Wc <= 0) continue;
+        g.rf = (pch + g.ph) % g.sh;
+        g.sf = (pcw + g.pw) % g.sw;
+        g.nr = g.rf < g.R ? (g.R - 1 - g.rf) / g.sh + 1 : 0;
+        g.ns = g.sf < g.S ? (g.S - 1 - g.sf) / g.sw + 1 : 0;
+        g.M = g.N * g.Hc * g.Wc;
+        g.KG = g.nr * g.ns * g.K;
+        const int blocks = ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn);
+        launch<MODE_DGRAD>(g, bn, blocks, st);
+      }
+    FFK_LAUNCH_CHECK("conv2d_dgrad");
+    return;
+  }
+  g.M = g.N * g.H * g.W;
+  g.KG = g.R * g.S * g.K;
   const int blocks = ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn);
   launch<MODE_DGRAD>(g, bn, blocks, st);
   FFK_LAUNCH_CHECK("conv2d_dgrad");
@@ -563,7 +662,10 @@ WgradPlan wgrad_plan(const ConvShape& cs, int splits) {
 
 int64_t conv2d_wgrad_ws_floats(const ConvShape& cs, int splits) {
   const WgradPlan p = wgrad_plan(cs, splits);
-  return p.splits > 1 ? static_cast<int64_t>(p.splits) * cs.K * cs.R * cs.S * cs.C : 0;
+  const int64_t W = static_cast<int64_t>(cs.K) * cs.R * cs.S * cs.C;
+  if (p.splits <= 1) return 0;
+  // slabs + the two-pass reduce scratch when there are many slabs
+  return static_cast<int64_t>(p.splits) * W + (p.splits >= 64 ? kMaxChunks * W : 0);
 }
 
 void conv2d_wgrad(const ConvShape& cs, const void* x, const void* dy, float* dw, float* ws, int splits,
@@ -583,7 +685,8 @@ void conv2d_wgrad(const ConvShape& cs, const void* x, const void* dy, float* dw,
   launch<MODE_WGRAD>(g, p.bn, p.tiles * p.splits, st);
   FFK_LAUNCH_CHECK("conv2d_wgrad");
   if (p.splits > 1) {
-    reduce_rows(ws, dw, p.splits, static_cast<int64_t>(g.M) * g.NG, 1, st);
+    const int64_t W = static_cast<int64_t>(g.M) * g.NG;
+    reduce_rows(ws, dw, p.splits, W, 1, p.splits >= 64 ? ws + static_cast<int64_t>(p.splits) * W : nullptr, st);
     FFK_LAUNCH_CHECK("conv2d_wgrad reduce");
   }
 }
