@@ -60,6 +60,7 @@ class FFConfig:
     shard_optimizer: bool = False      # ZeRO-style sharded optimizer state (reduce-scatter + all-gather)
     bucket_mb: int = 64                # gradient all-reduce bucket size
     enable_hipgraph: bool = True       # fit(): capture the training iteration as a hipGraph (1 GPU)
+    parameter_sync: str = "nccl"       # "nccl" (all-reduce) | "ps" (reference ParamSync::PS)
     native_data_loader: bool = True    # fit() on arrays: C++ prefetcher + pinned async H2D (runtime/dataloader.py)
     shuffle_data: bool = False         # native loader: reshuffle the samples every epoch
     _start_time: float = dataclasses.field(default_factory=time.time)
@@ -153,6 +154,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--bucket-mb", dest="bucket_mb", type=int)
     a("--disable-hipgraph", dest="enable_hipgraph", action="store_const", const=False)
     a("--python-data-loader", dest="native_data_loader", action="store_const", const=False)
+    a("--param-sync", dest="parameter_sync", choices=["nccl", "ps"])
     a("--shuffle", dest="shuffle_data", action="store_const", const=True)
     a("--seed", dest="seed", type=int)
     # Legion / Realm flags: accepted, ignored

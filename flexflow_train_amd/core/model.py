@@ -195,6 +195,12 @@ class AdamOptimizer:
         self.cfg.lr = learning_rate
 
 
+def _param_sync_str(v) -> str:
+    """FFConfig.parameter_sync: "nccl" / "ps" or a ParameterSyncType."""
+    name = getattr(v, "name", str(v)).lower()
+    return "ps" if name in ("ps", "parameter_server") else "nccl"
+
+
 class SingleDataLoader:
     """Holds the full dataset on the host and yields global batches (the
     executor keeps only this rank's piece).  Parity: flexflow_cffi.py:2449."""
@@ -531,6 +537,7 @@ class FFModel:
         cfg = ExecConfig(compute_dtype=cdt, device=device, seed=self.ffconfig.seed,
                          profiling=self.ffconfig.profiling, fuse_add_layernorm=self.ffconfig.perform_fusion,
                          shard_optimizer=bool(self.ffconfig.shard_optimizer),
+                         param_sync=_param_sync_str(self.ffconfig.parameter_sync),
                          bucket_bytes=int(self.ffconfig.bucket_mb) << 20)
         out_v = None
         if output is not None:

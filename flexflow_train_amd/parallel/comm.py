@@ -100,6 +100,22 @@ class DistContext:
                                               async_op=async_op)
         return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
 
+    def reduce_(self, t: torch.Tensor, ranks: Sequence[int], dst: int, async_op: bool = False):
+        """Sum ``t`` over ``ranks`` into rank ``dst`` (parameter-server gradient
+        gather, the reference's ParamSync::PS, optimizer_kernel.cu:43-70)."""
+        if len(ranks) <= 1 or not self.distributed:
+            return None
+        self.stats["reduce"] = self.stats.get("reduce", 0) + 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+        return dist.reduce(t, dst=dst, group=self.group(ranks), async_op=async_op)
+
+    def broadcast_(self, t: torch.Tensor, ranks: Sequence[int], src: int, async_op: bool = False):
+        if len(ranks) <= 1 or not self.distributed:
+            return None
+        self.stats["broadcast"] = self.stats.get("broadcast", 0) + 1
+        self.stats["bytes"] += t.numel() * t.element_size()
+        return dist.broadcast(t, src=src, group=self.group(ranks), async_op=async_op)
+
     def all_gather_(self, t: torch.Tensor, ranks: Sequence[int]):
         """In-place all-gather of the equal chunks of the 1-D ``t`` (chunk i
         comes from the i-th rank of sorted(ranks))."""

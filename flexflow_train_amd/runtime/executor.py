@@ -67,6 +67,11 @@ class ExecConfig:
     # of a data-parallel group updates (and keeps Adam state for) one shard
     # of every bucket, and the updated weights are all-gathered.
     shard_optimizer: bool = False
+    # gradient synchronisation of replicated weights: "nccl" = bucketed RCCL
+    # all-reduce + update on every replica; "ps" = parameter server (the
+    # reference's ParamSync::PS): reduce to the group leader, the leader
+    # updates, the updated weights are broadcast.
+    param_sync: str = "nccl"
 
 
 @dataclasses.dataclass
@@ -513,7 +518,8 @@ class Executor:
             else:
                 opt = FlatOptimizer(self.optimizer_cfg, master, grad, compute)
             self.flats.append({"group": g, "params": plist, "master": master, "grad": grad, "compute": compute,
-                               "buckets": binfo, "opt": opt, "zero": zero})
+                               "buckets": binfo, "opt": opt, "zero": zero,
+                               "ps": (not zero) and self.cfg.param_sync == "ps" and len(g) > 1})
         self._param_bucket = {}
         for f in self.flats:
             for bi, b in enumerate(f["buckets"]):
@@ -894,6 +900,9 @@ class Executor:
             if f["zero"]:
                 # sharded optimizer: each rank only needs the sum of its shard
                 w = self.dist.reduce_scatter_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
+            elif f["ps"]:
+                # parameter server: only the group leader needs the summed gradient
+                w = self.dist.reduce_(f["grad"][b["lo"]:b["hi"]], f["group"], min(f["group"]), async_op=True)
             else:
                 w = self.dist.all_reduce_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
             b["launched"] = True
@@ -937,9 +946,22 @@ class Executor:
             if norm > self.cfg.grad_clip:
                 scale = self.cfg.grad_clip / (norm + 1e-6)
         for f in self.flats:
+            if f.get("ps") and self.dist.distributed and self.rank != min(f["group"]):
+                continue  # PS: only the leader updates (its optimizer state is the only one)
             f["opt"].step(lr=lr, grad_scale=scale)
         self._gather_updated()
+        self._broadcast_ps()
         self.step_num += 1
+
+    def _broadcast_ps(self):
+        """Parameter server: the leader's updated weights go back to the replicas."""
+        for f in self.flats:
+            if not f.get("ps") or not self.dist.distributed:
+                continue
+            leader = min(f["group"])
+            self.dist.broadcast_(f["master"], f["group"], leader)
+            if f["compute"] is not None:
+                self.dist.broadcast_(f["compute"], f["group"], leader)
 
     def grad_norm(self) -> float:
         # every logical gradient element counted once: only the canonical

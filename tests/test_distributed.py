@@ -142,3 +142,14 @@ def test_recompile_switches_strategy(tmp_path):
     out = run_recompile(M.mlp, 2, path, steps_before=2, steps_after=2)
     assert out["recompilations"] == 1
     assert_params_close(out["params"], ref["params"], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("optimizer", ["sgd", "adam"])
+def test_parameter_server_sync_matches(optimizer):
+    """ParamSync::PS (reference config.h:38-42, optimizer_kernel.cu:43-70):
+    gradients reduced to the group leader, leader-only update, weights
+    broadcast back — same trajectory as the single-process run."""
+    ref = run_single(M.mlp, steps=3, optimizer=optimizer)
+    out = run_distributed(M.mlp, 2, steps=3, optimizer=optimizer, cfg_over={"parameter_sync": "ps"})
+    assert_params_close(out["params"], ref["params"], rtol=1e-4, atol=1e-5)
+    assert out["stats"].get("reduce", 0) > 0 and out["stats"].get("broadcast", 0) > 0
