@@ -1,0 +1,29 @@
+"""Every example program runs end to end (small sample counts, CPU) and
+prints the reference's THROUGHPUT line."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXAMPLES = ["native/mnist_mlp.py", "native/cifar10_cnn.py", "native/multi_head_attention.py", "native/bert_proxy.py",
+            "native/dlrm.py", "keras/seq_mnist_mlp.py", "keras/func_cifar10_cnn.py", "pytorch/mnist_mlp_torch.py"]
+
+
+@pytest.mark.parametrize("script", EXAMPLES)
+def test_example_runs(script):
+    env = dict(os.environ, FF_EXAMPLE_SAMPLES="128", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", script), "-b", "32"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "THROUGHPUT" in r.stdout, r.stdout[-2000:]
+
+
+def test_model_zoo_runner():
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "train.py"), "--model", "mlp_unify",
+                        "--steps", "2", "--warmup", "1", "--config", '{"batch_size": 16, "input_dim": 64, "hidden_dims": [64, 64]}'],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "THROUGHPUT" in r.stdout
