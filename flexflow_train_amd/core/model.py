@@ -547,6 +547,9 @@ class FFModel:
                                  metrics=self.metrics, optimizer=self._optimizer.cfg, output=out_v,
                                  valid_classes=self.valid_classes)
         self.executor.init_parameters()
+        self.local_backing = None
+        if self.ffconfig.local_execution:
+            self._init_local_backing(loss_type)
         # label tensor (reference: created in compile, [batch, 1] int32 for sparse CE)
         out_lay = self.executor.value_layout[self.executor.loss_value]
         if loss_type is not None and normalize_loss_type(loss_type) == "sparse_categorical_crossentropy":
@@ -662,6 +665,8 @@ class FFModel:
         ex = self.executor
         xs = x if isinstance(x, (list, tuple)) else [x]
         bs = batch_size or self.ffconfig.batch_size
+        if getattr(self, "local_backing", None) is not None:
+            return self._fit_local(xs, y, bs, epochs)
         native = self._native_loader(xs, y, bs)
         if native is not None:
             return self._fit_native(native, epochs)
@@ -723,6 +728,54 @@ class FFModel:
                                     shuffle=bool(self.ffconfig.shuffle_data), seed=self.ffconfig.seed)
         except (ValueError, KeyError):
             return None
+
+    def _init_local_backing(self, loss_type):
+        """--local-execution: train through the native C++ CPU executor
+        (csrc/ffcore/src/local_exec.cc, the reference's lib/local-execution),
+        starting from the executor's initial weights."""
+        if self.dist.world != 1 or self.executor.cfg.device.type != "cpu":
+            raise RuntimeError("local execution runs on one CPU process (BASELINE config 1)")
+        from ..runtime.optimizer import AdamConfig
+        oc = self._optimizer.cfg
+        kw = dict(lr=oc.lr, weight_decay=oc.weight_decay)
+        if isinstance(oc, AdamConfig):
+            if oc.decoupled:
+                raise RuntimeError("local execution implements the reference Adam (L2 folded into the gradient)")
+            kw.update(optimizer="adam", beta1=oc.beta1, beta2=oc.beta2, epsilon=oc.epsilon)
+        else:
+            kw.update(optimizer="sgd", momentum=oc.momentum, nesterov=oc.nesterov)
+        lt = normalize_loss_type(loss_type) if loss_type is not None else "identity"
+        b = C.LocalTrainingBacking(self.cg, loss=lt, seed=self.ffconfig.seed, **kw)
+        for n in self.executor.parameter_names():
+            b.set_weight(n, self.executor.get_parameter(n).numpy())
+        self.local_backing = b
+
+    def _fit_local(self, xs, y, bs, epochs):
+        b = self.local_backing
+        arrays = [np.asarray(d.full if isinstance(d, SingleDataLoader) else d) for d in xs]
+        labels = np.asarray(y.full if isinstance(y, SingleDataLoader) else y)
+        names = [t.name for t in self._inputs]
+        iters = len(labels) // bs
+        t0 = time.time()
+        for epoch in range(epochs):
+            b.reset_metrics()
+            for it in range(iters):
+                sl = slice(it * bs, (it + 1) * bs)
+                for n, a in zip(names, arrays):
+                    b.set_input(n, a[sl])
+                b.train_step(labels[sl].astype(np.float32))
+            mm = b.metrics()
+            if self.dist.rank == 0 and iters:
+                acc = 100.0 * mm["correct"] / max(mm["samples"], 1)
+                print(f"epoch {epoch}: samples={mm['samples']} accuracy={acc:.2f}% "
+                      f"loss={mm['loss_sum'] / max(mm['samples'], 1):.4f} (local execution)", flush=True)
+        elapsed = time.time() - t0
+        for n in self.executor.parameter_names():   # keep the executor's view current
+            self.executor.set_parameter(n, torch.from_numpy(np.array(b.get_weight(n))))
+        thr = iters * bs * epochs / max(elapsed, 1e-9)
+        print(f"ELAPSED TIME = {elapsed:.4f}s, THROUGHPUT = {thr:.2f} samples/s", flush=True)
+        self.last_throughput = thr
+        return thr
 
     def _fit_native(self, loader, epochs):
         ex = self.executor
