@@ -61,6 +61,7 @@ class FFConfig:
     bucket_mb: int = 64                # gradient all-reduce bucket size
     enable_hipgraph: bool = True       # fit(): capture the training iteration as a hipGraph (1 GPU)
     parameter_sync: str = "nccl"       # "nccl" (all-reduce) | "ps" (reference ParamSync::PS)
+    cpu_only: bool = False             # run on the host even when a GPU is visible
     local_execution: bool = False      # train on the native C++ CPU executor (lib/local-execution parity)
     native_data_loader: bool = True    # fit() on arrays: C++ prefetcher + pinned async H2D (runtime/dataloader.py)
     shuffle_data: bool = False         # native loader: reshuffle the samples every epoch
@@ -156,6 +157,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--disable-hipgraph", dest="enable_hipgraph", action="store_const", const=False)
     a("--python-data-loader", dest="native_data_loader", action="store_const", const=False)
     a("--local-execution", dest="local_execution", action="store_const", const=True)
+    a("--cpu", dest="cpu_only", action="store_const", const=True)
     a("--param-sync", dest="parameter_sync", choices=["nccl", "ps"])
     a("--shuffle", dest="shuffle_data", action="store_const", const=True)
     a("--seed", dest="seed", type=int)

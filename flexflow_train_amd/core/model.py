@@ -520,7 +520,7 @@ class FFModel:
             self._optimizer = SGDOptimizer(self, lr=self.ffconfig.learning_rate)
         self.loss_type = loss_type
         self.metrics = [normalize_metric(m) for m in (metrics or [])]
-        cuda = torch.cuda.is_available()
+        cuda = torch.cuda.is_available() and not self.ffconfig.cpu_only and not self.ffconfig.local_execution
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         device = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
         if cuda:

@@ -41,6 +41,7 @@ def _embed_concat(m, B):
 def _run(build, opt, loss, feeds, labels, steps=3, B=8):
     cfg = FFConfig()
     cfg.batch_size = B
+    cfg.cpu_only = True
     m = FFModel(cfg)
     build(m, B)
     ce = loss == "ce"
