@@ -158,4 +158,15 @@ struct PoolShape {
 void pool2d_fwd(const PoolShape& s, const void* x, void* y, void* argmax, hipStream_t st);
 void pool2d_bwd(const PoolShape& s, const void* dy, const void* argmax, void* dx, float beta, hipStream_t st);
 
+// ---- blaslt.hip: hipBLASLt GEMMs with fused epilogues (row-major operands,
+// bf16 in, bf16 / fp32 out).  bias: bf16 input (BIAS, GELU_BIAS) or fp32
+// bias-gradient output (BGRADB); aux: reserved (no aux epilogue is usable).
+enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU_BIAS = 3, EPI_BGRADB = 4 };
+int blaslt_probe(int M, int N, int K, bool ta, bool tb, int raw_epi, int bias_t, int aux_t, int out_f32);
+bool blaslt_supported(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int epi, int out_f32,
+                      bool has_beta, int aux_ld, size_t ws_bytes);
+void blaslt_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool ta,
+                 bool tb, int epi, const void* bias, void* aux, int aux_ld, float alpha, float beta, int out_f32,
+                 void* ws, size_t ws_bytes, hipStream_t st);
+
 }  // namespace ffk

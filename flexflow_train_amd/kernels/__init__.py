@@ -852,3 +852,65 @@ def pool2d_bwd(dy, arg, x_shape, k, s, p, avg: bool, count_pad: bool = False):
     ext().pool2d_bwd(g, _p(dy), _p(arg), _p(dx), 0.0, _stream())
     STATS["pool2d_bwd"] += 1
     return dx
+
+
+# ---------------------------------------------------------------------------
+# hipBLASLt GEMMs with fused epilogues (csrc/kernels/blaslt.hip)
+EPI_NONE, EPI_BIAS, EPI_GELU_BIAS, EPI_BGRADB = 0, 1, 3, 4
+_BLT_WS = {}
+_BLT_WS_BYTES = 64 << 20
+
+
+def _blaslt_ws(dev):
+    w = _BLT_WS.get(dev)
+    if w is None:
+        w = torch.empty(_BLT_WS_BYTES, dtype=torch.uint8, device=dev)
+        _BLT_WS[dev] = w
+    return w
+
+
+def _gemm_dims(a, b, trans_a, trans_b):
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm: inner dims differ ({K} vs {Kb})")
+    return M, N, K
+
+
+def blaslt_ok(a, b, trans_a=False, trans_b=False, epilogue=EPI_NONE, out_f32=False, beta=0.0) -> bool:
+    """True when hipBLASLt has an algorithm for this GEMM + epilogue (cached)."""
+    if not (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        return False
+    if not (a.is_contiguous() and b.is_contiguous()):
+        return False
+    M, N, K = _gemm_dims(a, b, trans_a, trans_b)
+    return ext().blaslt_supported(M, N, K, a.shape[1], b.shape[1], N, bool(trans_a), bool(trans_b), int(epilogue),
+                                  int(out_f32), bool(beta), N, _BLT_WS_BYTES)
+
+
+def blaslt_gemm(a, b, trans_a=False, trans_b=False, epilogue=EPI_NONE, bias=None, aux=None, out=None,
+                beta: float = 0.0, alpha: float = 1.0, out_f32: bool = False):
+    """C = op(a) @ op(b) with a hipBLASLt epilogue (see blaslt.hip).  ``bias``:
+    bf16 [N] input for BIAS / GELU_BIAS, fp32 OUTPUT (overwritten) for
+    BGRADB = colsum of op(a) over K."""
+    for name, t in (("a", a), ("b", b)):
+        _check(t, name, torch.bfloat16)
+    M, N, K = _gemm_dims(a, b, trans_a, trans_b)
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        beta = 0.0
+    else:
+        out_f32 = out.dtype == torch.float32
+        if tuple(out.shape) != (M, N) and out.numel() != M * N:
+            raise ValueError("blaslt_gemm: out has the wrong shape")
+        _check(out, "out")
+    if epilogue in (EPI_BIAS, EPI_GELU_BIAS):
+        _check(bias, "bias", torch.bfloat16, N)
+    elif epilogue == EPI_BGRADB:
+        _check(bias, "bias grad", torch.float32, M)
+    ws = _blaslt_ws(a.device)
+    ext().blaslt_gemm(_p(a), _p(b), _p(out), M, N, K, a.shape[1], b.shape[1], N, bool(trans_a), bool(trans_b),
+                      int(epilogue), _p(bias), _p(aux), N, float(alpha), float(beta), int(out_f32), _p(ws),
+                      _BLT_WS_BYTES, _stream())
+    STATS["blaslt_gemm"] += 1
+    return out

@@ -71,7 +71,7 @@ def write_ninja(targets: list[str]) -> str:
         "  command = $cxx -shared -o $out $in -lpthread",
         "  description = LINK $out",
         "rule link_hip",
-        f"  command = $hipcc -shared --offload-arch={ARCH} -o $out $in",
+        f"  command = $hipcc -shared --offload-arch={ARCH} -o $out $in -L{os.path.join(ROCM, 'lib')} -lhipblaslt",
         "  description = LINK $out",
     ]
     defaults = []
