@@ -75,6 +75,13 @@ bool is_mp_capable(const OpAttrs& op, MPKind k) {
     case OpType::MULTIHEAD_ATTENTION: return k == MPKind::HEADS;
     case OpType::EXPERTS: return k == MPKind::EXPERTS;
     case OpType::EMBEDDING: return k == MPKind::COLUMN && op.s("aggr") == "none";
+    // conv channel parallelism (op-attrs conv_2d.cc:85-142): COLUMN = output
+    // channels (weight sharded on K), ROW = input channels (partial sums)
+    case OpType::CONV2D:
+      if (op.i("groups") != 1) return false;
+      if (k == MPKind::COLUMN) return true;
+      if (k == MPKind::ROW) return activation_from_string(op.s("activation")) == Activation::NONE;
+      return false;
     default: return false;
   }
 }
@@ -130,8 +137,10 @@ std::optional<std::vector<ParallelTensorShape>> required_input_shapes(const Comp
         break;
       }
       case MPKind::ROW: {
-        if (ref.dims.back() % cfg.model) return std::nullopt;
-        ps[0].shard_dims.back().degree = cfg.model;
+        // the reduction (input-feature) dim: channels (dim 1) for a conv, the last dim otherwise
+        const int rd = op.type == OpType::CONV2D ? 1 : ref.num_dims() - 1;
+        if (ref.dims[rd] % cfg.model) return std::nullopt;
+        ps[0].shard_dims[rd].degree = cfg.model;
         break;
       }
       case MPKind::HEADS: {

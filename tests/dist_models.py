@@ -96,3 +96,19 @@ def moe_replicated(m):
 
 def moe_alltoall(m):
     return _moe(m, "alltoall")
+
+
+def cnn(m):
+    """conv -> pool -> conv(+residual add) -> relu -> flat -> dense (no BatchNorm:
+    per-replica batch statistics make BN intentionally rank-local)."""
+    from flexflow_train_amd.core import PoolType
+    x = m.create_tensor([8, 3, 12, 12], DataType.DT_FLOAT, name="img")
+    t = m.conv2d(x, 8, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="c1")
+    t = m.pool2d(t, 2, 2, 2, 2, 0, 0, PoolType.POOL_MAX, name="p1")
+    u = m.conv2d(t, 8, 3, 3, 1, 1, 1, 1, name="c2")
+    t = m.relu(m.add(t, u, name="res"), name="r2")
+    t = m.pool2d(t, 2, 2, 2, 2, 0, 0, PoolType.POOL_AVG, name="p2")
+    t = m.dense(m.flat(t, name="flat"), 6, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(11)
+    return {"img": torch.randn(8, 3, 12, 12, generator=g)}, torch.randint(0, 6, (8,), generator=g)

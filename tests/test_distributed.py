@@ -153,3 +153,29 @@ def test_parameter_server_sync_matches(optimizer):
     out = run_distributed(M.mlp, 2, steps=3, optimizer=optimizer, cfg_over={"parameter_sync": "ps"})
     assert_params_close(out["params"], ref["params"], rtol=1e-4, atol=1e-5)
     assert out["stats"].get("reduce", 0) > 0 and out["stats"].get("broadcast", 0) > 0
+
+
+def test_cnn_data_parallel():
+    """Conv / pool / residual CNN: data parallel on 2 ranks matches 1 process."""
+    ref = run_single(M.cnn, steps=2)
+    out = run_distributed(M.cnn, 2, steps=2)
+    assert_params_close(out["params"], ref["params"], rtol=1e-4, atol=1e-5)
+
+
+def test_cnn_channel_parallel_conv(tmp_path):
+    """Output-channel (model) parallel conv: the weight is split on its out
+    channels, the activations re-combined (op-attrs conv_2d.cc:85-142)."""
+    ref = run_single(M.cnn, steps=2)
+    path = str(tmp_path / "conv_tp.json")
+    write_strategy(M.cnn, 2, {"c2": {"batch": 1, "model": 2, "kind": "column"}}, path)
+    out = run_distributed(M.cnn, 2, path, steps=2)
+    assert_params_close(out["params"], ref["params"], rtol=1e-4, atol=1e-5)
+
+
+def test_cnn_input_channel_parallel_conv(tmp_path):
+    """Input-channel (row) parallel conv: partial-sum outputs reduced by RCCL/gloo."""
+    ref = run_single(M.cnn, steps=2)
+    path = str(tmp_path / "conv_row.json")
+    write_strategy(M.cnn, 2, {"c2": {"batch": 1, "model": 2, "kind": "row"}}, path)
+    out = run_distributed(M.cnn, 2, path, steps=2)
+    assert_params_close(out["params"], ref["params"], rtol=1e-4, atol=1e-5)
