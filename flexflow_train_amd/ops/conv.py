@@ -87,30 +87,29 @@ class Conv2DOp(OpImpl):
             if stats is not None:
                 y._ff_bn_stats = stats
             return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape))
-        xw = x.contiguous(memory_format=torch.channels_last) if x.is_cuda else x
-        with torch.no_grad():
-            y = _ACTS[act](F.conv2d(xw, _oihw(W).to(x.dtype), b.to(x.dtype) if b is not None else None,
-                                    stride=stride, padding=pad, groups=groups))
-        return [y], ("torch", x, W, b)
+        # library path (grouped convs, CPU): the autograd graph recorded here is
+        # replayed in backward — no forward recomputation
+        xi = x.detach().requires_grad_(ctx.training and x.is_floating_point())
+        Wr = W.detach().requires_grad_(ctx.training)
+        with torch.enable_grad():
+            xw = xi.contiguous(memory_format=torch.channels_last) if xi.is_cuda else xi
+            u = F.conv2d(xw, _oihw(Wr).to(x.dtype), None, stride=stride, padding=pad, groups=groups)
+            if ctx.training:
+                u.retain_grad()
+            y = _ACTS[act](u + b.to(u.dtype).view(1, -1, 1, 1) if b is not None else u)
+        return [y.detach()], ("torch", xi, Wr, u, y)
 
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
         stride, pad, groups, act = _geom(ctx)
         if saved[0] == "torch":
-            _, x, W, b = saved
-            xi = x.detach().requires_grad_(bool(need_input_grad[0]))
-            Wr = W.detach().requires_grad_(weight_grads[0] is not None)
-            with torch.enable_grad():
-                xw = xi.contiguous(memory_format=torch.channels_last) if xi.is_cuda else xi
-                u = F.conv2d(xw, _oihw(Wr).to(x.dtype), None, stride=stride, padding=pad, groups=groups)
-                u.retain_grad()
-                y = _ACTS[act](u + b.to(u.dtype).view(1, -1, 1, 1) if b is not None else u)
+            _, xi, Wr, u, y = saved
             torch.autograd.backward([y], [grad_outputs[0].to(y.dtype)])
             if weight_grads[0] is not None and Wr.grad is not None:
                 acc_grad(weight_grads[0], Wr.grad)
             if len(weight_grads) > 1 and weight_grads[1] is not None:
                 # every partial-sum replica computes the (identical) bias gradient
                 acc_grad(weight_grads[1], u.grad.float().sum((0, 2, 3)))
-            return [xi.grad if xi.requires_grad else None]
+            return [xi.grad if (xi.requires_grad and need_input_grad[0]) else None]
 
         _, xin, wp, y, xshape = saved
         Kc, R, S, Cp = wp.shape

@@ -53,6 +53,8 @@ def _hip_ok(a, b, trans_a, trans_b) -> bool:
         return False
     if (not trans_a and Kd % 8) or (trans_a and M % 8) or (not trans_b and N % 8) or (trans_b and Kd % 8):
         return False
+    if N % 4:  # the output rows are written in 8 / 16-byte pieces
+        return False
     return a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
 
 
@@ -166,7 +168,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
     """C = act(op(a) @ op(b) + bias) (+ beta * out).  2-D operands."""
     if not a.is_cuda:
         return _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre)
-    hip_ok = _hip_ok(a, b, trans_a, trans_b) and (out is None or out.stride(1) == 1)
+    hip_ok = _hip_ok(a, b, trans_a, trans_b) and (
+        out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0))
     if not hip_ok or _MODE == "blas":
         return _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre)
     if _MODE == "hip":
