@@ -152,8 +152,7 @@ def main():
                 "model": args.model + ("" if not args.layers else f"-{args.layers}L(debug)"),
                 "global_batch": global_batch,
                 "seq_len": args.seq,
-                "parallelism": ("dp%d" % world) if par in ("data_parallel", "single_device",
-                                                            "data_parallel_fallback") else par,
+                "parallelism": _parallelism(model, world),
                 "strategy_source": par,
                 "layers": bcfg.num_encoder_layers,
                 "hidden": bcfg.hidden_size,
@@ -172,6 +171,26 @@ def main():
             rep = ex.profile_report()
             print(json.dumps({"profile_ms_total": {k: round(v, 3) for k, v in list(rep.items())[:40]}}),
                   file=sys.stderr)
+
+
+def _parallelism(model, world: int) -> str:
+    """"dpN" when every operator is only batch-sharded (searched or not),
+    else a summary of the non-DP degrees the search chose."""
+    from flexflow_train_amd import _ffcore as C
+    pcg = model.pcg
+    other = set()
+    for n in pcg.topo_order():
+        op = pcg.layer_op(n)
+        if op.op_type in ("INPUT", "WEIGHT") or pcg.is_weight_path(n) or C.is_parallel_op(op.type):
+            continue
+        ps = pcg.shape(C.ValueRef(n, 0))
+        deg = list(ps.shard_degrees())
+        if deg[1:] and max(deg[1:]) > 1 or ps.sum_degree > 1 or ps.discard_copy_degree > 1 or deg[0] != world:
+            other.add(f"{op.op_type.lower()}:{'x'.join(map(str, deg))}/s{ps.sum_degree}/c{ps.discard_copy_degree}")
+    src = model.search_report.get("source", "")
+    if not other:
+        return f"dp{world}"
+    return f"hybrid({src}; " + ", ".join(sorted(other)[:6]) + ")"
 
 
 _ZOO = {
@@ -263,8 +282,7 @@ def bench_zoo(args, world, rank):
     if rank == 0:
         par = model.search_report.get("source", "")
         conf = {"model": args.model, "global_batch": global_batch,
-                "parallelism": ("dp%d" % world) if par in ("data_parallel", "single_device",
-                                                            "data_parallel_fallback") else par,
+                "parallelism": _parallelism(model, world),
                 "strategy_source": par, "optimizer": opt, "compile_s": round(compile_s, 2), "hipgraph": graphed,
                 "final_loss": round(pm.loss, 4)}
         conf.update(extra)
