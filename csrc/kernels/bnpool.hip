@@ -45,6 +45,8 @@ __device__ __forceinline__ float ldp(const void* p, int dt, int i) {
   return dt == 1 ? bf2f(static_cast<const bf16*>(p)[i]) : static_cast<const float*>(p)[i];
 }
 
+constexpr int kBnBuckets = 16;
+
 struct RedGeom {
   int GL, RL, G;  // group lanes, row lanes, channel groups
 };
@@ -128,7 +130,10 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__
     float s = 0.f;
     for (int l = 0; l < RL; ++l) s += red[q][(l * GL + lg) * 8 + e];
     const int ch = blockIdx.y * GL * 8 + col;
-    if (ch < C) atomicAdd(out + q * C + ch, s);
+    // MODE 1 spreads blocks over kBnBuckets copies of [2][C] (the coefficient
+    // kernel sums them): a few hundred same-address atomics, not thousands
+    float* dst = MODE == 1 ? out + static_cast<int64_t>(blockIdx.x % kBnBuckets) * 2 * C : out;
+    if (ch < C) atomicAdd(dst + q * C + ch, s);
   }
 }
 
@@ -194,7 +199,11 @@ __global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* 
                                    float* dgamma, float* dbeta, int C, float inv_count) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const float s1 = sums[c], s2 = sums[C + c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < kBnBuckets; ++k) {
+    s1 += sums[static_cast<int64_t>(k) * 2 * C + c];
+    s2 += sums[static_cast<int64_t>(k) * 2 * C + C + c];
+  }
   const float A = (gamma ? ldp(gamma, pdt, c) : 1.f) * rstd[c];
   const float B = -A * rstd[c] * s2 * inv_count;
   coef[c] = A;
@@ -362,7 +371,9 @@ void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st) {
   if (C % 8) throw std::invalid_argument("bn_stats: C must be a multiple of 8");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
-  hipLaunchKernelGGL((bn_reduce_kernel<0>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x), nullptr,
+  dim3 grid = red_grid(r, M);
+  grid.x = std::min(grid.x, 256u);  // single [2][C] target: bound the same-address atomics
+  hipLaunchKernelGGL((bn_reduce_kernel<0>), grid, dim3(256), 0, st, static_cast<const bf16*>(x), nullptr,
                      nullptr, nullptr, nullptr, stats, M, C, r.GL, 0);
   FFK_LAUNCH_CHECK("bn_stats");
 }
@@ -391,10 +402,10 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   if (C % 8) throw std::invalid_argument("bn_bwd: C must be a multiple of 8");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C, st);
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
   hipLaunchKernelGGL((bn_reduce_kernel<1>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x),
                      static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean, rstd, ws, M, C, r.GL, relu);
-  float* coef = ws + 2 * C;
+  float* coef = ws + 2 * C * kBnBuckets;
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, mean, rstd, gamma,
                      param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M));
   const int64_t nvec = M * C / 8;

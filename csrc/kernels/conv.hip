@@ -495,6 +495,7 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restric
   float* o = out + static_cast<int64_t>(blockIdx.y) * W;
   if (j + 3 < W) {
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
     for (int r = r0; r < r1; ++r) s += *reinterpret_cast<const f32x4*>(ws + static_cast<int64_t>(r) * W + j);
     f32x4* d = reinterpret_cast<f32x4*>(o + j);
     *d = accumulate ? *d + s : s;
@@ -514,7 +515,7 @@ void reduce_rows(const float* ws, float* out, int rows, int64_t W, int accumulat
   const int64_t cols = (W + 1023) / 1024;
   int chunks = 1;
   if (tmp && rows >= 64)
-    chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({rows / 32, kMaxChunks, 2048 / cols})));
+    chunks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({rows / 64, kMaxChunks / 2, 2048 / cols})));
   const int per = (rows + chunks - 1) / chunks;
   chunks = (rows + per - 1) / per;
   if (chunks == 1) {

@@ -145,7 +145,7 @@ void bn_finalize(const float* stats, const void* gamma, const void* beta, int pa
                  float momentum, float eps, hipStream_t st);
 void bn_apply(const void* x, const void* residual, const float* scale, const float* shift, void* y, int64_t M, int C,
               int relu, hipStream_t st);
-// ws: 5*C floats; dgamma / dbeta (fp32) accumulate; dres (optional) = dy
+// ws: 35*C floats (16 partial [2][C] buckets + 3C coefficients); dgamma / dbeta (fp32) accumulate; dres (optional) = dy
 // masked by the ReLU (the residual branch's gradient of relu(bn(x) + res))
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,

@@ -811,7 +811,7 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, wan
     pdt = _dt(gamma) if gamma is not None else DT_BF16
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     dres = torch.empty_like(x, memory_format=torch.channels_last) if want_masked else None
-    ws = torch.empty(5 * C, device=x.device, dtype=torch.float32)
+    ws = torch.empty(35 * C, device=x.device, dtype=torch.float32)
     ext().bn_bwd(_p(dy), _p(x), _p(y if relu else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx), _p(dres),
                  _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, int(relu), _stream())
     STATS["bn_bwd"] += 1
