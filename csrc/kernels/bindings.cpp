@@ -238,11 +238,12 @@ PYBIND11_MODULE(_ffkernels, m) {
                           uintptr_t st) { pool2d_bwd(pshape(shp), P(dy), P(arg), P(dx), beta, S(st)); });
 
   m.def("blaslt_supported", &blaslt_supported);
+  m.def("blaslt_num_algos", &blaslt_num_algos);
   m.def("blaslt_probe", &blaslt_probe);
   m.def("blaslt_gemm", [](uintptr_t A, uintptr_t B, uintptr_t C, int M, int N, int K, int lda, int ldb, int ldc,
                           bool ta, bool tb, int epi, uintptr_t bias, uintptr_t aux, int aux_ld, float alpha, float beta,
-                          int out_f32, uintptr_t ws, size_t ws_bytes, uintptr_t st) {
+                          int out_f32, uintptr_t ws, size_t ws_bytes, uintptr_t st, int algo) {
     blaslt_gemm(P(A), P(B), P(C), M, N, K, lda, ldb, ldc, ta, tb, epi, P(bias), P(aux), aux_ld, alpha, beta, out_f32,
-                P(ws), ws_bytes, S(st));
+                P(ws), ws_bytes, S(st), algo);
   });
 }

@@ -44,11 +44,16 @@ namespace {
                                std::to_string(static_cast<int>(s_)));                                \
   } while (0)
 
+constexpr int kMaxAlgos = 16;
+
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
-  hipblasLtMatmulAlgo_t algo{};
-  size_t ws_needed = 0;
+  // the heuristic's top candidates: index 0 is the library's pick, the
+  // GEMM autotuner (ops/gemm.py) times the others per shape
+  hipblasLtMatmulAlgo_t algo[kMaxAlgos]{};
+  size_t ws_needed[kMaxAlgos]{};
+  int n_algos = 0;
 };
 
 using Key = std::tuple<int, int, int, int, int, int, bool, bool, int, int, bool, int>;
@@ -105,16 +110,19 @@ Plan& get_plan(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb,
   FFK_BLT(hipblasLtMatmulPreferenceCreate(&pref));
   uint64_t wsb = ws_bytes;
   FFK_BLT(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
-  hipblasLtMatmulHeuristicResult_t res[8];
+  hipblasLtMatmulHeuristicResult_t res[kMaxAlgos];
   int n = 0;
-  FFK_BLT(hipblasLtMatmulAlgoGetHeuristic(handle(), p.desc, p.a, p.b, p.c, p.c, pref, 8, res, &n));
+  FFK_BLT(hipblasLtMatmulAlgoGetHeuristic(handle(), p.desc, p.a, p.b, p.c, p.c, pref, kMaxAlgos, res, &n));
   hipblasLtMatmulPreferenceDestroy(pref);
   if (n <= 0)
     throw std::runtime_error("hipBLASLt: no algorithm for this GEMM / epilogue (M=" + std::to_string(M) +
                              " N=" + std::to_string(N) + " K=" + std::to_string(K) + " epi=" + std::to_string(epi) +
                              ")");
-  p.algo = res[0].algo;
-  p.ws_needed = res[0].workspaceSize;
+  for (int i = 0; i < n && i < kMaxAlgos; ++i) {
+    p.algo[p.n_algos] = res[i].algo;
+    p.ws_needed[p.n_algos] = res[i].workspaceSize;
+    ++p.n_algos;
+  }
   return plans().emplace(key, p).first->second;
 }
 
@@ -164,32 +172,37 @@ int blaslt_probe(int M, int N, int K, bool ta, bool tb, int raw_epi, int bias_t,
   return n;
 }
 
-bool blaslt_supported(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int epi, int out_f32,
-                      bool has_beta, int aux_ld, size_t ws_bytes) {
+int blaslt_num_algos(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int epi, int out_f32,
+                     bool has_beta, int aux_ld, size_t ws_bytes) {
   std::lock_guard<std::mutex> g(mu);
   try {
-    get_plan(M, N, K, lda, ldb, ldc, ta, tb, epi, out_f32, has_beta, aux_ld, ws_bytes);
-    return true;
+    return get_plan(M, N, K, lda, ldb, ldc, ta, tb, epi, out_f32, has_beta, aux_ld, ws_bytes).n_algos;
   } catch (const std::runtime_error&) {
-    return false;
+    return 0;
   }
+}
+
+bool blaslt_supported(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int epi, int out_f32,
+                      bool has_beta, int aux_ld, size_t ws_bytes) {
+  return blaslt_num_algos(M, N, K, lda, ldb, ldc, ta, tb, epi, out_f32, has_beta, aux_ld, ws_bytes) > 0;
 }
 
 void blaslt_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool ta,
                  bool tb, int epi, const void* bias, void* aux, int aux_ld, float alpha, float beta, int out_f32,
-                 void* ws, size_t ws_bytes, hipStream_t st) {
+                 void* ws, size_t ws_bytes, hipStream_t st, int algo) {
   if (M <= 0 || N <= 0 || K <= 0) return;
   if ((epi == EPI_BIAS || epi == EPI_GELU_BIAS) && !bias)
     throw std::invalid_argument("blaslt: epilogue needs a bias");
   if (epi == EPI_BGRADB && !bias) throw std::invalid_argument("blaslt: BGRADB needs its fp32 output vector");
   std::lock_guard<std::mutex> g(mu);
   Plan& p = get_plan(M, N, K, lda, ldb, ldc, ta, tb, epi, out_f32, beta != 0.f, aux_ld, ws_bytes);
-  if (p.ws_needed > ws_bytes) throw std::invalid_argument("blaslt: workspace too small");
+  if (algo < 0 || algo >= p.n_algos) throw std::invalid_argument("blaslt: algorithm index out of range");
+  if (p.ws_needed[algo] > ws_bytes) throw std::invalid_argument("blaslt: workspace too small");
   if (epi != EPI_NONE)
     FFK_BLT(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
   (void)aux;
   (void)aux_ld;
-  FFK_BLT(hipblasLtMatmul(handle(), p.desc, &alpha, B, p.a, A, p.b, &beta, C, p.c, C, p.c, &p.algo, ws, ws_bytes, st));
+  FFK_BLT(hipblasLtMatmul(handle(), p.desc, &alpha, B, p.a, A, p.b, &beta, C, p.c, C, p.c, &p.algo[algo], ws, ws_bytes, st));
 }
 
 }  // namespace ffk

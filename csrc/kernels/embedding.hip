@@ -104,6 +104,34 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const I* __restrict__ id
   }
 }
 
+// Same scatter-add, one wave per gradient row (D >= 64): lane l owns columns
+// l, l+64, ... so every atomic instruction of the wave covers 256 contiguous
+// bytes (two full cache lines) instead of 4-byte pieces of sixteen lines —
+// the L2 atomic units see ~8x fewer requests.
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void embed_bwd_wave_kernel(const I* __restrict__ idx, const T* __restrict__ dout,
+                                                             float* __restrict__ dW, int64_t rows, int L, int D,
+                                                             int mode, int64_t num_entries, int copies) {
+  const int lane = threadIdx.x & 63;
+  const float scale = (mode == 2 && L > 0) ? 1.f / L : 1.f;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+  for (int64_t bj = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); bj < rows; bj += nw) {
+    const int64_t r = static_cast<int64_t>(idx[bj]);
+    if (r < 0 || r >= num_entries) continue;
+    const T* src = dout + (bj / L) * D;
+    float* dst = dW + (static_cast<int64_t>(bj % copies) * num_entries + r) * D;
+    int c = lane;
+    for (; c + 7 * 64 < D; c += 8 * 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = static_cast<float>(src[c + u * 64]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) atomicAdd(dst + c + u * 64, v[u] * scale);
+    }
+    for (; c < D; c += 64) atomicAdd(dst + c, static_cast<float>(src[c]) * scale);
+  }
+}
+
 // dW[i] += sum_c ws[c][i]   (i over num_entries*D, vectorised by 4)
 __global__ __launch_bounds__(256) void embed_reduce_copies_kernel(const float* __restrict__ ws,
                                                                   float* __restrict__ dW, int64_t n4, int copies) {
@@ -140,10 +168,16 @@ void embedding_bwd(int dtype, int index_bits, const void* idx, const void* dout,
   if (copies < 1) copies = 1;
   if (copies > 1 && workspace == nullptr) throw std::invalid_argument("embedding_bwd: copies > 1 needs a workspace");
   float* target = copies > 1 ? workspace : dW;
-  int grid = grid_for(B * L * (D / 8), 256, 256 * 16);
+  const bool wave = D >= 64;
+  int grid = wave ? grid_for(B * L, 4, 256 * 16) : grid_for(B * L * (D / 8), 256, 256 * 16);
 #define FFK_EB(T, I)                                                                                          \
-  hipLaunchKernelGGL((embed_bwd_kernel<T, I>), dim3(grid), dim3(256), 0, st, static_cast<const I*>(idx),      \
-                     static_cast<const T*>(dout), target, B, L, D, mode, num_entries, copies)
+  if (wave)                                                                                                   \
+    hipLaunchKernelGGL((embed_bwd_wave_kernel<T, I>), dim3(grid), dim3(256), 0, st,                           \
+                       static_cast<const I*>(idx), static_cast<const T*>(dout), target, B * L, L, D, mode,   \
+                       num_entries, copies);                                                                  \
+  else                                                                                                        \
+    hipLaunchKernelGGL((embed_bwd_kernel<T, I>), dim3(grid), dim3(256), 0, st, static_cast<const I*>(idx),    \
+                       static_cast<const T*>(dout), target, B, L, D, mode, num_entries, copies)
   if (dtype == kBF16) {
     if (index_bits == 64) FFK_EB(bf16, int64_t);
     else FFK_EB(bf16, int32_t);

@@ -165,8 +165,11 @@ enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU_BIAS = 3, EPI_BGRADB = 4 };
 int blaslt_probe(int M, int N, int K, bool ta, bool tb, int raw_epi, int bias_t, int aux_t, int out_f32);
 bool blaslt_supported(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int epi, int out_f32,
                       bool has_beta, int aux_ld, size_t ws_bytes);
+// number of heuristic candidates (0: unsupported); `algo` picks one of them
+int blaslt_num_algos(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int epi, int out_f32,
+                     bool has_beta, int aux_ld, size_t ws_bytes);
 void blaslt_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool ta,
                  bool tb, int epi, const void* bias, void* aux, int aux_ld, float alpha, float beta, int out_f32,
-                 void* ws, size_t ws_bytes, hipStream_t st);
+                 void* ws, size_t ws_bytes, hipStream_t st, int algo = 0);
 
 }  // namespace ffk

@@ -877,6 +877,45 @@ def _gemm_dims(a, b, trans_a, trans_b):
     return M, N, K
 
 
+def _rowmajor(t, name):
+    if not t.is_cuda or t.dim() != 2 or t.stride(1) != 1 or t.data_ptr() % 16 or t.stride(0) % 8:
+        raise ValueError(f"{name}: expected a 2-D row-major GPU matrix (16-byte aligned rows)")
+    return t.stride(0)
+
+
+def blaslt_num_algos(a, b, trans_a, trans_b, out, beta: float = 0.0, bias_epilogue: bool = False) -> int:
+    """Heuristic candidates hipBLASLt offers for C(out) = op(a) op(b) [+ bias]
+    (row-strided operands allowed); 0 when unsupported."""
+    M, N, K = _gemm_dims(a, b, trans_a, trans_b)
+    odt = torch.bfloat16 if out is None else out.dtype
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or odt not in (torch.bfloat16, torch.float32):
+        return 0
+    try:
+        lda, ldb = _rowmajor(a, "a"), _rowmajor(b, "b")
+        ldc = N if out is None else _rowmajor(out, "out")
+    except ValueError:
+        return 0
+    return ext().blaslt_num_algos(M, N, K, lda, ldb, ldc, bool(trans_a), bool(trans_b),
+                                  EPI_BIAS if bias_epilogue else EPI_NONE, int(odt == torch.float32),
+                                  bool(beta), N, _BLT_WS_BYTES)
+
+
+def blaslt_matmul(a, b, trans_a, trans_b, out, beta: float = 0.0, bias=None, algo: int = 0):
+    """out = op(a) op(b) [+ bias] (+ beta * out) with hipBLASLt's ``algo``-th
+    heuristic candidate; operands may be row-strided views."""
+    M, N, K = _gemm_dims(a, b, trans_a, trans_b)
+    lda, ldb, ldc = _rowmajor(a, "a"), _rowmajor(b, "b"), _rowmajor(out, "out")
+    if tuple(out.shape) != (M, N):
+        raise ValueError("blaslt_matmul: out has the wrong shape")
+    if bias is not None:
+        _check(bias, "bias", torch.bfloat16, N)
+    ext().blaslt_gemm(_p(a), _p(b), _p(out), M, N, K, lda, ldb, ldc, bool(trans_a), bool(trans_b),
+                      EPI_BIAS if bias is not None else EPI_NONE, _p(bias), 0, N, 1.0, float(beta),
+                      int(out.dtype == torch.float32), _p(_blaslt_ws(a.device)), _BLT_WS_BYTES, _stream(), int(algo))
+    STATS["blaslt_gemm"] += 1
+    return out
+
+
 def blaslt_ok(a, b, trans_a=False, trans_b=False, epilogue=EPI_NONE, out_f32=False, beta=0.0) -> bool:
     """True when hipBLASLt has an algorithm for this GEMM + epilogue (cached)."""
     if not (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
@@ -911,6 +950,6 @@ def blaslt_gemm(a, b, trans_a=False, trans_b=False, epilogue=EPI_NONE, bias=None
     ws = _blaslt_ws(a.device)
     ext().blaslt_gemm(_p(a), _p(b), _p(out), M, N, K, a.shape[1], b.shape[1], N, bool(trans_a), bool(trans_b),
                       int(epilogue), _p(bias), _p(aux), N, float(alpha), float(beta), int(out_f32), _p(ws),
-                      _BLT_WS_BYTES, _stream())
+                      _BLT_WS_BYTES, _stream(), 0)
     STATS["blaslt_gemm"] += 1
     return out

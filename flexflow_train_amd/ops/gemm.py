@@ -6,9 +6,12 @@ torch.mm / addmm) is the plain library GEMM.  ``FF_GEMM`` selects:
 
 * ``auto`` (default): time every candidate once per (shape, layout,
   epilogue) signature outside graph capture and keep the fastest — "measure,
-  don't guess".  Candidates: hipBLASLt, the 128² register-staged MFMA kernel,
-  and the 256² LDS-DMA kernel (csrc/kernels/gemm256.hip) at several split-K
-  degrees (the long-K weight-gradient GEMMs are where split-K wins);
+  don't guess".  Candidates: hipBLASLt through torch.mm (its heuristic's first
+  pick), hipBLASLt called directly with each of its top ``FF_GEMM_LT_ALGOS``
+  (default 4) heuristic candidates (``lt:i``, csrc/kernels/blaslt.hip, bias
+  in the library epilogue), the 128² register-staged MFMA kernel, and the
+  256² LDS-DMA kernel (csrc/kernels/gemm256.hip) at several split-K degrees
+  (the long-K weight-gradient GEMMs are where split-K wins);
 * ``hip``: always the MFMA kernel; ``blas``: always hipBLASLt.
 
 On CPU everything is a torch matmul in the compute dtype.
@@ -130,9 +133,45 @@ def _hip256(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
                      splits=splits)
 
 
-def _candidates(a, b, trans_a, trans_b, bias, act, pre):
+def _lt(a, b, trans_a, trans_b, bias, act, out, beta, pre, algo=0):
+    """hipBLASLt called directly with the ``algo``-th heuristic candidate
+    (torch.mm always takes the first); bias in the GEMM epilogue, the
+    activation in the HIP element-wise kernel."""
+    M = a.shape[1] if trans_a else a.shape[0]
+    N = b.shape[0] if trans_b else b.shape[1]
+    if act != "none":
+        u = pre if pre is not None else torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        K.blaslt_matmul(a, b, trans_a, trans_b, u, 0.0, bias, algo)
+        y = K.bias_act_fwd(u, None, act)[0] if N % 8 == 0 else _ACT[act](u)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+        beta = 0.0
+    return K.blaslt_matmul(a, b, trans_a, trans_b, out, beta, bias, algo)
+
+
+_LT_MAX = int(os.environ.get("FF_GEMM_LT_ALGOS", "4"))
+
+
+def _lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre):
+    if _LT_MAX <= 0 or not hasattr(K.ext(), "blaslt_num_algos"):
+        return {}
+    if bias is not None and (bias.dtype != torch.bfloat16 or (out is not None and out.dtype != torch.bfloat16)):
+        return {}
+    if act != "none" and out is not None and out.dtype != torch.bfloat16:
+        return {}
+    target = pre if act != "none" else out
+    n = K.blaslt_num_algos(a, b, trans_a, trans_b, target, beta if act == "none" else 0.0, bias is not None)
+    return {f"lt:{i}": (lambda i_: (lambda *args: _lt(*args, algo=i_)))(i) for i in range(min(n, _LT_MAX))}
+
+
+def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
     """name -> callable(a, b, ta, tb, bias, act, out, beta, pre) tried by the autotuner."""
     c = {"hip": _hip, "blas": _blas}
+    c.update(_lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre))
     if os.environ.get("FF_GEMM256", "1") != "0" and K.gemm256_supported(a, b, trans_a, trans_b):
         M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
         N = b.shape[0] if trans_b else b.shape[1]
@@ -176,9 +215,9 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         return _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre)
     key = (tuple(a.shape), tuple(b.shape), trans_a, trans_b, bias is not None, act,
            None if out is None else out.dtype, bool(beta), pre is not None)
-    cands = _candidates(a, b, trans_a, trans_b, bias, act, pre)
     choice = _CHOICE.get(key)
     if choice is None:
+        cands = _candidates(a, b, trans_a, trans_b, bias, act, pre, out, beta)
         if torch.cuda.is_current_stream_capturing():
             choice = "hip"
         else:
@@ -188,4 +227,15 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
                      for name, fn in cands.items()}
             choice = min(times, key=times.get)
         _CHOICE[key] = choice
-    return cands[choice](a, b, trans_a, trans_b, bias, act, out, beta, pre)
+    return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
+
+
+def _resolve(name: str):
+    if name == "hip":
+        return _hip
+    if name == "blas":
+        return _blas
+    kind, _, arg = name.partition(":")
+    if kind == "lt":
+        return lambda *args: _lt(*args, algo=int(arg))
+    return lambda *args: _hip256(*args, splits=int(arg))

@@ -36,3 +36,40 @@ def test_dw_transposed_with_bias_grad(T, I, O):
 def test_probe_reports_support():
     import flexflow_train_amd._ffkernels as k
     assert k.blaslt_probe(1024, 1024, 512, False, False, 4, 14, -1, 0) > 0   # BIAS, bf16 bias
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
+def test_every_heuristic_candidate_matches(ta, tb):
+    # the GEMM autotuner times hipBLASLt's candidates; each must compute the same
+    # product, including row-strided operand views, fp32 output and beta = 1
+    M, N, Kd = 384, 512, 256
+    a = _r(Kd, M + 8)[:, :M] if ta else _r(M, Kd + 8)[:, :Kd]
+    b = _r(N, Kd) if tb else _r(Kd, N)
+    A = a.float().t() if ta else a.float()
+    B = b.float().t() if tb else b.float()
+    bias = _r(N)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    n = K.blaslt_num_algos(a, b, ta, tb, out, 0.0, True)
+    assert n >= 1
+    for i in range(n):
+        K.blaslt_matmul(a, b, ta, tb, out, 0.0, bias, algo=i)
+        torch.testing.assert_close(out.float(), A @ B + bias.float(), rtol=2e-2, atol=5e-2)
+    acc = torch.ones(M, N, device="cuda")
+    n32 = K.blaslt_num_algos(a, b, ta, tb, acc, 1.0)
+    for i in range(n32):
+        acc.fill_(1.0)
+        K.blaslt_matmul(a, b, ta, tb, acc, 1.0, None, algo=i)
+        torch.testing.assert_close(acc, A @ B + 1.0, rtol=1e-2, atol=2e-2)
+
+
+def test_autotuner_lt_candidate_runs():
+    from flexflow_train_amd.ops import gemm as G
+    a, b, bias = _r(1024, 512), _r(512, 768), _r(768)
+    G._CHOICE.clear()
+    c = G._candidates(a, b, False, False, bias, "gelu", None)
+    lts = [k for k in c if k.startswith("lt:")]
+    assert lts, c.keys()
+    ref = F.gelu(a.float() @ b.float() + bias.float(), approximate="tanh")
+    for k in lts:
+        y = c[k](a, b, False, False, bias, "gelu", None, 0.0, None)
+        torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=5e-2)
