@@ -14,8 +14,12 @@ to the cheapest primitive that implements it:
   * all_reduce over a group — Reduction (sum of partials), the backward of
     Replicate (sum of copy gradients);
   * all_gather over a group — Combine;
-  * batched point-to-point (isend/irecv of the intersecting boxes) — any
-    other view change (different machine views, all-to-all style reshards).
+  * one all_to_all_single with per-rank split sizes — any other view change
+    (resharding to a different dim, DLRM table-sharded -> batch-sharded
+    embeddings, different machine views); each (receiver, sender) pair moves
+    at most one box, zero-size splits for pairs that exchange nothing;
+  * batched point-to-point (isend/irecv of the intersecting boxes) — the
+    fallback (``FF_REDIST_P2P=1``).
 
 Parity: replaces Legion region copies + the NCCL weight-sync-only path of the
 reference (lib/runtime/src/legion_backing.cc:173-257, optimizer_kernel.cu:83);
@@ -24,6 +28,7 @@ SURVEY §2.8 "MI355X-native equivalent".
 from __future__ import annotations
 
 import dataclasses
+import math
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -41,7 +46,7 @@ class DistContext:
         self.world = world
         self.device = device or torch.device("cpu")
         self._groups: Dict[Tuple[int, ...], object] = {}
-        self.stats = {"all_reduce": 0, "all_gather": 0, "p2p": 0, "local": 0, "bytes": 0}
+        self.stats = {"all_reduce": 0, "all_gather": 0, "all_to_all": 0, "p2p": 0, "local": 0, "bytes": 0}
 
     @classmethod
     def from_env(cls, device: Optional[torch.device] = None, backend: Optional[str] = None) -> "DistContext":
@@ -149,7 +154,7 @@ class Contribution:
 
 @dataclasses.dataclass
 class Plan:
-    kind: str                                   # local | all_reduce | all_gather | p2p | none
+    kind: str                                   # local | all_reduce | all_gather | all_to_all | p2p
     contributions: Dict[int, List[Contribution]]
     dst_boxes: Dict[int, Optional[Box]]
     src_boxes: Dict[int, Optional[Box]]
@@ -259,6 +264,13 @@ def make_plan(src: Layout, dst: Layout, world: int) -> Plan:
                 groups.append(g)
     if ok and gdim >= 0:
         return Plan("all_gather", contributions, dst_boxes, src_boxes, groups, gather_dim=gdim)
+    # general resharding (e.g. DLRM's table-sharded embeddings -> batch-sharded
+    # MLP input): every (receiver, sender) pair moves at most one box, so the
+    # whole exchange is ONE all_to_all with per-rank split sizes (RCCL spreads
+    # it over all xGMI links at once) instead of a batch of point-to-point ops
+    pairs = [(r, c.src_rank) for r, cl in contributions.items() for c in cl]
+    if len(pairs) == len(set(pairs)) and os.environ.get("FF_REDIST_P2P", "0") != "1":
+        return Plan("all_to_all", contributions, dst_boxes, src_boxes, [])
     return Plan("p2p", contributions, dst_boxes, src_boxes, [])
 
 
@@ -299,6 +311,8 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
             seen.add(b)
             parts.append(outs[i])
         return torch.cat(parts, dim=plan.gather_dim)
+    if plan.kind == "all_to_all":
+        return _exchange_all_to_all(plan, x, ctx, dst_shape, dtype, device)
     # ---- generic point-to-point
     ctx.stats["p2p"] += 1
     ops = []
@@ -323,6 +337,40 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
             w.wait()
     for c, buf in recv_bufs:
         result[rel_slices(c.part, my_dst)] += buf
+    return result
+
+
+def _exchange_all_to_all(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_shape: Sequence[int],
+                         dtype: torch.dtype, device: torch.device) -> Optional[torch.Tensor]:
+    me, world = ctx.rank, ctx.world
+    my_dst, my_src = plan.dst_boxes.get(me), plan.src_boxes.get(me)
+    ctx.stats["all_to_all"] += 1
+    send = [None] * world
+    for r in range(world):
+        for c in plan.contributions.get(r) or ():
+            if c.src_rank == me:
+                send[r] = x[rel_slices(c.part, my_src)].reshape(-1)
+    recv_c = [None] * world
+    if my_dst is not None:
+        for c in plan.contributions[me]:
+            recv_c[c.src_rank] = c
+    in_sizes = [0 if p is None else p.numel() for p in send]
+    out_sizes = [0 if c is None else math.prod(h - l for l, h in c.part) for c in recv_c]
+    parts = [p for p in send if p is not None and p.numel()]
+    sendbuf = torch.cat(parts) if parts else torch.empty(0, dtype=dtype, device=device)
+    recvbuf = torch.empty(sum(out_sizes), dtype=sendbuf.dtype, device=device)
+    dist.all_to_all_single(recvbuf, sendbuf.to(device), output_split_sizes=out_sizes, input_split_sizes=in_sizes)
+    if my_dst is None:
+        return None
+    result = torch.zeros(dst_shape, dtype=dtype, device=device)
+    off = 0
+    for m in range(world):
+        c = recv_c[m]
+        if c is None:
+            continue
+        n = out_sizes[m]
+        result[rel_slices(c.part, my_dst)] += recvbuf[off:off + n].view([h - l for l, h in c.part]).to(dtype)
+        off += n
     return result
 
 
