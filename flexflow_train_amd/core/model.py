@@ -522,6 +522,9 @@ class FFModel:
         self.metrics = [normalize_metric(m) for m in (metrics or [])]
         cuda = torch.cuda.is_available() and not self.ffconfig.cpu_only and not self.ffconfig.local_execution
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if cuda and local_rank >= torch.cuda.device_count():
+            # more ranks than GPUs (gloo rehearsal of a multi-GPU run on one card)
+            local_rank %= torch.cuda.device_count()
         device = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
         if cuda:
             torch.cuda.set_device(device)

@@ -53,6 +53,7 @@ class DistContext:
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         if world > 1 and not dist.is_initialized():
+            backend = backend or os.environ.get("FF_DIST_BACKEND") or None
             if backend is None:
                 backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
             kw = {}
