@@ -20,10 +20,13 @@ through PyTorch (the weight is viewed back to OIHW).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from .. import kernels as K
+from . import gemm as G
 from .base import OpImpl, acc_grad, register
 
 _ACTS = {"none": lambda t: t, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
@@ -34,6 +37,38 @@ def _geom(ctx):
     return ((int(ctx.a("stride_h", 1)), int(ctx.a("stride_w", 1))),
             (int(ctx.a("padding_h", 0)), int(ctx.a("padding_w", 0))),
             int(ctx.a("groups", 1)), ctx.a("activation", "none"))
+
+
+_CHOICE = {}
+
+
+def _pick(key, cands):
+    """Per-shape choice between the implicit-GEMM kernels and a library GEMM
+    (1x1 stride-1 convolutions are plain GEMMs over NHWC pixels): each
+    candidate runs once untimed, then the faster of two timed repeats wins —
+    outside graph capture; under capture the native kernel is used."""
+    c = _CHOICE.get(key)
+    if c is None:
+        if len(cands) == 1 or torch.cuda.is_current_stream_capturing() or _MODE != "auto":
+            c = "gemm" if (_MODE == "gemm" and "gemm" in cands) else "native"
+        else:
+            from .gemm import _time
+            times = {name: _time(fn, iters=3) for name, fn in cands.items()}
+            c = min(times, key=times.get)
+        _CHOICE[key] = c
+    return c
+
+
+_MODE = os.environ.get("FF_CONV1X1", "auto")   # auto | native | gemm
+
+
+def _pointwise(R, S, stride, pad, groups) -> bool:
+    return R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and groups == 1
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """channels_last [N, C, H, W] -> its [N*H*W, C] row-major view (no copy)."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
 
 
 def _oihw(W: torch.Tensor) -> torch.Tensor:
@@ -83,7 +118,22 @@ class Conv2DOp(OpImpl):
             if ctx.extra.get("emit_bn_stats"):
                 stats = torch.empty(2 * Kc, device=x.device, dtype=torch.float32)
             bias = None if b is None else b.to(torch.bfloat16).contiguous()
-            y = K.conv2d_fwd(xin, wp, bias, stride, pad, act=act, stats=stats)
+            if _pointwise(R, S, stride, pad, groups) and C % 8 == 0:
+                def via_gemm(st=stats):
+                    y2 = G.matmul(_rows(xin), wp.view(Kc, C), trans_b=True, bias=bias, act=act)
+                    yv = y2.view(x.shape[0], x.shape[2], x.shape[3], Kc).permute(0, 3, 1, 2)
+                    if st is not None:
+                        st.zero_()
+                        K.bn_stats(yv, st)
+                    return yv
+                key = ("fwd", tuple(xin.shape), Kc, act, bias is not None, stats is not None)
+                scratch = None if stats is None else torch.empty_like(stats)
+                choice = _pick(key, {"native": lambda: K.conv2d_fwd(xin, wp, bias, stride, pad, act=act,
+                                                                   stats=scratch),
+                                     "gemm": lambda: via_gemm(scratch)})
+                y = via_gemm() if choice == "gemm" else K.conv2d_fwd(xin, wp, bias, stride, pad, act=act, stats=stats)
+            else:
+                y = K.conv2d_fwd(xin, wp, bias, stride, pad, act=act, stats=stats)
             if stats is not None:
                 y._ff_bn_stats = stats
             return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape))
@@ -131,7 +181,18 @@ class Conv2DOp(OpImpl):
             K.colsum_act(d2, None, "none", weight_grads[1], write_dx=False)
         dW = weight_grads[0]
         if dW is not None:
-            if Cp == xshape[1]:
+            if Cp == xshape[1] and _pointwise(R, S, stride, pad, 1):
+                key = ("wgrad", tuple(xin.shape), Kc)
+                if key not in _CHOICE:
+                    tmp = torch.zeros_like(dW.view(-1))
+                    _pick(key, {"native": lambda: K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad),
+                                "gemm": lambda: G.matmul(_rows(dy), _rows(xin), trans_a=True, out=tmp.view(Kc, Cp),
+                                                         beta=1.0)})
+                if _CHOICE[key] == "gemm":
+                    G.matmul(_rows(dy), _rows(xin), trans_a=True, out=dW.view(Kc, Cp), beta=1.0)
+                else:
+                    K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
+            elif Cp == xshape[1]:
                 K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
             else:  # padded stem: wgrad into a padded buffer, keep the real channels
                 tmp = torch.zeros(Kc * R * S * Cp, device=dy.device, dtype=torch.float32)
@@ -143,8 +204,24 @@ class Conv2DOp(OpImpl):
             dx = K.conv2d_dgrad(dy, wp, (xshape[0], Cp, xshape[2], xshape[3]), stride, pad)
             return [dx[:, :xshape[1]]]
         acc = ctx.extra.get("grad_acc", [None])[0]
-        if (acc is not None and acc.is_cuda and acc.dtype == torch.bfloat16 and tuple(acc.shape) == tuple(xshape)
-                and acc.is_contiguous(memory_format=torch.channels_last)):
+        use_acc = (acc is not None and acc.is_cuda and acc.dtype == torch.bfloat16 and tuple(acc.shape) == tuple(xshape)
+                   and acc.is_contiguous(memory_format=torch.channels_last))
+        if _pointwise(R, S, stride, pad, 1):
+            def dgrad_gemm(out):
+                if out is not None:
+                    G.matmul(_rows(dy), wp.view(Kc, Cp), out=_rows(out), beta=1.0)
+                    return out
+                dx2 = G.matmul(_rows(dy), wp.view(Kc, Cp))
+                return dx2.view(xshape[0], xshape[2], xshape[3], Cp).permute(0, 3, 1, 2)
+            key = ("dgrad", tuple(xshape), Kc, use_acc)
+            if key not in _CHOICE:
+                tmp = acc.clone() if use_acc else None
+                _pick(key, {"native": lambda: K.conv2d_dgrad(dy, wp, xshape, stride, pad, out=tmp,
+                                                             beta=1.0 if use_acc else 0.0),
+                            "gemm": lambda: dgrad_gemm(tmp)})
+            if _CHOICE[key] == "gemm":
+                return [dgrad_gemm(acc if use_acc else None)]
+        if use_acc:
             K.conv2d_dgrad(dy, wp, xshape, stride, pad, out=acc, beta=1.0)
             return [acc]
         return [K.conv2d_dgrad(dy, wp, xshape, stride, pad)]

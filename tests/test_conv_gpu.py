@@ -187,3 +187,45 @@ def test_resnet_gpu_step_matches_cpu_fp32():
     for name in ("conv2d_dgrad", "conv2d_wgrad", "bn_bwd", "pool2d_bwd"):
         assert K.STATS[name] > before.get(name, 0), f"{name} did not run on the HIP path"
     assert np.isfinite(ex.perf_metrics().loss)
+
+
+@pytest.mark.parametrize("mode", ["native", "gemm"])
+@pytest.mark.parametrize("C,Ko,acc", [(64, 256, False), (256, 64, True)])
+def test_pointwise_conv_paths(mode, C, Ko, acc):
+    """1x1 stride-1 convolutions: the implicit-GEMM kernels and the library
+    GEMM path (ops/conv.py picks per shape) both match fp32 — forward with the
+    BN statistics, dgrad (fresh or accumulated) and the accumulated wgrad."""
+    from flexflow_train_amd.ops import conv as CV
+    from flexflow_train_amd.ops.base import OpContext
+
+    old = CV._MODE
+    CV._MODE, CV._CHOICE = mode, {}
+    try:
+        N, H = 4, 14
+        x = _rand_nhwc((N, C, H, H))
+        W = (torch.randn(Ko, 1, 1, C, device="cuda") * 0.1).to(torch.bfloat16)   # physical [K, R, S, C]
+        ctx = OpContext("CONV2D", {"kernel_h": 1, "kernel_w": 1}, "c", device=torch.device("cuda"),
+                        compute_dtype=torch.bfloat16)
+        ctx.extra["emit_bn_stats"] = True
+        op = CV.Conv2DOp()
+        Wl = W.view(Ko, 1, 1, C).reshape(Ko, C, 1, 1)  # logical-shaped piece over the physical data
+        (y,), saved = op.forward(ctx, [x], [Wl])
+        ref = F.conv2d(x.float(), W.float().permute(0, 3, 1, 2))
+        torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+        st = y._ff_bn_stats
+        torch.testing.assert_close(st[:Ko], y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+        dy = _rand_nhwc(tuple(y.shape))
+        dW = torch.full((Ko * C,), 0.5, device="cuda")
+        if acc:
+            base = _rand_nhwc(tuple(x.shape))
+            ctx.extra["grad_acc"] = [base.clone()]
+        (dx,) = op.backward(ctx, saved, [dy], [dW], [True])
+        xr = x.float().requires_grad_(True)
+        wr = W.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+        F.conv2d(xr, wr).backward(dy.float())
+        want_dx = xr.grad + (base.float() if acc else 0)
+        torch.testing.assert_close(dx.float(), want_dx, rtol=2e-2, atol=5e-2)
+        torch.testing.assert_close(dW.view(Ko, C), wr.grad.view(Ko, C) + 0.5, rtol=1e-2, atol=5e-2)
+        assert set(CV._CHOICE.values()) == {mode}
+    finally:
+        CV._MODE, CV._CHOICE = old, {}

@@ -64,6 +64,15 @@ def main():
         m_b = timeit(lambda: torch.autograd.grad(out, (xr, wr), dy, retain_graph=True))
         P = y.shape[2]
         fl = 2.0 * N * P * P * Ko * R * R * C
+        lib = {}
+        if R == 1 and st == 1:  # a 1x1 stride-1 NHWC conv is a plain GEMM: time hipBLASLt on it
+            x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+            w2 = w.reshape(Ko, C)
+            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, Ko)
+            dwf = torch.empty(Ko, C, device="cuda")
+            lib = {"blas_fwd_ms": round(timeit(lambda: x2 @ w2.t()), 4),
+                   "blas_dgrad_ms": round(timeit(lambda: dy2 @ w2), 4),
+                   "blas_wgrad_ms": round(timeit(lambda: torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=dwf)), 4)}
         ours = t_f + t_d + t_w
         tot["ours"] += cnt * ours
         tot["miopen"] += cnt * (m_f + m_b)
@@ -71,7 +80,7 @@ def main():
                           "fwd_ms": round(t_f, 4), "dgrad_ms": round(t_d, 4), "wgrad_ms": round(t_w, 4),
                           "fwd_tflops": round(fl / t_f / 1e9, 1), "dgrad_tflops": round(fl / t_d / 1e9, 1),
                           "wgrad_tflops": round(fl / t_w / 1e9, 1),
-                          "miopen_fwd_ms": round(m_f, 4), "miopen_bwd_ms": round(m_b, 4)}), flush=True)
+                          "miopen_fwd_ms": round(m_f, 4), "miopen_bwd_ms": round(m_b, 4), **lib}), flush=True)
     print(json.dumps({"bench": "conv_total_resnet50", "batch": N, "ours_ms": round(tot["ours"], 3),
                       "miopen_ms": round(tot["miopen"], 3)}), flush=True)
 
