@@ -207,8 +207,8 @@ PYBIND11_MODULE(_ffkernels, m) {
                             uintptr_t st) { conv2d_dgrad(cshape(shp), P(dy), P(w), P(dx), beta, S(st)); });
   m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws, int splits,
                             uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), F(ws), splits, S(st)); });
-  m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st) {
-    bn_stats(P(x), F(stats), M, C, S(st));
+  m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st, uintptr_t ws) {
+    bn_stats(P(x), F(stats), M, C, S(st), F(ws));
   });
   m.def("bn_finalize", [](uintptr_t stats, uintptr_t g, uintptr_t b, int pdt, uintptr_t rm, uintptr_t rv,
                           uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t rstd, int C, double count,
@@ -220,8 +220,9 @@ PYBIND11_MODULE(_ffkernels, m) {
                        int relu, uintptr_t st) { bn_apply(P(x), P(res), F(scale), F(shift), P(y), M, C, relu, S(st)); });
   m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t g, int pdt,
                      uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, uintptr_t ws, int64_t M, int C,
-                     int relu, uintptr_t st) {
-    bn_bwd(P(dy), P(x), P(y), F(mean), F(rstd), P(g), pdt, P(dx), P(dres), F(dg), F(db), F(ws), M, C, relu, S(st));
+                     int relu, uintptr_t st, uintptr_t ss) {
+    bn_bwd(P(dy), P(x), P(y), F(mean), F(rstd), P(g), pdt, P(dx), P(dres), F(dg), F(db), F(ws), M, C, relu, S(st),
+           F(ss));
   });
   // pool geometry: [N,H,W,C,R,S,sh,sw,ph,pw,avg,count_pad]
   auto pshape = [](const std::vector<int>& v) {

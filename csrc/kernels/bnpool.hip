@@ -72,14 +72,15 @@ template <int MODE>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                         const bf16* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ out,
-                                                        int64_t M, int C, int GL, int relu) {
+                                                        int64_t M, int C, int GL, int relu,
+                                                        const float* __restrict__ ss, int nbuckets) {
   __shared__ float red[2][256 * 8 + 8];
   const int RL = 256 / GL;
   const int gl = threadIdx.x % GL, rl = threadIdx.x / GL;
   const int grp = blockIdx.y * GL + gl;
   const bool gok = grp * 8 < C;
   const int c0 = grp * 8;
-  float a[8], b[8], mu[8], rs[8];
+  float a[8], b[8], mu[8], rs[8], sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) a[i] = b[i] = 0.f;
   if (MODE == 1 && gok) {
@@ -87,6 +88,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__
     for (int i = 0; i < 8; ++i) {
       mu[i] = mean[c0 + i];
       rs[i] = rstd[c0 + i];
+      sc[i] = relu == 2 ? ss[c0 + i] : 0.f;
+      sh[i] = relu == 2 ? ss[C + c0 + i] : 0.f;
     }
   }
   if (gok) {
@@ -103,11 +106,14 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__
       } else {
         float g[8];
         load8(dy + off, g);
-        if (relu) {
+        if (relu == 1) {
           float yv[8];
           load8(y + off, yv);
 #pragma unroll
           for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+        } else if (relu == 2) {  // ReLU mask recomputed from x (the forward's y is not re-read)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[i] = xv[i] * sc[i] + sh[i] > 0.f ? g[i] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -130,9 +136,9 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__
     float s = 0.f;
     for (int l = 0; l < RL; ++l) s += red[q][(l * GL + lg) * 8 + e];
     const int ch = blockIdx.y * GL * 8 + col;
-    // MODE 1 spreads blocks over kBnBuckets copies of [2][C] (the coefficient
-    // kernel sums them): a few hundred same-address atomics, not thousands
-    float* dst = MODE == 1 ? out + static_cast<int64_t>(blockIdx.x % kBnBuckets) * 2 * C : out;
+    // blocks spread over `nbuckets` copies of [2][C] (the consumer sums them):
+    // a few hundred same-address atomics, not thousands
+    float* dst = out + static_cast<int64_t>(blockIdx.x % nbuckets) * 2 * C;
     if (ch < C) atomicAdd(dst + q * C + ch, s);
   }
 }
@@ -216,7 +222,8 @@ __global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ y, const float* __restrict__ coef,
                                                            bf16* __restrict__ dx, bf16* __restrict__ dres,
-                                                           int64_t nvec, int C, int relu) {
+                                                           int64_t nvec, int C, int relu,
+                                                           const float* __restrict__ ss) {
   for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvec;
        v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t off = v * 8;
@@ -224,11 +231,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     float g[8], xv[8];
     load8(dy + off, g);
     load8(x + off, xv);
-    if (relu) {
+    if (relu == 1) {
       float yv[8];
       load8(y + off, yv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+    } else if (relu == 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 s4 = *reinterpret_cast<const f32x4*>(ss + c0 + 4 * h);
+        const f32x4 h4 = *reinterpret_cast<const f32x4*>(ss + C + c0 + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[4 * h + i] = xv[4 * h + i] * s4[i] + h4[i] > 0.f ? g[4 * h + i] : 0.f;
+      }
     }
     if (dres) store8(dres + off, g);
 #pragma unroll
@@ -367,14 +382,25 @@ int ew_blocks(int64_t n) { return static_cast<int>(std::min<int64_t>((n + 255) /
 
 }  // namespace
 
-void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st) {
+__global__ void bn_fold_buckets_kernel(const float* __restrict__ ws, float* __restrict__ stats, int C2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C2) return;
+  float s = 0.f;
+  for (int k = 0; k < kBnBuckets; ++k) s += ws[static_cast<int64_t>(k) * C2 + c];
+  stats[c] += s;
+}
+
+void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws) {
   if (C % 8) throw std::invalid_argument("bn_stats: C must be a multiple of 8");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
   dim3 grid = red_grid(r, M);
-  grid.x = std::min(grid.x, 256u);  // single [2][C] target: bound the same-address atomics
+  if (!ws) grid.x = std::min(grid.x, 256u);  // single [2][C] target: bound the same-address atomics
+  else (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
   hipLaunchKernelGGL((bn_reduce_kernel<0>), grid, dim3(256), 0, st, static_cast<const bf16*>(x), nullptr,
-                     nullptr, nullptr, nullptr, stats, M, C, r.GL, 0);
+                     nullptr, nullptr, nullptr, ws ? ws : stats, M, C, r.GL, 0, nullptr, ws ? kBnBuckets : 1);
+  if (ws)
+    hipLaunchKernelGGL(bn_fold_buckets_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, ws, stats, 2 * C);
   FFK_LAUNCH_CHECK("bn_stats");
 }
 
@@ -398,20 +424,23 @@ void bn_apply(const void* x, const void* residual, const float* scale, const flo
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
-            int relu, hipStream_t st) {
+            int relu, hipStream_t st, const float* scale_shift) {
   if (C % 8) throw std::invalid_argument("bn_bwd: C must be a multiple of 8");
+  if (relu == 1 && !y) throw std::invalid_argument("bn_bwd: ReLU mask from y needs y");
+  if (relu == 2 && !scale_shift) throw std::invalid_argument("bn_bwd: ReLU mask from x needs the scale / shift");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
   (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
   hipLaunchKernelGGL((bn_reduce_kernel<1>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x),
-                     static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean, rstd, ws, M, C, r.GL, relu);
+                     static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean, rstd, ws, M, C, r.GL, relu,
+                     scale_shift, kBnBuckets);
   float* coef = ws + 2 * C * kBnBuckets;
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, mean, rstd, gamma,
                      param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M));
   const int64_t nvec = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, st, static_cast<const bf16*>(dy),
                      static_cast<const bf16*>(x), static_cast<const bf16*>(y), coef, static_cast<bf16*>(dx),
-                     static_cast<bf16*>(dres), nvec, C, relu);
+                     static_cast<bf16*>(dres), nvec, C, relu, scale_shift);
   FFK_LAUNCH_CHECK("bn_bwd");
 }
 

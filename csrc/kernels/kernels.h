@@ -139,17 +139,20 @@ void conv2d_wgrad(const ConvShape& s, const void* x, const void* dy, float* dw, 
                   hipStream_t st);
 
 // ---- bnpool.hip: BatchNorm (training) + pooling over NHWC bf16 [M][C]
-void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st);
+// ws (optional, 32*C floats): 16 atomic buckets -> full-grid reduction (else the grid is capped)
+void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws = nullptr);
 void bn_finalize(const float* stats, const void* gamma, const void* beta, int param_dtype, float* running_mean,
                  float* running_var, float* scale, float* shift, float* mean, float* rstd, int C, double count,
                  float momentum, float eps, hipStream_t st);
 void bn_apply(const void* x, const void* residual, const float* scale, const float* shift, void* y, int64_t M, int C,
               int relu, hipStream_t st);
 // ws: 35*C floats (16 partial [2][C] buckets + 3C coefficients); dgamma / dbeta (fp32) accumulate; dres (optional) = dy
-// masked by the ReLU (the residual branch's gradient of relu(bn(x) + res))
+// masked by the ReLU (the residual branch's gradient of relu(bn(x) + res)).
+// relu: 0 none, 1 mask from y, 2 mask recomputed from x with the forward's
+// scale_shift ([2][C]: scale, shift) — y is not read
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
-            int relu, hipStream_t st);
+            int relu, hipStream_t st, const float* scale_shift = nullptr);
 struct PoolShape {
   int N = 0, H = 0, W = 0, C = 0, R = 1, S = 1, sh = 1, sw = 1, ph = 0, pw = 0;
   int avg = 0, count_pad = 0;

@@ -760,7 +760,8 @@ def bn_stats(x, stats):
     _check_nhwc(x, "x")
     C = x.shape[1]
     _check(stats, "stats", torch.float32, 2 * C)
-    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream())
+    ws = torch.empty(32 * C, device=x.device, dtype=torch.float32)
+    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream(), _p(ws))
     STATS["bn_stats"] += 1
 
 
@@ -798,13 +799,21 @@ def bn_apply(x, scale, shift, relu: bool, residual=None):
     return y
 
 
-def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, want_masked: bool = False):
-    """-> (dx, masked dy or None)."""
+def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, want_masked: bool = False,
+           scale_shift=None):
+    """-> (dx, masked dy or None).  With ``relu`` the mask comes from ``y``,
+    or — when ``y`` is None — is recomputed from ``x`` with the forward's
+    ``scale_shift`` (fp32 [2, C]: scale, shift), so y is never re-read."""
     _check_nhwc(dy, "dy")
     _check_nhwc(x, "x")
-    if relu:
-        _check_nhwc(y, "y")
     C = x.shape[1]
+    relu_code = 0
+    if relu and y is not None:
+        _check_nhwc(y, "y")
+        relu_code = 1
+    elif relu:
+        _check(scale_shift, "scale_shift", torch.float32, 2 * C)
+        relu_code = 2
     for name, t in (("dgamma", dgamma), ("dbeta", dbeta)):
         if t is not None and (t.dtype != torch.float32 or t.numel() != C or not t.is_contiguous()):
             raise ValueError(f"bn_bwd: {name} must be fp32 [{C}]")
@@ -812,8 +821,9 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, wan
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     dres = torch.empty_like(x, memory_format=torch.channels_last) if want_masked else None
     ws = torch.empty(35 * C, device=x.device, dtype=torch.float32)
-    ext().bn_bwd(_p(dy), _p(x), _p(y if relu else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx), _p(dres),
-                 _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, int(relu), _stream())
+    ext().bn_bwd(_p(dy), _p(x), _p(y if relu_code == 1 else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx),
+                 _p(dres), _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, relu_code, _stream(),
+                 _p(scale_shift if relu_code == 2 else None))
     STATS["bn_bwd"] += 1
     return dx, dres
 

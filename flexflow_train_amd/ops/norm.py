@@ -140,7 +140,13 @@ class BatchNormOp(OpImpl):
                 scale = (gf * rstd).contiguous()
                 shift = (bf - mean * gf * rstd).contiguous()
             y = K.bn_apply(xin, scale, shift, relu, residual=None if res is None else K.nhwc(res))
-            return [y], ("hip", xin, y if relu else None, mean, rstd, g, relu, fused)
+            ss = None
+            if relu and not fused and ctx.training:
+                # backward recomputes the ReLU mask from x (scale / shift are
+                # rows 0 and 1 of bn_finalize's [4, C] buffer): y is not kept
+                assert shift.data_ptr() == scale.data_ptr() + 4 * C
+                ss = torch.as_strided(scale, (2 * C,), (1,))
+            return [y], ("hip", xin, y if (relu and ss is None) else None, mean, rstd, g, relu, fused, ss)
         train = ctx.training
         xf = x.float()
         y = torch.nn.functional.batch_norm(
@@ -158,9 +164,10 @@ class BatchNormOp(OpImpl):
         dg = weight_grads[0] if weight_grads else None
         db = weight_grads[1] if len(weight_grads) > 1 else None
         if saved[0] == "hip":
-            _, xin, y, mean, rstd, g, relu, fused = saved
+            _, xin, y, mean, rstd, g, relu, fused, ss = saved
             dyn = K.nhwc(dy.to(torch.bfloat16))
-            dx, dres = K.bn_bwd(dyn, xin, y, mean, rstd, g, relu, dgamma=dg, dbeta=db, want_masked=fused)
+            dx, dres = K.bn_bwd(dyn, xin, y, mean, rstd, g, relu, dgamma=dg, dbeta=db, want_masked=fused,
+                                scale_shift=ss)
             return [dx, dres] if fused else [dx]
         _, x, res, g, b, relu = saved
         eps = float(ctx.a("eps", 1e-5))

@@ -108,6 +108,14 @@ def test_batchnorm_fwd_bwd(C, relu, residual):
     torch.testing.assert_close(db, br.grad, rtol=2e-2, atol=0.5)
     if residual:
         torch.testing.assert_close(dres.float(), rr.grad, rtol=1e-2, atol=1e-2)
+    if relu and not residual:
+        # ReLU mask recomputed from x with the forward's scale / shift: same result, y unread
+        ss = torch.stack([scale, shift]).reshape(-1)
+        dg2, db2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        dx2, _ = K.bn_bwd(dy, x, None, mean, rstd, g, True, dgamma=dg2, dbeta=db2, scale_shift=ss)
+        torch.testing.assert_close(dx2.float(), dx.float(), rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(dg2, dg, rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(db2, db, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("k,s,p,avg", [((3, 3), (2, 2), (1, 1), False), ((2, 2), (2, 2), (0, 0), False),

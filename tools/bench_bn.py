@@ -26,11 +26,15 @@ def main():
         y = K.bn_apply(x, scale, shift, True)
         t_apply_res = timeit(lambda: K.bn_apply(x, scale, shift, True, residual=dy))
         t_bwd = timeit(lambda: K.bn_bwd(dy, x, y, mean, rstd, g, True))
+        ss = torch.stack([scale, shift]).reshape(-1)
+        t_bwd_x = timeit(lambda: K.bn_bwd(dy, x, None, mean, rstd, g, True, scale_shift=ss))
         print(json.dumps({"bench": "batchnorm", "shape": [N, C, H, H], "MB": round(nb / 1e6, 1),
                           "stats_ms": round(t_stats, 4), "stats_GBps": round(nb / t_stats / 1e6, 1),
                           "apply_ms": round(t_apply, 4), "apply_GBps": round(2 * nb / t_apply / 1e6, 1),
                           "apply_res_GBps": round(3 * nb / t_apply_res / 1e6, 1),
-                          "bwd_ms": round(t_bwd, 4), "bwd_GBps": round(7 * nb / t_bwd / 1e6, 1)}), flush=True)
+                          "bwd_ms": round(t_bwd, 4), "bwd_GBps": round(7 * nb / t_bwd / 1e6, 1),
+                          "bwd_mask_from_x_ms": round(t_bwd_x, 4),
+                          "bwd_mask_from_x_GBps": round(5 * nb / t_bwd_x / 1e6, 1)}), flush=True)
     s = torch.empty(1 << 28, device="cuda", dtype=torch.bfloat16)
     d = torch.empty_like(s)
     t = timeit(lambda: d.copy_(s))
