@@ -817,12 +817,18 @@ class Executor:
             g = self.redist(g, want.dual(), lay.dual(), g.dtype, self.cfg.device)
         return g
 
-    def backward(self, dlogits: Optional[torch.Tensor]):
+    def backward(self, dlogits: Optional[torch.Tensor], zero_grads: bool = True, accumulate: bool = False,
+                 sync: bool = True):
+        """Reverse pass.  Micro-batching (``train_step_pipelined``) calls it
+        once per micro-batch: ``zero_grads`` only for the first, ``accumulate``
+        (every dW adds, beta = 1) for the rest, ``sync`` (bucketed gradient
+        all-reduces overlapped with this pass) only for the last."""
         grads: Dict[Value, torch.Tensor] = {}
         if dlogits is not None:
             grads[self.loss_value] = dlogits
         for f in self.flats:
-            f["grad"].zero_()
+            if zero_grads:
+                f["grad"].zero_()
             for b in f["buckets"]:
                 b["pending"] = sum(1 for p in b["params"] if p.trainable)
         self._works = []
@@ -860,7 +866,8 @@ class Executor:
                     # sole-consumer weights may be overwritten (beta = 0) by their dW GEMM;
                     # shared ones accumulate.  Existing input grads are offered for in-place
                     # accumulation (ops return the same tensor when they used it).
-                    s.ctx.extra["wgrad_beta"] = [0.0 if p.n_consumers == 1 else 1.0 for p in s.weights]
+                    s.ctx.extra["wgrad_beta"] = [0.0 if (p.n_consumers == 1 and not accumulate) else 1.0
+                                                 for p in s.weights]
                     s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
                     impl = opbase.get_impl(s.op_type)
                     t0 = self.tracer.begin(f"{s.name}:bwd", "compute", self.step_num) if prof else None
@@ -869,12 +876,14 @@ class Executor:
                     for v, g, nd in zip(s.inputs, gins, need):
                         if g is not None and nd:
                             self._acc(grads, v, g)
-            for p in s.weights:
-                if p.final_step == i and p.trainable:
-                    self._param_done(p)
+            if sync:
+                for p in s.weights:
+                    if p.final_step == i and p.trainable:
+                        self._param_done(p)
         self._saved = {}
         self._env = {}
-        self._finish_grad_sync()
+        if sync:
+            self._finish_grad_sync()
 
     def _acc(self, grads, v, g):
         if g is None:
@@ -990,6 +999,36 @@ class Executor:
         self.forward(feeds, training=True)
         g = self.compute_loss(labels)
         self.backward(g)
+        self.update(lr)
+
+    def train_step_pipelined(self, feeds_list: Sequence[Dict[str, torch.Tensor]], labels_list: Sequence[torch.Tensor],
+                             lr: Optional[float] = None):
+        """One optimizer step over ``len(feeds_list)`` micro-batches (each of
+        the compiled batch shape), GPipe order: every forward, then every
+        backward in reverse, gradients accumulated, one synchronisation + update.
+
+        With a strategy that places consecutive layers on disjoint device
+        blocks (machine views = pipeline stages), every rank walks the same
+        step list, so stage s runs micro-batch i+1's forward while stage s+1
+        runs micro-batch i's (the stage-boundary transfers are the only
+        rendezvous) — pipeline parallelism with the fill / drain bubble of
+        GPipe; with one stage it is plain gradient accumulation.  The loss
+        gradient of each micro-batch is scaled by 1/m, so the update equals
+        the one of a single batch m times larger."""
+        m = len(feeds_list)
+        if m == 0 or m != len(labels_list):
+            raise ValueError("train_step_pipelined: need one label tensor per micro-batch")
+        stash = []
+        for f, lab in zip(feeds_list, labels_list):
+            self.forward(f, training=True)
+            g = self.compute_loss(lab)
+            if g is not None and m > 1:
+                g = g / m
+            stash.append((self._saved, self._env, g))
+        for i in range(m - 1, -1, -1):
+            self._saved, self._env, g = stash[i]
+            stash[i] = None
+            self.backward(g, zero_grads=(i == m - 1), accumulate=(i != m - 1), sync=(i == 0))
         self.update(lr)
 
     def make_graphed_train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, warmup: int = 2):

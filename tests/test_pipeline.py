@@ -1,0 +1,113 @@
+"""Pipeline parallelism (GPipe micro-batching, Executor.train_step_pipelined):
+the MLP's layers split over two pipeline stages (machine views on rank 0 and
+rank 1, 2 gloo ranks) and trained on 2 micro-batches must match one
+single-process step on the whole batch; on one rank the same call is plain
+gradient accumulation."""
+import json
+import os
+import tempfile
+
+import torch
+import torch.multiprocessing as mp
+
+import dist_models as M
+from dist_util import assert_params_close, free_port, run_single
+from flexflow_train_amd.core import ActiMode, DataType
+
+
+def mlp8(m):
+    x = m.create_tensor([8, 32], DataType.DT_FLOAT, name="x")
+    t = m.dense(x, 64, ActiMode.AC_MODE_RELU, name="fc0")
+    t = m.dense(t, 48, name="fc1")
+    t = m.relu(t, name="act1")
+    t = m.dense(t, 8, name="out")
+    m.softmax(t, name="sm")
+
+
+def _micro():
+    feeds, labels = _full()
+    return [{"x": feeds["x"][:8]}, {"x": feeds["x"][8:]}], [labels[:8], labels[8:]]
+
+
+def _full():
+    g = torch.Generator().manual_seed(7)
+    return {"x": torch.randn(16, 32, generator=g)}, torch.randint(0, 8, (16,), generator=g)
+
+
+def _build(strategy_file=None, seed=0):
+    from flexflow_train_amd.core import FFConfig, FFModel, LossType, MetricsType, SGDOptimizer
+
+    cfg = FFConfig()
+    cfg.seed = seed
+    if strategy_file:
+        cfg.import_strategy_file = strategy_file
+    else:
+        cfg.only_data_parallel = True
+    model = FFModel(cfg)
+    mlp8(model)
+    model.compile(optimizer=SGDOptimizer(model, lr=0.05), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY])
+    ex = model.executor
+    g = torch.Generator().manual_seed(seed)
+    for name in sorted(ex.parameter_names()):
+        ex.set_parameter(name, torch.randn(ex.get_parameter(name).shape, generator=g) * 0.2)
+    return ex
+
+
+def _train(ex, steps=2):
+    feeds, labels = _micro()
+    for _ in range(steps):
+        ex.train_step_pipelined(feeds, labels)
+    return {n: ex.get_parameter(n).detach().cpu().clone() for n in sorted(ex.parameter_names())}
+
+
+def _stage_strategy(path):
+    """Every layer unsharded; x, fc0, fc1 (and their weights) on rank 0, the rest on rank 1."""
+    from flexflow_train_amd import _ffcore as C
+    from flexflow_train_amd.core import FFConfig, FFModel
+    from flexflow_train_amd.search.strategy import export_strategy
+
+    m = FFModel(FFConfig())
+    mlp8(m)
+    s = json.loads(C.data_parallel_strategy(m.cg, 2))
+    for v in s.values():
+        v["batch"] = 1
+    pcg, _, _ = C.lower_strategy(m.cg, json.dumps(s), 2)
+    views = {}
+    for n in pcg.topo_order():
+        name = pcg.layer_name(n).split(".")[0]
+        views[n] = (0, 1) if name in ("x", "fc0", "fc1") else (1, 1)
+    export_strategy(path, pcg, views, {"world": 2, "source": "test"})
+
+
+def _worker(rank, world, port, strategy, out):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    ex = _build(strategy)
+    params = _train(ex)
+    if rank == 0:
+        torch.save({"params": params, "stats": dict(ex.dist.stats)}, out)
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gradient_accumulation_matches_full_batch():
+    ref = run_single(M.mlp)
+    got = _train(_build())
+    assert_params_close(got, ref["params"], rtol=1e-4, atol=1e-5)
+
+
+def test_two_stage_pipeline_matches_full_batch():
+    ref = run_single(M.mlp)
+    with tempfile.TemporaryDirectory() as d:
+        strat = os.path.join(d, "pp.json")
+        _stage_strategy(strat)
+        out = os.path.join(d, "out.pt")
+        mp.start_processes(_worker, args=(2, free_port(), strat, out), nprocs=2, join=True, start_method="spawn")
+        res = torch.load(out, weights_only=True)
+    assert_params_close(res["params"], ref["params"], rtol=1e-4, atol=1e-5)
+    # the stage boundary moved activations / gradients between the ranks
+    assert res["stats"].get("all_to_all", 0) + res["stats"].get("p2p", 0) > 0, res["stats"]
