@@ -217,10 +217,12 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
            None if out is None else out.dtype, bool(beta), pre is not None)
     choice = _CHOICE.get(key)
     if choice is None:
-        cands = _candidates(a, b, trans_a, trans_b, bias, act, pre, out, beta)
         if torch.cuda.is_current_stream_capturing():
+            # no library queries / timing inside a capture (hipBLASLt's
+            # heuristic may allocate): the MFMA kernel, decided on the host
             choice = "hip"
         else:
+            cands = _candidates(a, b, trans_a, trans_b, bias, act, pre, out, beta)
             scratch = None if out is None else out.clone()
             pscratch = None if pre is None else pre.clone()
             times = {name: _time(lambda fn=fn: fn(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))

@@ -22,6 +22,7 @@ local_training_backing.cc:50-163):
 from __future__ import annotations
 
 import dataclasses
+import gc
 import hashlib
 import json
 import math
@@ -1062,8 +1063,16 @@ class Executor:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize(self.cfg.device)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            self.train_step(static_feeds, static_labels)
+        # no garbage collection inside the capture: a collected cycle that owns
+        # a HIP event / stream would call its destroy API mid-capture (abort)
+        gc_was_on = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(graph):
+                self.train_step(static_feeds, static_labels)
+        finally:
+            if gc_was_on:
+                gc.enable()
         self._graph = graph
 
         def step(new_feeds: Optional[Dict[str, torch.Tensor]] = None, new_labels: Optional[torch.Tensor] = None):
