@@ -18,7 +18,8 @@ Other BASELINE.json configs run through the same contract with --model:
   resnet50     ResNet-50, synthetic 224x224 ImageNet batches (1000 classes),
                per-GPU batch 256, SGD momentum 0.9
   dlrm         DLRM (8 tables x 1M rows, sparse 64, bot 64-512-512-64,
-               top 576-1024-1024-1024-1), per-GPU batch 1024, SGD
+               top 576-1024-1024-1024-1), per-GPU batch 1024, plain SGD lr 0.01
+               (the reference's dlrm.cc:171; row-sparse table update)
   gpt3-medium  GPT-3 medium (24 layers, hidden 1024, 16 heads, seq 2048,
                vocab 50257), per-GPU batch 8, AdamW
 """
@@ -224,7 +225,7 @@ def bench_zoo(args, world, rank):
     model = FFModel(cfg)
     inputs, out, mcfg = Z.build(zname, model, batch_size=global_batch, **over)
     ce = Z.loss_of(zname) == Z.LOSS_CE
-    optimizer = (SGDOptimizer(model, lr=0.01, momentum=0.9) if opt == "sgd"
+    optimizer = (SGDOptimizer(model, lr=0.01, momentum=0.9 if zname == "resnet50" else 0.0) if opt == "sgd"
                  else AdamOptimizer(model, alpha=1e-4, weight_decay=0.01, decoupled=True))
     t0 = time.time()
     model.compile(optimizer=optimizer,

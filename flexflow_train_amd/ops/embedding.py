@@ -39,6 +39,9 @@ class EmbeddingOp(OpImpl):
             return [None]
         g = grad_outputs[0]
         aggr = ctx.a("aggr", "none")
+        if ctx.extra.get("track_rows"):
+            # row-sparse update (executor): the optimizer touches only these rows
+            ctx.extra.setdefault("touched_rows", []).append(idx.reshape(-1))
         if g.is_cuda and K.available() and wshape[1] % 8 == 0 and dW.is_contiguous():
             K.embedding_bwd(idx.contiguous(), g.contiguous(), dW, aggr)
         else:

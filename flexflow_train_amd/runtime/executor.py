@@ -60,6 +60,8 @@ class ExecConfig:
     grad_clip: float = 0.0
     overlap_grad_sync: bool = True
     bf16_weight_grads: bool = True
+    # row-sparse SGD update of embedding tables (plain SGD only; exact)
+    sparse_embedding_update: bool = True
     # "counter": every rank generates only its own piece from a counter-based
     # RNG keyed by the global element index (on-device on GPU);
     # "host": full weight from a torch.Generator on every rank, then sliced.
@@ -93,6 +95,7 @@ class ParamPiece:
     final_step: int = -1          # forward index of first consumer
     n_consumers: int = 0
     grad_dtype: torch.dtype = torch.float32
+    sparse: bool = False          # row-sparse SGD update (embedding tables)
     master: Optional[torch.Tensor] = None
     compute: Optional[torch.Tensor] = None
     grad: Optional[torch.Tensor] = None
@@ -471,11 +474,22 @@ class Executor:
             if (self.cfg.bf16_weight_grads and cd == torch.bfloat16 and p.n_consumers == 1
                     and p.consumer_op in ("LINEAR", "MULTIHEAD_ATTENTION") and self._weight_index(p) == 0):
                 p.grad_dtype = torch.bfloat16
+        # Embedding tables under plain SGD (the reference's DLRM optimizer:
+        # no momentum / weight decay) that no other rank holds: a row the batch
+        # did not touch has a zero gradient and stays unchanged, so the update
+        # (and the gradient reset) visits only the touched rows instead of
+        # sweeping gigabytes of table every step.  Exact, not an approximation.
+        oc = self.optimizer_cfg
+        plain_sgd = isinstance(oc, SGDConfig) and not oc.momentum and not oc.weight_decay
+        for p in held:
+            p.sparse = bool(self.cfg.sparse_embedding_update and plain_sgd and p.consumer_op == "EMBEDDING"
+                            and p.n_consumers == 1 and len(p.group) <= 1 and p.layout.degrees[0] == 1
+                            and self._weight_index(p) == 0 and len(p.layout.piece_shape) == 2)
         groups: Dict[Tuple, List[ParamPiece]] = {}
         for p in held:
-            groups.setdefault((p.group, str(p.grad_dtype)), []).append(p)
+            groups.setdefault((p.group, str(p.grad_dtype), p.sparse), []).append(p)
         self.flats = []
-        for fid, ((g, gdt), plist) in enumerate(sorted(groups.items(), key=lambda kv: kv[0])):
+        for fid, ((g, gdt, sparse), plist) in enumerate(sorted(groups.items(), key=lambda kv: kv[0])):
             zero = self.cfg.shard_optimizer and len(g) > 1
             esize = torch.tensor([], dtype=plist[0].grad_dtype).element_size()
             # buckets: contiguous param ranges, finalised in backward order
@@ -519,8 +533,11 @@ class Executor:
             else:
                 opt = FlatOptimizer(self.optimizer_cfg, master, grad, compute)
             self.flats.append({"group": g, "params": plist, "master": master, "grad": grad, "compute": compute,
-                               "buckets": binfo, "opt": opt, "zero": zero,
+                               "buckets": binfo, "opt": opt, "zero": zero, "sparse": sparse,
                                "ps": (not zero) and self.cfg.param_sync == "ps" and len(g) > 1})
+        for p in self.params:
+            if p.sparse and 0 <= p.final_step < len(self.steps):
+                self.steps[p.final_step].ctx.extra["track_rows"] = True
         self._param_bucket = {}
         for f in self.flats:
             for bi, b in enumerate(f["buckets"]):
@@ -828,7 +845,7 @@ class Executor:
         if dlogits is not None:
             grads[self.loss_value] = dlogits
         for f in self.flats:
-            if zero_grads:
+            if zero_grads and not f["sparse"]:   # sparse flats: rows reset by the update
                 f["grad"].zero_()
             for b in f["buckets"]:
                 b["pending"] = sum(1 for p in b["params"] if p.trainable)
@@ -958,10 +975,34 @@ class Executor:
         for f in self.flats:
             if f.get("ps") and self.dist.distributed and self.rank != min(f["group"]):
                 continue  # PS: only the leader updates (its optimizer state is the only one)
+            if f["sparse"]:
+                self._sparse_sgd(f, lr, scale)
+                continue
             f["opt"].step(lr=lr, grad_scale=scale)
         self._gather_updated()
         self._broadcast_ps()
         self.step_num += 1
+
+    def _sparse_sgd(self, f, lr: Optional[float], scale: float):
+        """w[r] -= lr * g[r]; g[r] = 0 for the rows the step touched (ids
+        recorded by the embedding backward; duplicates write identical values,
+        out-of-range ids clamp onto rows whose update is then still exact)."""
+        lr = f["opt"].cfg.lr if lr is None else lr
+        f["opt"].step_num += 1
+        for p in f["params"]:
+            if not p.trainable:
+                continue
+            rows = self.steps[p.final_step].ctx.extra.pop("touched_rows", None)
+            if not rows:
+                continue
+            n = p.grad.shape[0]
+            idx = torch.cat([r.to(torch.long) for r in rows]).clamp_(0, n - 1)
+            m2, g2 = p.master.view(n, -1), p.grad.view(n, -1)
+            vals = m2.index_select(0, idx) - (lr * scale) * g2.index_select(0, idx).float()
+            m2.index_copy_(0, idx, vals)
+            g2.index_fill_(0, idx, 0)
+            if p.compute is not p.master:
+                p.compute.view(n, -1).index_copy_(0, idx, vals.to(p.compute.dtype))
 
     def _broadcast_ps(self):
         """Parameter server: the leader's updated weights go back to the replicas."""
