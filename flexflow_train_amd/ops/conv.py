@@ -63,7 +63,15 @@ _MODE = os.environ.get("FF_CONV1X1", "auto")   # auto | native | gemm
 
 
 def _pointwise(R, S, stride, pad, groups) -> bool:
-    return R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and groups == 1
+    """1x1, unpadded, ungrouped: a GEMM over (strided-subsampled) NHWC pixels."""
+    return R == 1 and S == 1 and tuple(pad) == (0, 0) and groups == 1
+
+
+def _sub(x: torch.Tensor, stride) -> torch.Tensor:
+    """The pixels a strided 1x1 convolution reads, packed (channels_last)."""
+    if tuple(stride) == (1, 1):
+        return x
+    return x[:, :, ::stride[0], ::stride[1]].contiguous(memory_format=torch.channels_last)
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -120,13 +128,14 @@ class Conv2DOp(OpImpl):
             bias = None if b is None else b.to(torch.bfloat16).contiguous()
             if _pointwise(R, S, stride, pad, groups) and C % 8 == 0:
                 def via_gemm(st=stats):
-                    y2 = G.matmul(_rows(xin), wp.view(Kc, C), trans_b=True, bias=bias, act=act)
-                    yv = y2.view(x.shape[0], x.shape[2], x.shape[3], Kc).permute(0, 3, 1, 2)
+                    xs = _sub(xin, stride)
+                    y2 = G.matmul(_rows(xs), wp.view(Kc, C), trans_b=True, bias=bias, act=act)
+                    yv = y2.view(xs.shape[0], xs.shape[2], xs.shape[3], Kc).permute(0, 3, 1, 2)
                     if st is not None:
                         st.zero_()
                         K.bn_stats(yv, st)
                     return yv
-                key = ("fwd", tuple(xin.shape), Kc, act, bias is not None, stats is not None)
+                key = ("fwd", tuple(xin.shape), Kc, tuple(stride), act, bias is not None, stats is not None)
                 scratch = None if stats is None else torch.empty_like(stats)
                 choice = _pick(key, {"native": lambda: K.conv2d_fwd(xin, wp, bias, stride, pad, act=act,
                                                                    stats=scratch),
@@ -182,14 +191,14 @@ class Conv2DOp(OpImpl):
         dW = weight_grads[0]
         if dW is not None:
             if Cp == xshape[1] and _pointwise(R, S, stride, pad, 1):
-                key = ("wgrad", tuple(xin.shape), Kc)
+                key = ("wgrad", tuple(xin.shape), Kc, tuple(stride))
                 if key not in _CHOICE:
                     tmp = torch.zeros_like(dW.view(-1))
                     _pick(key, {"native": lambda: K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad),
-                                "gemm": lambda: G.matmul(_rows(dy), _rows(xin), trans_a=True, out=tmp.view(Kc, Cp),
-                                                         beta=1.0)})
+                                "gemm": lambda: G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True,
+                                                         out=tmp.view(Kc, Cp), beta=1.0)})
                 if _CHOICE[key] == "gemm":
-                    G.matmul(_rows(dy), _rows(xin), trans_a=True, out=dW.view(Kc, Cp), beta=1.0)
+                    G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True, out=dW.view(Kc, Cp), beta=1.0)
                 else:
                     K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
             elif Cp == xshape[1]:
@@ -208,12 +217,22 @@ class Conv2DOp(OpImpl):
                    and acc.is_contiguous(memory_format=torch.channels_last))
         if _pointwise(R, S, stride, pad, 1):
             def dgrad_gemm(out):
-                if out is not None:
-                    G.matmul(_rows(dy), wp.view(Kc, Cp), out=_rows(out), beta=1.0)
-                    return out
-                dx2 = G.matmul(_rows(dy), wp.view(Kc, Cp))
-                return dx2.view(xshape[0], xshape[2], xshape[3], Cp).permute(0, 3, 1, 2)
-            key = ("dgrad", tuple(xshape), Kc, use_acc)
+                if tuple(stride) == (1, 1):
+                    if out is not None:
+                        G.matmul(_rows(dy), wp.view(Kc, Cp), out=_rows(out), beta=1.0)
+                        return out
+                    dx2 = G.matmul(_rows(dy), wp.view(Kc, Cp))
+                    return dx2.view(xshape[0], xshape[2], xshape[3], Cp).permute(0, 3, 1, 2)
+                # strided: the gradient lands on the sampled pixels only
+                ds = G.matmul(_rows(dy), wp.view(Kc, Cp)).view(dy.shape[0], dy.shape[2], dy.shape[3], Cp)
+                if out is None:
+                    out = torch.empty(tuple(xshape), device=dy.device, dtype=dy.dtype,
+                                      memory_format=torch.channels_last).zero_()
+                    out[:, :, ::stride[0], ::stride[1]] = ds.permute(0, 3, 1, 2)
+                else:
+                    out[:, :, ::stride[0], ::stride[1]] += ds.permute(0, 3, 1, 2)
+                return out
+            key = ("dgrad", tuple(xshape), Kc, tuple(stride), use_acc)
             if key not in _CHOICE:
                 tmp = acc.clone() if use_acc else None
                 _pick(key, {"native": lambda: K.conv2d_dgrad(dy, wp, xshape, stride, pad, out=tmp,

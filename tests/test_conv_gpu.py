@@ -198,8 +198,9 @@ def test_resnet_gpu_step_matches_cpu_fp32():
 
 
 @pytest.mark.parametrize("mode", ["native", "gemm"])
-@pytest.mark.parametrize("C,Ko,acc", [(64, 256, False), (256, 64, True)])
-def test_pointwise_conv_paths(mode, C, Ko, acc):
+@pytest.mark.parametrize("C,Ko,acc,st", [(64, 256, False, 1), (256, 64, True, 1), (64, 128, False, 2),
+                                         (128, 64, True, 2)])
+def test_pointwise_conv_paths(mode, C, Ko, acc, st):
     """1x1 stride-1 convolutions: the implicit-GEMM kernels and the library
     GEMM path (ops/conv.py picks per shape) both match fp32 — forward with the
     BN statistics, dgrad (fresh or accumulated) and the accumulated wgrad."""
@@ -212,16 +213,17 @@ def test_pointwise_conv_paths(mode, C, Ko, acc):
         N, H = 4, 14
         x = _rand_nhwc((N, C, H, H))
         W = (torch.randn(Ko, 1, 1, C, device="cuda") * 0.1).to(torch.bfloat16)   # physical [K, R, S, C]
-        ctx = OpContext("CONV2D", {"kernel_h": 1, "kernel_w": 1}, "c", device=torch.device("cuda"),
+        ctx = OpContext("CONV2D", {"kernel_h": 1, "kernel_w": 1, "stride_h": st, "stride_w": st}, "c",
+                        device=torch.device("cuda"),
                         compute_dtype=torch.bfloat16)
         ctx.extra["emit_bn_stats"] = True
         op = CV.Conv2DOp()
         Wl = W.view(Ko, 1, 1, C).reshape(Ko, C, 1, 1)  # logical-shaped piece over the physical data
         (y,), saved = op.forward(ctx, [x], [Wl])
-        ref = F.conv2d(x.float(), W.float().permute(0, 3, 1, 2))
+        ref = F.conv2d(x.float(), W.float().permute(0, 3, 1, 2), stride=st)
         torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
-        st = y._ff_bn_stats
-        torch.testing.assert_close(st[:Ko], y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
+        sts = y._ff_bn_stats
+        torch.testing.assert_close(sts[:Ko], y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-1)
         dy = _rand_nhwc(tuple(y.shape))
         dW = torch.full((Ko * C,), 0.5, device="cuda")
         if acc:
@@ -230,7 +232,7 @@ def test_pointwise_conv_paths(mode, C, Ko, acc):
         (dx,) = op.backward(ctx, saved, [dy], [dW], [True])
         xr = x.float().requires_grad_(True)
         wr = W.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
-        F.conv2d(xr, wr).backward(dy.float())
+        F.conv2d(xr, wr, stride=st).backward(dy.float())
         want_dx = xr.grad + (base.float() if acc else 0)
         torch.testing.assert_close(dx.float(), want_dx, rtol=2e-2, atol=5e-2)
         torch.testing.assert_close(dW.view(Ko, C), wr.grad.view(Ko, C) + 0.5, rtol=1e-2, atol=5e-2)
