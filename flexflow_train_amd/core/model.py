@@ -523,7 +523,13 @@ class FFModel:
         cuda = torch.cuda.is_available() and not self.ffconfig.cpu_only and not self.ffconfig.local_execution
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if cuda and local_rank >= torch.cuda.device_count():
-            # more ranks than GPUs (gloo rehearsal of a multi-GPU run on one card)
+            # more ranks than GPUs (gloo rehearsal of a multi-GPU run on one
+            # card).  RCCL cannot put two ranks on one GPU: refuse before any
+            # process-group init instead of hanging inside it.
+            if os.environ.get("FF_DIST_BACKEND", "").lower() != "gloo":
+                raise RuntimeError(
+                    f"LOCAL_RANK {local_rank} >= {torch.cuda.device_count()} visible GPUs: launch at most one rank "
+                    "per GPU, or set FF_DIST_BACKEND=gloo to rehearse several ranks on a shared GPU")
             local_rank %= torch.cuda.device_count()
         device = torch.device(f"cuda:{local_rank}") if cuda else torch.device("cpu")
         if cuda:
@@ -656,8 +662,7 @@ class FFModel:
     def zero_gradients(self):
         if self._traced():
             return
-        for f in self.executor.flats:
-            f["grad"].zero_()
+        self.executor.zero_gradients()
 
     def _input_name(self, t):
         return t.name

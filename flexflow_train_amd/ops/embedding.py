@@ -24,7 +24,11 @@ class EmbeddingOp(OpImpl):
         if (W.is_cuda and K.available() and W.dtype in (torch.bfloat16, torch.float32) and W.shape[1] % 8 == 0):
             out = K.embedding_fwd(idx.contiguous(), W.contiguous(), aggr)
         else:
-            e = torch.nn.functional.embedding(idx.long().clamp(0, W.shape[0] - 1), W)
+            # out-of-range ids read a zero row (as the HIP kernel does) and
+            # get no gradient (both backward paths drop them)
+            li = idx.long()
+            ok = (li >= 0) & (li < W.shape[0])
+            e = torch.nn.functional.embedding(li.clamp(0, W.shape[0] - 1), W) * ok.unsqueeze(-1).to(W.dtype)
             if aggr == "sum":
                 e = e.sum(-2)
             elif aggr == "avg":
@@ -40,7 +44,8 @@ class EmbeddingOp(OpImpl):
         g = grad_outputs[0]
         aggr = ctx.a("aggr", "none")
         if ctx.extra.get("track_rows"):
-            # row-sparse update (executor): the optimizer touches only these rows
+            # row-sparse update (executor): the optimizer touches only these
+            # rows; the list is consumed by the update or by zero_gradients
             ctx.extra.setdefault("touched_rows", []).append(idx.reshape(-1))
         if g.is_cuda and K.available() and wshape[1] % 8 == 0 and dW.is_contiguous():
             K.embedding_bwd(idx.contiguous(), g.contiguous(), dW, aggr)

@@ -213,8 +213,12 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         return _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre)
     if _MODE == "hip":
         return _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre)
+    # leading dims and pointer alignment are part of the signature: the
+    # hipBLASLt plans behind ``lt:i`` are keyed by them and gemm256 checks them
     key = (tuple(a.shape), tuple(b.shape), trans_a, trans_b, bias is not None, act,
-           None if out is None else out.dtype, bool(beta), pre is not None)
+           None if out is None else out.dtype, bool(beta), pre is not None,
+           a.stride(0), b.stride(0), None if out is None else out.stride(0),
+           _align(a), _align(b), None if out is None else _align(out))
     choice = _CHOICE.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
@@ -229,7 +233,14 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
                      for name, fn in cands.items()}
             choice = min(times, key=times.get)
         _CHOICE[key] = choice
+    if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
+        choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
+
+
+def _align(t: torch.Tensor) -> int:
+    p = t.data_ptr()
+    return 16 if p % 16 == 0 else (8 if p % 8 == 0 else 2)
 
 
 def _resolve(name: str):

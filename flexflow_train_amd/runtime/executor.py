@@ -844,9 +844,10 @@ class Executor:
         grads: Dict[Value, torch.Tensor] = {}
         if dlogits is not None:
             grads[self.loss_value] = dlogits
+        self._sync_row_tracking()
         for f in self.flats:
-            if zero_grads and not f["sparse"]:   # sparse flats: rows reset by the update
-                f["grad"].zero_()
+            if zero_grads:
+                self._zero_flat(f)
             for b in f["buckets"]:
                 b["pending"] = sum(1 for p in b["params"] if p.trainable)
         self._works = []
@@ -902,6 +903,38 @@ class Executor:
         self._env = {}
         if sync:
             self._finish_grad_sync()
+
+    def _sync_row_tracking(self):
+        """Embedding backward records touched rows only for tables whose flat
+        is on the sparse path (the flag may be cleared after compile)."""
+        for f in self.flats:
+            for p in f["params"]:
+                if 0 <= p.final_step < len(self.steps):
+                    ex = self.steps[p.final_step].ctx.extra
+                    ex["track_rows"] = bool(f["sparse"] and p.sparse)
+                    if not ex["track_rows"]:
+                        ex.pop("touched_rows", None)
+
+    def _zero_flat(self, f):
+        """Reset a flat's gradients.  Sparse flats only hold non-zero rows the
+        last backward touched and no update consumed: clear just those."""
+        if not f["sparse"]:
+            f["grad"].zero_()
+            return
+        for p in f["params"]:
+            if not (0 <= p.final_step < len(self.steps)):
+                continue
+            rows = self.steps[p.final_step].ctx.extra.pop("touched_rows", None)
+            if rows:
+                n = p.grad.shape[0]
+                idx = torch.cat([r.to(torch.long) for r in rows]).clamp_(0, n - 1)
+                p.grad.view(n, -1).index_fill_(0, idx, 0)
+
+    def zero_gradients(self):
+        """FFModel.zero_gradients: every gradient buffer back to zero."""
+        self._sync_row_tracking()
+        for f in self.flats:
+            self._zero_flat(f)
 
     def _acc(self, grads, v, g):
         if g is None:
@@ -986,7 +1019,8 @@ class Executor:
     def _sparse_sgd(self, f, lr: Optional[float], scale: float):
         """w[r] -= lr * g[r]; g[r] = 0 for the rows the step touched (ids
         recorded by the embedding backward; duplicates write identical values,
-        out-of-range ids clamp onto rows whose update is then still exact)."""
+        out-of-range ids clamp onto the last row, which then gets the same
+        value the dense update gives it -- capture-safe, no boolean mask)."""
         lr = f["opt"].cfg.lr if lr is None else lr
         f["opt"].step_num += 1
         for p in f["params"]:
