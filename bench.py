@@ -48,8 +48,8 @@ def main():
     ap.add_argument("--gemm", default=os.environ.get("FF_GEMM", "auto"))
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="replay the training step from a hipGraph (1) or run eagerly (0); default: graphs on a "
-                         "single GPU, eager across ranks (collective capture is validated on 1 GPU only)")
+                    help="replay the training step from a hipGraph (1) or run eagerly (0); default 1: one graph "
+                         "on a single GPU, graph segments cut at every RCCL collective across ranks")
     args = ap.parse_args()
 
     os.environ["FF_GEMM"] = args.gemm
@@ -107,7 +107,7 @@ def main():
         ex.train_step(feeds, labels)
 
     graphed = False
-    use_graph = args.graph if args.graph >= 0 else int(world == 1)
+    use_graph = args.graph if args.graph >= 0 else 1
     if use_graph and dev.type == "cuda" and not args.profile:
         try:
             step = ex.make_graphed_train_step(feeds, labels)
@@ -162,6 +162,7 @@ def main():
                 "optimizer": "adamw",
                 "compile_s": round(compile_s, 2),
                 "hipgraph": graphed,
+                "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
                 "gemm_choices": dict(collections.Counter(gemm_choices().values())),
                 "tokens_per_sec": round(sps * args.seq, 1),
                 "final_loss": round(pm.loss, 4),
@@ -254,7 +255,7 @@ def bench_zoo(args, world, rank):
         ex.train_step(feeds, labels)
 
     graphed = False
-    use_graph = args.graph if args.graph >= 0 else int(world == 1)
+    use_graph = args.graph if args.graph >= 0 else 1
     if use_graph and dev.type == "cuda" and not args.profile:
         try:
             step = ex.make_graphed_train_step(feeds, labels)

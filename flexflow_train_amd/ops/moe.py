@@ -29,6 +29,8 @@ from typing import List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ..runtime.graphs import check_capturable
+
 from .base import OpImpl, acc_grad, register
 from .gemm import _blas
 
@@ -178,6 +180,7 @@ class ExpertsOp(OpImpl):
         order = torch.argsort(owner, stable=True)
         send_counts = torch.bincount(owner, minlength=grp.size)
         recv_counts = torch.empty_like(send_counts)
+        check_capturable("MoE all-to-all dispatch (data-dependent split sizes)")
         dist.all_to_all_single(recv_counts, send_counts, group=grp.pg)
         sc, rc = send_counts.tolist(), recv_counts.tolist()
         xr = _a2a_rows(x[tok[order]], sc, rc, grp)

@@ -35,6 +35,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..runtime.graphs import check_capturable
 from .layout import Box, Layout, intersect, rel_slices
 
 
@@ -47,6 +48,14 @@ class DistContext:
         self.device = device or torch.device("cpu")
         self._groups: Dict[Tuple[int, ...], object] = {}
         self.stats = {"all_reduce": 0, "all_gather": 0, "all_to_all": 0, "p2p": 0, "local": 0, "bytes": 0}
+        # runtime/graphs.SegmentRecorder while a distributed step is being
+        # captured: in-place collectives become segment boundaries
+        self.recorder = None
+
+    def _issue(self, fn, async_op: bool):
+        if self.recorder is not None:
+            return self.recorder.collective(fn, async_op)
+        return fn()
 
     @classmethod
     def from_env(cls, device: Optional[torch.device] = None, backend: Optional[str] = None) -> "DistContext":
@@ -87,7 +96,8 @@ class DistContext:
             return None
         self.stats["all_reduce"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
-        return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
+        grp = self.group(ranks)
+        return self._issue(lambda: dist.all_reduce(t, group=grp, async_op=async_op), async_op)
 
     def reduce_scatter_(self, t: torch.Tensor, ranks: Sequence[int], async_op: bool = False):
         """In-place reduce-scatter of the 1-D ``t``: afterwards chunk i (of
@@ -102,8 +112,9 @@ class DistContext:
             n = len(ranks)
             i = sorted(ranks).index(self.rank)
             chunk = t.numel() // n
-            return dist.reduce_scatter_tensor(t[i * chunk:(i + 1) * chunk], t, group=self.group(ranks),
-                                              async_op=async_op)
+            grp = self.group(ranks)
+            out = t[i * chunk:(i + 1) * chunk]
+            return self._issue(lambda: dist.reduce_scatter_tensor(out, t, group=grp, async_op=async_op), async_op)
         return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
 
     def reduce_(self, t: torch.Tensor, ranks: Sequence[int], dst: int, async_op: bool = False):
@@ -113,14 +124,16 @@ class DistContext:
             return None
         self.stats["reduce"] = self.stats.get("reduce", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
-        return dist.reduce(t, dst=dst, group=self.group(ranks), async_op=async_op)
+        grp = self.group(ranks)
+        return self._issue(lambda: dist.reduce(t, dst=dst, group=grp, async_op=async_op), async_op)
 
     def broadcast_(self, t: torch.Tensor, ranks: Sequence[int], src: int, async_op: bool = False):
         if len(ranks) <= 1 or not self.distributed:
             return None
         self.stats["broadcast"] = self.stats.get("broadcast", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
-        return dist.broadcast(t, src=src, group=self.group(ranks), async_op=async_op)
+        grp = self.group(ranks)
+        return self._issue(lambda: dist.broadcast(t, src=src, group=grp, async_op=async_op), async_op)
 
     def all_gather_(self, t: torch.Tensor, ranks: Sequence[int]):
         """In-place all-gather of the equal chunks of the 1-D ``t`` (chunk i
@@ -133,13 +146,16 @@ class DistContext:
         self.stats["all_gather"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
         if t.is_cuda:
-            dist.all_gather_into_tensor(t, t[i * chunk:(i + 1) * chunk], group=self.group(ranks))
+            grp = self.group(ranks)
+            piece = t[i * chunk:(i + 1) * chunk]
+            self._issue(lambda: dist.all_gather_into_tensor(t, piece, group=grp), False)
         else:
             dist.all_gather(list(t.split(chunk)), t[i * chunk:(i + 1) * chunk].clone(), group=self.group(ranks))
 
     def max_scalar(self, v: float) -> float:
         if not self.distributed:
             return v
+        check_capturable("max_scalar")
         t = torch.tensor([v], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
@@ -301,7 +317,8 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
         ctx.stats["all_gather"] += 1
         xs = x.contiguous()
         outs = [torch.empty_like(xs) for _ in g]
-        dist.all_gather(outs, xs, group=ctx.group(g))
+        grp = ctx.group(g)
+        ctx._issue(lambda: dist.all_gather(outs, xs, group=grp), False)
         order = sorted(range(len(g)), key=lambda i: plan.src_boxes[g[i]][plan.gather_dim][0])
         # members holding identical boxes (implicit replicas) appear once
         seen, parts = set(), []
@@ -334,8 +351,10 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
                 ops.append(dist.P2POp(dist.irecv, buf, c.src_rank))
                 recv_bufs.append((c, buf))
     if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        def _p2p():
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        ctx._issue(_p2p, False)
     for c, buf in recv_bufs:
         result[rel_slices(c.part, my_dst)] += buf
     return result
@@ -360,7 +379,9 @@ def _exchange_all_to_all(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext
     parts = [p for p in send if p is not None and p.numel()]
     sendbuf = torch.cat(parts) if parts else torch.empty(0, dtype=dtype, device=device)
     recvbuf = torch.empty(sum(out_sizes), dtype=sendbuf.dtype, device=device)
-    dist.all_to_all_single(recvbuf, sendbuf.to(device), output_split_sizes=out_sizes, input_split_sizes=in_sizes)
+    sendbuf = sendbuf.to(device)
+    ctx._issue(lambda: dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=out_sizes,
+                                              input_split_sizes=in_sizes), False)
     if my_dst is None:
         return None
     result = torch.zeros(dst_shape, dtype=dtype, device=device)

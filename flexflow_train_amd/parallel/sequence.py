@@ -32,6 +32,8 @@ from typing import List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ..runtime.graphs import check_capturable
+
 from .. import kernels as K
 
 LOG2E = 1.4426950408889634
@@ -113,7 +115,8 @@ def merge(o, lse, o_j, lse_j):
 # ------------------------------------------------------------------ Ulysses
 def _a2a(x: torch.Tensor, grp: SeqGroup) -> torch.Tensor:
     out = torch.empty_like(x)
-    dist.all_to_all_single(out, x, group=grp.pg)
+    pg = grp.pg
+    grp.dist_ctx._issue(lambda: dist.all_to_all_single(out, x, group=pg), False)
     grp.dist_ctx.stats["sp_all_to_all"] = grp.dist_ctx.stats.get("sp_all_to_all", 0) + 1
     return out
 
@@ -152,6 +155,7 @@ def ulysses_bwd(do, saved, causal, scale, grp: SeqGroup):
 # --------------------------------------------------------------------- ring
 def _exchange(tensors: List[torch.Tensor], grp: SeqGroup) -> List[torch.Tensor]:
     """Send ``tensors`` to the next rank, receive the previous rank's."""
+    check_capturable("ring attention exchange")
     recv = [torch.empty_like(t) for t in tensors]
     ops = []
     for t in tensors:

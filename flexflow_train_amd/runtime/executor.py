@@ -40,6 +40,7 @@ from ..parallel.layout import Layout, layout_from_pshape
 from ..parallel.sequence import SeqGroup
 from ..ops.moe import ExpertGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig, ShardedOptimizer
+from .graphs import SegmentRecorder
 from .initializers import make_initializer_tensor
 from ..utils.tracing import Tracer
 
@@ -1137,14 +1138,21 @@ class Executor:
                 self.train_step(static_feeds, static_labels)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize(self.cfg.device)
-        graph = torch.cuda.CUDAGraph()
         # no garbage collection inside the capture: a collected cycle that owns
         # a HIP event / stream would call its destroy API mid-capture (abort)
         gc_was_on = gc.isenabled()
         gc.disable()
         try:
-            with torch.cuda.graph(graph):
-                self.train_step(static_feeds, static_labels)
+            if self.dist.distributed:
+                # across ranks: one graph segment between consecutive collectives
+                # (runtime/graphs.py); the RCCL calls are re-issued at replay
+                graph = self._capture_segments(side, static_feeds, static_labels)
+                replay = graph.replay
+            else:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    self.train_step(static_feeds, static_labels)
+                replay = graph.replay
         finally:
             if gc_was_on:
                 gc.enable()
@@ -1157,12 +1165,39 @@ class Executor:
                         static_feeds[k].copy_(self._local_piece(k, v), non_blocking=True)
             if new_labels is not None and static_labels is not None:
                 static_labels.copy_(self.local_labels(new_labels), non_blocking=True)
-            graph.replay()
+            replay()
             self.step_num += 1
             for f in self.flats:
                 f["opt"].step_num += 1
 
         return step
+
+    def _capture_segments(self, side, static_feeds, static_labels):
+        """Capture one training step as hipGraph segments cut at every
+        collective (runtime/graphs.SegmentRecorder).  Raises NotCapturable
+        (after leaving capture mode cleanly) when the step reaches a
+        collective that cannot be re-issued from a recorded closure."""
+        rec = SegmentRecorder()
+        torch.cuda.synchronize(self.cfg.device)
+        self.dist.recorder = rec
+        try:
+            with torch.cuda.stream(side):
+                rec.begin()
+                self.train_step(static_feeds, static_labels)
+                rec.end()
+        except BaseException:
+            rec.abort()
+            self._works = []
+            for f in self.flats:
+                for b in f["buckets"]:
+                    b["launched"] = False
+            raise
+        finally:
+            self.dist.recorder = None
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize(self.cfg.device)
+        self.graph_segments = (rec.n_graphs(), rec.n_collectives())
+        return rec
 
     def zero_metrics(self):
         self.metrics_buf.zero_()
