@@ -13,6 +13,8 @@ Strategy file (JSON, "ffmi355x.strategy.v1"):
             "sum_degree", "discard_copy_degree", "device_ids": [...]}]}
 The "ops" list mirrors the reference's per-op FFProtoBuf::Strategy records
 (keyed by op name) and is informational; the PCG + views are authoritative.
+A ``.pb`` path reads / writes the reference's protobuf strategy format itself
+(legacy_strategy.py), e.g. examples/cpp/DLRM/strategies/*.pb.
 """
 from __future__ import annotations
 
@@ -22,6 +24,7 @@ from typing import Dict, Tuple
 
 from .. import _ffcore as C
 from ..utils.logging import get_logger
+from . import legacy_strategy as legacy
 
 
 def _cg_to_pcg_map_by_name(cg, pcg) -> Dict[int, int]:
@@ -40,7 +43,12 @@ def _cg_to_pcg_map_by_name(cg, pcg) -> Dict[int, int]:
 
 def build_pcg(cg, ffconfig, world: int):
     report = {"world": world}
-    if ffconfig.import_strategy_file:
+    if ffconfig.import_strategy_file and legacy.is_legacy_file(ffconfig.import_strategy_file):
+        # the reference's FFProtoBuf::Strategy (.pb) files, keyed by op name
+        with open(ffconfig.import_strategy_file, "rb") as f:
+            pcg, views, rep = legacy.to_pcg(cg, legacy.decode(f.read()), world)
+        report.update(rep)
+    elif ffconfig.import_strategy_file:
         pcg, views = import_strategy(ffconfig.import_strategy_file, world)
         report["source"] = "import"
     elif world == 1:
@@ -63,6 +71,12 @@ def build_pcg(cg, ffconfig, world: int):
 
 
 def export_strategy(path: str, pcg, views: Dict[int, Tuple[int, int]], report=None):
+    if path.endswith(".pb"):
+        # the reference's protobuf format (per-op degrees + device ids)
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "wb") as f:
+            f.write(legacy.encode(legacy.from_pcg(pcg, views)))
+        return
     ops = []
     for n in pcg.topo_order():
         op = pcg.layer_op(n)

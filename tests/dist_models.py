@@ -112,3 +112,22 @@ def cnn(m):
     m.softmax(t, name="sm")
     g = torch.Generator().manual_seed(11)
     return {"img": torch.randn(8, 3, 12, 12, generator=g)}, torch.randint(0, 6, (8,), generator=g)
+
+
+def dlrm_small(m):
+    """DLRM-shaped: 4 SUM-bag tables + bottom MLP -> concat -> top MLP ->
+    softmax; table layers named like the reference's strategy records
+    expect them by index ("embedding<i>" = the i-th embedding)."""
+    B, T, V, E = 8, 4, 40, 8
+    ids = [m.create_tensor([B, 2], DataType.DT_INT32, create_grad=False, name=f"sparse{i}") for i in range(T)]
+    d = m.create_tensor([B, 6], DataType.DT_FLOAT, name="dense")
+    x = m.dense(d, E, ActiMode.AC_MODE_RELU, name="bot0")
+    embs = [m.embedding(ids[i], V, E, AggrMode.AGGR_MODE_SUM, name=f"emb{i}") for i in range(T)]
+    z = m.concat([x] + embs, -1, name="interact")
+    t = m.dense(z, 16, ActiMode.AC_MODE_RELU, name="top0")
+    t = m.dense(t, 4, name="top1")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(23)
+    feeds = {f"sparse{i}": torch.randint(0, V, (B, 2), generator=g, dtype=torch.int32) for i in range(T)}
+    feeds["dense"] = torch.randn(B, 6, generator=g)
+    return feeds, torch.randint(0, 4, (B,), generator=g)
