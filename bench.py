@@ -169,6 +169,9 @@ def main():
             },
         }
         print(json.dumps(res), flush=True)
+        if os.environ.get("FF_GEMM_REPORT"):
+            from flexflow_train_amd.ops.gemm import report
+            print(report(), file=sys.stderr)
         if args.profile:
             rep = ex.profile_report()
             print(json.dumps({"profile_ms_total": {k: round(v, 3) for k, v in list(rep.items())[:40]}}),

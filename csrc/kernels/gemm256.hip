@@ -250,6 +250,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 }  // namespace
 
+void splitk_reduce(const float* ws, void* out, int M, int N, int ldc, int S, float beta, int out_f32,
+                   hipStream_t st) {
+  const int64_t n4 = static_cast<int64_t>(M) * N / 4;
+  const int rgrid = static_cast<int>(std::min<int64_t>((n4 + 255) / 256, 2048));
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rgrid), dim3(256), 0, st, ws, out, M, N, ldc, S, beta, out_f32);
+  FFK_LAUNCH_CHECK("splitk_reduce");
+}
+
 bool gemm256_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b) {
   if (M < 8 || N < 8 || K < TK || K % TK) return false;
   if (M % 8 || N % 8 || lda % 8 || ldb % 8) return false;
@@ -284,13 +292,7 @@ void gemm256_bf16(const void* A, const void* B, void* C, const void* bias, void*
   else if (trans_a && !trans_b) hipLaunchKernelGGL((gemm256_kernel<true, false>), grid, block, 0, st, g);
   else hipLaunchKernelGGL((gemm256_kernel<true, true>), grid, block, 0, st, g);
   FFK_LAUNCH_CHECK("gemm256");
-  if (splits > 1) {
-    const int64_t n4 = static_cast<int64_t>(M) * N / 4;
-    const int rgrid = static_cast<int>(std::min<int64_t>((n4 + 255) / 256, 2048));
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rgrid), dim3(256), 0, st, workspace, C, M, N, ldc, splits, beta,
-                       out_f32);
-    FFK_LAUNCH_CHECK("splitk_reduce");
-  }
+  if (splits > 1) splitk_reduce(workspace, C, M, N, ldc, splits, beta, out_f32, st);
 }
 
 }  // namespace ffk

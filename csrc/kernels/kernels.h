@@ -79,6 +79,31 @@ void gemm256_bf16(const void* A, const void* B, void* C, const void* bias, void*
                   int ldb, int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
                   int splits, float* workspace, hipStream_t st);
 
+// out[m][n] = sum_s ws[s][m][n] + beta * out[m][n] (split-K reduce; gemm256.hip)
+void splitk_reduce(const float* ws, void* out, int M, int N, int ldc, int S, float beta, int out_f32,
+                   hipStream_t st);
+
+// ---- gemmp.hip: phase-pipelined 256x256 GEMM with fused training epilogues
+struct GemmPParams {
+  const void* A = nullptr;
+  const void* B = nullptr;
+  void* C = nullptr;
+  const void* bias = nullptr;   // [N] bf16
+  void* pre = nullptr;          // pre-activation out, bf16 (ldc)
+  const void* aux = nullptr;    // pre-activation in for act_bwd, bf16 (ldc)
+  float* dbias = nullptr;       // += column sums of the result (fp32 atomics)
+  float* workspace = nullptr;   // split-K fp32 [splits][M][N]
+  int M = 0, N = 0, K = 0, lda = 0, ldb = 0, ldc = 0;
+  bool trans_a = false, trans_b = false;
+  int act = 0;                  // activation code (elementwise.hip numbering 0-4)
+  bool act_bwd = false;         // result = acc * act'(aux) instead of act(acc)
+  float alpha = 1.f, beta = 0.f;
+  int out_f32 = 0, splits = 1;
+  int dbg = 0;                  // ablation bits for timing experiments (gemmp.hip)
+};
+bool gemmp_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b);
+void gemmp_bf16(const GemmPParams& p, hipStream_t st);
+
 // ---- tensorops.hip: general tensor operators (N-d, <= 6 dims)
 struct NdShape {
   int nd = 0;

@@ -70,6 +70,28 @@ __device__ __forceinline__ bf16x8 tr_frag_nat(const unsigned char* img, int k0, 
   return cat44(lds_tr(img, oa), lds_tr(img, ob));
 }
 
+// Same read issued from inline asm.  hipcc cannot see which LDS bytes an
+// intrinsic ds_read_b64_tr_b16 touches and waits vmcnt(0) for every LDS-DMA
+// in flight before it, draining a DMA pipeline that spans barriers (gemmp.hip).
+// The asm form is invisible to that analysis: the CALLER must retire the
+// reads itself (s_waitcnt lgkmcnt(0) + sched_barrier before the consumer).
+__device__ __forceinline__ bf16x4 lds_tr_asm(const unsigned char* base, int off) {
+  bf16x4 r;
+  const unsigned addr = static_cast<unsigned>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const unsigned char*)(base + off)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <int ROW_BYTES>
+__device__ __forceinline__ bf16x8 tr_frag_nat_asm(const unsigned char* img, int k0, int x0, int lane) {
+  const int h = lane >> 5, g = (lane >> 4) & 1, i = lane & 15;
+  const int col = x0 + 16 * g + 4 * (i & 3);
+  const int ra = k0 + 8 * h + (i >> 2);
+  const int oa = img_off<ROW_BYTES>(ra, col >> 3) + (col & 7) * 2;
+  const int ob = img_off<ROW_BYTES>(ra + 4, col >> 3) + (col & 7) * 2;
+  return cat44(lds_tr_asm(img, oa), lds_tr_asm(img, ob));
+}
+
 // Transposed operand with the ACCUMULATOR k order (pairs with an f32x16
 // accumulator converted by acc_to_frag): element j of lane half h holds
 // image[k0 + 8*(j>>2) + 4*h + (j&3)][x0 + (lane&31)].

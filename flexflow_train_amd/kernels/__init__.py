@@ -463,6 +463,59 @@ def gemm256(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0
     return out
 
 
+def gemmp_supported(a, b, trans_a=False, trans_b=False) -> bool:
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
+        return False
+    if a.stride(1) != 1 or b.stride(1) != 1 or a.data_ptr() % 16 or b.data_ptr() % 16:
+        return False
+    if not hasattr(ext(), "gemmp"):
+        return False
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N = b.shape[0] if trans_b else b.shape[1]
+    return bool(ext().gemmp_supported(M, N, K, a.stride(0), b.stride(0), bool(trans_a), bool(trans_b)))
+
+
+def gemmp(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, beta=0.0, out=None,
+          out_dtype=None, pre=None, aux=None, act_bwd=False, dbias=None, splits=1, _dbg=0):
+    """Phase-pipelined 256x256 MFMA GEMM (csrc/kernels/gemmp.hip):
+    C = epi(alpha * op(a) op(b)); epi = [+bias] [pre := .] [act(.) or, with
+    ``act_bwd``, . * act'(aux)] [dbias += colsum] [+ beta * C].  Split-K
+    (``splits`` > 1): fp32 partial slabs + a reduce pass, plain epilogue only."""
+    if not gemmp_supported(a, b, trans_a, trans_b):
+        raise ValueError("gemmp: unsupported operands (bf16, 16-B aligned, K % 64, dims % 8)")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemmp: inner dims differ ({K} vs {Kb})")
+    dt = out_dtype or (out.dtype if out is not None else torch.bfloat16)
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=dt)
+    if out.shape != (M, N) or out.stride(1) != 1:
+        raise ValueError("gemmp: bad output")
+    for t, nm, n in ((bias, "bias", N), (pre, "pre", M * N), (aux, "aux", M * N)):
+        if t is not None:
+            _check(t, nm, torch.bfloat16, n)
+    if dbias is not None:
+        _check(dbias, "dbias", torch.float32, N)
+    if act_bwd and (aux is None or act == "none"):
+        raise ValueError("gemmp: act_bwd needs aux and an activation")
+    s = max(1, int(splits))
+    if bias is not None or pre is not None or act != "none" or dbias is not None:
+        s = 1
+    ws = None
+    if s > 1:
+        key = (a.device, s * M * N)
+        ws = _WS_CACHE.get(key)
+        if ws is None:
+            ws = torch.empty(s * M * N, device=a.device, dtype=torch.float32)
+            _WS_CACHE[key] = ws
+    ext().gemmp(a.data_ptr(), b.data_ptr(), out.data_ptr(), _p(bias), _p(pre), _p(aux), _p(dbias), M, N, K,
+                a.stride(0), b.stride(0), out.stride(0), bool(trans_a), bool(trans_b), ACT_CODES[act], bool(act_bwd),
+                float(alpha), float(beta), int(out.dtype == torch.float32), s, _p(ws), _stream(), int(_dbg))
+    STATS["gemmp"] += 1
+    return out
+
+
 # ---------------------------------------------------------------------------
 # General tensor operators (csrc/kernels/tensorops.hip).  Inputs: contiguous
 # GPU tensors in bf16 or fp32; _check's 16-byte alignment is not required.

@@ -61,6 +61,10 @@ class LinearOp(OpImpl):
         # stored copies stay in sync; only replica 0 adds the bias in forward
         db = weight_grads[1] if has_bias else None
         dW = weight_grads[0]
+        if ctx.extra.pop("grad_is_preact", False):
+            # the consumer's dX GEMM already applied act' and accumulated db (gemmp epilogue)
+            act = "none"
+            db = None
         if dy2.is_cuda and dy2.dtype == torch.bfloat16 and K.available() and dy2.shape[1] % 8 == 0:
             if act != "none":
                 g = K.colsum_act(dy2, pre, act, db, write_dx=True)
@@ -84,6 +88,19 @@ class LinearOp(OpImpl):
             else:
                 acc_grad(dW, x2.float().t() @ g.float())
         dx = None
+        dact = ctx.extra.pop("dact", None)
+        if need_input_grad[0] and dact is not None and g.is_cuda and g.dtype == torch.bfloat16:
+            act_p, pre_p, db_p, pctx = dact
+            pre2 = pre_p.reshape(-1, W.shape[0])
+            ok = (W.dtype == torch.bfloat16 and pre2.dtype == torch.bfloat16 and pre2.is_contiguous()
+                  and pre2.shape[0] == g.shape[0] and (db_p is None or (db_p.dtype == torch.float32
+                                                                      and db_p.is_contiguous()))
+                  and K.gemmp_supported(g, W, False, True))
+            if ok and _dact_fused_wins(g, W, pre2, act_p, db_p is not None):
+                dx = K.gemmp(g, W, trans_b=True, act=act_p, aux=pre2, act_bwd=True,
+                             dbias=db_p.reshape(-1) if db_p is not None else None)
+                pctx.extra["grad_is_preact"] = True
+                return [dx.reshape(*dy.shape[:-1], W.shape[0])]
         if need_input_grad[0]:
             acc = ctx.extra.get("grad_acc", [None])[0]
             if acc is not None and acc.is_cuda and acc.dtype == g.dtype and acc.is_contiguous():
@@ -92,6 +109,30 @@ class LinearOp(OpImpl):
             dx = matmul(g, W, trans_b=True) if g.is_cuda else (g @ W.to(g.dtype).t())
             dx = dx.reshape(*dy.shape[:-1], W.shape[0])
         return [dx]
+
+
+_DACT_CHOICE = {}
+
+
+def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:
+    """Measure once per shape (outside graph capture): the fused input-gradient
+    GEMM with the activation-gradient + bias-gradient epilogue (gemmp) against
+    the autotuned plain GEMM followed by the producer's colsum_act pass."""
+    key = (tuple(g.shape), tuple(W.shape), act, has_bias)
+    hit = _DACT_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    from .gemm import _time
+    db = torch.zeros(W.shape[0], device=g.device, dtype=torch.float32)
+    fused = _time(lambda: K.gemmp(g, W, trans_b=True, act=act, aux=pre, act_bwd=True,
+                                  dbias=db if has_bias else None))
+    dx = matmul(g, W, trans_b=True)   # settles the autotuner's pick first
+    plain = _time(lambda: (matmul(g, W, trans_b=True),
+                           K.colsum_act(dx, pre, act, db if has_bias else None, write_dx=True)))
+    _DACT_CHOICE[key] = fused < plain
+    return _DACT_CHOICE[key]
 
 
 @register("BATCHMATMUL", "MATMUL")

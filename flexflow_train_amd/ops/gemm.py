@@ -9,9 +9,11 @@ torch.mm / addmm) is the plain library GEMM.  ``FF_GEMM`` selects:
   don't guess".  Candidates: hipBLASLt through torch.mm (its heuristic's first
   pick), hipBLASLt called directly with each of its top ``FF_GEMM_LT_ALGOS``
   (default 4) heuristic candidates (``lt:i``, csrc/kernels/blaslt.hip, bias
-  in the library epilogue), the 128² register-staged MFMA kernel, and the
-  256² LDS-DMA kernel (csrc/kernels/gemm256.hip) at several split-K degrees
-  (the long-K weight-gradient GEMMs are where split-K wins);
+  in the library epilogue), the 128² register-staged MFMA kernel, the
+  256² LDS-DMA kernel (csrc/kernels/gemm256.hip) and the phase-pipelined
+  persistent 256² kernel (``p:s``, csrc/kernels/gemmp.hip, fused bias /
+  activation / pre-activation epilogue) at several split-K degrees (the
+  long-K weight-gradient GEMMs are where split-K wins);
 * ``hip``: always the MFMA kernel; ``blas``: always hipBLASLt.
 
 On CPU everything is a torch matmul in the compute dtype.
@@ -27,6 +29,7 @@ from .. import kernels as K
 
 _MODE = os.environ.get("FF_GEMM", "auto")
 _CHOICE: Dict[Tuple, str] = {}
+_TIMES: Dict[Tuple, Dict[str, float]] = {}   # autotuner measurements (ms), for reports
 _ACT = {
     "none": lambda t: t,
     "relu": torch.relu,
@@ -45,6 +48,20 @@ def set_mode(mode: str):
 
 def choices() -> Dict[Tuple, str]:
     return dict(_CHOICE)
+
+
+def report() -> str:
+    """One line per tuned GEMM signature: shape, transposes, epilogue, the
+    candidates' times (ms) and the pick."""
+    lines = []
+    for key, ch in _CHOICE.items():
+        (ash, bsh, ta, tb, bias, act, odt, beta, pre) = key[:9]
+        t = _TIMES.get(key, {})
+        best = sorted(t.items(), key=lambda kv: kv[1])[:4]
+        lines.append(f"a{list(ash)} b{list(bsh)} ta={int(ta)} tb={int(tb)} bias={int(bias)} act={act} "
+                     f"out={str(odt).replace('torch.', '')} beta={int(beta)} pre={int(pre)} -> {ch}  "
+                     + " ".join(f"{k}:{v:.3f}" for k, v in best))
+    return "\n".join(lines)
 
 
 def _hip_ok(a, b, trans_a, trans_b) -> bool:
@@ -133,6 +150,20 @@ def _hip256(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
                      splits=splits)
 
 
+def _gp(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
+    return K.gemmp(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
+                   splits=splits)
+
+
+def _gp_ok(bias, act, out, beta, pre) -> bool:
+    """Epilogues gemmp implements: plain (alpha/beta, bf16 or fp32 out) or
+    bias/activation/pre-activation into a fresh bf16 output."""
+    if bias is None and act == "none" and pre is None:
+        return True
+    return not beta and (out is None or out.dtype == torch.bfloat16) and act in ("none", "relu", "sigmoid", "tanh",
+                                                                                   "gelu")
+
+
 def _lt(a, b, trans_a, trans_b, bias, act, out, beta, pre, algo=0):
     """hipBLASLt called directly with the ``algo``-th heuristic candidate
     (torch.mm always takes the first); bias in the GEMM epilogue, the
@@ -182,6 +213,16 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
             splits |= {s for s in (d // 2, d, d * 2) if 1 <= s <= max(1, Kd // 512)}
         for s in sorted(splits):
             c[f"hip256:{s}"] = (lambda s_: (lambda *args: _hip256(*args, splits=s_)))(s)
+    if os.environ.get("FF_GEMMP", "1") != "0" and K.gemmp_supported(a, b, trans_a, trans_b) and _gp_ok(
+            bias, act, out, beta, pre):
+        M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+        N = b.shape[0] if trans_b else b.shape[1]
+        splits = {1}
+        if bias is None and act == "none" and pre is None:
+            d = K.default_splits(M, N, Kd)
+            splits |= {s for s in (d // 2, d, d * 2) if 1 <= s <= max(1, Kd // 512) and (Kd // 64) % s == 0}
+        for s in sorted(splits):
+            c[f"p:{s}"] = (lambda s_: (lambda *args: _gp(*args, splits=s_)))(s)
     return c
 
 
@@ -232,8 +273,11 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
             times = {name: _time(lambda fn=fn: fn(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))
                      for name, fn in cands.items()}
             choice = min(times, key=times.get)
+            _TIMES[key] = times
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
+        choice = "hip"
+    if choice.startswith("p:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -251,4 +295,6 @@ def _resolve(name: str):
     kind, _, arg = name.partition(":")
     if kind == "lt":
         return lambda *args: _lt(*args, algo=int(arg))
+    if kind == "p":
+        return lambda *args: _gp(*args, splits=int(arg))
     return lambda *args: _hip256(*args, splits=int(arg))

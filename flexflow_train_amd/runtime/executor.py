@@ -26,6 +26,7 @@ import gc
 import hashlib
 import json
 import math
+import os
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -346,6 +347,8 @@ class Executor:
         if self.cfg.fuse_add_layernorm:
             self._fuse_add_layernorm()
             self._fuse_conv_bn()
+            if os.environ.get("FF_FUSE_DACT", "1") != "0":
+                self._fuse_linear_dact()
         self._mark_requires_grad()
         self._assign_params_to_buffers()
 
@@ -430,6 +433,32 @@ class Executor:
             else:
                 keep.append(s)
         self.steps = keep
+
+    def _fuse_linear_dact(self):
+        """LINEAR(act) -> LINEAR: the second layer's input-gradient GEMM
+        applies the first layer's activation derivative and accumulates its
+        bias gradient in its epilogue (gemmp act_bwd + dbias), so the first
+        layer's backward starts from the pre-activation gradient and skips its
+        own activation-backward / bias-gradient pass (colsum_act: a read of the
+        gradient and the pre-activation plus a write).  Decided per step at
+        run time (GPU bf16 operands the kernel supports); otherwise both
+        layers run unfused."""
+        by_out = {o: s for s in self.steps for o in s.outputs}
+        uses: Dict[Value, List[Step]] = {}
+        for s in self.steps:
+            for v in s.inputs:
+                uses.setdefault(v, []).append(s)
+        for s in self.steps:
+            if s.kind != "compute" or s.op_type != "LINEAR" or not s.inputs:
+                continue
+            v = s.inputs[0]
+            prod = by_out.get(v)
+            if (prod is None or prod.kind != "compute" or prod.op_type != "LINEAR"
+                    or prod.ctx.a("activation", "none") not in ("relu", "sigmoid", "tanh", "gelu")
+                    or len(uses.get(v, [])) != 1 or v == self.loss_value or prod.ctx.sum_degree != 1
+                    or self.value_layout[v] != self.value_layout[prod.outputs[0]]):
+                continue
+            s.ctx.extra["dact_src"] = prod
 
     def _mark_requires_grad(self):
         rg: Dict[Value, bool] = {}
@@ -854,6 +883,12 @@ class Executor:
         self._works = []
         prof = self.cfg.profiling
         n = len(self.steps)
+        if getattr(self, "_step_index", None) is None or len(self._step_index) != n:
+            self._step_index = {id(st): k for k, st in enumerate(self.steps)}
+            self._dact_srcs = [st.ctx.extra["dact_src"] for st in self.steps
+                               if st.ctx is not None and "dact_src" in st.ctx.extra]
+        for src in self._dact_srcs:
+            src.ctx.extra.pop("grad_is_preact", None)
         for i in range(n - 1, -1, -1):
             s = self.steps[i]
             if s is self.softmax_fused_step and self.loss is not None and self.loss.fuses_softmax:
@@ -889,6 +924,15 @@ class Executor:
                     s.ctx.extra["wgrad_beta"] = [0.0 if (p.n_consumers == 1 and not accumulate) else 1.0
                                                  for p in s.weights]
                     s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
+                    src = s.ctx.extra.get("dact_src")
+                    s.ctx.extra.pop("dact", None)
+                    if src is not None and need[0] and s.inputs[0] not in self.retain:
+                        # (activation, pre-activation, producer's fp32 bias grad, producer ctx)
+                        ps = self._saved.get(self._step_index[id(src)])
+                        if ps is not None and ps[1] is not None:
+                            bw = src.weights[1] if len(src.weights) > 1 else None
+                            db = bw.grad if (bw is not None and bw.trainable) else None
+                            s.ctx.extra["dact"] = (src.ctx.a("activation"), ps[1], db, src.ctx)
                     impl = opbase.get_impl(s.op_type)
                     t0 = self.tracer.begin(f"{s.name}:bwd", "compute", self.step_num) if prof else None
                     gins = impl.backward(s.ctx, saved, gouts, wgs, need)

@@ -129,3 +129,43 @@ def test_fit_uses_hipgraph():
     m.fit(x=xs, y=ys, epochs=6)
     assert getattr(m.executor, "_graph", None) is not None
     assert m.executor.perf_metrics().get_accuracy() > 50.0
+
+
+def _mlp_gelu(fuse: bool):
+    from flexflow_train_amd.core import ActiMode, DataType
+    cfg = FFConfig()
+    cfg.perform_fusion = fuse
+    m = FFModel(cfg)
+    x = m.create_tensor([256, 128], DataType.DT_FLOAT, name="x")
+    t = m.dense(x, 512, ActiMode.AC_MODE_GELU, name="fc1")
+    t = m.dense(t, 128, name="fc2")
+    t = m.dense(t, 16, name="out")
+    m.softmax(t, name="sm")
+    m.compile(optimizer=AdamOptimizer(m, alpha=1e-3), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+    ex = m.executor
+    g = torch.Generator().manual_seed(5)
+    for n in sorted(ex.parameter_names()):
+        ex.set_parameter(n, torch.randn(ex.get_parameter(n).shape, generator=g) * 0.1)
+    dev = ex.cfg.device
+    feeds = {"x": torch.randn(256, 128, generator=g).to(dev)}
+    labels = torch.randint(0, 16, (256,), generator=g).to(dev)
+    return ex, feeds, labels
+
+
+def test_linear_activation_gradient_fusion():
+    """fc1(GELU) -> fc2: fc2's input-gradient GEMM applies GELU' and fc1's
+    bias gradient in its epilogue (gemmp); the result equals the unfused
+    backward (colsum_act) parameter by parameter."""
+    a, feeds, labels = _mlp_gelu(True)
+    b, _, _ = _mlp_gelu(False)
+    fc2 = next(s for s in a.steps if s.name == "fc2")
+    assert "dact_src" in fc2.ctx.extra
+    before = K.STATS["gemmp"]
+    for _ in range(3):
+        a.train_step(feeds, labels)
+        b.train_step(feeds, labels)
+    torch.cuda.synchronize()
+    assert K.STATS["gemmp"] > before, "fused path not taken"
+    for n in a.parameter_names():
+        torch.testing.assert_close(a.get_parameter(n), b.get_parameter(n), rtol=2e-2, atol=2e-3)

@@ -235,6 +235,43 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
+                                            (296, 136, 1024, 3), (2048, 1536, 640, 1)])
+def test_gemmp(ta, tb, M, N, Kd, splits):
+    """Phase-pipelined persistent GEMM: plain / beta / split-K, the fused
+    bias+activation+pre-activation epilogue and the activation-gradient +
+    bias-gradient epilogue, against fp32 torch."""
+    torch.manual_seed(13)
+    a = torch.randn(Kd, M, device=DEV, dtype=torch.bfloat16) if ta else torch.randn(M, Kd, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    b = torch.randn(N, Kd, device=DEV, dtype=torch.bfloat16) if tb else torch.randn(Kd, N, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    af = a.float().t() if ta else a.float()
+    bf = b.float().t() if tb else b.float()
+    ref = af @ bf
+    c = K.gemmp(a, b, trans_a=ta, trans_b=tb, splits=splits)
+    assert _rel(c, ref) < 1e-2
+    c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
+    K.gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
+    assert _rel(c3, ref + 1) < 1e-2
+    if splits == 1:
+        bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+        pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        c2 = K.gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
+        u = ref + bias.float()
+        assert _rel(pre, u) < 1e-2
+        assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
+        aux = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        db = torch.full((N,), 0.5, device=DEV)
+        g = K.gemmp(a, b, trans_a=ta, trans_b=tb, act="gelu", aux=aux, act_bwd=True, dbias=db)
+        x = aux.float().requires_grad_(True)
+        torch.nn.functional.gelu(x, approximate="tanh").backward(torch.ones_like(x))
+        gr = ref * x.grad
+        assert _rel(g, gr) < 1e-2
+        assert _rel(db, g.float().sum(0) + 0.5) < 1e-4
+
+
 def test_dropout_and_cast():
     x = torch.randn(1 << 16, device=DEV, dtype=torch.bfloat16)
     y = K.dropout(x, 0.25, 1234)
