@@ -14,6 +14,13 @@ compile() (searched, or --strategy dp for the data-parallel baseline).
 Each timed step = forward + loss + backward + gradient all-reduce + Adam
 update over all parameters.  Rank 0 prints ONE JSON line.
 
+Speedup over data parallelism (the reference's Unity-vs-DP protocol,
+scripts/osdi22ae/*.sh): with N > 1 and the searched strategy, the line
+carries ``speedup_over_dp`` — 1.0 when the search itself chose pure data
+parallelism, else the searched samples/s over a data-parallel run of the
+same model and batch measured right after (same K / W, outside the headline
+timed region) — plus the search's simulated prediction.
+
 Other BASELINE.json configs run through the same contract with --model:
   resnet50     ResNet-50, synthetic 224x224 ImageNet batches (1000 classes),
                per-GPU batch 256, SGD momentum 0.9
@@ -24,6 +31,8 @@ Other BASELINE.json configs run through the same contract with --model:
                vocab 50257), per-GPU batch 8, AdamW
 """
 import argparse
+import collections
+import gc
 import json
 import os
 import sys
@@ -45,6 +54,8 @@ def main():
                     choices=["bert-large", "bert-base", "resnet50", "dlrm", "gpt3-medium"])
     ap.add_argument("--layers", type=int, default=None, help="override (debug only; invalidates the metric)")
     ap.add_argument("--strategy", default="search", choices=["search", "dp"])
+    ap.add_argument("--no-dp-compare", action="store_true",
+                    help="skip the data-parallel reference run behind speedup_over_dp")
     ap.add_argument("--gemm", default=os.environ.get("FF_GEMM", "auto"))
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--graph", type=int, default=-1,
@@ -53,21 +64,101 @@ def main():
     args = ap.parse_args()
 
     os.environ["FF_GEMM"] = args.gemm
-    import torch
-
-    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType)
-    from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
-    from flexflow_train_amd.ops.gemm import choices as gemm_choices
-    import collections
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    if args.model not in ("bert-large", "bert-base"):
-        return bench_zoo(args, world, rank)
-    args.batch_per_gpu = args.batch_per_gpu or 32
-    global_batch = args.batch_per_gpu * world
+    runner = _run_bert if args.model in ("bert-large", "bert-base") else _run_zoo
+
+    res = runner(args, world, rank, only_dp=args.strategy == "dp")
+    speed = {}
+    if world > 1 and args.strategy == "search":
+        pred = res["search"].get("predicted_speedup_over_dp")
+        if pred is not None:
+            speed["predicted_speedup_over_dp"] = round(float(pred), 3)
+        if res["config"]["parallelism"].startswith("dp"):
+            speed["speedup_over_dp"] = 1.0
+            speed["dp_reference"] = "the searched strategy is data parallel"
+        elif not args.no_dp_compare:
+            sps = res["value"]
+            _release(res)
+            dp = runner(args, world, rank, only_dp=True)
+            speed["dp_samples_per_sec"] = round(dp["value"], 2)
+            speed["speedup_over_dp"] = round(sps / dp["value"], 3)
+            speed["dp_reference"] = "measured: data-parallel run of the same model / batch after the timed run"
+    if rank == 0:
+        conf = res["config"]
+        conf.update(speed)
+        print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(res["value"], 2),
+                          "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "bf16", "data": res["data"], "config": conf}), flush=True)
+        if os.environ.get("FF_GEMM_REPORT"):
+            from flexflow_train_amd.ops.gemm import report
+            print(report(), file=sys.stderr)
+        if args.profile and res.get("profile"):
+            print(json.dumps({"profile_ms_total": res["profile"]}), file=sys.stderr)
+
+
+def _release(res):
+    """Drop a finished run's model, executor and captured graphs before the
+    next one (the DP reference) allocates its own."""
+    import torch
+    for k in ("model", "ex", "step"):
+        res.pop(k, None)
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def _time_steps(args, ex, feeds, labels, global_batch):
+    """W untimed warm-up steps, then EXACTLY K timed steps bracketed by a
+    barrier + device synchronisation on both sides; max over ranks."""
+    import torch
+
+    dev = ex.cfg.device
+
+    def step():
+        ex.train_step(feeds, labels)
+
+    graphed = False
+    use_graph = args.graph if args.graph >= 0 else 1
+    if use_graph and dev.type == "cuda" and not args.profile:
+        try:
+            step = ex.make_graphed_train_step(feeds, labels)
+            graphed = True
+        except Exception as e:  # noqa: BLE001 — fall back to eager execution
+            print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
+    for _ in range(args.warmup):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ex.dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ex.dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = ex.dist.max_scalar(time.perf_counter() - t0)
+    return {"value": global_batch * args.steps / elapsed, "ms": elapsed / args.steps * 1000.0, "graphed": graphed,
+            "step": step}
+
+
+def _run_bert(args, world, rank, only_dp: bool):
+    import torch
+
+    from flexflow_train_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+    from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
+    from flexflow_train_amd.ops.gemm import choices as gemm_choices
+
+    bpg = args.batch_per_gpu or 32
+    global_batch = bpg * world
     mk = bert_large if args.model == "bert-large" else bert_base
     kw = dict(batch_size=global_batch, sequence_length=args.seq)
     if args.layers:
@@ -78,9 +169,9 @@ def main():
     cfg.batch_size = global_batch
     cfg.print_freq = 0
     cfg.profiling = args.profile
-    cfg.only_data_parallel = args.strategy == "dp"
+    cfg.only_data_parallel = only_dp
     model = FFModel(cfg)
-    inputs, out = build_bert(model, bcfg)
+    build_bert(model, bcfg)
     t0 = time.time()
     model.compile(optimizer=AdamOptimizer(model, alpha=1e-4, weight_decay=0.01, decoupled=True),
                   loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
@@ -103,79 +194,32 @@ def main():
     lshape = ex._loss_layout().piece_shape[:-1]
     labels = torch.randint(0, bcfg.vocab_size, lshape, generator=g, device=dev, dtype=torch.int64)
 
-    def step():
-        ex.train_step(feeds, labels)
-
-    graphed = False
-    use_graph = args.graph if args.graph >= 0 else 1
-    if use_graph and dev.type == "cuda" and not args.profile:
-        try:
-            step = ex.make_graphed_train_step(feeds, labels)
-            graphed = True
-        except Exception as e:  # noqa: BLE001 — fall back to eager execution
-            print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
-
-    for _ in range(args.warmup):
-        step()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    ex.dist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    ex.dist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    elapsed = ex.dist.max_scalar(time.perf_counter() - t0)
-    ms = elapsed / args.steps * 1000.0
-    sps = global_batch * args.steps / elapsed
+    t = _time_steps(args, ex, feeds, labels, global_batch)
     pm = ex.perf_metrics()
-    if rank == 0:
-        par = model.search_report.get("source", "")
-        res = {
-            "metric": "samples_per_sec_whole_node",
-            "value": round(sps, 2),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic token ids, random-init weights",
-            "config": {
-                "model": args.model + ("" if not args.layers else f"-{args.layers}L(debug)"),
-                "global_batch": global_batch,
-                "seq_len": args.seq,
-                "parallelism": _parallelism(model, world),
-                "strategy_source": par,
-                "layers": bcfg.num_encoder_layers,
-                "hidden": bcfg.hidden_size,
-                "heads": bcfg.num_heads,
-                "vocab": bcfg.vocab_size,
-                "optimizer": "adamw",
-                "compile_s": round(compile_s, 2),
-                "hipgraph": graphed,
-                "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
-                "gemm_choices": dict(collections.Counter(gemm_choices().values())),
-                "tokens_per_sec": round(sps * args.seq, 1),
-                "final_loss": round(pm.loss, 4),
-            },
-        }
-        print(json.dumps(res), flush=True)
-        if os.environ.get("FF_GEMM_REPORT"):
-            from flexflow_train_amd.ops.gemm import report
-            print(report(), file=sys.stderr)
-        if args.profile:
-            rep = ex.profile_report()
-            print(json.dumps({"profile_ms_total": {k: round(v, 3) for k, v in list(rep.items())[:40]}}),
-                  file=sys.stderr)
+    conf = {
+        "model": args.model + ("" if not args.layers else f"-{args.layers}L(debug)"),
+        "global_batch": global_batch,
+        "seq_len": args.seq,
+        "parallelism": _parallelism(model, world),
+        "strategy_source": model.search_report.get("source", ""),
+        "layers": bcfg.num_encoder_layers,
+        "hidden": bcfg.hidden_size,
+        "heads": bcfg.num_heads,
+        "vocab": bcfg.vocab_size,
+        "optimizer": "adamw",
+        "compile_s": round(compile_s, 2),
+        "hipgraph": t["graphed"],
+        "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
+        "gemm_choices": dict(collections.Counter(gemm_choices().values())),
+        "tokens_per_sec": round(t["value"] * args.seq, 1),
+        "final_loss": round(pm.loss, 4),
+    }
+    prof = None
+    if args.profile:
+        prof = {k: round(v, 3) for k, v in list(ex.profile_report().items())[:40]}
+    return {"value": t["value"], "ms": t["ms"], "config": conf, "search": dict(model.search_report),
+            "data": "synthetic token ids, random-init weights", "model": model, "ex": ex, "step": t["step"],
+            "profile": prof}
 
 
 def _parallelism(model, world: int) -> str:
@@ -208,7 +252,7 @@ _ZOO = {
 }
 
 
-def bench_zoo(args, world, rank):
+def _run_zoo(args, world, rank, only_dp: bool):
     """The other BASELINE configs: model-zoo network + synthetic data of its
     shape, same timing contract as the BERT path."""
     import dataclasses
@@ -225,7 +269,7 @@ def bench_zoo(args, world, rank):
     cfg.batch_size = global_batch
     cfg.print_freq = 0
     cfg.profiling = args.profile
-    cfg.only_data_parallel = args.strategy == "dp"
+    cfg.only_data_parallel = only_dp
     model = FFModel(cfg)
     inputs, out, mcfg = Z.build(zname, model, batch_size=global_batch, **over)
     ce = Z.loss_of(zname) == Z.LOSS_CE
@@ -238,7 +282,6 @@ def bench_zoo(args, world, rank):
                   metrics=[MetricsType.METRICS_ACCURACY] if ce else [MetricsType.METRICS_MEAN_SQUARED_ERROR])
     compile_s = time.time() - t0
     ex = model.executor
-    dev = ex.cfg.device
 
     # synthetic data of the model's shape, generated at this rank's batch
     first = next(iter(ex.inputs))
@@ -254,50 +297,21 @@ def bench_zoo(args, world, rank):
         labels = ex.local_labels(torch.as_tensor(labels_np))
     del feeds_np, labels_np
 
-    def step():
-        ex.train_step(feeds, labels)
-
-    graphed = False
-    use_graph = args.graph if args.graph >= 0 else 1
-    if use_graph and dev.type == "cuda" and not args.profile:
-        try:
-            step = ex.make_graphed_train_step(feeds, labels)
-            graphed = True
-        except Exception as e:  # noqa: BLE001
-            print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
-    for _ in range(args.warmup):
-        step()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    ex.dist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    ex.dist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    elapsed = ex.dist.max_scalar(time.perf_counter() - t0)
-    ms = elapsed / args.steps * 1000.0
-    sps = global_batch * args.steps / elapsed
+    t = _time_steps(args, ex, feeds, labels, global_batch)
     pm = ex.perf_metrics()
-    if rank == 0:
-        par = model.search_report.get("source", "")
-        conf = {"model": args.model, "global_batch": global_batch,
-                "parallelism": _parallelism(model, world),
-                "strategy_source": par, "optimizer": opt, "compile_s": round(compile_s, 2), "hipgraph": graphed,
-                "final_loss": round(pm.loss, 4)}
-        conf.update(extra)
-        if zname == "gpt":
-            conf["tokens_per_sec"] = round(sps * mcfg.sequence_length, 1)
-        print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(sps, 2), "unit": "samples/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-                          "data": "synthetic inputs of the model's shape, random-init weights", "config": conf}),
-              flush=True)
+    conf = {"model": args.model, "global_batch": global_batch, "parallelism": _parallelism(model, world),
+            "strategy_source": model.search_report.get("source", ""), "optimizer": opt,
+            "compile_s": round(compile_s, 2), "hipgraph": t["graphed"],
+            "graph_segments": list(getattr(ex, "graph_segments", ())) or None, "final_loss": round(pm.loss, 4)}
+    conf.update(extra)
+    if zname == "gpt":
+        conf["tokens_per_sec"] = round(t["value"] * mcfg.sequence_length, 1)
+    prof = None
+    if args.profile:
+        prof = {k: round(v, 3) for k, v in list(ex.profile_report().items())[:40]}
+    return {"value": t["value"], "ms": t["ms"], "config": conf, "search": dict(model.search_report),
+            "data": "synthetic inputs of the model's shape, random-init weights", "model": model, "ex": ex,
+            "step": t["step"], "profile": prof}
 
 
 if __name__ == "__main__":
