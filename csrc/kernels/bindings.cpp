@@ -35,9 +35,13 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("layernorm_bwd_grid", &layernorm_bwd_grid);
   m.def("layernorm_bwd", [](int dt, uintptr_t dy, uintptr_t s, uintptr_t mean, uintptr_t rstd, uintptr_t g,
-                            uintptr_t dx, uintptr_t dg, uintptr_t db, uintptr_t ws, int M, int N, uintptr_t st) {
-    layernorm_bwd(dt, P(dy), P(s), F(mean), F(rstd), P(g), P(dx), F(dg), F(db), F(ws), M, N, S(st));
-  });
+                            uintptr_t dx, uintptr_t dg, uintptr_t db, uintptr_t ws, int M, int N, uintptr_t st,
+                            uintptr_t dres, uintptr_t dsum) {
+    layernorm_bwd(dt, P(dy), P(s), F(mean), F(rstd), P(g), P(dx), F(dg), F(db), F(ws), M, N, S(st), P(dres),
+                  F(dsum));
+  }, py::arg("dt"), py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("g"), py::arg("dx"),
+        py::arg("dg"), py::arg("db"), py::arg("ws"), py::arg("M"), py::arg("N"), py::arg("st"), py::arg("dres") = 0,
+        py::arg("dsum") = 0);
   m.def("bias_act_fwd", [](int dt, uintptr_t x, uintptr_t bias, uintptr_t pre, uintptr_t y, int64_t M, int64_t N,
                            int op, float alpha, uintptr_t st) {
     bias_act_fwd(dt, P(x), P(bias), P(pre), P(y), M, N, op, alpha, S(st));

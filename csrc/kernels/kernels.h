@@ -11,11 +11,13 @@ namespace ffk {
 // ---- layernorm.hip
 void layernorm_fwd(int dtype, const void* x, const void* res, void* sum_out, const void* gamma, const void* beta,
                    void* y, float* mean, float* rstd, int M, int N, float eps, hipStream_t st);
-// ws: 2 * layernorm_bwd_grid(M, N) * N floats (block partials of dgamma/dbeta)
+// ws: 3 * layernorm_bwd_grid(M, N) * N floats (block partials of dgamma/dbeta/dsum).
+// dx = LN'(dy) [+ dres]; dsum += colsum(dx) (the producer Linear's bias grad).
 int layernorm_bwd_grid(int M, int N);
 void layernorm_bwd(int dtype, const void* dy, const void* s, const float* mean, const float* rstd,
                    const void* gamma, void* dx, float* dgamma, float* dbeta, float* ws, int M, int N,
-                   hipStream_t st);
+                   hipStream_t st, const void* dres = nullptr,
+                   float* dsum = nullptr);
 
 // ---- elementwise.hip  (op: 0 identity, 1 relu, 2 sigmoid, 3 tanh, 4 gelu, 5 elu, 6 exp)
 void bias_act_fwd(int dtype, const void* x, const void* bias, void* pre, void* y, int64_t M, int64_t N, int op,

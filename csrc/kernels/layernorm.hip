@@ -186,9 +186,18 @@ template <typename T, int C>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ s,
                                                      const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const T* __restrict__ gamma,
-                                                     T* __restrict__ dx, float* __restrict__ ws, int M) {
+                                                     T* __restrict__ dx, float* __restrict__ ws, int M,
+                                                     const T* __restrict__ dres, float* __restrict__ ws_dx) {
   constexpr int N = C * 512;
   __shared__ float red[4][2][512];
+  // ws_dx: per-block column sums of the final dx (the producing Linear's bias
+  // gradient, reduced with the dgamma/dbeta partials); dres: a gradient that
+  // reached the normalised SUM from another consumer (pre-LN residual stream)
+  float pd[C][8];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pd[c][i] = 0.f;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   float pg[C][8], pb[C][8], gm[C][8];
@@ -253,8 +262,30 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           o[i] = rstd[k] * (dv[k][c][i] * gm[c][i] - sum_g[k] - sv[k][c][i] * sum_gx[k]);
+        if (dres) {
+          float r[8];
+          Vec8<T>::load(dres + base + c * 512 + lane * 8, r);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += r[i];
+        }
         Vec8<T>::store(dx + base + c * 512 + lane * 8, o);
+        if (ws_dx) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) pd[c][i] += o[i];
+        }
       }
+    }
+  }
+  if (ws_dx) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wave][0][lane * 8 + i] = pd[c][i];
+      __syncthreads();
+      for (int j = threadIdx.x; j < 512; j += 256)
+        ws_dx[static_cast<size_t>(blockIdx.x) * N + c * 512 + j] =
+            red[0][0][j] + red[1][0][j] + red[2][0][j] + red[3][0][j];
+      __syncthreads();
     }
   }
   if (!ws) return;
@@ -282,7 +313,7 @@ __global__ __launch_bounds__(256) void ln_bwd_generic(const T* __restrict__ dy, 
                                                       const float* __restrict__ rstd_in,
                                                       const T* __restrict__ gamma, T* __restrict__ dx,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
-                                                      int N) {
+                                                      int N, const T* __restrict__ dres, float* __restrict__ dsum) {
   __shared__ float scratch[4];
   const int row = blockIdx.x;
   const size_t base = static_cast<size_t>(row) * N;
@@ -319,7 +350,16 @@ __global__ __launch_bounds__(256) void ln_bwd_generic(const T* __restrict__ dy, 
       float xh = (sv[i] - mean) * rstd;
       o[i] = rstd * (dv[i] * gm[i] - sum_g - xh * sum_gx);
     }
+    if (dres) {
+      float r[8];
+      Vec8<T>::load(dres + base + col, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] += r[i];
+    }
     Vec8<T>::store(dx + base + col, o);
+    if (dsum)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) atomicAdd(dsum + col + i, o[i]);
   }
 }
 
@@ -350,19 +390,23 @@ static void ln_fwd_t(const void* x, const void* res, void* sum_out, const void* 
 
 template <typename T>
 static void ln_bwd_t(const void* dy, const void* s, const float* mean, const float* rstd, const void* gamma,
-                     void* dx, float* dgamma, float* dbeta, float* ws, int M, int N, hipStream_t st) {
+                     void* dx, float* dgamma, float* dbeta, float* ws, int M, int N, const void* dres, float* dsum,
+                     hipStream_t st) {
   auto DY = static_cast<const T*>(dy);
   auto S = static_cast<const T*>(s);
   auto G = static_cast<const T*>(gamma);
   auto DX = static_cast<T*>(dx);
+  auto DR = static_cast<const T*>(dres);
   if (N % 512 == 0 && N <= 4096) {
     const int grid = layernorm_bwd_grid(M, N);
     float* W = (dgamma || dbeta) ? ws : nullptr;
-    if ((dgamma || dbeta) && ws == nullptr) throw std::invalid_argument("layernorm_bwd: workspace required");
+    if ((dgamma || dbeta || dsum) && ws == nullptr) throw std::invalid_argument("layernorm_bwd: workspace required");
+    float* WD = dsum ? ws + static_cast<size_t>(2) * grid * N : nullptr;
     switch (N / 512) {
 #define FFK_LNB_CASE(c)                                                                                      \
   case c:                                                                                                    \
-    hipLaunchKernelGGL((ln_bwd_kernel<T, c>), dim3(grid), dim3(256), 0, st, DY, S, mean, rstd, G, DX, W, M); \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, c>), dim3(grid), dim3(256), 0, st, DY, S, mean, rstd, G, DX, W, M, DR, \
+                       WD);                                                                                  \
     break;
       FFK_LNB_CASE(1) FFK_LNB_CASE(2) FFK_LNB_CASE(3) FFK_LNB_CASE(4) FFK_LNB_CASE(5) FFK_LNB_CASE(6)
       FFK_LNB_CASE(7) FFK_LNB_CASE(8)
@@ -371,10 +415,11 @@ static void ln_bwd_t(const void* dy, const void* s, const float* mean, const flo
     FFK_LAUNCH_CHECK("layernorm_bwd");
     if (dgamma) colsum_act(kF32, ws, nullptr, nullptr, dgamma, grid, N, 0, 1.f, st);
     if (dbeta) colsum_act(kF32, ws + static_cast<size_t>(grid) * N, nullptr, nullptr, dbeta, grid, N, 0, 1.f, st);
+    if (dsum) colsum_act(kF32, WD, nullptr, nullptr, dsum, grid, N, 0, 1.f, st);
     return;
   } else {
     hipLaunchKernelGGL((ln_bwd_generic<T>), dim3(M), dim3(256), 0, st, DY, S, mean, rstd, G, DX, dgamma, dbeta, M,
-                       N);
+                       N, DR, dsum);
   }
   FFK_LAUNCH_CHECK("layernorm_bwd");
 }
@@ -394,10 +439,10 @@ int layernorm_bwd_grid(int M, int N) {
 
 void layernorm_bwd(int dtype, const void* dy, const void* s, const float* mean, const float* rstd,
                    const void* gamma, void* dx, float* dgamma, float* dbeta, float* ws, int M, int N,
-                   hipStream_t st) {
+                   hipStream_t st, const void* dres, float* dsum) {
   if (N % 8 != 0) throw std::invalid_argument("layernorm: N must be a multiple of 8");
-  if (dtype == kBF16) ln_bwd_t<bf16>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, ws, M, N, st);
-  else if (dtype == kF32) ln_bwd_t<float>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, ws, M, N, st);
+  if (dtype == kBF16) ln_bwd_t<bf16>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, ws, M, N, dres, dsum, st);
+  else if (dtype == kF32) ln_bwd_t<float>(dy, s, mean, rstd, gamma, dx, dgamma, dbeta, ws, M, N, dres, dsum, st);
   else throw std::invalid_argument("layernorm: unsupported dtype");
 }
 

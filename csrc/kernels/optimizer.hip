@@ -28,6 +28,76 @@ __device__ __forceinline__ f32x4 load_grad4<bf16>(const bf16* g, int64_t i) {
 
 // Gradients are fp32 (atomically accumulated parameters) or bf16 (GEMM
 // weight gradients written straight by the dW GEMM epilogue).
+// 8 consecutive elements per thread per iteration: two 16-byte loads of each
+// fp32 stream and one 16-byte load of a bf16 gradient, so a wave keeps ~2x the
+// bytes in flight of the 4-wide form (the update is purely HBM-bound:
+// 30 bytes / parameter).
+template <typename GT>
+__device__ __forceinline__ void load_grad8(const GT* g, int64_t i, f32x4& a, f32x4& b);
+template <>
+__device__ __forceinline__ void load_grad8<float>(const float* g, int64_t i, f32x4& a, f32x4& b) {
+  a = reinterpret_cast<const f32x4*>(g)[2 * i];
+  b = reinterpret_cast<const f32x4*>(g)[2 * i + 1];
+}
+template <>
+__device__ __forceinline__ void load_grad8<bf16>(const bf16* g, int64_t i, f32x4& a, f32x4& b) {
+  const u16x8 u = reinterpret_cast<const u16x8*>(g)[i];
+  a = f32x4{u2f(u[0]), u2f(u[1]), u2f(u[2]), u2f(u[3])};
+  b = f32x4{u2f(u[4]), u2f(u[5]), u2f(u[6]), u2f(u[7])};
+}
+
+template <typename GT>
+__global__ __launch_bounds__(256) void adam8_kernel(float* __restrict__ w, const GT* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16* __restrict__ w_bf16, int64_t n8, float lr, float beta1,
+                                                    float beta2, float eps, float weight_decay, float bc1,
+                                                    float bc2_sqrt, float grad_scale, int decoupled,
+                                                    const float* __restrict__ hp) {
+  if (hp) {  // device-resident {lr, step}: hipGraph replays see the current values
+    lr = hp[0];
+    bc1 = 1.f - __powf(beta1, hp[1]);
+    bc2_sqrt = sqrtf(1.f - __powf(beta2, hp[1]));
+  }
+  const float inv_bc1 = 1.f / bc1, inv_bc2s = 1.f / bc2_sqrt;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    f32x4 W[2], G[2], Mm[2], Vv[2];
+    W[0] = reinterpret_cast<f32x4*>(w)[2 * i];
+    W[1] = reinterpret_cast<f32x4*>(w)[2 * i + 1];
+    load_grad8<GT>(g, i, G[0], G[1]);
+    Mm[0] = reinterpret_cast<f32x4*>(m)[2 * i];
+    Mm[1] = reinterpret_cast<f32x4*>(m)[2 * i + 1];
+    Vv[0] = reinterpret_cast<f32x4*>(v)[2 * i];
+    Vv[1] = reinterpret_cast<f32x4*>(v)[2 * i + 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float gg = G[h][k] * grad_scale;
+        if (!decoupled) gg += weight_decay * W[h][k];
+        Mm[h][k] = beta1 * Mm[h][k] + (1.f - beta1) * gg;
+        Vv[h][k] = beta2 * Vv[h][k] + (1.f - beta2) * gg * gg;
+        float upd = (Mm[h][k] * inv_bc1) / (sqrtf(Vv[h][k]) * inv_bc2s + eps);
+        if (decoupled) upd += weight_decay * W[h][k];
+        W[h][k] -= lr * upd;
+      }
+    reinterpret_cast<f32x4*>(w)[2 * i] = W[0];
+    reinterpret_cast<f32x4*>(w)[2 * i + 1] = W[1];
+    reinterpret_cast<f32x4*>(m)[2 * i] = Mm[0];
+    reinterpret_cast<f32x4*>(m)[2 * i + 1] = Mm[1];
+    reinterpret_cast<f32x4*>(v)[2 * i] = Vv[0];
+    reinterpret_cast<f32x4*>(v)[2 * i + 1] = Vv[1];
+    if (w_bf16) {
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[k] = f2bf(W[0][k]);
+        o[4 + k] = f2bf(W[1][k]);
+      }
+      reinterpret_cast<bf16x8*>(w_bf16)[i] = o;
+    }
+  }
+}
+
 template <typename GT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ w, const GT* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -119,6 +189,19 @@ void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void
   need4(n, "adam");
   float bc1 = 1.f - powf(beta1, static_cast<float>(step));
   float bc2s = sqrtf(1.f - powf(beta2, static_cast<float>(step)));
+  if (n % 8 == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0 && (reinterpret_cast<uintptr_t>(w_bf16) & 15) == 0) {
+    const int grid8 = grid_for(n / 8, 256, 256 * 16);
+    if (grad_dtype == kBF16)
+      hipLaunchKernelGGL(adam8_kernel<bf16>, dim3(grid8), dim3(256), 0, st, w, static_cast<const bf16*>(g), m, v,
+                         static_cast<bf16*>(w_bf16), n / 8, lr, beta1, beta2, eps, weight_decay, bc1, bc2s,
+                         grad_scale, decoupled, hp);
+    else
+      hipLaunchKernelGGL(adam8_kernel<float>, dim3(grid8), dim3(256), 0, st, w, static_cast<const float*>(g), m, v,
+                         static_cast<bf16*>(w_bf16), n / 8, lr, beta1, beta2, eps, weight_decay, bc1, bc2s,
+                         grad_scale, decoupled, hp);
+    FFK_LAUNCH_CHECK("adam");
+    return;
+  }
   int grid = grid_for(n / 4, 256, 256 * 8);
   if (grad_dtype == kBF16)
     hipLaunchKernelGGL(adam_kernel<bf16>, dim3(grid), dim3(256), 0, st, w, static_cast<const bf16*>(g), m, v,

@@ -115,21 +115,26 @@ def layernorm_fwd(x, gamma, beta, eps, residual=None, save_sum=True):
     return y, (s if residual is not None else x), mean, rstd
 
 
-def layernorm_bwd(dy, s, mean, rstd, gamma, dgamma=None, dbeta=None):
+def layernorm_bwd(dy, s, mean, rstd, gamma, dgamma=None, dbeta=None, dres=None, dsum=None):
+    """dx = LN'(dy) [+ dres]; dgamma/dbeta/dsum (fp32) accumulate the column
+    sums of dy*xhat, dy and the final dx (dsum: the producing Linear's bias
+    gradient, fused here instead of a separate pass)."""
     N = dy.shape[-1]
     M = dy.numel() // N
     _check(dy, "dy")
     _check(s, "s", dy.dtype, dy.numel())
+    if dres is not None:
+        _check(dres, "dres", dy.dtype, dy.numel())
     dx = torch.empty_like(dy)
-    for name, w in (("dgamma", dgamma), ("dbeta", dbeta)):
+    for name, w in (("dgamma", dgamma), ("dbeta", dbeta), ("dsum", dsum)):
         if w is not None:
             _check(w, name, torch.float32, N)
     grid = ext().layernorm_bwd_grid(M, N)
     ws = None
-    if grid and (dgamma is not None or dbeta is not None):
-        ws = torch.empty(2 * grid * N, device=dy.device, dtype=torch.float32)
+    if grid and (dgamma is not None or dbeta is not None or dsum is not None):
+        ws = torch.empty(3 * grid * N, device=dy.device, dtype=torch.float32)
     ext().layernorm_bwd(_dt(dy), _p(dy), _p(s), _p(mean), _p(rstd), _p(gamma), _p(dx), _p(dgamma), _p(dbeta),
-                        _p(ws), M, N, _stream())
+                        _p(ws), M, N, _stream(), _p(dres), _p(dsum))
     STATS["layernorm_bwd"] += 1
     return dx
 

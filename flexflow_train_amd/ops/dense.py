@@ -61,6 +61,8 @@ class LinearOp(OpImpl):
         # stored copies stay in sync; only replica 0 adds the bias in forward
         db = weight_grads[1] if has_bias else None
         dW = weight_grads[0]
+        if ctx.extra.pop("db_done", False):
+            db = None   # accumulated by the consuming add+LayerNorm's backward (layernorm_bwd dsum)
         if ctx.extra.pop("grad_is_preact", False):
             # the consumer's dX GEMM already applied act' and accumulated db (gemmp epilogue)
             act = "none"

@@ -40,7 +40,10 @@ class _LayerNormBase(OpImpl):
             b = beta.reshape(-1) if beta is not None else None
             y, s, mean, rstd = K.layernorm_fwd(xc.view(-1, N), g, b, eps,
                                                residual=rc.view(-1, N) if rc is not None else None)
-            return [y.view(x.shape)], ("hip", s, mean, rstd, gamma, N)
+            outs = [y.view(x.shape)]
+            if ctx.extra.get("emit_sum"):
+                outs.append(s.view(x.shape))
+            return outs, ("hip", s, mean, rstd, gamma, N)
         xs = x + res if res is not None else x
         shape = x.shape[x.dim() - nax:] if trailing else None
         if not trailing:
@@ -48,18 +51,35 @@ class _LayerNormBase(OpImpl):
         with torch.no_grad():
             y = torch.nn.functional.layer_norm(xs.float(), shape, gamma.float() if gamma is not None else None,
                                                beta.float() if beta is not None else None, eps).to(x.dtype)
-        return [y], ("torch", xs, gamma, beta, shape, eps)
+        outs = [y]
+        if ctx.extra.get("emit_sum"):
+            outs.append(xs)
+        return outs, ("torch", xs, gamma, beta, shape, eps)
 
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
         dy = grad_outputs[0]
+        dsum_in = grad_outputs[1] if len(grad_outputs) > 1 else None   # other consumers of the sum
         dg = weight_grads[0] if len(weight_grads) > 0 else None
         db = weight_grads[1] if len(weight_grads) > 1 else None
+        target = ctx.extra.pop("dsum_target", None)
         if saved[0] == "hip":
             _, s, mean, rstd, gamma, N = saved
+            dres = None
+            if dsum_in is not None:
+                dres = dsum_in.contiguous().view(-1, N)
+                if dres.dtype != dy.dtype:
+                    dres = dres.to(dy.dtype)
+            dsum = None
+            if target is not None and target[0] is not None and target[0].dtype == torch.float32 \
+                    and target[0].is_contiguous() and target[0].numel() == N:
+                dsum = target[0].reshape(-1)
             dx = K.layernorm_bwd(dy.contiguous().view(-1, N), s, mean, rstd,
                                  gamma.reshape(-1) if gamma is not None else None,
                                  dg.reshape(-1) if dg is not None else None,
-                                 db.reshape(-1) if db is not None else None).view(dy.shape)
+                                 db.reshape(-1) if db is not None else None,
+                                 dres=dres, dsum=dsum).view(dy.shape)
+            if dsum is not None:
+                target[1].extra["db_done"] = True
         else:
             _, xs, gamma, beta, shape, eps = saved
             xf = xs.detach().float().requires_grad_(True)
@@ -69,6 +89,8 @@ class _LayerNormBase(OpImpl):
                 y = torch.nn.functional.layer_norm(xf, shape, gf, bf, eps)
             y.backward(dy.float())
             dx = xf.grad.to(dy.dtype)
+            if dsum_in is not None:
+                dx = dx + dsum_in.to(dx.dtype)
             if dg is not None:
                 acc_grad(dg, gf.grad)
             if db is not None:

@@ -356,22 +356,57 @@ class Executor:
         by_out = {o: s for s in self.steps for o in s.outputs}
         keep = []
         drop = set()
+        uses: Dict[Value, List[Step]] = {}
+        for s in self.steps:
+            for v in s.inputs:
+                uses.setdefault(v, []).append(s)
         for s in self.steps:
             if s.kind == "compute" and s.op_type == "LAYERNORM" and len(s.inputs) == 1:
                 v = s.inputs[0]
                 prod = by_out.get(v)
-                if (prod is not None and prod.kind == "compute" and prod.op_type == "EW_ADD"
-                        and len(self._uses.get(v, [])) == 1 and v != self.loss_value
+                if (prod is not None and prod.kind == "compute" and prod.op_type == "EW_ADD" and id(prod) not in drop
+                        and v != self.loss_value
                         and self.value_layout[prod.inputs[0]] == self.value_layout[prod.inputs[1]]
-                        and self.value_layout[v] == self.value_layout[prod.inputs[0]]):
+                        and self.value_layout[v] == self.value_layout[prod.inputs[0]]
+                        and tuple(self.value_layout[v].piece_shape)
+                        == tuple(self.value_layout[prod.inputs[0]].piece_shape)):
                     s.op_type = "FUSED_ADD_LAYERNORM"
                     s.ctx.op_type = "FUSED_ADD_LAYERNORM"
                     s.inputs = list(prod.inputs)
+                    if len(uses.get(v, [])) > 1:
+                        # pre-LN residual stream: the sum also feeds the next
+                        # residual add; the fused kernel writes it as a second output
+                        s.outputs = [s.outputs[0], v]
+                        s.ctx.extra["emit_sum"] = True
                     drop.add(id(prod))
         for s in self.steps:
             if id(s) not in drop:
                 keep.append(s)
         self.steps = keep
+        self._fuse_linear_bias_into_ln()
+
+    def _fuse_linear_bias_into_ln(self):
+        """LINEAR(+bias, no activation) -> FUSED_ADD_LAYERNORM: the input
+        gradient of the add+norm IS the Linear's output gradient, so the norm
+        backward accumulates its column sums straight into the Linear's bias
+        gradient (layernorm_bwd dsum) and the Linear skips its own column-sum
+        pass over the same tensor.  Taken at run time only on the HIP path."""
+        by_out = {o: s for s in self.steps for o in s.outputs}
+        uses: Dict[Value, List[Step]] = {}
+        for s in self.steps:
+            for v in s.inputs:
+                uses.setdefault(v, []).append(s)
+        for s in self.steps:
+            if s.kind != "compute" or s.op_type != "FUSED_ADD_LAYERNORM":
+                continue
+            for v in s.inputs:
+                prod = by_out.get(v)
+                if (prod is not None and prod.kind == "compute" and prod.op_type == "LINEAR"
+                        and prod.ctx.a("activation", "none") == "none" and len(prod.weights) > 1
+                        and prod.ctx.sum_degree == 1 and len(uses.get(v, [])) == 1 and v != self.loss_value
+                        and self.value_layout[v] == self.value_layout[s.inputs[0]]):
+                    s.ctx.extra["dbias_src"] = prod
+                    break
 
     def _fuse_conv_bn(self):
         """CNN fusions (the reference's FusedOp grouping, lib/runtime/src/ops/fused.cc,
@@ -885,10 +920,11 @@ class Executor:
         n = len(self.steps)
         if getattr(self, "_step_index", None) is None or len(self._step_index) != n:
             self._step_index = {id(st): k for k, st in enumerate(self.steps)}
-            self._dact_srcs = [st.ctx.extra["dact_src"] for st in self.steps
-                               if st.ctx is not None and "dact_src" in st.ctx.extra]
-        for src in self._dact_srcs:
-            src.ctx.extra.pop("grad_is_preact", None)
+            self._flag_ctxs = [st.ctx.extra[k].ctx for st in self.steps if st.ctx is not None
+                               for k in ("dact_src", "dbias_src") if k in st.ctx.extra]
+        for c in self._flag_ctxs:   # run-time hand-off flags never outlive a backward pass
+            c.extra.pop("grad_is_preact", None)
+            c.extra.pop("db_done", None)
         for i in range(n - 1, -1, -1):
             s = self.steps[i]
             if s is self.softmax_fused_step and self.loss is not None and self.loss.fuses_softmax:
@@ -924,6 +960,10 @@ class Executor:
                     s.ctx.extra["wgrad_beta"] = [0.0 if (p.n_consumers == 1 and not accumulate) else 1.0
                                                  for p in s.weights]
                     s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
+                    bsrc = s.ctx.extra.get("dbias_src")
+                    s.ctx.extra.pop("dsum_target", None)
+                    if bsrc is not None and bsrc.weights[1] is not None and bsrc.weights[1].trainable:
+                        s.ctx.extra["dsum_target"] = (bsrc.weights[1].grad, bsrc.ctx)
                     src = s.ctx.extra.get("dact_src")
                     s.ctx.extra.pop("dact", None)
                     if src is not None and need[0] and s.inputs[0] not in self.retain:

@@ -1,0 +1,65 @@
+"""Executor fusion passes against the unfused step (FFConfig.perform_fusion
+= False), parameter by parameter after a few training steps:
+
+* pre-LN residual stream (GPT): EW_ADD -> LAYERNORM where the sum also feeds
+  the next residual add -> one FUSED_ADD_LAYERNORM step with two outputs;
+  its backward adds the other consumers' gradient (layernorm_bwd dres);
+* LINEAR(+bias) -> add+LayerNorm: the norm backward accumulates the Linear's
+  bias gradient (layernorm_bwd dsum) — GPU path only;
+* LINEAR(GELU) -> LINEAR: input-gradient GEMM with the activation-gradient
+  epilogue (gemmp) — GPU path, when measured faster.
+
+CPU runs the torch fallbacks of the same steps; the gpu-marked test runs the
+HIP kernels in bf16."""
+import pytest
+import torch
+
+from flexflow_train_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+from flexflow_train_amd.models.transformer import GPTConfig, build_gpt
+
+
+def _gpt(fuse: bool):
+    cfg = FFConfig()
+    cfg.perform_fusion = fuse
+    m = FFModel(cfg)
+    gc = GPTConfig(vocab_size=128, hidden_size=64, num_layers=2, num_heads=2, sequence_length=16, batch_size=4,
+                   pad_vocab_to=64)
+    build_gpt(m, gc)
+    m.compile(optimizer=AdamOptimizer(m, alpha=1e-3), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+    ex = m.executor
+    g = torch.Generator().manual_seed(1)
+    for n in sorted(ex.parameter_names()):
+        ex.set_parameter(n, torch.randn(ex.get_parameter(n).shape, generator=g) * 0.05)
+    dev = ex.cfg.device
+    ids = torch.randint(0, 128, (4, 17), generator=g, dtype=torch.int32)
+    feeds = {"input_ids": ids[:, :16].contiguous().to(dev),
+             "position_ids": torch.arange(16, dtype=torch.int32).expand(4, 16).contiguous().to(dev)}
+    return ex, feeds, ids[:, 1:].long().to(dev)
+
+
+def _compare(tol):
+    a, feeds, labels = _gpt(True)
+    b, _, _ = _gpt(False)
+    fused = [s for s in a.steps if s.op_type == "FUSED_ADD_LAYERNORM"]
+    assert sum(1 for s in fused if s.ctx.extra.get("emit_sum")) >= 4, "pre-LN add+norm not fused"
+    assert any("dbias_src" in s.ctx.extra for s in fused)
+    assert not any(s.op_type == "FUSED_ADD_LAYERNORM" for s in b.steps)
+    for _ in range(3):
+        a.train_step(feeds, labels)
+        b.train_step(feeds, labels)
+    for n in a.parameter_names():
+        torch.testing.assert_close(a.get_parameter(n), b.get_parameter(n), **tol)
+    return a
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="exercises the CPU fallback path")
+def test_pre_ln_fusion_matches_unfused_cpu():
+    _compare(dict(rtol=1e-4, atol=1e-5))
+
+
+@pytest.mark.gpu
+def test_pre_ln_and_bias_fusions_match_unfused_gpu():
+    from flexflow_train_amd import kernels as K
+    a = _compare(dict(rtol=3e-2, atol=3e-3))
+    assert a.cfg.device.type == "cuda" and K.available()
