@@ -218,6 +218,8 @@ class MultiHeadAttentionOp(OpImpl):
         gpu = dout.is_cuda and dout.dtype == torch.bfloat16 and K.available()
         # ---- output projection
         dW_views = _split_weights(dW, E, Hl, kd, vd, Eq, Ek, Ev) if dW is not None else None
+        if ctx.extra.pop("db_done", False):
+            db_out = None   # accumulated by the consuming add+LayerNorm's backward (layernorm_bwd dsum)
         if db_out is not None:
             if gpu:
                 K.colsum_act(dout, None, "none", db_out, write_dx=False)

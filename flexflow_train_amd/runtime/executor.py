@@ -401,11 +401,19 @@ class Executor:
                 continue
             for v in s.inputs:
                 prod = by_out.get(v)
-                if (prod is not None and prod.kind == "compute" and prod.op_type == "LINEAR"
-                        and prod.ctx.a("activation", "none") == "none" and len(prod.weights) > 1
-                        and prod.ctx.sum_degree == 1 and len(uses.get(v, [])) == 1 and v != self.loss_value
+                if prod is None or prod.kind != "compute" or prod.ctx.sum_degree != 1:
+                    continue
+                # (producer, index of its output-bias weight)
+                if (prod.op_type == "LINEAR" and prod.ctx.a("activation", "none") == "none"
+                        and len(prod.weights) > 1):
+                    widx = 1
+                elif prod.op_type == "MULTIHEAD_ATTENTION" and len(prod.weights) > 2:
+                    widx = 2
+                else:
+                    continue
+                if (len(uses.get(v, [])) == 1 and v != self.loss_value
                         and self.value_layout[v] == self.value_layout[s.inputs[0]]):
-                    s.ctx.extra["dbias_src"] = prod
+                    s.ctx.extra["dbias_src"] = (prod, widx)
                     break
 
     def _fuse_conv_bn(self):
@@ -920,8 +928,10 @@ class Executor:
         n = len(self.steps)
         if getattr(self, "_step_index", None) is None or len(self._step_index) != n:
             self._step_index = {id(st): k for k, st in enumerate(self.steps)}
-            self._flag_ctxs = [st.ctx.extra[k].ctx for st in self.steps if st.ctx is not None
-                               for k in ("dact_src", "dbias_src") if k in st.ctx.extra]
+            self._flag_ctxs = [st.ctx.extra["dact_src"].ctx for st in self.steps
+                               if st.ctx is not None and "dact_src" in st.ctx.extra]
+            self._flag_ctxs += [st.ctx.extra["dbias_src"][0].ctx for st in self.steps
+                                if st.ctx is not None and "dbias_src" in st.ctx.extra]
         for c in self._flag_ctxs:   # run-time hand-off flags never outlive a backward pass
             c.extra.pop("grad_is_preact", None)
             c.extra.pop("db_done", None)
@@ -962,8 +972,10 @@ class Executor:
                     s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
                     bsrc = s.ctx.extra.get("dbias_src")
                     s.ctx.extra.pop("dsum_target", None)
-                    if bsrc is not None and bsrc.weights[1] is not None and bsrc.weights[1].trainable:
-                        s.ctx.extra["dsum_target"] = (bsrc.weights[1].grad, bsrc.ctx)
+                    if bsrc is not None:
+                        bw = bsrc[0].weights[bsrc[1]]
+                        if bw is not None and bw.trainable:
+                            s.ctx.extra["dsum_target"] = (bw.grad, bsrc[0].ctx)
                     src = s.ctx.extra.get("dact_src")
                     s.ctx.extra.pop("dact", None)
                     if src is not None and need[0] and s.inputs[0] not in self.retain:

@@ -43,7 +43,8 @@ def _compare(tol):
     b, _, _ = _gpt(False)
     fused = [s for s in a.steps if s.op_type == "FUSED_ADD_LAYERNORM"]
     assert sum(1 for s in fused if s.ctx.extra.get("emit_sum")) >= 4, "pre-LN add+norm not fused"
-    assert any("dbias_src" in s.ctx.extra for s in fused)
+    srcs = [s.ctx.extra["dbias_src"][0].op_type for s in fused if "dbias_src" in s.ctx.extra]
+    assert "LINEAR" in srcs
     assert not any(s.op_type == "FUSED_ADD_LAYERNORM" for s in b.steps)
     for _ in range(3):
         a.train_step(feeds, labels)
@@ -63,3 +64,46 @@ def test_pre_ln_and_bias_fusions_match_unfused_gpu():
     from flexflow_train_amd import kernels as K
     a = _compare(dict(rtol=3e-2, atol=3e-3))
     assert a.cfg.device.type == "cuda" and K.available()
+
+
+def _bert(fuse: bool):
+    from flexflow_train_amd.models.bert import BertConfig, build_bert
+    cfg = FFConfig()
+    cfg.perform_fusion = fuse
+    m = FFModel(cfg)
+    bc = BertConfig(vocab_size=128, hidden_size=64, num_heads=2, dim_feedforward=128, num_encoder_layers=2,
+                    sequence_length=16, batch_size=4, max_position_embeddings=16, type_vocab_size=2)
+    build_bert(m, bc)
+    m.compile(optimizer=AdamOptimizer(m, alpha=1e-3), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+    ex = m.executor
+    g = torch.Generator().manual_seed(2)
+    for n in sorted(ex.parameter_names()):
+        ex.set_parameter(n, torch.randn(ex.get_parameter(n).shape, generator=g) * 0.05)
+    dev = ex.cfg.device
+    feeds = {"input_ids": torch.randint(0, 128, (4, 16), generator=g, dtype=torch.int32).to(dev),
+             "position_ids": torch.arange(16, dtype=torch.int32).expand(4, 16).contiguous().to(dev),
+             "token_type_ids": torch.randint(0, 2, (4, 16), generator=g, dtype=torch.int32).to(dev)}
+    return ex, feeds, torch.randint(0, 128, (4, 16), generator=g).to(dev)
+
+
+def _compare_bert(tol):
+    a, feeds, labels = _bert(True)
+    b, _, _ = _bert(False)
+    srcs = [s.ctx.extra["dbias_src"][0].op_type for s in a.steps if "dbias_src" in s.ctx.extra]
+    assert "MULTIHEAD_ATTENTION" in srcs and "LINEAR" in srcs, srcs
+    for _ in range(3):
+        a.train_step(feeds, labels)
+        b.train_step(feeds, labels)
+    for n in a.parameter_names():
+        torch.testing.assert_close(a.get_parameter(n), b.get_parameter(n), **tol)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="exercises the CPU fallback path")
+def test_post_ln_bias_fusion_matches_unfused_cpu():
+    _compare_bert(dict(rtol=1e-4, atol=1e-5))
+
+
+@pytest.mark.gpu
+def test_post_ln_bias_fusion_matches_unfused_gpu():
+    _compare_bert(dict(rtol=3e-2, atol=3e-3))
