@@ -47,6 +47,7 @@ struct AttnParams {
   int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
   float* lse;    // [B, H, Sq] log2-domain
   float* delta;  // [B, H, Sq]
+  float *dbq, *dbk, *dbv;  // optional [H*D] projection-bias gradients (column sums of dq / dk / dv)
   int B, H, Sq, Sk;
   float scale;       // softmax scale (1/sqrt(D) by default)
   float scale_log2;  // scale * log2(e)
@@ -59,6 +60,25 @@ __device__ __forceinline__ int lds_off(int r, int c) {  // byte offset of chunk 
 template <int D>
 __device__ __forceinline__ bf16x8 tr_frag(const unsigned char* img, int row0, int dt, int lane) {
   return tr_frag_acc<D * 2>(img, row0, dt * 32, lane);
+}
+
+// Bias gradient of a projection: add the column sums of a wave's 32-row
+// output tile (C^T accumulator: lane&31 -> row, registers -> d) times `mul`
+// into db[d] — shuffles over the 32 rows of each lane half, then one fp32
+// atomic per column (32 per lane half).  Rows outside the sequence must hold
+// zeros (they do: masked rows contribute nothing to the accumulators).
+template <int DT>
+__device__ __forceinline__ void bias_colsum(const f32x16 (&acc)[DT], float mul, float* db, int lane) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = acc[dt][r];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if ((lane & 31) == 0) atomicAdd(db + dt * 32 + 8 * (r >> 2) + 4 * h + (r & 3), v * mul);
+    }
 }
 
 // Global [rows][D] tile -> registers (each thread `per` chunks of 16 B).
@@ -349,6 +369,7 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(Att
     }
     __syncthreads();
   }
+  if (P.dbq) bias_colsum<DT>(dq, P.scale, P.dbq + hh * D, lane);
   if (q_ok) {
     bf16* row = P.dq + b * P.dq_sb + static_cast<int64_t>(q) * P.dq_ss + hh * P.dq_sh;
 #pragma unroll
@@ -513,6 +534,11 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
   }
 #pragma unroll
   for (int j = 0; j < NKT; ++j) {
+    if (P.dbk) bias_colsum<DT>(dk[j], P.scale, P.dbk + hh * D, lane);
+    if (P.dbv) bias_colsum<DT>(dv[j], 1.f, P.dbv + hh * D, lane);
+  }
+#pragma unroll
+  for (int j = 0; j < NKT; ++j) {
     if (!k_ok[j]) continue;
     bf16* krow = P.dk + b * P.dk_sb + static_cast<int64_t>(key[j]) * P.dk_ss + hh * P.dk_sh;
     bf16* vrow = P.dv + b * P.dv_sb + static_cast<int64_t>(key[j]) * P.dv_ss + hh * P.dv_sh;
@@ -553,6 +579,9 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
   P.dv_sb = t.dv.sb; P.dv_ss = t.dv.ss; P.dv_sh = t.dv.sh;
   P.lse = t.lse;
   P.delta = t.delta;
+  P.dbq = t.dbq;
+  P.dbk = t.dbk;
+  P.dbv = t.dbv;
   P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
   P.scale = scale;
   P.scale_log2 = scale * 1.4426950408889634f;

@@ -58,6 +58,11 @@ struct AttnTensors {
   T q, k, v, o, dout, dq, dk, dv;
   float* lse = nullptr;
   float* delta = nullptr;
+  // optional fp32 [H*D] bias gradients of the q / k / v projections: the
+  // backward adds the column sums of dq / dk / dv (sum over batch and sequence)
+  float* dbq = nullptr;
+  float* dbk = nullptr;
+  float* dbv = nullptr;
 };
 void attention_fwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, float scale, bool causal,
                    hipStream_t st);

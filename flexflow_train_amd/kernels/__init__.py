@@ -365,7 +365,10 @@ def attention_fwd(q, k, v, causal=False, scale=None, out=None):
     return out, lse
 
 
-def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None):
+def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None, dbias=None):
+    """Flash-attention backward into dq / dk / dv.  ``dbias`` = optional
+    (dbq, dbk, dbv) fp32 [H*D] projection-bias gradients: the kernels add the
+    column sums of dq / dk / dv (over batch and sequence) in their epilogues."""
     B, Sq, H, D = q.shape
     Sk = k.shape[1]
     for name, t, shp in (("o", o, (B, Sq, H, D)), ("do", do, (B, Sq, H, D)), ("dq", dq, (B, Sq, H, D)),
@@ -376,8 +379,14 @@ def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None):
         raise ValueError("attention_bwd: bad lse")
     delta = torch.empty(B, H, Sq, device=q.device, dtype=torch.float32)
     sc = float(scale) if scale is not None else 1.0 / math.sqrt(D)
+    dbs = [0, 0, 0]
+    if dbias is not None:
+        for i, t in enumerate(dbias):
+            if t is not None:
+                _check(t, "dbias", torch.float32, H * D)
+                dbs[i] = t.data_ptr()
     ext().attention_bwd(_view4(q), _view4(k), _view4(v), _view4(o), _view4(do), _view4(dq), _view4(dk), _view4(dv),
-                        lse.data_ptr(), delta.data_ptr(), B, H, Sq, Sk, D, sc, bool(causal), _stream())
+                        lse.data_ptr(), delta.data_ptr(), B, H, Sq, Sk, D, sc, bool(causal), _stream(), *dbs)
     STATS["attention_bwd"] += 1
 
 

@@ -253,7 +253,15 @@ class MultiHeadAttentionOp(OpImpl):
                 dq, dk, dv = d5[:, :, 0], d5[:, :, 1], d5[:, :, 2]
             else:
                 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-            K.attention_bwd(q, k, v, o, lse, do4, dq, dk, dv, causal=causal, scale=scale)
+            fused_db = None
+            if self_attn and db_in is not None and kd == vd and db_in.dtype == torch.float32 \
+                    and db_in.is_contiguous():
+                dbf = db_in.reshape(-1)
+                n = Hl * kd
+                fused_db = (dbf[:n], dbf[n:2 * n], dbf[2 * n:3 * n])
+            K.attention_bwd(q, k, v, o, lse, do4, dq, dk, dv, causal=causal, scale=scale, dbias=fused_db)
+            if fused_db is not None:
+                db_in = None   # accumulated by the attention backward kernels
         else:
             qf, kf, vf = (t.detach().float().requires_grad_(True) for t in (q, k, v))
             ref = _torch_attention(qf, kf, vf, causal, scale)

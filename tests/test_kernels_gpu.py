@@ -179,10 +179,14 @@ def test_attention_fwd_bwd(causal, D, S):
     do = torch.randn_like(o)
     ref.backward(do.float())
     dqkv = torch.empty_like(qkv)
-    K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal)
+    dbias = [torch.full((H * D,), 0.25, device=DEV) for _ in range(3)]
+    K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal, dbias=dbias)
     assert _rel(dqkv[:, :, 2], vf.grad) < 3e-2, "dV"
     assert _rel(dqkv[:, :, 1], kf.grad) < 3e-2, "dK"
     assert _rel(dqkv[:, :, 0], qf.grad) < 3e-2, "dQ"
+    # fused projection-bias gradients = column sums over (batch, sequence) of dq / dk / dv
+    for i, g in enumerate((qf.grad, kf.grad, vf.grad)):
+        assert _rel(dbias[i] - 0.25, g.sum((0, 1)).reshape(-1)) < 3e-2, ("dbias", i)
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
