@@ -61,6 +61,12 @@ class ExecConfig:
     profiling: bool = False
     grad_clip: float = 0.0
     overlap_grad_sync: bool = True
+    # single-device gradient buckets: run each bucket's optimizer update on a
+    # side stream as soon as the backward pass finalises it (train_step only).
+    # Off by default: measured neutral on BERT-large / GPT-3 medium
+    # (profiles/ab_overlap_update_r2.txt) — the backward GEMMs occupy every CU,
+    # so the memory-bound update cannot run beside them.
+    overlap_update: bool = dataclasses.field(default_factory=lambda: os.environ.get("FF_OVERLAP_UPDATE", "0") != "0")
     bf16_weight_grads: bool = True
     # row-sparse SGD update of embedding tables (plain SGD only; exact)
     sparse_embedding_update: bool = True
@@ -151,6 +157,9 @@ class Executor:
         self.retained_grads: Dict[Value, torch.Tensor] = {}
         self._env: Dict[Value, torch.Tensor] = {}
         self._works = []
+        self._upd_stream = None
+        self._ov_flats = set()
+        self._overlap_lr = None
 
     # ------------------------------------------------------------------ build
     def _view(self, node: int) -> Tuple[int, int]:
@@ -918,6 +927,12 @@ class Executor:
         if dlogits is not None:
             grads[self.loss_value] = dlogits
         self._sync_row_tracking()
+        ov = getattr(self, "_overlap_lr", None)
+        self._ov_flats = set()
+        if ov is not None and sync and not accumulate:
+            for f in self._overlap_flats():
+                f["opt"].begin_step()
+                self._ov_flats.add(id(f))
         for f in self.flats:
             if zero_grads:
                 self._zero_flat(f)
@@ -1000,6 +1015,14 @@ class Executor:
         self._env = {}
         if sync:
             self._finish_grad_sync()
+        if self._ov_flats:
+            # buckets whose params never finalised (untrainable) update now, then join
+            for f in self.flats:
+                if id(f) in self._ov_flats:
+                    for b in f["buckets"]:
+                        if not b.get("updated"):
+                            self._update_bucket(f, b)
+            torch.cuda.current_stream(self.cfg.device).wait_stream(self._upd_stream)
 
     def _sync_row_tracking(self):
         """Embedding backward records touched rows only for tables whose flat
@@ -1049,7 +1072,9 @@ class Executor:
             return
         f, b = fb
         b["pending"] -= 1
-        if b["pending"] == 0 and self.cfg.overlap_grad_sync:
+        if b["pending"] == 0 and id(f) in self._ov_flats:
+            self._update_bucket(f, b)
+        elif b["pending"] == 0 and self.cfg.overlap_grad_sync:
             self._launch_bucket(f, b)
 
     def _launch_bucket(self, f, b):
@@ -1102,13 +1127,19 @@ class Executor:
             norm = self.grad_norm()
             if norm > self.cfg.grad_clip:
                 scale = self.cfg.grad_clip / (norm + 1e-6)
+        pre = getattr(self, "_ov_flats", set())
         for f in self.flats:
+            if id(f) in pre:   # updated bucket by bucket during the backward pass
+                for b in f["buckets"]:
+                    b["updated"] = False
+                continue
             if f.get("ps") and self.dist.distributed and self.rank != min(f["group"]):
                 continue  # PS: only the leader updates (its optimizer state is the only one)
             if f["sparse"]:
                 self._sparse_sgd(f, lr, scale)
                 continue
             f["opt"].step(lr=lr, grad_scale=scale)
+        self._ov_flats = set()
         self._gather_updated()
         self._broadcast_ps()
         self.step_num += 1
@@ -1171,8 +1202,39 @@ class Executor:
     def train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
         self.forward(feeds, training=True)
         g = self.compute_loss(labels)
-        self.backward(g)
+        self._overlap_lr = (True, lr)
+        try:
+            self.backward(g)
+        finally:
+            self._overlap_lr = None
         self.update(lr)
+
+    def _overlap_flats(self) -> List[dict]:
+        """Flats whose buckets may be updated during the backward pass: one
+        device, no gradient collective, no global gradient norm, dense."""
+        if not self.cfg.overlap_update or self.cfg.grad_clip > 0 or self.cfg.device.type != "cuda":
+            return []
+        out = []
+        for f in self.flats:
+            if f["zero"] or f["ps"] or f["sparse"] or (len(f["group"]) > 1 and self.dist.distributed):
+                continue
+            if isinstance(f["opt"], FlatOptimizer) and f["opt"].range_capable():
+                out.append(f)
+        return out
+
+    def _update_bucket(self, f, b):
+        """Run bucket ``b``'s optimizer update on the side stream once the
+        compute stream has produced its last gradient (event fork); the main
+        stream joins before the next step reads the weights."""
+        if self._upd_stream is None:
+            self._upd_stream = torch.cuda.Stream(device=self.cfg.device)
+        cur = torch.cuda.current_stream(self.cfg.device)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._upd_stream.wait_event(ev)
+        with torch.cuda.stream(self._upd_stream):
+            f["opt"].step_range(b["lo"], b["hi"], lr=self._overlap_lr[1])
+        b["updated"] = True
 
     def train_step_pipelined(self, feeds_list: Sequence[Dict[str, torch.Tensor]], labels_list: Sequence[torch.Tensor],
                              lr: Optional[float] = None):

@@ -68,6 +68,30 @@ class FlatOptimizer:
         if self.hp is not None:
             self.hp[0].fill_(float(lr))
 
+    # ---- bucket-wise update (executor: overlapped with the backward pass)
+    def range_capable(self) -> bool:
+        return self.master.is_cuda and K.available() and self.master.numel() % 8 == 0
+
+    def begin_step(self):
+        """Advance the step counters once; ``step_range`` then updates slices."""
+        self.step_num += 1
+        if self.hp is not None:
+            self.hp[1:].add_(1.0)
+
+    def step_range(self, lo: int, hi: int, lr: Optional[float] = None, grad_scale: float = 1.0):
+        """Update elements [lo, hi) with the counters of the current step
+        (after ``begin_step``); HIP path only (``range_capable``)."""
+        c = self.cfg
+        lr = c.lr if lr is None else lr
+        sl = slice(lo, hi)
+        bf = self.bf16[sl] if self.bf16 is not None else None
+        if isinstance(c, AdamConfig):
+            K.adam_step(self.master[sl], self.grad[sl], self.m[sl], self.v[sl], bf, lr, c.beta1, c.beta2, c.epsilon,
+                        c.weight_decay, self.step_num, grad_scale, c.decoupled, hp=self.hp)
+        else:
+            K.sgd_step(self.master[sl], self.grad[sl], self.mom[sl] if self.mom is not None else None, bf, lr,
+                       c.momentum, c.weight_decay, c.nesterov, grad_scale)
+
     def step(self, lr: Optional[float] = None, grad_scale: float = 1.0):
         self.step_num += 1
         c = self.cfg

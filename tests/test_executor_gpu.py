@@ -169,3 +169,32 @@ def test_linear_activation_gradient_fusion():
     assert K.STATS["gemmp"] > before, "fused path not taken"
     for n in a.parameter_names():
         torch.testing.assert_close(a.get_parameter(n), b.get_parameter(n), rtol=2e-2, atol=2e-3)
+
+
+def test_overlapped_bucket_update_matches_end_of_step_update():
+    """Bucket-wise optimizer updates on a side stream during the backward
+    pass (ExecConfig.overlap_update) equal the single update at the end,
+    eagerly and inside a captured hipGraph."""
+    torch.manual_seed(0)
+    a, feeds, labels = _model()
+    b, _, _ = _model()
+    dev = a.executor.cfg.device
+    feeds = {k: v.to(dev) for k, v in feeds.items()}
+    labels = labels.to(dev)
+    a.executor.cfg.overlap_update = True
+    b.executor.cfg.overlap_update = False
+    assert a.executor._overlap_flats(), "no flat eligible for the overlapped update"
+    for _ in range(3):
+        a.executor.train_step(feeds, labels)
+        b.executor.train_step(feeds, labels)
+    torch.cuda.synchronize()
+    for n in a.executor.parameter_names():
+        torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=1e-5, atol=1e-6)
+    sa = a.executor.make_graphed_train_step(feeds, labels, warmup=1)
+    sb = b.executor.make_graphed_train_step(feeds, labels, warmup=1)
+    for _ in range(3):
+        sa()
+        sb()
+    torch.cuda.synchronize()
+    for n in a.executor.parameter_names():
+        torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=1e-5, atol=1e-6)

@@ -186,7 +186,12 @@ def test_attention_fwd_bwd(causal, D, S):
     assert _rel(dqkv[:, :, 0], qf.grad) < 3e-2, "dQ"
     # fused projection-bias gradients = column sums over (batch, sequence) of dq / dk / dv
     for i, g in enumerate((qf.grad, kf.grad, vf.grad)):
-        assert _rel(dbias[i] - 0.25, g.sum((0, 1)).reshape(-1)) < 3e-2, ("dbias", i)
+        ref_sum = g.sum((0, 1)).reshape(-1)
+        err = (dbias[i] - 0.25 - ref_sum).abs().max()
+        # the key-bias gradient is 0 in exact arithmetic (softmax rows sum to 1):
+        # bound the error by the size of the summed terms instead of the sum
+        scale = g.abs().sum((0, 1)).max()
+        assert err < 3e-2 * scale, ("dbias", i, float(err), float(scale))
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
