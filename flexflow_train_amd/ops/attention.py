@@ -20,6 +20,7 @@ backward needs exactly one GEMM for dW_qkv and one for dX.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -27,6 +28,13 @@ from .. import kernels as K
 from ..parallel import sequence as SP
 from .base import OpContext, OpImpl, acc_grad, register
 from .gemm import matmul
+
+# q/k/v projection-bias gradients accumulated inside the attention backward
+# kernels (one atomic per column per wave) instead of one column-sum pass over
+# dQKV.  Off by default: at BERT-large shapes the atomics onto H*D addresses
+# made dK/dV 117 -> 220 us and dQ 76 -> 150 us per call, far more than the
+# ~25 us column-sum pass they replace (profiles/ab_attn_dbias_r2.txt).
+_FUSED_DBIAS = os.environ.get("FF_ATTN_FUSED_DBIAS", "0") == "1"
 
 
 def _dims(ctx: OpContext, q, k, v, W):
@@ -254,8 +262,8 @@ class MultiHeadAttentionOp(OpImpl):
             else:
                 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
             fused_db = None
-            if self_attn and db_in is not None and kd == vd and db_in.dtype == torch.float32 \
-                    and db_in.is_contiguous():
+            if _FUSED_DBIAS and self_attn and db_in is not None and kd == vd \
+                    and db_in.dtype == torch.float32 and db_in.is_contiguous():
                 dbf = db_in.reshape(-1)
                 n = Hl * kd
                 fused_db = (dbf[:n], dbf[n:2 * n], dbf[2 * n:3 * n])
