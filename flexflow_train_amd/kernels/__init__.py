@@ -939,10 +939,13 @@ _BLT_WS_BYTES = 64 << 20
 
 
 def _blaslt_ws(dev):
-    w = _BLT_WS.get(dev)
+    # one workspace per (device, stream): GEMMs on the weight-gradient stream
+    # run concurrently with those on the compute stream
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    w = _BLT_WS.get(key)
     if w is None:
         w = torch.empty(_BLT_WS_BYTES, dtype=torch.uint8, device=dev)
-        _BLT_WS[dev] = w
+        _BLT_WS[key] = w
     return w
 
 

@@ -27,7 +27,7 @@ import torch
 from .. import kernels as K
 from ..parallel import sequence as SP
 from .base import OpContext, OpImpl, acc_grad, register
-from .gemm import matmul
+from .gemm import matmul, wgrad_matmul
 
 # q/k/v projection-bias gradients accumulated inside the attention backward
 # kernels (one atomic per column per wave) instead of one column-sum pass over
@@ -236,7 +236,7 @@ class MultiHeadAttentionOp(OpImpl):
         wbeta = ctx.extra.get("wgrad_beta", [1.0])[0]
         if dW_views is not None:
             if gpu:
-                matmul(o2, dout, trans_a=True, out=dW_views["o"], beta=wbeta)
+                wgrad_matmul(ctx, o2, dout, dW_views["o"], wbeta)
             else:
                 acc_grad(dW_views["o"], o2.float().t() @ dout.float())
         do = matmul(dout, ws["o"], trans_b=True) if gpu else dout @ ws["o"].to(dout.dtype).t()
@@ -288,7 +288,7 @@ class MultiHeadAttentionOp(OpImpl):
                     acc_grad(db_in, d2.float().sum(0))
             if dW_views is not None:
                 if gpu:
-                    matmul(x2, d2, trans_a=True, out=dW_views["qkv"], beta=wbeta)
+                    wgrad_matmul(ctx, x2, d2, dW_views["qkv"], wbeta)
                 else:
                     acc_grad(dW_views["qkv"], x2.float().t() @ d2.float())
             if need_input_grad[0]:
@@ -308,7 +308,7 @@ class MultiHeadAttentionOp(OpImpl):
                 acc_grad(seg, d2.float().sum(0))
             if dW_views is not None:
                 if gpu:
-                    matmul(xin, d2, trans_a=True, out=dW_views[key], beta=wbeta)
+                    wgrad_matmul(ctx, xin, d2, dW_views[key], wbeta)
                 else:
                     acc_grad(dW_views[key], xin.float().t() @ d2.float())
             if need_input_grad[j]:

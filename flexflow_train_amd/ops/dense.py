@@ -16,7 +16,7 @@ import torch
 
 from .. import kernels as K
 from .base import OpContext, OpImpl, acc_grad, register
-from .gemm import matmul
+from .gemm import matmul, wgrad_matmul
 
 _ACT_T = {
     "none": lambda t: t,
@@ -86,7 +86,7 @@ class LinearOp(OpImpl):
                 acc_grad(db, g.float().sum(0))
         if dW is not None:
             if dW.is_cuda and g.dtype == torch.bfloat16:
-                matmul(x2, g, trans_a=True, out=dW, beta=ctx.extra.get("wgrad_beta", [1.0])[0])
+                wgrad_matmul(ctx, x2, g, dW, ctx.extra.get("wgrad_beta", [1.0])[0])
             else:
                 acc_grad(dW, x2.float().t() @ g.float())
         dx = None

@@ -304,3 +304,22 @@ def _resolve(name: str):
     if kind == "p":
         return lambda *args: _gp(*args, splits=int(arg))
     return lambda *args: _hip256(*args, splits=int(arg))
+
+
+def wgrad_matmul(ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float):
+    """Weight gradient ``out = a^T b (+ beta * out)``.  When the executor
+    attached its weight-gradient stream (``ctx.extra["wgrad_stream"]`` =
+    (stream, keep-list, storage pointers)), the GEMM is queued there after the
+    compute stream's work so far, and runs beside the rest of the backward
+    pass; ``a`` / ``b`` stay referenced until the executor joins the stream."""
+    wg = ctx.extra.get("wgrad_stream")
+    if wg is None or not a.is_cuda:
+        return matmul(a, b, trans_a=True, out=out, beta=beta)
+    stream, keep, ptrs = wg
+    stream.wait_stream(torch.cuda.current_stream(a.device))
+    with torch.cuda.stream(stream):
+        r = matmul(a, b, trans_a=True, out=out, beta=beta)
+    for t in (a, b):
+        keep.append(t)
+        ptrs.add(t.untyped_storage().data_ptr())
+    return r

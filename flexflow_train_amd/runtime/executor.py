@@ -68,6 +68,15 @@ class ExecConfig:
     # so the memory-bound update cannot run beside them.
     overlap_update: bool = dataclasses.field(default_factory=lambda: os.environ.get("FF_OVERLAP_UPDATE", "0") != "0")
     bf16_weight_grads: bool = True
+    # weight-gradient GEMMs (LINEAR / attention projections) on a second HIP
+    # stream: the dW GEMM of a layer runs beside the input-gradient chain
+    # (dX GEMM, activation / LayerNorm / attention backward) instead of in
+    # series with it; joined before every gradient collective and at the end
+    # of the backward pass.  Off by default: measured 2 % slower on BERT-large
+    # and GPT-3 medium (profiles/ab_wgrad_stream_r2.txt) — concurrent GEMMs
+    # contend for the CUs, and residual gradients read by a queued dW GEMM
+    # cannot be accumulated in place (one extra add each).
+    wgrad_stream: bool = dataclasses.field(default_factory=lambda: os.environ.get("FF_WGRAD_STREAM", "0") != "0")
     # row-sparse SGD update of embedding tables (plain SGD only; exact)
     sparse_embedding_update: bool = True
     # "counter": every rank generates only its own piece from a counter-based
@@ -940,6 +949,7 @@ class Executor:
                 b["pending"] = sum(1 for p in b["params"] if p.trainable)
         self._works = []
         prof = self.cfg.profiling
+        wg_on = self._wg_enabled()
         n = len(self.steps)
         if getattr(self, "_step_index", None) is None or len(self._step_index) != n:
             self._step_index = {id(st): k for k, st in enumerate(self.steps)}
@@ -984,7 +994,20 @@ class Executor:
                     # accumulation (ops return the same tensor when they used it).
                     s.ctx.extra["wgrad_beta"] = [0.0 if (p.n_consumers == 1 and not accumulate) else 1.0
                                                  for p in s.weights]
-                    s.ctx.extra["grad_acc"] = [grads.get(v) if nd else None for v, nd in zip(s.inputs, need)]
+                    # an input gradient still read by a pending side-stream dW GEMM
+                    # (or aliasing this op's output gradient, which its own dW GEMM
+                    # reads) is not offered for in-place accumulation: the op
+                    # returns a fresh tensor and _acc adds
+                    side = wg_on and s.op_type in ("LINEAR", "MULTIHEAD_ATTENTION")
+                    busy = {g.untyped_storage().data_ptr() for g in gouts if g is not None} if side else set()
+                    s.ctx.extra["grad_acc"] = [
+                        a if (nd and a is not None and not self._wg_reads(a)
+                              and a.untyped_storage().data_ptr() not in busy) else None
+                        for a, nd in ((grads.get(v), nd) for v, nd in zip(s.inputs, need))]
+                    if side:
+                        s.ctx.extra["wgrad_stream"] = self._wg
+                    else:
+                        s.ctx.extra.pop("wgrad_stream", None)
                     bsrc = s.ctx.extra.get("dbias_src")
                     s.ctx.extra.pop("dsum_target", None)
                     if bsrc is not None:
@@ -1013,6 +1036,7 @@ class Executor:
                         self._param_done(p)
         self._saved = {}
         self._env = {}
+        self._wg_join()
         if sync:
             self._finish_grad_sync()
         if self._ov_flats:
@@ -1073,9 +1097,37 @@ class Executor:
         f, b = fb
         b["pending"] -= 1
         if b["pending"] == 0 and id(f) in self._ov_flats:
+            self._wg_join()
             self._update_bucket(f, b)
         elif b["pending"] == 0 and self.cfg.overlap_grad_sync:
+            if len(f["group"]) > 1 and self.dist.distributed:
+                self._wg_join()
             self._launch_bucket(f, b)
+
+    # ---- weight-gradient side stream
+    def _wg_enabled(self) -> bool:
+        """Side-stream dW GEMMs: CUDA only, from the second step on (the
+        first step's GEMMs are autotuned alone on the compute stream)."""
+        if not (self.cfg.wgrad_stream and self.cfg.device.type == "cuda" and self.step_num >= 1):
+            return False
+        if getattr(self, "_wg", None) is None:
+            # (stream, tensors its queued GEMMs read, their storage pointers)
+            self._wg = (torch.cuda.Stream(device=self.cfg.device), [], set())
+        return True
+
+    def _wg_reads(self, t: Optional[torch.Tensor]) -> bool:
+        wg = getattr(self, "_wg", None)
+        return bool(t is not None and wg is not None and wg[2] and t.untyped_storage().data_ptr() in wg[2])
+
+    def _wg_join(self):
+        """The compute stream waits for every queued dW GEMM; the tensors
+        they read may be freed / overwritten from here on."""
+        wg = getattr(self, "_wg", None)
+        if wg is None or not wg[1]:
+            return
+        torch.cuda.current_stream(self.cfg.device).wait_stream(wg[0])
+        wg[1].clear()
+        wg[2].clear()
 
     def _launch_bucket(self, f, b):
         if len(f["group"]) > 1 and self.dist.distributed and not b.get("launched"):

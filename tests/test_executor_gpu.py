@@ -198,3 +198,34 @@ def test_overlapped_bucket_update_matches_end_of_step_update():
     torch.cuda.synchronize()
     for n in a.executor.parameter_names():
         torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=1e-5, atol=1e-6)
+
+
+def test_wgrad_stream_matches_single_stream():
+    """Weight-gradient GEMMs on the side stream (ExecConfig.wgrad_stream)
+    train like the single-stream backward, eagerly and inside a captured
+    hipGraph (residual gradients shared with a dW GEMM's input are not
+    accumulated in place)."""
+    torch.manual_seed(0)
+    a, feeds, labels = _model()
+    b, _, _ = _model()
+    dev = a.executor.cfg.device
+    feeds = {k: v.to(dev) for k, v in feeds.items()}
+    labels = labels.to(dev)
+    a.executor.cfg.wgrad_stream = True
+    b.executor.cfg.wgrad_stream = False
+    for _ in range(3):
+        a.executor.train_step(feeds, labels)
+        b.executor.train_step(feeds, labels)
+    torch.cuda.synchronize()
+    assert getattr(a.executor, "_wg", None) is not None, "side stream never used"
+    assert not a.executor._wg[1], "side stream not joined at the end of the backward pass"
+    for n in a.executor.parameter_names():
+        torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=2e-2, atol=2e-3)
+    sa = a.executor.make_graphed_train_step(feeds, labels, warmup=1)
+    sb = b.executor.make_graphed_train_step(feeds, labels, warmup=1)
+    for _ in range(3):
+        sa()
+        sb()
+    torch.cuda.synchronize()
+    for n in a.executor.parameter_names():
+        torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=2e-2, atol=2e-3)
