@@ -175,14 +175,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
           s[kt] = mfma32(kf, qf[ks], s[kt]);
         }
       }
-      // ---- scale, mask (only tiles that cross the sequence end or the
-      // causal diagonal — a wave-uniform branch), tile max
+      // ---- mask (only tiles that cross the sequence end or the causal
+      // diagonal — a wave-uniform branch), tile max of the RAW scores: the
+      // softmax scale is folded into one FMA per score inside exp2 below
       const bool need_mask = (k0 + KV > P.Sk) || (CAUSAL && k0 + KV - 1 > qw);
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kt][r] *= P.scale_log2;
       if (need_mask) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
@@ -192,27 +188,35 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
             if (key >= P.Sk || (CAUSAL && key > q)) s[kt][r] = -INFINITY;
           }
       }
+      float tmax = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kt][r]);
+        for (int r = 0; r < 16; r += 2) tmax = fmaxf(tmax, fmaxf(s[kt][r], s[kt][r + 1]));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m, tmax);
-      const float alpha = (m_new == -INFINITY) ? 1.f : fexp2(m - m_new);
-      const float msub = (m_new == -INFINITY) ? 0.f : m_new;
-      m = m_new;
+      // ---- lazy rescale: the running max m only moves when some lane's
+      // tile max exceeds it by more than 8 in the log2 domain (p <= 256 is
+      // exact enough in fp32 and bf16-relative); a wave-uniform branch, so
+      // the o *= alpha pass runs on a few early tiles instead of every tile
+      if (__any(tmax > m + 8.f / P.scale_log2)) {
+        const float m_new = fmaxf(m, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : fexp2((m - m_new) * P.scale_log2);
+        m = m_new;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      }
+      const float mc = (m == -INFINITY) ? 0.f : m * P.scale_log2;
       float psum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float pv = fexp2(s[kt][r] - msub);
+          const float pv = fexp2(fmaf(s[kt][r], P.scale_log2, -mc));
           s[kt][r] = pv;
           psum += pv;
         }
-      l = l * alpha + psum;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      l += psum;
       // ---- O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * g4 + e] * inv);
         *reinterpret_cast<bf16x4*>(orow + dt * 32 + 8 * g4 + 4 * h) = v;
       }
-    if (h == 0) P.lse[static_cast<int64_t>(bh) * P.Sq + q] = (lt > 0.f) ? m + log2f(lt) : -INFINITY;
+    if (h == 0) P.lse[static_cast<int64_t>(bh) * P.Sq + q] = (lt > 0.f) ? m * P.scale_log2 + log2f(lt) : -INFINITY;
   }
 }
 

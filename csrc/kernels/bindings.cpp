@@ -274,4 +274,12 @@ PYBIND11_MODULE(_ffkernels, m) {
     blaslt_gemm(P(A), P(B), P(C), M, N, K, lda, ldb, ldc, ta, tb, epi, P(bias), P(aux), aux_ld, alpha, beta, out_f32,
                 P(ws), ws_bytes, S(st), algo);
   });
+  m.def("blaslt_solutions", &blaslt_solutions);
+  m.def("blaslt_solution_name", &blaslt_solution_name);
+  m.def("blaslt_gemm_solution", [](uintptr_t A, uintptr_t B, uintptr_t C, int M, int N, int K, int lda, int ldb,
+                                   int ldc, bool ta, bool tb, float alpha, float beta, int out_f32, uintptr_t ws,
+                                   size_t ws_bytes, uintptr_t st, int index) {
+    blaslt_gemm_solution(P(A), P(B), P(C), M, N, K, lda, ldb, ldc, ta, tb, alpha, beta, out_f32, P(ws), ws_bytes,
+                         S(st), index);
+  });
 }

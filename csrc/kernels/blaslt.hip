@@ -25,6 +25,7 @@
 // launches are asynchronous and capturable (no allocation: the caller passes
 // the workspace).
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
 #include <map>
 #include <mutex>
@@ -54,6 +55,10 @@ struct Plan {
   hipblasLtMatmulAlgo_t algo[kMaxAlgos]{};
   size_t ws_needed[kMaxAlgos]{};
   int n_algos = 0;
+  // library solutions addressed by their solution index (beyond the
+  // heuristic's top 16: an offline sweep over every solution that supports
+  // the problem, tools/blaslt_sweep.py), resolved + checked once per plan
+  std::map<int, std::pair<hipblasLtMatmulAlgo_t, size_t>> by_index;
 };
 
 using Key = std::tuple<int, int, int, int, int, int, bool, bool, int, int, bool, int>;
@@ -203,6 +208,66 @@ void blaslt_gemm(const void* A, const void* B, void* C, int M, int N, int K, int
   (void)aux;
   (void)aux_ld;
   FFK_BLT(hipblasLtMatmul(handle(), p.desc, &alpha, B, p.a, A, p.b, &beta, C, p.c, C, p.c, &p.algo[algo], ws, ws_bytes, st));
+}
+
+// Every library solution (index) that supports this problem, in the library's
+// order; plain GEMMs only (no epilogue).
+std::vector<int> blaslt_solutions(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int out_f32,
+                                  bool has_beta, size_t ws_bytes) {
+  std::lock_guard<std::mutex> g(mu);
+  Plan& p = get_plan(M, N, K, lda, ldb, ldc, ta, tb, EPI_NONE, out_f32, has_beta, 0, ws_bytes);
+  const hipblasOperation_t opa = tb ? HIPBLAS_OP_T : HIPBLAS_OP_N, opb = ta ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  std::vector<hipblasLtMatmulHeuristicResult_t> all;
+  const hipDataType ct = out_f32 ? HIP_R_32F : HIP_R_16BF;
+  FFK_BLT(hipblaslt_ext::getAllAlgos(handle(), hipblaslt_ext::GemmType::HIPBLASLT_GEMM, opa, opb, HIP_R_16BF,
+                                     HIP_R_16BF, ct, ct, HIPBLAS_COMPUTE_32F, all));
+  const float alpha = 1.f, beta = has_beta ? 1.f : 0.f;
+  std::vector<int> out;
+  for (auto& r : all) {
+    size_t ws = 0;
+    hipblasLtMatmulAlgo_t a = r.algo;
+    if (hipblaslt_ext::matmulIsAlgoSupported(handle(), p.desc, &alpha, p.a, p.b, &beta, p.c, p.c, a, ws) !=
+        HIPBLAS_STATUS_SUCCESS || ws > ws_bytes)
+      continue;
+    const int idx = hipblaslt_ext::getIndexFromAlgo(a);
+    p.by_index[idx] = {a, ws};
+    out.push_back(idx);
+  }
+  return out;
+}
+
+std::string blaslt_solution_name(int index) {
+  std::vector<int> ids{index};
+  std::vector<hipblasLtMatmulHeuristicResult_t> r;
+  if (hipblaslt_ext::getAlgosFromIndex(handle(), ids, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) return "";
+  return hipblaslt_ext::getKernelNameFromAlgo(handle(), r[0].algo);
+}
+
+// Plain GEMM with the library solution `index` (from blaslt_solutions or a
+// tuned table); throws if that solution does not support the problem.
+void blaslt_gemm_solution(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                          bool ta, bool tb, float alpha, float beta, int out_f32, void* ws, size_t ws_bytes,
+                          hipStream_t st, int index) {
+  if (M <= 0 || N <= 0 || K <= 0) return;
+  std::lock_guard<std::mutex> g(mu);
+  Plan& p = get_plan(M, N, K, lda, ldb, ldc, ta, tb, EPI_NONE, out_f32, beta != 0.f, 0, ws_bytes);
+  auto it = p.by_index.find(index);
+  if (it == p.by_index.end()) {
+    std::vector<int> ids{index};
+    std::vector<hipblasLtMatmulHeuristicResult_t> r;
+    if (hipblaslt_ext::getAlgosFromIndex(handle(), ids, r) != HIPBLAS_STATUS_SUCCESS || r.empty())
+      throw std::invalid_argument("blaslt: unknown solution index " + std::to_string(index));
+    size_t need = 0;
+    hipblasLtMatmulAlgo_t a = r[0].algo;
+    const float al = 1.f, be = beta != 0.f ? 1.f : 0.f;
+    if (hipblaslt_ext::matmulIsAlgoSupported(handle(), p.desc, &al, p.a, p.b, &be, p.c, p.c, a, need) !=
+        HIPBLAS_STATUS_SUCCESS)
+      throw std::invalid_argument("blaslt: solution " + std::to_string(index) + " does not support this GEMM");
+    it = p.by_index.emplace(index, std::make_pair(a, need)).first;
+  }
+  if (it->second.second > ws_bytes) throw std::invalid_argument("blaslt: workspace too small");
+  FFK_BLT(hipblasLtMatmul(handle(), p.desc, &alpha, B, p.a, A, p.b, &beta, C, p.c, C, p.c, &it->second.first, ws,
+                          ws_bytes, st));
 }
 
 }  // namespace ffk

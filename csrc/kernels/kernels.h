@@ -2,6 +2,8 @@
 // asynchronous on the given stream; pointers are device pointers).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
 
 #include <algorithm>
 #include <cstdint>
@@ -206,5 +208,11 @@ int blaslt_num_algos(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bo
 void blaslt_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool ta,
                  bool tb, int epi, const void* bias, void* aux, int aux_ld, float alpha, float beta, int out_f32,
                  void* ws, size_t ws_bytes, hipStream_t st, int algo = 0);
+std::vector<int> blaslt_solutions(int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int out_f32,
+                                  bool has_beta, size_t ws_bytes);
+std::string blaslt_solution_name(int index);
+void blaslt_gemm_solution(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                          bool ta, bool tb, float alpha, float beta, int out_f32, void* ws, size_t ws_bytes,
+                          hipStream_t st, int index);
 
 }  // namespace ffk

@@ -388,6 +388,32 @@ static void ln_fwd_t(const void* x, const void* res, void* sum_out, const void* 
   FFK_LAUNCH_CHECK("layernorm_fwd");
 }
 
+// Finishes the backward's column sums in ONE launch: out_j[c] += sum over the
+// `rows` partial rows of slice j of ws[3][rows][N] (j = dgamma, dbeta, dsum;
+// absent outputs are skipped).  Block = 64 columns x 4 row groups; a single
+// writer per column (no atomics).
+__global__ __launch_bounds__(256) void ln_ws_reduce_kernel(const float* __restrict__ ws, float* out0, float* out1,
+                                                           float* out2, int rows, int N) {
+  __shared__ float red[4][64];
+  float* out = blockIdx.y == 0 ? out0 : (blockIdx.y == 1 ? out1 : out2);
+  if (out == nullptr) return;
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  const float* src = ws + static_cast<size_t>(blockIdx.y) * rows * N;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    int r = ry;
+    for (; r + 12 < rows; r += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += src[static_cast<size_t>(r + 4 * u) * N + c];
+    }
+    for (; r < rows; r += 4) acc[0] += src[static_cast<size_t>(r) * N + c];
+  }
+  red[ry][cx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (ry == 0 && c < N) out[c] += (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
+}
+
 template <typename T>
 static void ln_bwd_t(const void* dy, const void* s, const float* mean, const float* rstd, const void* gamma,
                      void* dx, float* dgamma, float* dbeta, float* ws, int M, int N, const void* dres, float* dsum,
@@ -413,9 +439,11 @@ static void ln_bwd_t(const void* dy, const void* s, const float* mean, const flo
 #undef FFK_LNB_CASE
     }
     FFK_LAUNCH_CHECK("layernorm_bwd");
-    if (dgamma) colsum_act(kF32, ws, nullptr, nullptr, dgamma, grid, N, 0, 1.f, st);
-    if (dbeta) colsum_act(kF32, ws + static_cast<size_t>(grid) * N, nullptr, nullptr, dbeta, grid, N, 0, 1.f, st);
-    if (dsum) colsum_act(kF32, WD, nullptr, nullptr, dsum, grid, N, 0, 1.f, st);
+    if (dgamma || dbeta || dsum) {
+      hipLaunchKernelGGL(ln_ws_reduce_kernel, dim3((N + 63) / 64, dsum ? 3 : 2), dim3(256), 0, st, ws, dgamma, dbeta,
+                         dsum, grid, N);
+      FFK_LAUNCH_CHECK("layernorm_bwd_reduce");
+    }
     return;
   } else {
     hipLaunchKernelGGL((ln_bwd_generic<T>), dim3(M), dim3(256), 0, st, DY, S, mean, rstd, G, DX, dgamma, dbeta, M,

@@ -996,6 +996,28 @@ def blaslt_matmul(a, b, trans_a, trans_b, out, beta: float = 0.0, bias=None, alg
     return out
 
 
+def blaslt_solutions(a, b, trans_a, trans_b, out, beta: float = 0.0):
+    """Library solution indices (every hipBLASLt kernel, not just the
+    heuristic's top candidates) that support C(out) = op(a) op(b) [+ out]."""
+    M, N, K = _gemm_dims(a, b, trans_a, trans_b)
+    return list(ext().blaslt_solutions(M, N, K, _rowmajor(a, "a"), _rowmajor(b, "b"), _rowmajor(out, "out"),
+                                       bool(trans_a), bool(trans_b), int(out.dtype == torch.float32), bool(beta),
+                                       _BLT_WS_BYTES))
+
+
+def blaslt_matmul_solution(a, b, trans_a, trans_b, out, beta: float = 0.0, index: int = 0):
+    """C = op(a) op(b) (+ beta * out) with hipBLASLt solution ``index``."""
+    M, N, K = _gemm_dims(a, b, trans_a, trans_b)
+    if tuple(out.shape) != (M, N):
+        raise ValueError("blaslt_matmul_solution: out has the wrong shape")
+    ext().blaslt_gemm_solution(_p(a), _p(b), _p(out), M, N, K, _rowmajor(a, "a"), _rowmajor(b, "b"),
+                               _rowmajor(out, "out"), bool(trans_a), bool(trans_b), 1.0, float(beta),
+                               int(out.dtype == torch.float32), _p(_blaslt_ws(a.device)), _BLT_WS_BYTES, _stream(),
+                               int(index))
+    STATS["blaslt_gemm"] += 1
+    return out
+
+
 def blaslt_ok(a, b, trans_a=False, trans_b=False, epilogue=EPI_NONE, out_f32=False, beta=0.0) -> bool:
     """True when hipBLASLt has an algorithm for this GEMM + epilogue (cached)."""
     if not (a.is_cuda and b.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):

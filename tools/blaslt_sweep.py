@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Sweep EVERY hipBLASLt solution (hipblaslt_ext::getAllAlgos, filtered by
+matmulIsAlgoSupported) against torch.mm and the autotuner's own candidates on
+the BERT-large / GPT-3-medium training GEMM shapes; one JSON line per shape
+with the top solutions by time.  Feeds the tuned table in
+flexflow_train_amd/ops/gemm_tuned_gfx950.json.
+
+    python tools/blaslt_sweep.py [bert|gpt|all] [--top 5]
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from flexflow_train_amd import kernels as K  # noqa: E402
+from flexflow_train_amd.ops import gemm as G  # noqa: E402
+
+
+def shapes(tokens, hidden, ffn, vocab):
+    h, f = hidden, ffn
+    out = []
+    for name, n_in, n_out in (("qkv", h, 3 * h), ("o", h, h), ("ffn1", h, f), ("ffn2", f, h)):
+        out.append((f"{name}_fwd", tokens, n_out, n_in, False, False))   # x[T,in] @ W[in,out]
+        out.append((f"{name}_dx", tokens, n_in, n_out, False, True))    # dy[T,out] @ W^T
+        out.append((f"{name}_dw", n_in, n_out, tokens, True, False))    # x^T dy
+    out.append(("head_fwd", tokens, vocab, h, False, False))
+    out.append(("head_dx", tokens, h, vocab, False, True))
+    out.append(("head_dw", h, vocab, tokens, True, False))
+    return out
+
+
+def timeit(fn, iters=10, rounds=3):
+    fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / iters)
+    return best
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "all"
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 5
+    cfgs = []
+    if which in ("bert", "all"):
+        cfgs.append(("bert", shapes(32 * 512, 1024, 4096, 30528)))
+    if which in ("gpt", "all"):
+        cfgs.append(("gpt", shapes(8 * 2048, 1024, 4096, 50304)))
+    seen = set()
+    for model, cases in cfgs:
+        for name, M, N, Kd, ta, tb in cases:
+            key = (M, N, Kd, ta, tb)
+            if key in seen:
+                continue
+            seen.add(key)
+            a = torch.randn((Kd, M) if ta else (M, Kd), device="cuda", dtype=torch.bfloat16)
+            b = torch.randn((N, Kd) if tb else (Kd, N), device="cuda", dtype=torch.bfloat16)
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            flop = 2.0 * M * N * Kd
+            res = {}
+            res["blas"] = timeit(lambda: G._blas(a, b, ta, tb, None, "none", out, 0.0, None))
+            for nm, fn in G._candidates(a, b, ta, tb, None, "none", None, out, 0.0).items():
+                if nm in ("blas", "hip"):
+                    continue
+                try:
+                    res[nm] = timeit(lambda fn=fn: fn(a, b, ta, tb, None, "none", out, 0.0, None))
+                except Exception as ex:  # noqa: BLE001
+                    res[nm] = float("inf")
+            sols = K.blaslt_solutions(a, b, ta, tb, out, 0.0)
+            for idx in sols:
+                try:
+                    res[f"ls:{idx}"] = timeit(lambda idx=idx: K.blaslt_matmul_solution(a, b, ta, tb, out, 0.0, idx),
+                                              iters=5, rounds=2)
+                except Exception:  # noqa: BLE001
+                    pass
+            best = sorted(res.items(), key=lambda kv: kv[1])[:top]
+            # re-time the finalists interleaved (guide: one-shot timings rank near-ties at random)
+            fin = {}
+            for _ in range(3):
+                for nm, _t in best + [("blas", res["blas"])]:
+                    if nm.startswith("ls:"):
+                        f = (lambda i=int(nm[3:]): K.blaslt_matmul_solution(a, b, ta, tb, out, 0.0, i))
+                    elif nm == "blas":
+                        f = (lambda: G._blas(a, b, ta, tb, None, "none", out, 0.0, None))
+                    else:
+                        f = (lambda nm=nm: G._resolve(nm)(a, b, ta, tb, None, "none", out, 0.0, None))
+                    t = timeit(f, iters=20, rounds=2)
+                    fin[nm] = min(fin.get(nm, float("inf")), t)
+            ranked = sorted(fin.items(), key=lambda kv: kv[1])
+            print(json.dumps({"model": model, "case": name, "M": M, "N": N, "K": Kd, "ta": ta, "tb": tb,
+                              "n_solutions": len(sols),
+                              "blas_us": round(fin["blas"] * 1e3, 1), "blas_TF": round(flop / fin["blas"] / 1e9, 1),
+                              "best": [[nm, round(t * 1e3, 1), round(flop / t / 1e9, 1)] for nm, t in ranked[:top]],
+                              "best_name": (K.ext().blaslt_solution_name(int(ranked[0][0][3:]))
+                                            if ranked[0][0].startswith("ls:") else ranked[0][0])}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
