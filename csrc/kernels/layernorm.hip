@@ -12,6 +12,8 @@
 //    reduce across the block's 4 waves through LDS, then one fp32 atomic per
 //    column per block (grid is capped, so atomics are ~N * grid, not N * M).
 #include "common.h"
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace ffk {
@@ -390,8 +392,9 @@ static void ln_fwd_t(const void* x, const void* res, void* sum_out, const void* 
 
 // Finishes the backward's column sums in ONE launch: out_j[c] += sum over the
 // `rows` partial rows of slice j of ws[3][rows][N] (j = dgamma, dbeta, dsum;
-// absent outputs are skipped).  Block = 64 columns x 4 row groups; a single
-// writer per column (no atomics).
+// absent outputs are skipped).  Block = 64 columns x 4 row groups over a
+// 64-row chunk (grid.z chunks, so every thread has only 16 loads in flight
+// and the reduction is not latency bound); one fp32 atomic per column per block.
 __global__ __launch_bounds__(256) void ln_ws_reduce_kernel(const float* __restrict__ ws, float* out0, float* out1,
                                                            float* out2, int rows, int N) {
   __shared__ float red[4][64];
@@ -400,18 +403,18 @@ __global__ __launch_bounds__(256) void ln_ws_reduce_kernel(const float* __restri
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cx;
   const float* src = ws + static_cast<size_t>(blockIdx.y) * rows * N;
+  const int r0 = blockIdx.z * 64, r1 = min(rows, r0 + 64);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < N) {
-    int r = ry;
-    for (; r + 12 < rows; r += 16) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] += src[static_cast<size_t>(r + 4 * u) * N + c];
+    for (int u = 0; u < 16; ++u) {
+      const int r = r0 + ry + 4 * u;
+      if (r < r1) acc[u & 3] += src[static_cast<size_t>(r) * N + c];
     }
-    for (; r < rows; r += 4) acc[0] += src[static_cast<size_t>(r) * N + c];
   }
   red[ry][cx] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  if (ry == 0 && c < N) out[c] += (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
+  if (ry == 0 && c < N) atomicAdd(out + c, (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]));
 }
 
 template <typename T>
@@ -440,8 +443,8 @@ static void ln_bwd_t(const void* dy, const void* s, const float* mean, const flo
     }
     FFK_LAUNCH_CHECK("layernorm_bwd");
     if (dgamma || dbeta || dsum) {
-      hipLaunchKernelGGL(ln_ws_reduce_kernel, dim3((N + 63) / 64, dsum ? 3 : 2), dim3(256), 0, st, ws, dgamma, dbeta,
-                         dsum, grid, N);
+      hipLaunchKernelGGL(ln_ws_reduce_kernel, dim3((N + 63) / 64, dsum ? 3 : 2, (grid + 63) / 64), dim3(256), 0, st,
+                         ws, dgamma, dbeta, dsum, grid, N);
       FFK_LAUNCH_CHECK("layernorm_bwd_reduce");
     }
     return;
@@ -461,7 +464,14 @@ void layernorm_fwd(int dtype, const void* x, const void* res, void* sum_out, con
 }
 
 int layernorm_bwd_grid(int M, int N) {
-  if (N % 512 == 0 && N <= 4096) return std::max(1, std::min((M + 7) / 8, 512));
+  // blocks of 4 waves; more blocks = more rows in flight (the kernel is
+  // HBM-latency bound at 2 waves / SIMD), at the price of a larger partial-sum
+  // workspace ws[3][grid][N] for the final reduction
+  static const int cap = [] {
+    const char* e = getenv("FFK_LN_BWD_GRID");
+    return e ? std::max(64, atoi(e)) : 512;
+  }();
+  if (N % 512 == 0 && N <= 4096) return std::max(1, std::min((M + 7) / 8, cap));
   return 0;
 }
 

@@ -193,6 +193,75 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(T* __restrict__ logits,
   }
 }
 
+// bf16 rows that fit in registers (V <= 2048 * NIT): the row is loaded ONCE
+// (every chunk's load issued up front), reduced, and the gradient written
+// from the same registers — one HBM read + one write per logit instead of
+// the two reads of the streaming kernel above.
+template <typename L, int NIT>
+__global__ __launch_bounds__(256) void softmax_ce_reg_kernel(bf16* __restrict__ logits, const L* __restrict__ labels,
+                                                             float* __restrict__ row_loss, float* __restrict__ metrics,
+                                                             int M, int V, int V_valid, float grad_scale,
+                                                             int ignore_index, int write_grad) {
+  const int row = blockIdx.x;
+  bf16* x = logits + static_cast<size_t>(row) * V;
+  u16x8 u[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * 256 + threadIdx.x) * 8;
+    if (c < V) u[it] = *reinterpret_cast<const u16x8*>(x + c);
+  }
+  MaxSum ms{-INFINITY, 0.f};
+  float best = -INFINITY;
+  int best_idx = 0;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * 256 + threadIdx.x) * 8;
+    if (c >= V) break;
+    float v[8];
+    float lm = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = (c + k < V_valid) ? u2f(u[it][k]) : -INFINITY;
+      lm = fmaxf(lm, v[k]);
+      if (v[k] > best) {
+        best = v[k];
+        best_idx = c + k;
+      }
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ls += (v[k] == -INFINITY) ? 0.f : __expf(v[k] - lm);
+    if (lm != -INFINITY) ms = ms_merge(ms, MaxSum{lm, ls});
+  }
+  block_reduce_msa(ms, best, best_idx);
+  const float lse = ms.m + __logf(ms.s);
+  const long long lab = static_cast<long long>(labels[row]);
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V_valid;
+  if (threadIdx.x == 0) {
+    float loss = valid ? lse - u2f(reinterpret_cast<const unsigned short*>(x)[lab]) : 0.f;
+    if (row_loss) row_loss[row] = loss;
+    if (metrics && valid) {
+      atomicAdd(metrics + 0, loss);
+      atomicAdd(metrics + 1, best_idx == lab ? 1.f : 0.f);
+      atomicAdd(metrics + 2, 1.f);
+    }
+  }
+  if (!write_grad) return;
+  const float scale = valid ? grad_scale : 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * 256 + threadIdx.x) * 8;
+    if (c >= V) break;
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float p = (c + k < V_valid) ? __expf(u2f(u[it][k]) - lse) : 0.f;
+      o[k] = f2bf((p - ((c + k) == lab ? 1.f : 0.f)) * scale);
+    }
+    *reinterpret_cast<bf16x8*>(x + c) = o;
+  }
+}
+
 // Row softmax forward / backward (last dim).  One block per row.
 template <typename T>
 __global__ __launch_bounds__(256) void softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N) {
@@ -228,7 +297,21 @@ void softmax_ce(int dtype, int label_bits, void* logits, const void* labels, flo
   hipLaunchKernelGGL((softmax_ce_kernel<T, L, VEC>), grid, block, 0, st, static_cast<T*>(logits),           \
                      static_cast<const L*>(labels), row_loss, metrics, M, V, V_valid, grad_scale, ignore_index, \
                      write_grad)
-  if (dtype == kBF16) {
+  if (dtype == kBF16 && vec && V <= 2048 * 32) {
+    // register-resident rows (one read + one write per logit)
+#define FFK_CE_REG(L, NIT)                                                                                     \
+  hipLaunchKernelGGL((softmax_ce_reg_kernel<L, NIT>), grid, block, 0, st, static_cast<bf16*>(logits),        \
+                     static_cast<const L*>(labels), row_loss, metrics, M, V, V_valid, grad_scale, ignore_index, \
+                     write_grad)
+    if (label_bits == 64) {
+      if (V <= 2048 * 16) FFK_CE_REG(int64_t, 16);
+      else FFK_CE_REG(int64_t, 32);
+    } else {
+      if (V <= 2048 * 16) FFK_CE_REG(int32_t, 16);
+      else FFK_CE_REG(int32_t, 32);
+    }
+#undef FFK_CE_REG
+  } else if (dtype == kBF16) {
     if (label_bits == 64) {
       if (vec) FFK_CE(bf16, int64_t, true);
       else FFK_CE(bf16, int64_t, false);
