@@ -204,6 +204,10 @@ __global__ __launch_bounds__(256) void softmax_ce_reg_kernel(bf16* __restrict__ 
                                                              int ignore_index, int write_grad) {
   const int row = blockIdx.x;
   bf16* x = logits + static_cast<size_t>(row) * V;
+  const long long lab = static_cast<long long>(labels[row]);
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V_valid;
+  // the label's logit, read before any thread overwrites the row with gradients
+  const float lab_logit = (threadIdx.x == 0 && valid) ? u2f(reinterpret_cast<const unsigned short*>(x)[lab]) : 0.f;
   u16x8 u[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -235,10 +239,8 @@ __global__ __launch_bounds__(256) void softmax_ce_reg_kernel(bf16* __restrict__ 
   }
   block_reduce_msa(ms, best, best_idx);
   const float lse = ms.m + __logf(ms.s);
-  const long long lab = static_cast<long long>(labels[row]);
-  const bool valid = lab != ignore_index && lab >= 0 && lab < V_valid;
   if (threadIdx.x == 0) {
-    float loss = valid ? lse - u2f(reinterpret_cast<const unsigned short*>(x)[lab]) : 0.f;
+    float loss = valid ? lse - lab_logit : 0.f;
     if (row_loss) row_loss[row] = loss;
     if (metrics && valid) {
       atomicAdd(metrics + 0, loss);
