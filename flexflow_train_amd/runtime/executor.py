@@ -77,6 +77,11 @@ class ExecConfig:
     # contend for the CUs, and residual gradients read by a queued dW GEMM
     # cannot be accumulated in place (one extra add each).
     wgrad_stream: bool = dataclasses.field(default_factory=lambda: os.environ.get("FF_WGRAD_STREAM", "0") != "0")
+    # debug mode (the AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING
+    # analogue at operator granularity): synchronise the device after every
+    # operator's forward and backward and re-raise a device fault naming the
+    # operator that launched it.  Not usable inside a hipGraph capture.
+    sync_debug: bool = dataclasses.field(default_factory=lambda: os.environ.get("FF_SYNC_DEBUG", "0") != "0")
     # row-sparse SGD update of embedding tables (plain SGD only; exact)
     sparse_embedding_update: bool = True
     # "counter": every rank generates only its own piece from a counter-based
@@ -887,6 +892,8 @@ class Executor:
             t0 = self.tracer.begin(f"{s.name}:fwd", "compute", self.step_num) if prof else None
             outs, saved = impl.forward(s.ctx, ins, ws)
             self.tracer.end(t0)
+            if self.cfg.sync_debug:
+                self._debug_sync(s, "forward")
             for o, t in zip(s.outputs, outs):
                 env[o] = t
                 if o in self.retain:
@@ -1027,6 +1034,8 @@ class Executor:
                     t0 = self.tracer.begin(f"{s.name}:bwd", "compute", self.step_num) if prof else None
                     gins = impl.backward(s.ctx, saved, gouts, wgs, need)
                     self.tracer.end(t0)
+                    if self.cfg.sync_debug:
+                        self._debug_sync(s, "backward")
                     for v, g, nd in zip(s.inputs, gins, need):
                         if g is not None and nd:
                             self._acc(grads, v, g)
@@ -1103,6 +1112,16 @@ class Executor:
             if len(f["group"]) > 1 and self.dist.distributed:
                 self._wg_join()
             self._launch_bucket(f, b)
+
+    def _debug_sync(self, s, phase: str):
+        """sync_debug: wait for the operator's kernels; a fault surfaces here,
+        attributed to the operator."""
+        if self.cfg.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+            return
+        try:
+            torch.cuda.synchronize(self.cfg.device)
+        except RuntimeError as e:
+            raise RuntimeError(f"device error after {phase} of operator {s.name} ({s.op_type}): {e}") from e
 
     # ---- weight-gradient side stream
     def _wg_enabled(self) -> bool:

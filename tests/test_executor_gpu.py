@@ -229,3 +229,21 @@ def test_wgrad_stream_matches_single_stream():
     torch.cuda.synchronize()
     for n in a.executor.parameter_names():
         torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=2e-2, atol=2e-3)
+
+
+def test_sync_debug_mode_trains_like_default():
+    """ExecConfig.sync_debug (FF_SYNC_DEBUG=1): a device synchronisation after
+    every operator, faults attributed to the operator; same numbers."""
+    torch.manual_seed(0)
+    a, feeds, labels = _model()
+    b, _, _ = _model()
+    dev = a.executor.cfg.device
+    feeds = {k: v.to(dev) for k, v in feeds.items()}
+    labels = labels.to(dev)
+    a.executor.cfg.sync_debug = True
+    for _ in range(2):
+        a.executor.train_step(feeds, labels)
+        b.executor.train_step(feeds, labels)
+    torch.cuda.synchronize()
+    for n in a.executor.parameter_names():
+        torch.testing.assert_close(a.executor.get_parameter(n), b.executor.get_parameter(n), rtol=1e-5, atol=1e-6)

@@ -132,6 +132,42 @@ def write_ninja(targets: list[str]) -> str:
         exe = os.path.join(ROOT, "bin", "ffc-ffi-test")
         lines.append(f"build {exe}: cc_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_ffi.c')} | {lib}")
         defaults += [lib, exe]
+    if "asan" in targets:
+        # host-code sanitizer build (ASan/UBSan for host code): the
+        # C++ core + C ABI + native CLIs compiled with -fsanitize=address,undefined
+        # into standalone executables under bin/asan/ (tests/test_sanitizers.py)
+        san = "-O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined"
+        lines += [f"san_flags = -std=c++17 -fPIC -Wall -Wno-unused-function {core_inc} "
+                  f"-I{os.path.join(ROOT, 'csrc', 'ffi')} {san}",
+                  "rule cxx_san",
+                  "  command = $cxx $san_flags -MMD -MF $out.d -c $in -o $out",
+                  "  depfile = $out.d",
+                  "  deps = gcc",
+                  "  description = CXX(asan) $in",
+                  "rule cc_san",
+                  f"  command = gcc -std=c11 {san} -I{os.path.join(ROOT, 'csrc', 'ffi')} -c $in -o $out",
+                  "  description = CC(asan) $in",
+                  "rule link_san",
+                  f"  command = $cxx {san} -o $out $in -lpthread",
+                  "  description = LINK(asan) $out"]
+        san_objs = []
+        for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "ffcore", "src", "*.cc"))):
+            o = os.path.join("obj", "asan", os.path.basename(s) + ".o")
+            lines.append(f"build {o}: cxx_san {s}")
+            san_objs.append(o)
+        fo = os.path.join("obj", "asan", "flexflow_c.cc.o")
+        lines.append(f"build {fo}: cxx_san {os.path.join(ROOT, 'csrc', 'ffi', 'flexflow_c.cc')}")
+        to = os.path.join("obj", "asan", "test_ffi.c.o")
+        lines.append(f"build {to}: cc_san {os.path.join(ROOT, 'csrc', 'ffi', 'test_ffi.c')}")
+        exe = os.path.join(ROOT, "bin", "asan", "ffc-ffi-test")
+        lines.append(f"build {exe}: link_san {to} {fo} {' '.join(san_objs)}")
+        defaults.append(exe)
+        for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "tools", "*.cc"))):
+            o = os.path.join("obj", "asan", "tool_" + os.path.basename(s) + ".o")
+            lines.append(f"build {o}: cxx_san {s}")
+            exe = os.path.join(ROOT, "bin", "asan", "ffc-" + os.path.basename(s)[:-3].replace("_", "-"))
+            lines.append(f"build {exe}: link_san {o} {' '.join(san_objs)}")
+            defaults.append(exe)
     lines.append("default " + " ".join(defaults))
     os.makedirs(BUILD, exist_ok=True)
     path = os.path.join(BUILD, "build.ninja")
