@@ -65,6 +65,14 @@ class FFConfig:
     local_execution: bool = False      # train on the native C++ CPU executor (lib/local-execution parity)
     native_data_loader: bool = True    # fit() on arrays: C++ prefetcher + pinned async H2D (runtime/dataloader.py)
     shuffle_data: bool = False         # native loader: reshuffle the samples every epoch
+    # fault tolerance (the reference has neither): fit()
+    # writes an atomic sharded checkpoint every `checkpoint_every` iterations
+    # under `checkpoint_dir` (keeping the newest `keep_checkpoints`) and, when
+    # started again (e.g. by torchrun --max-restarts after a failed rank),
+    # resumes from the newest complete one at the iteration it recorded
+    checkpoint_dir: str = ""
+    checkpoint_every: int = 0
+    keep_checkpoints: int = 2
     _start_time: float = dataclasses.field(default_factory=time.time)
     _models: list = dataclasses.field(default_factory=list, repr=False, compare=False)
 
@@ -161,6 +169,9 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--param-sync", dest="parameter_sync", choices=["nccl", "ps"])
     a("--shuffle", dest="shuffle_data", action="store_const", const=True)
     a("--seed", dest="seed", type=int)
+    a("--checkpoint-dir", dest="checkpoint_dir", type=str)
+    a("--checkpoint-every", dest="checkpoint_every", type=int)
+    a("--keep-checkpoints", dest="keep_checkpoints", type=int)
     # Legion / Realm flags: accepted, ignored
     for f in ("-ll:fsize", "-ll:zsize", "-ll:util", "-ll:bgwork", "-ll:csize", "-lg:prof", "-lg:prof_logfile"):
         a(f, dest="_ignored_" + f.strip("-").replace(":", "_"), type=str)

@@ -687,29 +687,42 @@ class FFModel:
         iters = num_samples // bs
         use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
         graphed = None
+        start_epoch, start_it = self._resume_fit(iters)
         ex.zero_metrics()
         if ex.cfg.device.type == "cuda":
             torch.cuda.synchronize()
         t0 = time.time()
-        for epoch in range(epochs):
+        first = True
+        for epoch in range(start_epoch, epochs):
             for l in loaders + [ylo]:
                 l.reset()
             ex.zero_metrics()
-            for it in range(iters):
+            skip = start_it if epoch == start_epoch else 0
+            for _ in range(skip):   # resumed mid-epoch: the batches already trained on
+                for l in loaders + [ylo]:
+                    l.next_batch()
+            for it in range(skip, iters):
                 feeds = {self._inputs[i].name: torch.as_tensor(l.next_batch()) for i, l in enumerate(loaders)}
                 labels = torch.as_tensor(ylo.next_batch())
-                if use_graph and (epoch > 0 or it >= 1):
-                    # iteration 0 ran eagerly (autotune / allocator warm-up);
-                    # capture the next one and replay it from then on
+                if use_graph and not first:
+                    # the first iteration ran eagerly (autotune / allocator
+                    # warm-up); capture the next one and replay it from then on
                     if graphed is None:
                         graphed = ex.make_graphed_train_step(feeds, labels, warmup=0)
                     graphed(feeds, labels)
                 else:
                     ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
-                if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0 and self.dist.rank == 0:
-                    print(f"epoch {epoch} iter {it + 1}/{iters}: {ex.perf_metrics()}", flush=True)
-            if self.dist.rank == 0 and iters:
-                print(f"epoch {epoch}: {ex.perf_metrics()}", flush=True)
+                first = False
+                self._after_fit_step(epoch, it, iters)
+                # perf_metrics() all-reduces across ranks: every rank calls it, rank 0 prints
+                if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0:
+                    pm = ex.perf_metrics()
+                    if self.dist.rank == 0:
+                        print(f"epoch {epoch} iter {it + 1}/{iters}: {pm}", flush=True)
+            if iters:
+                pm = ex.perf_metrics()
+                if self.dist.rank == 0:
+                    print(f"epoch {epoch}: {pm}", flush=True)
         if ex.cfg.device.type == "cuda":
             torch.cuda.synchronize()
         elapsed = time.time() - t0
@@ -718,6 +731,42 @@ class FFModel:
             print(f"ELAPSED TIME = {elapsed:.4f}s, THROUGHPUT = {thr:.2f} samples/s", flush=True)
         self.last_throughput = thr
         return thr
+
+    # ------------------------------------------------------------ fault tolerance
+    def _resume_fit(self, iters: int):
+        """FFConfig.checkpoint_dir: load the newest complete step checkpoint
+        and return the (epoch, iteration) fit() continues from."""
+        d = self.ffconfig.checkpoint_dir
+        if not d:
+            return 0, 0
+        from ..utils.checkpoint import latest_checkpoint, load_checkpoint
+        path = latest_checkpoint(d)
+        if path is None:
+            return 0, 0
+        meta = load_checkpoint(self, path)
+        prog = meta.get("progress") or {}
+        if prog.get("iters_per_epoch") != iters:
+            return 0, 0
+        epoch, it = int(prog["epoch"]), int(prog["iter"])
+        if it >= iters:
+            epoch, it = epoch + 1, 0
+        if self.dist.rank == 0:
+            print(f"resumed from {path}: epoch {epoch} iteration {it} (step {meta['step']})", flush=True)
+        return epoch, it
+
+    def _after_fit_step(self, epoch: int, it: int, iters: int):
+        """Periodic atomic checkpoint; FF_FAULT_INJECT_STEP=N raises right
+        after executor step N (a failed-rank stand-in for the resume tests)."""
+        cfg = self.ffconfig
+        g = epoch * iters + it + 1
+        if cfg.checkpoint_dir and cfg.checkpoint_every > 0 and g % cfg.checkpoint_every == 0:
+            from ..utils.checkpoint import save_step_checkpoint
+            save_step_checkpoint(self, cfg.checkpoint_dir,
+                                 {"epoch": epoch, "iter": it + 1, "iters_per_epoch": iters},
+                                 keep=cfg.keep_checkpoints)
+        inj = os.environ.get("FF_FAULT_INJECT_STEP")
+        if inj and self.executor.step_num == int(inj):
+            raise RuntimeError(f"injected fault after step {inj} (FF_FAULT_INJECT_STEP)")
 
     def _native_loader(self, xs, y, bs):
         """Arrays (not loader objects) on a batch-split layout -> the native
@@ -791,25 +840,34 @@ class FFModel:
         num_samples = iters * loader.batch
         use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
         graphed = None
+        start_epoch, start_it = self._resume_fit(iters)
+        if start_epoch or start_it:
+            loader.start(start_epoch * iters + start_it)
         if ex.cfg.device.type == "cuda":
             torch.cuda.synchronize()
         t0 = time.time()
+        first = True
         try:
-            for epoch in range(epochs):
+            for epoch in range(start_epoch, epochs):
                 ex.zero_metrics()
-                for it in range(iters):
+                for it in range(start_it if epoch == start_epoch else 0, iters):
                     feeds, labels, _ = loader.next()
-                    if use_graph and (epoch > 0 or it >= 1):
+                    if use_graph and not first:
                         if graphed is None:
                             graphed = ex.make_graphed_train_step(feeds, labels, warmup=0)
                         graphed(feeds, labels)
                     else:
                         ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
-                    if (self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0
-                            and self.dist.rank == 0):
-                        print(f"epoch {epoch} iter {it + 1}/{iters}: {ex.perf_metrics()}", flush=True)
-                if self.dist.rank == 0 and iters:
-                    print(f"epoch {epoch}: {ex.perf_metrics()}", flush=True)
+                    first = False
+                    self._after_fit_step(epoch, it, iters)
+                    if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0:
+                        pm = ex.perf_metrics()   # a collective: every rank calls it
+                        if self.dist.rank == 0:
+                            print(f"epoch {epoch} iter {it + 1}/{iters}: {pm}", flush=True)
+                if iters:
+                    pm = ex.perf_metrics()
+                    if self.dist.rank == 0:
+                        print(f"epoch {epoch}: {pm}", flush=True)
         finally:
             loader.close()
         if ex.cfg.device.type == "cuda":

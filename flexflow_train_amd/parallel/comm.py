@@ -68,6 +68,14 @@ class DistContext:
             kw = {}
             if backend == "nccl" and device is not None:
                 kw["device_id"] = device
+            # a hung collective (a failed / stalled rank) fails after this many
+            # seconds instead of blocking forever, so an elastic launcher
+            # (torchrun --max-restarts) can restart the job from its last
+            # checkpoint (FFConfig.checkpoint_dir)
+            tmo = os.environ.get("FF_DIST_TIMEOUT_S")
+            if tmo:
+                import datetime
+                kw["timeout"] = datetime.timedelta(seconds=float(tmo))
             dist.init_process_group(backend=backend, **kw)
         if dist.is_initialized():
             rank, world = dist.get_rank(), dist.get_world_size()

@@ -18,7 +18,9 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Dict
+import re
+import shutil
+from typing import Dict, Optional
 
 import torch
 
@@ -28,18 +30,58 @@ def _fingerprint(ex) -> str:
         sorted((int(k), list(v)) for k, v in ex.views.items()))
 
 
-def save_checkpoint(model, path: str):
+def save_checkpoint(model, path: str, progress: Optional[dict] = None):
+    """Every rank writes its shard; rank 0 writes meta.json only after every
+    rank's file is complete (barrier), so a directory WITH meta.json is a
+    complete checkpoint.  ``progress``: training-loop position (fit resume)."""
     ex = model.executor if hasattr(model, "executor") else model
     os.makedirs(path, exist_ok=True)
     st = ex.state_dict()
-    torch.save(st, os.path.join(path, f"rank{ex.rank}.pt"))
+    tmp = os.path.join(path, f"rank{ex.rank}.pt.tmp")
+    torch.save(st, tmp)
+    os.replace(tmp, os.path.join(path, f"rank{ex.rank}.pt"))
+    ex.dist.barrier()
     if ex.rank == 0:
         meta = {"format": "ffmi355x.checkpoint.v1", "world": ex.world, "step": ex.step_num,
                 "fingerprint": _fingerprint(ex),
                 "params": {p.name: list(p.logical_shape) for p in ex.params}}
-        with open(os.path.join(path, "meta.json"), "w") as f:
+        if progress is not None:
+            meta["progress"] = progress
+        with open(os.path.join(path, "meta.json.tmp"), "w") as f:
             json.dump(meta, f, indent=1)
+        os.replace(os.path.join(path, "meta.json.tmp"), os.path.join(path, "meta.json"))
     ex.dist.barrier()
+
+
+_STEP_DIR = re.compile(r"^step-(\d+)$")
+
+
+def latest_checkpoint(root: str) -> Optional[str]:
+    """Newest COMPLETE step checkpoint under ``root`` (a ``step-N`` directory
+    holding meta.json), or None."""
+    if not root or not os.path.isdir(root):
+        return None
+    best = None
+    for d in os.listdir(root):
+        m = _STEP_DIR.match(d)
+        if m and os.path.exists(os.path.join(root, d, "meta.json")):
+            if best is None or int(m.group(1)) > best[0]:
+                best = (int(m.group(1)), d)
+    return os.path.join(root, best[1]) if best else None
+
+
+def save_step_checkpoint(model, root: str, progress: dict, keep: int = 2) -> str:
+    """``root/step-<N>`` for the executor's step N; older complete step
+    checkpoints beyond the newest ``keep`` are removed (rank 0)."""
+    ex = model.executor if hasattr(model, "executor") else model
+    path = os.path.join(root, f"step-{ex.step_num}")
+    save_checkpoint(model, path, progress)
+    if ex.rank == 0 and keep > 0:
+        done = sorted((int(m.group(1)), d) for d in os.listdir(root) for m in [_STEP_DIR.match(d)] if m)
+        for _n, d in done[:-keep]:
+            shutil.rmtree(os.path.join(root, d), ignore_errors=True)
+    ex.dist.barrier()
+    return path
 
 
 def _assemble_full(path: str, world: int) -> Dict[str, torch.Tensor]:
