@@ -1,0 +1,153 @@
+"""Compile a PyTorch module with FlexFlow and keep training it with an
+ordinary PyTorch loop (reference: the designed flow of
+docs/plantuml/figures/pytorch-tracing.puml:95-232,305-361 — ``model.compile
+(algorithm=..., optimizer=...)`` turns an fx-traced module into a
+ComputationGraph, optimises it and returns a CompiledModel; the user then
+runs ``loss.backward(); optimizer.step()`` as usual.  The reference only
+designed this; it has no implementation).
+
+    cm = flexflow.torch.compile(model, example_inputs)     # fx trace -> CG -> search -> executor
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    for x, y in data:
+        loss = loss_fn(cm(x), y)      # forward on the FlexFlow executor (HIP kernels, the searched strategy)
+        loss.backward()               # backward on the executor; grads land in model.parameters()
+        opt.step(); opt.zero_grad()   # any torch optimizer; changed weights are synced on the next call
+
+The torch module keeps owning the parameters: the executor's weights are
+refreshed from them whenever their version counters moved (an in-place
+optimizer update), and backward() hands the executor's weight gradients back
+in the torch layouts (Linear [out, in], MultiheadAttention in_proj / out_proj).
+Inputs get no gradient (they are data)."""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+from torch import nn
+
+from ..core import DataType, FFConfig, FFModel, SGDOptimizer
+from .torch_fx import PyTorchModel, _mha_logical_weight, copy_weights
+
+_DT = {torch.float32: DataType.DT_FLOAT, torch.float16: DataType.DT_HALF, torch.bfloat16: DataType.DT_BFLOAT16,
+       torch.int32: DataType.DT_INT32, torch.int64: DataType.DT_INT64}
+
+
+def _mha_grad_to_torch(mod: nn.MultiheadAttention, g: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Inverse of torch_fx._mha_logical_weight for a gradient: FlexFlow
+    [q|k|v|o per head, heads] -> (in_proj_weight [3E, E], out_proj.weight [E, E])."""
+    E, H = mod.embed_dim, mod.num_heads
+    d = E // H
+    win = torch.zeros(3 * E, E, dtype=g.dtype, device=g.device)
+    wo = torch.zeros(E, E, dtype=g.dtype, device=g.device)
+    for h in range(H):
+        col = g[:, h]
+        for j in range(3):
+            win[j * E + h * d: j * E + (h + 1) * d] = col[j * E * d:(j + 1) * E * d].view(E, d).t()
+        wo[:, h * d:(h + 1) * d] = col[3 * E * d:4 * E * d].view(d, E).t()
+    return win, wo
+
+
+class CompiledModel:
+    """``module`` compiled onto the FlexFlow executor (see module docstring)."""
+
+    def __init__(self, module: nn.Module, example_inputs: Sequence[torch.Tensor],
+                 ffconfig: Optional[FFConfig] = None, algorithm: Optional[str] = None):
+        self.module = module
+        cfg = ffconfig or FFConfig()
+        ex_in = [torch.as_tensor(t) for t in example_inputs]
+        cfg.batch_size = int(ex_in[0].shape[0])
+        if algorithm is not None:
+            if algorithm in ("data_parallel", "dp"):
+                cfg.only_data_parallel = True
+            else:
+                cfg.search_algorithm = algorithm
+        self.ff = FFModel(cfg)
+        self.pm = PyTorchModel(module)
+        self.input_tensors = [self.ff.create_tensor(list(t.shape), _DT[t.dtype], name=f"input{i}")
+                              for i, t in enumerate(ex_in)]
+        self.pm.torch_to_ff(self.ff, self.input_tensors)
+        self.ff.compile(optimizer=SGDOptimizer(self.ff, lr=0.0))
+        self.ex = self.ff.executor
+        self.weights = self.pm.weights()
+        # executor parameter name -> (kind, torch object), and the torch
+        # parameters in a fixed order (the autograd Function's extra inputs)
+        names = set(self.ex.parameter_names())
+        self.pmap: Dict[str, Tuple[str, object]] = {}
+        for layer, ws in self.weights.items():
+            for wname, (kind, t) in ws.items():
+                if f"{layer}.{wname}" in names:
+                    self.pmap[f"{layer}.{wname}"] = (kind, t)
+                if kind == "mha":
+                    for extra in ("input_bias", "output_bias"):
+                        if f"{layer}.{extra}" in names:
+                            self.pmap[f"{layer}.{extra}"] = ("mha_" + extra, t)
+        self.params: List[nn.Parameter] = [p for p in module.parameters() if p.requires_grad]
+        self._versions: Optional[List[int]] = None
+        self._sync_weights(force=True)
+
+    # ---------------------------------------------------------------- weights
+    def _sync_weights(self, force: bool = False):
+        vers = [p._version for p in self.params]
+        if force or vers != self._versions:
+            copy_weights(self.ff, self.weights)
+            self._versions = vers
+
+    def _grads_to_torch(self) -> Dict[nn.Parameter, torch.Tensor]:
+        out: Dict[nn.Parameter, torch.Tensor] = {}
+
+        def put(p, g):
+            g = g.reshape(p.shape).to(device=p.device, dtype=p.dtype)
+            out[p] = out[p] + g if p in out else g
+
+        for pname, (kind, t) in self.pmap.items():
+            g = self.ex.get_parameter_grad(pname)
+            if kind == "linear_t":
+                put(t, g.t())
+            elif kind == "mha":
+                win, wo = _mha_grad_to_torch(t, g)
+                put(t.in_proj_weight, win)
+                put(t.out_proj.weight, wo)
+            elif kind == "mha_input_bias":
+                E, H = t.embed_dim, t.num_heads
+                put(t.in_proj_bias, g.view(3, E // H, H).permute(0, 2, 1).reshape(3 * E))
+            elif kind == "mha_output_bias":
+                put(t.out_proj.bias, g)
+            elif isinstance(t, torch.Tensor):
+                put(t, g)
+        return out
+
+    # ---------------------------------------------------------------- call
+    def __call__(self, *inputs: torch.Tensor) -> torch.Tensor:
+        self._sync_weights()
+        return _FlexFlowFunction.apply(self, len(inputs), *inputs, *self.params)
+
+    forward = __call__
+
+
+class _FlexFlowFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cm: CompiledModel, n_in: int, *args):
+        feeds = {t.name: args[i] for i, t in enumerate(cm.input_tensors)}
+        out = cm.ex.forward(feeds, training=True, keep_outputs=True)
+        ctx.cm, ctx.n_in = cm, n_in
+        ctx.out_dtype = out.dtype
+        dev = args[0].device
+        return out.detach().to(device=dev, dtype=torch.float32).clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        cm = ctx.cm
+        # an autograd.Function's backward runs with grad mode off; the
+        # executor's host fallbacks differentiate with torch autograd
+        with torch.enable_grad():
+            cm.ex.backward(gout.to(device=cm.ex.cfg.device, dtype=ctx.out_dtype).contiguous())
+        grads = cm._grads_to_torch()
+        return (None, None) + (None,) * ctx.n_in + tuple(grads.get(p) for p in cm.params)
+
+
+def compile(module: nn.Module, example_inputs: Sequence[torch.Tensor], ffconfig: Optional[FFConfig] = None,
+            algorithm: Optional[str] = None) -> CompiledModel:
+    """fx-trace ``module`` at the shapes of ``example_inputs``, build its
+    ComputationGraph, search a strategy (``algorithm``: "unity" | "mcmc" |
+    "data_parallel"; default FFConfig's) and return the CompiledModel."""
+    return CompiledModel(module, example_inputs, ffconfig, algorithm)

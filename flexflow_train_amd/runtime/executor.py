@@ -159,6 +159,7 @@ class Executor:
         self.valid_classes = valid_classes
         self.step_num = 0
         self.tracer = Tracer(self.cfg.device, self.rank, enabled=self.cfg.profiling)
+        self._ce_loss = loss_type in ("categorical_crossentropy", "sparse_categorical_crossentropy")
         self._build(output)
         self.loss = LossFunction(loss_type, self._global_rows(), valid_cols=valid_classes) if loss_type else None
         self.metrics_buf = torch.zeros(N_SLOTS, device=cfg.device, dtype=torch.float32)
@@ -366,7 +367,12 @@ class Executor:
         prod_step = next((s for s in self.steps if output in s.outputs), None)
         if prod_step is not None and prod_step.op_type == "SOFTMAX":
             self.softmax_fused_step = prod_step
-            self.loss_value = prod_step.inputs[0]
+            # a trailing softmax fused with a cross-entropy loss: the loss
+            # gradient (softmax - onehot) is taken at the logits.  Without such
+            # a loss (none, MSE, identity) backward() starts at the softmax
+            # OUTPUT and runs the softmax backward.
+            if self._ce_loss:
+                self.loss_value = prod_step.inputs[0]
         if self.cfg.fuse_add_layernorm:
             self._fuse_add_layernorm()
             self._fuse_conv_bn()
@@ -752,6 +758,24 @@ class Executor:
         if owner:
             box = p.layout.box(c.shard)
             full[tuple(slice(lo, hi) for lo, hi in box)] = self._to_logical(p, p.master)
+        if self.dist.distributed:
+            import torch.distributed as dist
+            dist.all_reduce(full)
+        return full
+
+    def get_parameter_grad(self, name: str) -> torch.Tensor:
+        """Full logical gradient of a weight after backward() (summed over the
+        data-parallel replicas once the gradient sync ran), fp32."""
+        p = next(pp for pp in self.params if pp.name == name)
+        full = torch.zeros(p.logical_shape, dtype=torch.float32, device=self.cfg.device)
+        if p.grad is None or not p.group:
+            return full
+        if self.flats[p.flat_id]["zero"]:
+            raise RuntimeError("get_parameter_grad: gradients are reduce-scattered under the sharded optimizer")
+        c = p.layout.coord(self.rank)
+        if c is not None and c.b == 0 and c.rep == 0 and c.a == 0:
+            box = p.layout.box(c.shard)
+            full[tuple(slice(lo, hi) for lo, hi in box)] = self._to_logical(p, p.grad.float())
         if self.dist.distributed:
             import torch.distributed as dist
             dist.all_reduce(full)

@@ -1,0 +1,94 @@
+"""flexflow.torch.compile: a PyTorch module trained by an ordinary PyTorch
+loop (loss.backward(); optimizer.step()) while its forward / backward run on
+the FlexFlow executor (reference: the designed torch.compile flow of
+docs/plantuml/figures/pytorch-tracing.puml — design only in the reference).
+Parity: losses and parameter gradients against the same module run eagerly."""
+import pytest
+import torch
+import torch.nn as nn
+
+import flexflow.torch as fft
+from test_frontends import SmallCNN, TinyAttn
+
+
+class MLP(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(16, 32)
+        self.fc2 = nn.Linear(32, 5)
+
+    def forward(self, x):
+        return self.fc2(torch.relu(self.fc1(x)))
+
+
+class SmoothMLP(MLP):
+    """tanh instead of ReLU: bf16 rounding cannot flip an activation mask
+    (a flipped ReLU unit changes that unit's gradients wholesale)."""
+
+    def forward(self, x):
+        return self.fc2(torch.tanh(self.fc1(x)))
+
+
+CASES = {
+    "mlp": (MLP, lambda: torch.randn(8, 16), 5, False),
+    "smooth_mlp": (SmoothMLP, lambda: torch.randn(8, 16), 5, False),
+    "cnn": (SmallCNN, lambda: torch.randn(4, 3, 8, 8), 10, True),
+    "attention": (TinyAttn, lambda: torch.randn(2, 6, 16), 5, True),
+}
+
+
+def _loss(out, y, probs):
+    if probs:   # the module ends in softmax: NLL of its probabilities
+        return nn.functional.nll_loss(torch.log(out.reshape(-1, out.shape[-1]) + 1e-9), y.reshape(-1))
+    return nn.functional.cross_entropy(out, y)
+
+
+def _run(case, device, steps=3):
+    cls, mk, ncls, probs = CASES[case]
+    torch.manual_seed(0)
+    net, ref = cls(), cls()
+    ref.load_state_dict(net.state_dict())
+    x = mk()
+    y = torch.randint(0, ncls, x.shape[:-1] if case == "attention" else x.shape[:1])
+    from flexflow.core import FFConfig
+    cfg = FFConfig()
+    cfg.cpu_only = device == "cpu"     # on a GPU box the CPU case still runs the host executor
+    cm = fft.compile(net, [x.to(device)], ffconfig=cfg)
+    o_ff, o_ref = cm(x.to(device)).cpu(), ref(x)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9)
+    opt_r = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    losses, gerr = [], []
+    for _ in range(steps):
+        lf = _loss(cm(x.to(device)).cpu(), y, probs)
+        lr_ = _loss(ref(x), y, probs)
+        lf.backward()
+        lr_.backward()
+        losses.append((lf.item(), lr_.item()))
+        for p, q in zip(net.parameters(), ref.parameters()):
+            gerr.append(((p.grad.cpu() - q.grad).abs().max() / (q.grad.abs().max() + 1e-6)).item())
+        opt.step()
+        opt_r.step()
+        opt.zero_grad()
+        opt_r.zero_grad()
+    return o_ff, o_ref, losses, gerr
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_compiled_module_trains_like_eager(case):
+    o_ff, o_ref, losses, gerr = _run(case, "cpu")
+    torch.testing.assert_close(o_ff, o_ref, rtol=1e-4, atol=1e-5)
+    for a, b in losses:
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), losses
+    assert max(gerr) < 1e-3, gerr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["smooth_mlp", "attention"])
+def test_compiled_module_trains_like_eager_gpu(case):
+    """On the GPU the executor computes in bf16 (HIP kernels): same training
+    trajectory within bf16 tolerance."""
+    o_ff, o_ref, losses, gerr = _run(case, "cuda")
+    torch.testing.assert_close(o_ff, o_ref, rtol=5e-2, atol=5e-2)
+    for a, b in losses:
+        assert abs(a - b) <= 5e-2 * max(1.0, abs(b)), losses
+    assert max(gerr) < 0.1, gerr
