@@ -51,7 +51,15 @@ struct AttnParams {
   int B, H, Sq, Sk;
   float scale;       // softmax scale (1/sqrt(D) by default)
   float scale_log2;  // scale * log2(e)
+  int prio;          // raise wave priority around MFMA clusters (FFK_ATTN_PRIO; guide T5)
 };
+
+__device__ __forceinline__ void prio_hi(const AttnParams& P) {
+  if (P.prio) __builtin_amdgcn_s_setprio(1);
+}
+__device__ __forceinline__ void prio_lo(const AttnParams& P) {
+  if (P.prio) __builtin_amdgcn_s_setprio(0);
+}
 
 template <int D>
 __device__ __forceinline__ int lds_off(int r, int c) {  // byte offset of chunk c of row r
@@ -166,6 +174,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
     if (wave_active) {
       // ---- S^T[key][q] for two 32-key tiles
       f32x16 s[2];
+      prio_hi(P);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         s[kt] = f32x16{};
@@ -175,6 +184,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
           s[kt] = mfma32(kf, qf[ks], s[kt]);
         }
       }
+      prio_lo(P);
       // ---- mask (only tiles that cross the sequence end or the causal
       // diagonal — a wave-uniform branch), tile max of the RAW scores: the
       // softmax scale is folded into one FMA per score inside exp2 below
@@ -218,6 +228,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         }
       l += psum;
       // ---- O^T[d][q] += V^T[d][key] P^T[key][q]
+      prio_hi(P);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -229,6 +240,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
             o[dt] = mfma32(vf, pf, o[dt]);
           }
         }
+      prio_lo(P);
     }
     if (has_next) {
       unsigned char* nxt = smem + ((t + 1) & 1) * 2 * TILE_BYTES;
@@ -340,12 +352,14 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(Att
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         f32x16 s = f32x16{}, dp = f32x16{};
+        prio_hi(P);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int off = lds_off<D>(kt * 32 + (lane & 31), 2 * ks + h);
           s = mfma32(lds_read16(Kt, off), qf[ks], s);
           dp = mfma32(lds_read16(Vt, off), df[ks], dp);
         }
+        prio_lo(P);
         if (need_mask) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -358,12 +372,14 @@ __global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(Att
 #pragma unroll
           for (int r = 0; r < 16; ++r) s[r] = fexp2(s[r] * P.scale_log2 - lse) * (dp[r] - dlt);
         }
+        prio_hi(P);
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           bf16x8 sf = acc_to_frag(s, st);
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_frag<D>(Kt, kt * 32 + 16 * st, dt, lane), sf, dq[dt]);
         }
+        prio_lo(P);
       }
     }
     if (has_next) {
@@ -475,6 +491,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
         f32x16 s[NKT], dp[NKT];
 #pragma unroll
         for (int j = 0; j < NKT; ++j) s[j] = dp[j] = f32x16{};
+        prio_hi(P);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int off = lds_off<D>(qt * 32 + (lane & 31), 2 * ks + h);
@@ -485,6 +502,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
             dp[j] = mfma32(da, vf[j][ks], dp[j]);
           }
         }
+        prio_lo(P);
 #pragma unroll
         for (int j = 0; j < NKT; ++j) {
           if (need_mask) {
@@ -507,6 +525,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
             }
           }
         }
+        prio_hi(P);
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           bf16x8 pf[NKT], sf[NKT];
@@ -526,6 +545,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
             }
           }
         }
+        prio_lo(P);
       }
     }
     if (has_next) {
@@ -589,6 +609,11 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
   P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
   P.scale = scale;
   P.scale_log2 = scale * 1.4426950408889634f;
+  static const int prio = [] {
+    const char* e = getenv("FFK_ATTN_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  P.prio = prio;
   (void)D;
   return P;
 }
