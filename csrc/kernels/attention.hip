@@ -609,12 +609,13 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
   P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
   P.scale = scale;
   P.scale_log2 = scale * 1.4426950408889634f;
+  // default: on for D = 128 (forward -7 %, backward -1 %), off for D = 64
+  // where it measured neutral (profiles/ab_attn_prio_r2.txt)
   static const int prio = [] {
     const char* e = getenv("FFK_ATTN_PRIO");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
-  P.prio = prio;
-  (void)D;
+  P.prio = prio >= 0 ? prio : (D == 128 ? 1 : 0);
   return P;
 }
 
