@@ -1185,6 +1185,7 @@ class Executor:
             b["launched"] = True
             if w is not None:
                 self._works.append(w)
+                f.setdefault("works", []).append(w)
 
     def _gather_updated(self):
         """Sharded optimizer: all-gather every bucket's updated compute copy
@@ -1209,16 +1210,30 @@ class Executor:
             for b in f["buckets"]:
                 if not b.get("launched"):
                     self._launch_bucket(f, b)
-        for w in self._works:
-            w.wait()
-        self._works = []
         for f in self.flats:
             for b in f["buckets"]:
                 b["launched"] = False
+        if getattr(self, "_defer_grad_wait", False):
+            # train_step: update() waits flat by flat, so the optimizer step of
+            # a flat whose all-reduces finished (the bf16 GEMM weights) runs
+            # while the last buckets (the fp32 embedding tables, finalised at
+            # the very end of the backward pass) are still being reduced
+            return
+        self._wait_works()
+
+    def _wait_works(self, f=None):
+        """The compute stream waits for the pending gradient collectives of
+        flat ``f`` (all flats when None)."""
+        for ff in ([f] if f is not None else self.flats):
+            for w in ff.pop("works", []):
+                w.wait()
+        if f is None:
+            self._works = []
 
     def update(self, lr: Optional[float] = None):
         scale = 1.0
         if self.cfg.grad_clip > 0:
+            self._wait_works()
             norm = self.grad_norm()
             if norm > self.cfg.grad_clip:
                 scale = self.cfg.grad_clip / (norm + 1e-6)
@@ -1230,10 +1245,12 @@ class Executor:
                 continue
             if f.get("ps") and self.dist.distributed and self.rank != min(f["group"]):
                 continue  # PS: only the leader updates (its optimizer state is the only one)
+            self._wait_works(f)
             if f["sparse"]:
                 self._sparse_sgd(f, lr, scale)
                 continue
             f["opt"].step(lr=lr, grad_scale=scale)
+        self._wait_works()   # flats that skipped their step: before the next backward zeroes their grads
         self._ov_flats = set()
         self._gather_updated()
         self._broadcast_ps()
@@ -1298,10 +1315,12 @@ class Executor:
         self.forward(feeds, training=True)
         g = self.compute_loss(labels)
         self._overlap_lr = (True, lr)
+        self._defer_grad_wait = True
         try:
             self.backward(g)
         finally:
             self._overlap_lr = None
+            self._defer_grad_wait = False
         self.update(lr)
 
     def _overlap_flats(self) -> List[dict]:
@@ -1442,6 +1461,7 @@ class Executor:
             rec.abort()
             self._works = []
             for f in self.flats:
+                f.pop("works", None)
                 for b in f["buckets"]:
                     b["launched"] = False
             raise
