@@ -458,8 +458,11 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
     float* ds = ls + QT;
     if (threadIdx.x < QT) {
       const int qq = q0 + threadIdx.x;
-      ls[threadIdx.x] = qq < P.Sq ? P.lse[static_cast<int64_t>(bh) * P.Sq + qq] : INFINITY;
-      ds[threadIdx.x] = qq < P.Sq ? P.delta[static_cast<int64_t>(bh) * P.Sq + qq] : 0.f;
+      // row constants, pre-shaped to seed the S and dP accumulators (guide:
+      // "row constants as the initial accumulator"): S' = Q K^T - lse / c,
+      // dP' = dO V^T - delta, so p = exp2(c S') and dS = p dP' need no subtraction
+      ls[threadIdx.x] = qq < P.Sq ? -P.lse[static_cast<int64_t>(bh) * P.Sq + qq] / P.scale_log2 : -INFINITY;
+      ds[threadIdx.x] = qq < P.Sq ? -P.delta[static_cast<int64_t>(bh) * P.Sq + qq] : 0.f;
     }
   };
   if (t0 < n_q_tiles) {
@@ -490,7 +493,13 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
       for (int qt = 0; qt < 2; ++qt) {
         f32x16 s[NKT], dp[NKT];
 #pragma unroll
-        for (int j = 0; j < NKT; ++j) s[j] = dp[j] = f32x16{};
+        for (int j = 0; j < NKT; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            s[j][r] = ls[ql_];
+            dp[j][r] = ds[ql_];
+          }
         prio_hi(P);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -508,20 +517,18 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
           if (need_mask) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              const int qq = q0 + ql_;
-              float pv = fexp2(s[j][r] * P.scale_log2 - ls[ql_]);
+              const int qq = q0 + qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              float pv = fexp2(s[j][r] * P.scale_log2);
               if (qq >= P.Sq || (CAUSAL && key[j] > qq) || !k_ok[j]) pv = 0.f;
               s[j][r] = pv;
-              dp[j][r] = pv * (dp[j][r] - ds[ql_]);
+              dp[j][r] = pv * dp[j][r];
             }
           } else {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int ql_ = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              const float pv = fexp2(s[j][r] * P.scale_log2 - ls[ql_]);
+              const float pv = fexp2(s[j][r] * P.scale_log2);
               s[j][r] = pv;
-              dp[j][r] = pv * (dp[j][r] - ds[ql_]);
+              dp[j][r] = pv * dp[j][r];
             }
           }
         }
