@@ -151,3 +151,143 @@ def compile(module: nn.Module, example_inputs: Sequence[torch.Tensor], ffconfig:
     ComputationGraph, search a strategy (``algorithm``: "unity" | "mcmc" |
     "data_parallel"; default FFConfig's) and return the CompiledModel."""
     return CompiledModel(module, example_inputs, ffconfig, algorithm)
+
+
+# ----------------------------------------------------------------- dynamo
+# torch.compile(model, backend="flexflow"): dynamo hands the backend a flat
+# graph whose parameters are PLACEHOLDERS (nn.Parameter example inputs) used by
+# functional ops (torch._C._nn.linear, torch.conv2d, F.layer_norm, ...).  The
+# backend rebinds each such op to an nn.Module holding the SAME Parameter
+# objects (so gradients still reach the user's parameters), drops the
+# parameter placeholders, and compiles the resulting module-structured graph
+# with CompiledModel.  Graphs with ops the importer does not map run eagerly.
+def _rebind_parameter_ops(gm: torch.fx.GraphModule, example_inputs) -> Tuple[torch.fx.GraphModule, List[int]]:
+    import copy
+
+    import torch.nn.functional as F
+
+    # work on a copy: dynamo passes the caller's arguments by the ORIGINAL
+    # graph's placeholders
+    gm = torch.fx.GraphModule(gm, copy.deepcopy(gm.graph))
+    phs = [n for n in gm.graph.nodes if n.op == "placeholder"]
+    is_param = {n: isinstance(e, nn.Parameter) for n, e in zip(phs, example_inputs)}
+    pval = {n: e for n, e in zip(phs, example_inputs) if is_param[n]}
+    root = nn.Module()
+    k = 0
+
+    def param_of(a):
+        if a is None:
+            return None
+        if isinstance(a, torch.fx.Node) and is_param.get(a):
+            return pval[a]
+        raise NotImplementedError("a parameter op whose weight is not a module parameter")
+
+    for node in list(gm.graph.nodes):
+        if node.op != "call_function":
+            continue
+        t, args = node.target, list(node.args)
+        if t in (torch._C._nn.linear, F.linear):
+            x, w = args[0], param_of(args[1])
+            b = param_of(args[2] if len(args) > 2 else node.kwargs.get("bias"))
+            m = nn.Linear(w.shape[1], w.shape[0], bias=b is not None)
+            m.weight = w
+            if b is not None:
+                m.bias = b
+        elif t in (torch.conv2d, F.conv2d):
+            x, w = args[0], param_of(args[1])
+            b = param_of(args[2] if len(args) > 2 else node.kwargs.get("bias"))
+            stride, padding, dilation, groups = (list(args[3:7]) + [1, 0, 1, 1][len(args[3:7]):])
+            m = nn.Conv2d(w.shape[1] * groups, w.shape[0], tuple(w.shape[2:]), stride=stride, padding=padding,
+                          dilation=dilation, groups=groups, bias=b is not None)
+            m.weight = w
+            if b is not None:
+                m.bias = b
+        elif t is F.layer_norm:
+            x, shape = args[0], args[1]
+            w = param_of(args[2] if len(args) > 2 else node.kwargs.get("weight"))
+            b = param_of(args[3] if len(args) > 3 else node.kwargs.get("bias"))
+            eps = args[4] if len(args) > 4 else node.kwargs.get("eps", 1e-5)
+            m = nn.LayerNorm(shape, eps=eps, elementwise_affine=w is not None)
+            if w is not None:
+                m.weight, m.bias = w, b
+        elif t in (F.max_pool2d, torch.max_pool2d, F.avg_pool2d, torch._C._nn.avg_pool2d):
+            x = args[0]
+            ks = args[1] if len(args) > 1 else node.kwargs["kernel_size"]
+            st = args[2] if len(args) > 2 else node.kwargs.get("stride", None)
+            pd = args[3] if len(args) > 3 else node.kwargs.get("padding", 0)
+            cls = nn.MaxPool2d if t in (F.max_pool2d, torch.max_pool2d) else nn.AvgPool2d
+            m = cls(ks, stride=st or ks, padding=pd)
+        elif t in (F.embedding, torch.embedding):
+            x, w = (args[0], param_of(args[1])) if t is F.embedding else (args[1], param_of(args[0]))
+            m = nn.Embedding(w.shape[0], w.shape[1])
+            m.weight = w
+        else:
+            if any(isinstance(a, torch.fx.Node) and is_param.get(a) for a in args):
+                raise NotImplementedError(f"parameter used by {t}")
+            continue
+        name = f"ff_mod{k}"
+        k += 1
+        root.add_module(name, m)
+        gm.add_submodule(name, m)
+        with gm.graph.inserting_before(node):
+            new = gm.graph.call_module(name, (x,))
+        node.replace_all_uses_with(new)
+        gm.graph.erase_node(node)
+    data_pos = [i for i, n in enumerate(phs) if not is_param[n]]
+    for n in phs:
+        if is_param[n]:
+            if n.users:
+                raise NotImplementedError("a parameter is used outside a module-mapped op")
+            gm.graph.erase_node(n)
+    gm.graph.lint()
+    return torch.fx.GraphModule(root, gm.graph), data_pos
+
+
+COMPILED: List[CompiledModel] = []   # graphs the backend compiled (introspection / tests)
+
+
+def flexflow_backend(gm: torch.fx.GraphModule, example_inputs, ffconfig: Optional[FFConfig] = None):
+    """The ``backend="flexflow"`` entry point for torch.compile."""
+    import warnings
+
+    try:
+        mod, data_pos = _rebind_parameter_ops(gm, example_inputs)
+        cm = CompiledModel(mod, [example_inputs[i] for i in data_pos], ffconfig)
+    except Exception as e:  # noqa: BLE001 — unsupported graph: dynamo runs it eagerly
+        warnings.warn(f"flexflow backend: running this graph eagerly ({type(e).__name__}: {e})")
+        return gm.forward
+
+    def run(*args):
+        out = cm(*[args[i] for i in data_pos])
+        return (out,)
+
+    run.compiled_model = cm
+    COMPILED.append(cm)
+    return run
+
+
+def backend(**config):
+    """A configured backend: ``torch.compile(m, backend=flexflow.torch.backend(
+    cpu_only=True, search_algorithm="mcmc"))`` (FFConfig fields)."""
+    def _be(gm, example_inputs):
+        cfg = FFConfig()
+        for k, v in config.items():
+            if not hasattr(cfg, k):
+                raise AttributeError(f"FFConfig has no field {k}")
+            setattr(cfg, k, v)
+        return flexflow_backend(gm, example_inputs, cfg)
+    return _be
+
+
+def _register_dynamo_backend():
+    try:
+        from torch._dynamo import register_backend
+    except Exception:  # noqa: BLE001 — dynamo unavailable
+        return
+    try:
+        register_backend(name="flexflow")(flexflow_backend)
+    except Exception:  # noqa: BLE001 — already registered
+        pass
+
+
+_register_dynamo_backend()
