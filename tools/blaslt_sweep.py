@@ -29,6 +29,9 @@ def shapes(tokens, hidden, ffn, vocab):
     out.append(("head_fwd", tokens, vocab, h, False, False))
     out.append(("head_dx", tokens, h, vocab, False, True))
     out.append(("head_dw", h, vocab, tokens, True, False))
+    if os.environ.get("SWEEP_NT_DW"):
+        # the weight gradients as NT products (operands token-contiguous)
+        out = [(n + "_nt", M, N, Kd, False, True) for n, M, N, Kd, ta, tb in out if n.endswith("_dw")]
     return out
 
 
