@@ -198,12 +198,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
             if (key >= P.Sk || (CAUSAL && key > q)) s[kt][r] = -INFINITY;
           }
       }
-      float tmax = -INFINITY;
+      // two independent v_max3 chains over the 32 scores (16 issues)
+      float t0 = fmax3(s[0][0], s[0][1], s[0][2]);
+      float t1 = fmax3(s[1][0], s[1][1], s[1][2]);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) tmax = fmaxf(tmax, fmaxf(s[kt][r], s[kt][r + 1]));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      for (int r = 3; r < 15; r += 2) {
+        t0 = fmax3(t0, s[0][r], s[0][r + 1]);
+        t1 = fmax3(t1, s[1][r], s[1][r + 1]);
+      }
+      float tmax = fmax3(fmax3(t0, s[0][15], s[1][15]), t1, t1);
+      const float tother = __shfl_xor(tmax, 32, 64);
+      tmax = fmax3(tmax, tother, tother);
       // ---- lazy rescale: the running max m only moves when some lane's
       // tile max exceeds it by more than 8 in the log2 domain (p <= 256 is
       // exact enough in fp32 and bf16-relative); a wave-uniform branch, so
@@ -217,16 +222,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
       }
       const float mc = (m == -INFINITY) ? 0.f : m * P.scale_log2;
-      float psum = 0.f;
+      float psum[2] = {0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float pv = fexp2(fmaf(s[kt][r], P.scale_log2, -mc));
           s[kt][r] = pv;
-          psum += pv;
+          psum[kt] += pv;
         }
-      l += psum;
+      l += psum[0] + psum[1];
       // ---- O^T[d][q] += V^T[d][key] P^T[key][q]
       prio_hi(P);
 #pragma unroll

@@ -78,6 +78,16 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 // ldexp + 2 cndmask per element) that dominated the softmax VALU in attention
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// max of three in ONE v_max3_f32.  fmaxf on values the compiler cannot prove
+// canonical (MFMA accumulators) is lowered with a NaN-quieting v_max x,x per
+// operand before the max itself: a 32-score tile max cost ~56 VALU issues
+// instead of 16.  Scores here are never signalling NaNs.
+__device__ __forceinline__ float fmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // tanh from one v_exp_f32 + one v_rcp_f32 (libm tanhf is ~10x the
 // instructions and made the GELU backward VALU-bound); |err| < 1e-6 abs,
 // saturates correctly at +-inf.

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Time the flash-attention forward and backward (HIP events) on the BERT-large
+and GPT-3-medium shapes; FF_PKG_ROOT selects the package tree (same-box A/B of
+two builds: FF_PKG_ROOT=ab_prev python tools/attn_time.py).
+
+    python tools/attn_time.py [iters]
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("FF_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from flexflow_train_amd import kernels as K  # noqa: E402
+
+SHAPES = {"bert-large": (32, 512, 16, 64, False), "gpt3-medium": (8, 2048, 16, 64, True)}
+
+
+def _time(fn, iters):
+    for _ in range(3):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    for name, (B, S, H, D, causal) in SHAPES.items():
+        g = torch.Generator(device="cuda").manual_seed(0)
+        qkv = torch.randn(B, S, 3, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+        dqkv = torch.empty_like(qkv)
+        o, lse = K.attention_fwd(q, k, v, causal=causal)
+        fwd = _time(lambda: K.attention_fwd(q, k, v, causal=causal, out=o), iters)
+        bwd = _time(lambda: K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2],
+                                            causal=causal), iters)
+        fl = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+        print(json.dumps({"shape": name, "pkg": os.environ.get("FF_PKG_ROOT", "tree"), "fwd_ms": round(fwd, 4),
+                          "bwd_ms": round(bwd, 4), "fwd_tflops": round(fl / fwd / 1e9, 1),
+                          "bwd_tflops": round(2.5 * fl / bwd / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
