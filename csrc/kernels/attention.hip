@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams P) {
 //   S^T = K Q^T ; P^T = exp2(S^T*c - lse) ; dP^T = V dO^T ;
 //   dS^T = P^T (dP^T - delta) ; dQ^T += K^T dS^T ; dQ = scale * dQ
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, (D == 64 ? 2 : 1)) void attn_bwd_dq_kernel(AttnParams P) {
+__global__ __launch_bounds__(256, (D == 64 ? 3 : 1)) void attn_bwd_dq_kernel(AttnParams P) {
   constexpr int KS = D / 16, DT = D / 32, KV = 64;
   constexpr int TILE_BYTES = KV * D * 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];
