@@ -51,6 +51,7 @@ struct AttnParams {
   int B, H, Sq, Sk;
   float scale;       // softmax scale (1/sqrt(D) by default)
   float scale_log2;  // scale * log2(e)
+  float inv_scale_log2;  // 1 / scale_log2 (no IEEE divide in the loops)
   int prio;          // raise wave priority around MFMA clusters (FFK_ATTN_PRIO; guide T5)
 };
 
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
       // tile max exceeds it by more than 8 in the log2 domain (p <= 256 is
       // exact enough in fp32 and bf16-relative); a wave-uniform branch, so
       // the o *= alpha pass runs on a few early tiles instead of every tile
-      if (__any(tmax > m + 8.f / P.scale_log2)) {
+      if (__any(tmax > m + 8.f * P.inv_scale_log2)) {
         const float m_new = fmaxf(m, tmax);
         const float alpha = (m_new == -INFINITY) ? 1.f : fexp2((m - m_new) * P.scale_log2);
         m = m_new;
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
       // row constants, pre-shaped to seed the S and dP accumulators (guide:
       // "row constants as the initial accumulator"): S' = Q K^T - lse / c,
       // dP' = dO V^T - delta, so p = exp2(c S') and dS = p dP' need no subtraction
-      ls[threadIdx.x] = qq < P.Sq ? -P.lse[static_cast<int64_t>(bh) * P.Sq + qq] / P.scale_log2 : -INFINITY;
+      ls[threadIdx.x] = qq < P.Sq ? -P.lse[static_cast<int64_t>(bh) * P.Sq + qq] * P.inv_scale_log2 : -INFINITY;
       ds[threadIdx.x] = qq < P.Sq ? -P.delta[static_cast<int64_t>(bh) * P.Sq + qq] : 0.f;
     }
   };
@@ -621,6 +622,7 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
   P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
   P.scale = scale;
   P.scale_log2 = scale * 1.4426950408889634f;
+  P.inv_scale_log2 = 1.f / P.scale_log2;
   // default: on for D = 128 (forward -7 %, backward -1 %), off for D = 64
   // where it measured neutral (profiles/ab_attn_prio_r2.txt)
   static const int prio = [] {
