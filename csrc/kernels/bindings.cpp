@@ -62,10 +62,10 @@ PYBIND11_MODULE(_ffkernels, m) {
     axpby(dt, P(x), P(y), n, a, b, S(st));
   });
   m.def("softmax_ce", [](int dt, int label_bits, uintptr_t logits, uintptr_t labels, uintptr_t row_loss,
-                         uintptr_t metrics, int M, int V, int V_valid, float grad_scale, int ignore_index,
-                         int write_grad, uintptr_t st) {
-    softmax_ce(dt, label_bits, P(logits), P(labels), F(row_loss), F(metrics), M, V, V_valid, grad_scale,
-               ignore_index, write_grad, S(st));
+                         uintptr_t metrics, uintptr_t row_stats, int M, int V, int V_valid, float grad_scale,
+                         int ignore_index, int write_grad, uintptr_t st) {
+    softmax_ce(dt, label_bits, P(logits), P(labels), F(row_loss), F(metrics), F(row_stats), M, V, V_valid,
+               grad_scale, ignore_index, write_grad, S(st));
   });
   m.def("softmax_fwd", [](int dt, uintptr_t x, uintptr_t y, int M, int N, uintptr_t st) {
     softmax_fwd(dt, P(x), P(y), M, N, S(st));

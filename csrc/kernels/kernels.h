@@ -32,8 +32,11 @@ void cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, hipStr
 void axpby(int dtype, const void* x, void* y, int64_t n, float a, float b, hipStream_t st);
 
 // ---- softmax.hip
-void softmax_ce(int dtype, int label_bits, void* logits, const void* labels, float* row_loss, float* metrics, int M,
-                int V, int V_valid, float grad_scale, int ignore_index, int write_grad, hipStream_t st);
+// row_stats: optional [M, 3] fp32 scratch; with metrics, per-row metric terms
+// are written there and reduced by one block instead of per-row atomics
+void softmax_ce(int dtype, int label_bits, void* logits, const void* labels, float* row_loss, float* metrics,
+                float* row_stats, int M, int V, int V_valid, float grad_scale, int ignore_index, int write_grad,
+                hipStream_t st);
 void softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStream_t st);
 void softmax_bwd(int dtype, const void* dy, const void* y, void* dx, int M, int N, hipStream_t st);
 

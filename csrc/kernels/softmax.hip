@@ -81,11 +81,50 @@ __device__ __forceinline__ void block_reduce_msa(MaxSum& ms, float& best, int& b
   __syncthreads();
 }
 
+// Per-row metric contributions.  With `row_stats` ([M, 3]) each row writes
+// its own (loss, correct, counted) and ce_metrics_reduce_kernel sums them in
+// one block: three same-address float atomics per row from every XCD had cost
+// 0.32 ms per BERT-large step (16384 rows), most of the kernel.  Without it
+// (a caller that passes no scratch) the atomics remain.
+__device__ __forceinline__ void ce_row_metrics(float* metrics, float* row_stats, int row, float loss, bool correct,
+                                               bool valid) {
+  if (row_stats) {
+    float* rs = row_stats + 3 * static_cast<size_t>(row);
+    rs[0] = loss;
+    rs[1] = correct ? 1.f : 0.f;
+    rs[2] = valid ? 1.f : 0.f;
+  } else if (valid) {
+    atomicAdd(metrics + 0, loss);
+    atomicAdd(metrics + 1, correct ? 1.f : 0.f);
+    atomicAdd(metrics + 2, 1.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_metrics_reduce_kernel(const float* __restrict__ row_stats, int M,
+                                                                float* __restrict__ metrics) {
+  __shared__ float scratch[4];
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int r = threadIdx.x; r < M; r += 256) {
+    a += row_stats[3 * static_cast<size_t>(r)];
+    b += row_stats[3 * static_cast<size_t>(r) + 1];
+    c += row_stats[3 * static_cast<size_t>(r) + 2];
+  }
+  a = block_sum<256>(a, scratch);
+  b = block_sum<256>(b, scratch);
+  c = block_sum<256>(c, scratch);
+  if (threadIdx.x == 0) {
+    metrics[0] += a;
+    metrics[1] += b;
+    metrics[2] += c;
+  }
+}
+
 // logits: [M, V] (row stride V); labels: [M] int32 or int64.
 // Columns >= V_valid are padding (excluded from the softmax, grad 0).
 template <typename T, typename L, bool VEC>
 __global__ __launch_bounds__(256) void softmax_ce_kernel(T* __restrict__ logits, const L* __restrict__ labels,
                                                          float* __restrict__ row_loss, float* __restrict__ metrics,
+                                                         float* __restrict__ row_stats,
                                                          int M, int V, int V_valid, float grad_scale,
                                                          int ignore_index, int write_grad) {
   const int row = blockIdx.x;
@@ -140,11 +179,7 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(T* __restrict__ logits,
   if (threadIdx.x == 0) {
     float loss = valid ? lse - ldf<T>(x + lab) : 0.f;
     if (row_loss) row_loss[row] = loss;
-    if (metrics && valid) {
-      atomicAdd(metrics + 0, loss);
-      atomicAdd(metrics + 1, best_idx == lab ? 1.f : 0.f);
-      atomicAdd(metrics + 2, 1.f);
-    }
+    if (metrics) ce_row_metrics(metrics, row_stats, row, loss, valid && best_idx == lab, valid);
   }
   if (!write_grad) return;
   __syncthreads();  // the label logit must be read before it is overwritten
@@ -196,12 +231,22 @@ __global__ __launch_bounds__(256) void softmax_ce_kernel(T* __restrict__ logits,
 // bf16 rows that fit in registers (V <= 2048 * NIT): the row is loaded ONCE
 // (every chunk's load issued up front), reduced, and the gradient written
 // from the same registers — one HBM read + one write per logit instead of
-// the two reads of the streaming kernel above.
+// the two reads of the streaming kernel above.  Since the whole row is in
+// registers the reduction is three plain passes, ~12 VALU issues per logit
+// (it was ~25 with a per-chunk online max/sum merge, a NaN-canonicalising
+// fmaxf, a padding check and an argmax update per logit, and a label compare
+// per gradient):
+//   1. thread max with v_max3 (padding columns were set to -inf at load);
+//   2. sum of exp2(v log2e - m log2e) — one FMA + one exp2 + one add — and,
+//      only when metrics are requested, the first index of the maximum;
+//   3. gradient p * scale (one FMA + exp2 + mul); the label's "- 1" is one
+//      store by thread 0 after a barrier.
 template <typename L, int NIT>
 __global__ __launch_bounds__(256) void softmax_ce_reg_kernel(bf16* __restrict__ logits, const L* __restrict__ labels,
                                                              float* __restrict__ row_loss, float* __restrict__ metrics,
-                                                             int M, int V, int V_valid, float grad_scale,
+                                                             float* __restrict__ row_stats, int M, int V, int V_valid, float grad_scale,
                                                              int ignore_index, int write_grad) {
+  constexpr float L2E = 1.4426950408889634f;
   const int row = blockIdx.x;
   bf16* x = logits + static_cast<size_t>(row) * V;
   const long long lab = static_cast<long long>(labels[row]);
@@ -214,54 +259,78 @@ __global__ __launch_bounds__(256) void softmax_ce_reg_kernel(bf16* __restrict__ 
     const int c = (it * 256 + threadIdx.x) * 8;
     if (c < V) u[it] = *reinterpret_cast<const u16x8*>(x + c);
   }
-  MaxSum ms{-INFINITY, 0.f};
-  float best = -INFINITY;
-  int best_idx = 0;
+  // padding columns (>= V_valid, only in the row's last chunks) become -inf
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int c = (it * 256 + threadIdx.x) * 8;
-    if (c >= V) break;
-    float v[8];
-    float lm = -INFINITY;
+    if (c < V && c + 8 > V_valid) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      v[k] = (c + k < V_valid) ? u2f(u[it][k]) : -INFINITY;
-      lm = fmaxf(lm, v[k]);
-      if (v[k] > best) {
-        best = v[k];
-        best_idx = c + k;
+      for (int k = 0; k < 8; ++k)
+        if (c + k >= V_valid) u[it][k] = 0xFF80;
+    }
+  }
+  // ---- 1. thread max
+  float t0 = -INFINITY, t1 = -INFINITY;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * 256 + threadIdx.x) * 8;
+    if (c < V) {
+      float& t = (it & 1) ? t1 : t0;
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) t = fmax3(t, u2f(u[it][k]), u2f(u[it][k + 1]));
+    }
+  }
+  const float tm = fmax3(t0, t1, t1);
+  // ---- 2. thread sum relative to the thread max (+ first index of the max)
+  const float tmc = (tm == -INFINITY) ? 0.f : tm * L2E;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = (it * 256 + threadIdx.x) * 8;
+    if (c < V) {
+      float& sacc = (it & 1) ? s1 : s0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sacc += fexp2(fmaf(u2f(u[it][k]), L2E, -tmc));
+    }
+  }
+  int best_idx = 0;
+  if (metrics) {
+    best_idx = 0x7fffffff;
+#pragma unroll
+    for (int it = NIT - 1; it >= 0; --it) {
+      const int c = (it * 256 + threadIdx.x) * 8;
+      if (c < V) {
+#pragma unroll
+        for (int k = 7; k >= 0; --k) best_idx = (u2f(u[it][k]) == tm) ? c + k : best_idx;
       }
     }
-    float ls = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ls += (v[k] == -INFINITY) ? 0.f : __expf(v[k] - lm);
-    if (lm != -INFINITY) ms = ms_merge(ms, MaxSum{lm, ls});
   }
+  MaxSum ms{tm, s0 + s1};
+  float best = tm;
   block_reduce_msa(ms, best, best_idx);
   const float lse = ms.m + __logf(ms.s);
   if (threadIdx.x == 0) {
     float loss = valid ? lse - lab_logit : 0.f;
     if (row_loss) row_loss[row] = loss;
-    if (metrics && valid) {
-      atomicAdd(metrics + 0, loss);
-      atomicAdd(metrics + 1, best_idx == lab ? 1.f : 0.f);
-      atomicAdd(metrics + 2, 1.f);
-    }
+    if (metrics) ce_row_metrics(metrics, row_stats, row, loss, valid && best_idx == lab, valid);
   }
   if (!write_grad) return;
+  // ---- 3. gradient softmax * scale, in place
   const float scale = valid ? grad_scale : 0.f;
+  const float lsec = lse * L2E;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int c = (it * 256 + threadIdx.x) * 8;
-    if (c >= V) break;
-    bf16x8 o;
+    if (c < V) {
+      bf16x8 o;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float p = (c + k < V_valid) ? __expf(u2f(u[it][k]) - lse) : 0.f;
-      o[k] = f2bf((p - ((c + k) == lab ? 1.f : 0.f)) * scale);
+      for (int k = 0; k < 8; ++k) o[k] = f2bf(fexp2(fmaf(u2f(u[it][k]), L2E, -lsec)) * scale);
+      *reinterpret_cast<bf16x8*>(x + c) = o;
     }
-    *reinterpret_cast<bf16x8*>(x + c) = o;
   }
+  // the label column: softmax - 1, written after every thread's row stores
+  __syncthreads();
+  if (threadIdx.x == 0 && valid) x[lab] = f2bf((fexp2(fmaf(lab_logit, L2E, -lsec)) - 1.f) * scale);
 }
 
 // Row softmax forward / backward (last dim).  One block per row.
@@ -291,19 +360,21 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ 
   }
 }
 
-void softmax_ce(int dtype, int label_bits, void* logits, const void* labels, float* row_loss, float* metrics, int M,
-                int V, int V_valid, float grad_scale, int ignore_index, int write_grad, hipStream_t st) {
+void softmax_ce(int dtype, int label_bits, void* logits, const void* labels, float* row_loss, float* metrics,
+                float* row_stats, int M, int V, int V_valid, float grad_scale, int ignore_index, int write_grad,
+                hipStream_t st) {
+  if (!metrics) row_stats = nullptr;
   const bool vec = (V % 8 == 0);
   dim3 grid(M), block(256);
 #define FFK_CE(T, L, VEC)                                                                                   \
   hipLaunchKernelGGL((softmax_ce_kernel<T, L, VEC>), grid, block, 0, st, static_cast<T*>(logits),           \
-                     static_cast<const L*>(labels), row_loss, metrics, M, V, V_valid, grad_scale, ignore_index, \
+                     static_cast<const L*>(labels), row_loss, metrics, row_stats, M, V, V_valid, grad_scale, ignore_index, \
                      write_grad)
   if (dtype == kBF16 && vec && V <= 2048 * 32) {
     // register-resident rows (one read + one write per logit)
 #define FFK_CE_REG(L, NIT)                                                                                     \
   hipLaunchKernelGGL((softmax_ce_reg_kernel<L, NIT>), grid, block, 0, st, static_cast<bf16*>(logits),        \
-                     static_cast<const L*>(labels), row_loss, metrics, M, V, V_valid, grad_scale, ignore_index, \
+                     static_cast<const L*>(labels), row_loss, metrics, row_stats, M, V, V_valid, grad_scale, ignore_index, \
                      write_grad)
     if (label_bits == 64) {
       if (V <= 2048 * 16) FFK_CE_REG(int64_t, 16);
@@ -334,6 +405,10 @@ void softmax_ce(int dtype, int label_bits, void* logits, const void* labels, flo
   }
 #undef FFK_CE
   FFK_LAUNCH_CHECK("softmax_ce");
+  if (row_stats) {
+    hipLaunchKernelGGL(ce_metrics_reduce_kernel, dim3(1), dim3(256), 0, st, row_stats, M, metrics);
+    FFK_LAUNCH_CHECK("ce_metrics_reduce");
+  }
 }
 
 void softmax_fwd(int dtype, const void* x, void* y, int M, int N, hipStream_t st) {

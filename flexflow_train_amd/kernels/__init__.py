@@ -219,8 +219,12 @@ def softmax_ce(logits, labels, grad_scale: float, metrics=None, valid_cols: Opti
     if row_loss is not None:
         _check(row_loss, "row_loss", torch.float32, M)
     vv = V if valid_cols is None else int(valid_cols)
+    # per-row metric terms reduced by one block (no same-address atomics);
+    # a stream-ordered temporary, so it is also valid inside a hipGraph capture
+    row_stats = None if metrics is None else torch.empty(M * 3, device=logits.device, dtype=torch.float32)
     ext().softmax_ce(_dt(logits), 64 if labels.dtype == torch.int64 else 32, _p(logits), _p(labels), _p(row_loss),
-                     _p(metrics), M, V, vv, float(grad_scale), int(ignore_index), int(write_grad), _stream())
+                     _p(metrics), _p(row_stats), M, V, vv, float(grad_scale), int(ignore_index), int(write_grad),
+                     _stream())
     STATS["softmax_ce"] += 1
     return logits
 

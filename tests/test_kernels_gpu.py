@@ -71,21 +71,37 @@ def test_bias_act_and_colsum(act):
     assert _rel(dbias, uu.grad.sum(0)) < 2e-2
 
 
-def test_softmax_ce():
+@pytest.mark.parametrize("V,Vv,ldt", [(30528, 30522, torch.int64), (50264, 50257, torch.int32), (4096, 4096, torch.int64)])
+def test_softmax_ce(V, Vv, ldt):
+    """Register-resident fused softmax + CE (NIT 16 / 32 paths, padding
+    columns, ignored rows): loss, per-row loss, the gradient (the label column
+    explicitly), accuracy against torch."""
     torch.manual_seed(2)
-    M, V, Vv = 300, 30528, 30522
+    M = 300
     logits = torch.randn(M, V, device=DEV, dtype=torch.bfloat16) * 3
+    lf0 = logits.float()[:, :Vv]
     labels = torch.randint(0, Vv, (M,), device=DEV, dtype=torch.int64)
-    lf = logits.float()[:, :Vv].clone().requires_grad_(True)
-    ref_loss = torch.nn.functional.cross_entropy(lf, labels, reduction="mean")
-    ref_loss.backward()
+    labels[::2] = lf0[::2].argmax(1)            # half the rows are "correct"
+    labels[5] = -100                            # ignored row
+    lf = lf0.clone().requires_grad_(True)
+    ref_rows = torch.nn.functional.cross_entropy(lf, labels, reduction="none", ignore_index=-100)
+    (ref_rows.sum() / M).backward()
     metrics = torch.zeros(4, device=DEV)
+    row_loss = torch.zeros(M, device=DEV)
     g = logits.clone()
-    K.softmax_ce(g, labels, 1.0 / M, metrics=metrics, valid_cols=Vv)
-    assert abs(metrics[0].item() / M - ref_loss.item()) < 2e-2 * abs(ref_loss.item())
+    K.softmax_ce(g, labels.to(ldt), 1.0 / M, metrics=metrics, valid_cols=Vv, row_loss=row_loss)
+    torch.testing.assert_close(row_loss, ref_rows, rtol=1e-2, atol=1e-2)
+    assert abs(metrics[0].item() - ref_rows.sum().item()) < 1e-2 * abs(ref_rows.sum().item())
+    assert metrics[2].item() == M - 1
     assert _rel(g[:, :Vv], lf.grad) < 2e-2
-    assert g[:, Vv:].abs().max().item() == 0
-    acc = (lf.argmax(1) == labels).float().sum().item()
+    rows = torch.arange(M, device=DEV)[labels >= 0]
+    lab_g, lab_ref = g[rows, labels[rows]].float(), lf.grad[rows, labels[rows]]
+    assert (lab_g < 0).all() and _rel(lab_g, lab_ref) < 2e-2
+    assert g[5].abs().max().item() == 0         # ignored row: zero gradient
+    if V > Vv:
+        assert g[:, Vv:].abs().max().item() == 0
+    valid = labels >= 0
+    acc = (lf0.argmax(1) == labels)[valid].float().sum().item()
     assert abs(metrics[1].item() - acc) <= 2
 
 
