@@ -23,10 +23,17 @@ ENV = dict(os.environ,
 
 @pytest.fixture(scope="module", autouse=True)
 def _asan_built():
-    if not all(os.path.exists(os.path.join(ASAN, t)) for t in TOOLS):
-        from tools.build_native import build
+    # pytest-xdist workers share build/: serialise the ninja run so one worker
+    # never links while another is still rewriting the object files
+    import fcntl
 
-        build(["asan"])
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".asan.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not all(os.path.exists(os.path.join(ASAN, t)) for t in TOOLS):
+            from tools.build_native import build
+
+            build(["asan"])
 
 
 def _run(*args, timeout=600):
