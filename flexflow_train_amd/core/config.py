@@ -65,6 +65,7 @@ class FFConfig:
     local_execution: bool = False      # train on the native C++ CPU executor (lib/local-execution parity)
     native_data_loader: bool = True    # fit() on arrays: C++ prefetcher + pinned async H2D (runtime/dataloader.py)
     shuffle_data: bool = False         # native loader: reshuffle the samples every epoch
+    softmax_identity_backward: bool = False   # reference-parity softmax backward (a copy; docs/PARITY.md)
     # fault tolerance (the reference has neither): fit()
     # writes an atomic sharded checkpoint every `checkpoint_every` iterations
     # under `checkpoint_dir` (keeping the newest `keep_checkpoints`) and, when
@@ -168,6 +169,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--cpu", dest="cpu_only", action="store_const", const=True)
     a("--param-sync", dest="parameter_sync", choices=["nccl", "ps"])
     a("--shuffle", dest="shuffle_data", action="store_const", const=True)
+    a("--softmax-identity-backward", dest="softmax_identity_backward", action="store_const", const=True)
     a("--seed", dest="seed", type=int)
     a("--checkpoint-dir", dest="checkpoint_dir", type=str)
     a("--checkpoint-every", dest="checkpoint_every", type=int)

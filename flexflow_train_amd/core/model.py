@@ -548,6 +548,8 @@ class FFModel:
                          shard_optimizer=bool(self.ffconfig.shard_optimizer),
                          param_sync=_param_sync_str(self.ffconfig.parameter_sync),
                          bucket_bytes=int(self.ffconfig.bucket_mb) << 20)
+        if self.ffconfig.softmax_identity_backward:
+            cfg.softmax_identity_backward = True
         out_v = None
         if output is not None:
             out_v = self._pcg_value_of(output)
@@ -739,14 +741,19 @@ class FFModel:
         d = self.ffconfig.checkpoint_dir
         if not d:
             return 0, 0
-        from ..utils.checkpoint import latest_checkpoint, load_checkpoint
+        from ..utils.checkpoint import latest_checkpoint, load_checkpoint, read_checkpoint_meta
         path = latest_checkpoint(d)
         if path is None:
             return 0, 0
-        meta = load_checkpoint(self, path)
-        prog = meta.get("progress") or {}
+        # check the progress record BEFORE restoring anything: a checkpoint of
+        # a differently-sized epoch is not resumed (no weights, no step count)
+        prog = read_checkpoint_meta(path).get("progress") or {}
         if prog.get("iters_per_epoch") != iters:
+            import warnings
+            warnings.warn(f"{path}: recorded {prog.get('iters_per_epoch')} iterations per epoch, this fit() runs "
+                          f"{iters}; not resuming from it (training starts from the current weights)")
             return 0, 0
+        meta = load_checkpoint(self, path)
         epoch, it = int(prog["epoch"]), int(prog["iter"])
         if it >= iters:
             epoch, it = epoch + 1, 0

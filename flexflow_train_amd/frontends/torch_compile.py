@@ -62,7 +62,9 @@ class CompiledModel:
             else:
                 cfg.search_algorithm = algorithm
         self.ff = FFModel(cfg)
-        self.pm = PyTorchModel(module)
+        was_training = module.training
+        self.pm = PyTorchModel(module)     # traces in eval mode
+        module.train(was_training)         # the caller's mode decides dropout / BN per call
         self.input_tensors = [self.ff.create_tensor(list(t.shape), _DT[t.dtype], name=f"input{i}")
                               for i, t in enumerate(ex_in)]
         self.pm.torch_to_ff(self.ff, self.input_tensors)
@@ -96,7 +98,9 @@ class CompiledModel:
         out: Dict[nn.Parameter, torch.Tensor] = {}
 
         def put(p, g):
-            g = g.reshape(p.shape).to(device=p.device, dtype=p.dtype)
+            # always a copy: the executor's gradient buffers are overwritten by
+            # the next backward(), possibly before autograd has summed this one
+            g = g.reshape(p.shape).to(device=p.device, dtype=p.dtype, copy=True)
             out[p] = out[p] + g if p in out else g
 
         for pname, (kind, t) in self.pmap.items():
@@ -119,30 +123,49 @@ class CompiledModel:
     # ---------------------------------------------------------------- call
     def __call__(self, *inputs: torch.Tensor) -> torch.Tensor:
         self._sync_weights()
-        return _FlexFlowFunction.apply(self, len(inputs), *inputs, *self.params)
+        training = self.module.training
+        if not torch.is_grad_enabled():
+            # inference (torch.no_grad / inference_mode): nothing is saved
+            # for a backward; module.eval() turns dropout off and uses running
+            # statistics, as in eager PyTorch
+            out = self._run(inputs, training, save=False)
+            return out.detach().to(device=inputs[0].device, dtype=torch.float32).clone()
+        return _FlexFlowFunction.apply(self, training, len(inputs), *inputs, *self.params)
+
+    def _run(self, inputs, training: bool, save: bool) -> torch.Tensor:
+        feeds = {t.name: inputs[i] for i, t in enumerate(self.input_tensors)}
+        return self.ex.forward(feeds, training=training, keep_outputs=True, save=save)
 
     forward = __call__
 
 
 class _FlexFlowFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cm: CompiledModel, n_in: int, *args):
-        feeds = {t.name: args[i] for i, t in enumerate(cm.input_tensors)}
-        out = cm.ex.forward(feeds, training=True, keep_outputs=True)
+    def forward(ctx, cm: CompiledModel, training: bool, n_in: int, *args):
+        out = cm._run(args[:n_in], training, save=True)
         ctx.cm, ctx.n_in = cm, n_in
         ctx.out_dtype = out.dtype
+        # this call's saved activations: the executor keeps one set, which the
+        # next forward() replaces, so several forwards may be pending a
+        # backward (f(x1) + f(x2), micro-batches accumulated before backward)
+        ctx.exec_state = (cm.ex._saved, cm.ex._env)
         dev = args[0].device
         return out.detach().to(device=dev, dtype=torch.float32).clone()
 
     @staticmethod
     def backward(ctx, gout):
         cm = ctx.cm
+        if ctx.exec_state is None:
+            raise RuntimeError("flexflow: backward through the same compiled call twice "
+                               "(retain_graph=True is not supported)")
+        cm.ex._saved, cm.ex._env = ctx.exec_state
+        ctx.exec_state = None
         # an autograd.Function's backward runs with grad mode off; the
         # executor's host fallbacks differentiate with torch autograd
         with torch.enable_grad():
             cm.ex.backward(gout.to(device=cm.ex.cfg.device, dtype=ctx.out_dtype).contiguous())
         grads = cm._grads_to_torch()
-        return (None, None) + (None,) * ctx.n_in + tuple(grads.get(p) for p in cm.params)
+        return (None, None, None) + (None,) * ctx.n_in + tuple(grads.get(p) for p in cm.params)
 
 
 def compile(module: nn.Module, example_inputs: Sequence[torch.Tensor], ffconfig: Optional[FFConfig] = None,

@@ -427,6 +427,18 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, b
 _WS_CACHE: dict = {}
 
 
+def _splitk_ws(dev, numel: int) -> torch.Tensor:
+    """fp32 split-K partial slab, one per (device, stream, size): dW GEMMs on
+    the weight-gradient side stream may run beside same-sized compute-stream
+    GEMMs, which must not share a slab."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream, numel)
+    ws = _WS_CACHE.get(key)
+    if ws is None:
+        ws = torch.empty(numel, device=dev, dtype=torch.float32)
+        _WS_CACHE[key] = ws
+    return ws
+
+
 def gemm256_supported(a, b, trans_a=False, trans_b=False) -> bool:
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
         return False
@@ -469,11 +481,7 @@ def gemm256(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0
         s = 1
     ws = None
     if s > 1:
-        key = (a.device, s * M * N)
-        ws = _WS_CACHE.get(key)
-        if ws is None:
-            ws = torch.empty(s * M * N, device=a.device, dtype=torch.float32)
-            _WS_CACHE[key] = ws
+        ws = _splitk_ws(a.device, s * M * N)
     ext().gemm256(a.data_ptr(), b.data_ptr(), out.data_ptr(), _p(bias), _p(pre), M, N, K, a.stride(0), b.stride(0),
                   out.stride(0), bool(trans_a), bool(trans_b), ACT_CODES[act], float(alpha), float(beta),
                   int(out.dtype == torch.float32), s, _p(ws), _stream())
@@ -522,11 +530,7 @@ def gemmp(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, 
         s = 1
     ws = None
     if s > 1:
-        key = (a.device, s * M * N)
-        ws = _WS_CACHE.get(key)
-        if ws is None:
-            ws = torch.empty(s * M * N, device=a.device, dtype=torch.float32)
-            _WS_CACHE[key] = ws
+        ws = _splitk_ws(a.device, s * M * N)
     ext().gemmp(a.data_ptr(), b.data_ptr(), out.data_ptr(), _p(bias), _p(pre), _p(aux), _p(dbias), M, N, K,
                 a.stride(0), b.stride(0), out.stride(0), bool(trans_a), bool(trans_b), ACT_CODES[act], bool(act_bwd),
                 float(alpha), float(beta), int(out.dtype == torch.float32), s, _p(ws), _stream(), int(_dbg))

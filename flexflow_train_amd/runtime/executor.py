@@ -97,6 +97,12 @@ class ExecConfig:
     # reference's ParamSync::PS): reduce to the group leader, the leader
     # updates, the updated weights are broadcast.
     param_sync: str = "nccl"
+    # reference-parity mode for SOFTMAX backward: the reference's softmax
+    # backward is an identity copy (lib/kernels/src/cuda/ops/softmax_kernels.cu:
+    # 63-72), correct only under a fused cross-entropy loss.  Off: the true
+    # softmax Jacobian-vector product (docs/PARITY.md, "Deliberate divergences").
+    softmax_identity_backward: bool = dataclasses.field(
+        default_factory=lambda: os.environ.get("FF_SOFTMAX_IDENTITY_BWD", "0") != "0")
 
 
 @dataclasses.dataclass
@@ -378,13 +384,18 @@ class Executor:
             self._fuse_conv_bn()
             if os.environ.get("FF_FUSE_DACT", "1") != "0":
                 self._fuse_linear_dact()
+        if self.cfg.softmax_identity_backward:
+            for s in self.steps:
+                if s.kind == "compute" and s.op_type == "SOFTMAX":
+                    s.ctx.extra["identity_backward"] = True
         self._mark_requires_grad()
         self._assign_params_to_buffers()
 
     def _fuse_add_layernorm(self):
         by_out = {o: s for s in self.steps for o in s.outputs}
         keep = []
-        drop = set()
+        # id(dropped EW_ADD step) -> the fused step that takes its place
+        moves: Dict[int, Step] = {}
         uses: Dict[Value, List[Step]] = {}
         for s in self.steps:
             for v in s.inputs:
@@ -393,7 +404,7 @@ class Executor:
             if s.kind == "compute" and s.op_type == "LAYERNORM" and len(s.inputs) == 1:
                 v = s.inputs[0]
                 prod = by_out.get(v)
-                if (prod is not None and prod.kind == "compute" and prod.op_type == "EW_ADD" and id(prod) not in drop
+                if (prod is not None and prod.kind == "compute" and prod.op_type == "EW_ADD" and id(prod) not in moves
                         and v != self.loss_value
                         and self.value_layout[prod.inputs[0]] == self.value_layout[prod.inputs[1]]
                         and self.value_layout[v] == self.value_layout[prod.inputs[0]]
@@ -407,9 +418,19 @@ class Executor:
                         # residual add; the fused kernel writes it as a second output
                         s.outputs = [s.outputs[0], v]
                         s.ctx.extra["emit_sum"] = True
-                    drop.add(id(prod))
+                    moves[id(prod)] = s
+        # The fused step runs where the add ran: every other consumer of the
+        # sum (a residual add, a redistribution on the residual edge) may sit
+        # between the add and the norm in topological order, so it must see the
+        # sum already written in forward, and in backward (reverse order) its
+        # gradient contribution to the sum must land before the fused step's
+        # backward reads it.  The norm's remaining inputs are weights, always
+        # ready at the add's position.
+        moved = {id(s) for s in moves.values()}
         for s in self.steps:
-            if id(s) not in drop:
+            if id(s) in moves:
+                keep.append(moves[id(s)])
+            elif id(s) not in moved:
                 keep.append(s)
         self.steps = keep
         self._fuse_linear_bias_into_ln()
@@ -884,7 +905,13 @@ class Executor:
         return lay
 
     # -------------------------------------------------------------- execution
-    def forward(self, feeds: Dict[str, torch.Tensor], training: bool = True, keep_outputs: bool = False):
+    def forward(self, feeds: Dict[str, torch.Tensor], training: bool = True, keep_outputs: bool = False,
+                save: Optional[bool] = None):
+        """Forward pass.  ``training`` selects training-mode op semantics
+        (dropout masks, batch statistics); ``save`` (default: ``training``)
+        keeps each step's saved tensors for a following backward()."""
+        if save is None:
+            save = training
         env: Dict[Value, torch.Tensor] = {}
         for name, x in feeds.items():
             if name not in self.inputs:
@@ -922,7 +949,7 @@ class Executor:
                 env[o] = t
                 if o in self.retain:
                     self.retained[o] = t
-            if training:
+            if save:
                 self._saved[i] = saved
         self._env = env
         return env.get(self.output_value) if keep_outputs or not training else env.get(self.loss_value)

@@ -77,8 +77,17 @@ def save_step_checkpoint(model, root: str, progress: dict, keep: int = 2) -> str
     path = os.path.join(root, f"step-{ex.step_num}")
     save_checkpoint(model, path, progress)
     if ex.rank == 0 and keep > 0:
-        done = sorted((int(m.group(1)), d) for d in os.listdir(root) for m in [_STEP_DIR.match(d)] if m)
-        for _n, d in done[:-keep]:
+        # only COMPLETE checkpoints (meta.json written) count towards `keep`;
+        # a directory without meta.json is the leftover of a crashed save
+        # (every rank writes the same step and meets at the barrier below, so
+        # none is in progress here) and is removed on its own
+        done, stale = [], []
+        for d in os.listdir(root):
+            m = _STEP_DIR.match(d)
+            if m:
+                (done if os.path.exists(os.path.join(root, d, "meta.json")) else stale).append((int(m.group(1)), d))
+        done.sort()
+        for _n, d in done[:-keep] + stale:
             shutil.rmtree(os.path.join(root, d), ignore_errors=True)
     ex.dist.barrier()
     return path
@@ -100,10 +109,14 @@ def _assemble_full(path: str, world: int) -> Dict[str, torch.Tensor]:
     return full
 
 
+def read_checkpoint_meta(path: str) -> dict:
+    with open(os.path.join(path, "meta.json")) as f:
+        return json.load(f)
+
+
 def load_checkpoint(model, path: str, strict: bool = True):
     ex = model.executor if hasattr(model, "executor") else model
-    with open(os.path.join(path, "meta.json")) as f:
-        meta = json.load(f)
+    meta = read_checkpoint_meta(path)
     if meta.get("format") != "ffmi355x.checkpoint.v1":
         raise ValueError(f"{path}: not a checkpoint")
     same = meta["world"] == ex.world and meta["fingerprint"] == _fingerprint(ex)

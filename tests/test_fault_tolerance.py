@@ -81,6 +81,35 @@ def test_incomplete_checkpoint_is_ignored(tmp_path):
     assert latest_checkpoint(str(tmp_path / "none")) is None
 
 
+def test_pruning_counts_only_complete_checkpoints(tmp_path):
+    """A stale higher-numbered incomplete directory (a crashed save) neither
+    counts towards keep_checkpoints nor survives the next save."""
+    d = tmp_path / "ckpt"
+    (d / "step-50").mkdir(parents=True)          # no meta.json: a crashed save
+    (d / "step-50" / "rank0.pt").write_bytes(b"")
+    _fit(str(d), 4, True)
+    assert sorted(os.listdir(d)) == ["step-12", "step-8"]
+
+
+def test_resume_with_other_epoch_size_restores_nothing(tmp_path):
+    """A checkpoint recorded with a different iterations-per-epoch is not
+    resumed: neither its weights nor its step counter are loaded."""
+    import json
+    d = str(tmp_path / "ckpt")
+    _fit(d, 4, True)
+    meta_f = os.path.join(d, "step-12", "meta.json")
+    meta = json.load(open(meta_f))
+    meta["progress"]["iters_per_epoch"] = 99
+    json.dump(meta, open(meta_f, "w"))
+    os.remove(os.path.join(d, "step-8", "meta.json"))
+    ref, steps = _fit(None, 0, True)
+    with pytest.warns(UserWarning, match="not resuming"):
+        got, steps2 = _fit(d, 0, True)
+    assert steps2 == steps
+    for n in ref:
+        torch.testing.assert_close(got[n], ref[n], rtol=0, atol=0)
+
+
 def _rank(rank, world, port, d, fault, out):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})

@@ -107,3 +107,85 @@ def test_post_ln_bias_fusion_matches_unfused_cpu():
 @pytest.mark.gpu
 def test_post_ln_bias_fusion_matches_unfused_gpu():
     _compare_bert(dict(rtol=3e-2, atol=3e-3))
+
+
+def _side_consumer_model(fuse: bool):
+    """x -> dense -> s = add(h, x); a consumer of s ("side") is created BEFORE
+    the LayerNorm of s, so it sits between the add and the norm in
+    topological order.  The fused add+norm must run at the add's position."""
+    from flexflow_train_amd.core import ActiMode, DataType, SGDOptimizer
+    cfg = FFConfig()
+    cfg.perform_fusion = fuse
+    m = FFModel(cfg)
+    x = m.create_tensor([8, 16], DataType.DT_FLOAT, name="x")
+    h = m.dense(x, 16, ActiMode.AC_MODE_RELU, name="h")
+    s = m.add(h, x, name="sum")
+    r = m.dense(s, 16, name="side")
+    n = m.layer_norm(s, axes=[-1], name="ln")
+    o = m.add(n, r, name="join")
+    m.softmax(m.dense(o, 4, name="head"))
+    m.compile(optimizer=SGDOptimizer(m, lr=0.05), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_ACCURACY])
+    ex = m.executor
+    g = torch.Generator().manual_seed(3)
+    for nm in sorted(ex.parameter_names()):
+        ex.set_parameter(nm, torch.randn(ex.get_parameter(nm).shape, generator=g) * 0.2)
+    dev = ex.cfg.device
+    feeds = {"x": torch.randn(8, 16, generator=g).to(dev)}
+    return ex, feeds, torch.randint(0, 4, (8,), generator=g).to(dev)
+
+
+def test_add_ln_fusion_with_sum_consumer_before_norm():
+    a, feeds, labels = _side_consumer_model(True)
+    b, _, _ = _side_consumer_model(False)
+    names = [s.name for s in b.steps if s.kind == "compute"]
+    assert names.index("side") < names.index("ln"), names
+    fused = [s for s in a.steps if s.op_type == "FUSED_ADD_LAYERNORM"]
+    assert len(fused) == 1 and fused[0].ctx.extra.get("emit_sum")
+    order = [s.name for s in a.steps if s.kind == "compute"]
+    assert order.index("ln") < order.index("side"), order
+    for _ in range(3):
+        a.train_step(feeds, labels)
+        b.train_step(feeds, labels)
+    tol = dict(rtol=1e-4, atol=1e-5) if a.cfg.device.type == "cpu" else dict(rtol=3e-2, atol=3e-3)
+    for nm in a.parameter_names():
+        torch.testing.assert_close(a.get_parameter(nm), b.get_parameter(nm), **tol)
+
+
+def _softmax_mse(identity: bool):
+    from flexflow_train_amd.core import DataType, SGDOptimizer
+    cfg = FFConfig()
+    cfg.softmax_identity_backward = identity
+    m = FFModel(cfg)
+    x = m.create_tensor([8, 16], DataType.DT_FLOAT, name="x")
+    m.softmax(m.dense(x, 4, name="fc"))
+    m.compile(optimizer=SGDOptimizer(m, lr=0.1), loss_type=LossType.LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE,
+              metrics=[MetricsType.METRICS_MEAN_SQUARED_ERROR])
+    ex = m.executor
+    g = torch.Generator().manual_seed(4)
+    for nm in sorted(ex.parameter_names()):
+        ex.set_parameter(nm, torch.randn(ex.get_parameter(nm).shape, generator=g) * 0.3)
+    dev = ex.cfg.device
+    feeds = {"x": torch.randn(8, 16, generator=g).to(dev)}
+    return ex, feeds, torch.rand(8, 4, generator=g).to(dev)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="exercises the CPU fallback path")
+@pytest.mark.parametrize("identity", [False, True])
+def test_softmax_backward_under_mse(identity):
+    """MSE after a softmax.  Default: the loss gradient goes through the
+    softmax Jacobian.  Reference-parity flag: the softmax backward is the
+    reference's identity copy (softmax_kernels.cu:63-72), so the MSE
+    gradient lands on the logits unchanged.  Checked on the bias update."""
+    ex, feeds, y = _softmax_mse(identity)
+    assert any(s.ctx is not None and s.ctx.extra.get("identity_backward") for s in ex.steps) == identity
+    bname = next(n for n in ex.parameter_names() if n.endswith("bias"))
+    wname = next(n for n in ex.parameter_names() if n != bname)
+    W, b = ex.get_parameter(wname).clone().double(), ex.get_parameter(bname).clone().double()
+    x = feeds["x"].double()
+    z = x @ (W if W.shape[0] == 16 else W.t()) + b
+    p = torch.softmax(z, -1)
+    dp = 2.0 * (p - y.double()) / p.numel()
+    dz = dp if identity else p * (dp - (dp * p).sum(-1, keepdim=True))
+    ex.train_step(feeds, y)
+    torch.testing.assert_close(ex.get_parameter(bname).double(), b - 0.1 * dz.sum(0), rtol=1e-5, atol=1e-6)

@@ -160,3 +160,60 @@ def test_dynamo_backend_on_gpu():
         assert abs(lf.item() - lr_.item()) <= 5e-2 * max(1.0, abs(lr_.item()))
     assert len(TC.COMPILED) > before
     assert TC.COMPILED[-1].ex.cfg.device.type == "cuda"
+
+
+def _cpu_cfg():
+    from flexflow.core import FFConfig
+    cfg = FFConfig()
+    cfg.cpu_only = True
+    return cfg
+
+
+def test_two_forwards_before_one_backward():
+    """loss = f(x1) + f(x2): each compiled call keeps its own saved
+    activations until its backward, as eager autograd does."""
+    torch.manual_seed(0)
+    net, ref = SmoothMLP(), SmoothMLP()
+    ref.load_state_dict(net.state_dict())
+    x1, x2 = torch.randn(8, 16), torch.randn(8, 16)
+    y1, y2 = torch.randint(0, 5, (8,)), torch.randint(0, 5, (8,))
+    cm = fft.compile(net, [x1], ffconfig=_cpu_cfg())
+    ce = nn.functional.cross_entropy
+    lf = ce(cm(x1), y1) + 0.5 * ce(cm(x2), y2)
+    lr_ = ce(ref(x1), y1) + 0.5 * ce(ref(x2), y2)
+    lf.backward()
+    lr_.backward()
+    assert abs(lf.item() - lr_.item()) <= 1e-5
+    for p, q in zip(net.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6)
+
+
+class DropMLP(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(16, 32)
+        self.drop = nn.Dropout(0.5)
+        self.fc2 = nn.Linear(32, 5)
+
+    def forward(self, x):
+        return self.fc2(self.drop(torch.tanh(self.fc1(x))))
+
+
+def test_eval_mode_and_no_grad_follow_eager():
+    """module.eval() turns dropout off; torch.no_grad() saves nothing and
+    returns a tensor without a graph."""
+    torch.manual_seed(0)
+    net, ref = DropMLP(), DropMLP()
+    ref.load_state_dict(net.state_dict())
+    x = torch.randn(8, 16)
+    cm = fft.compile(net, [x], ffconfig=_cpu_cfg())
+    net.eval()
+    ref.eval()
+    torch.testing.assert_close(cm(x), ref(x), rtol=1e-4, atol=1e-5)
+    with torch.no_grad():
+        out = cm(x)
+    assert not out.requires_grad
+    torch.testing.assert_close(out, ref(x).detach(), rtol=1e-4, atol=1e-5)
+    assert cm.ex._saved == {}
+    net.train()
+    assert not torch.allclose(cm(x), ref(x))     # training mode: dropout active
