@@ -195,18 +195,19 @@ PYBIND11_MODULE(_ffkernels, m) {
   m.def("gemmp", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, uintptr_t aux,
                     uintptr_t dbias, int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int act,
                     bool act_bwd, float alpha, float beta, int out_f32, int splits, uintptr_t ws, uintptr_t st,
-                    int dbg) {
+                    int dbg, int variant) {
     GemmPParams p;
     p.A = P(A); p.B = P(B); p.C = P(C); p.bias = P(bias); p.pre = P(pre); p.aux = P(aux); p.dbias = F(dbias);
     p.workspace = F(ws);
     p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.trans_a = ta; p.trans_b = tb;
     p.act = act; p.act_bwd = act_bwd; p.alpha = alpha; p.beta = beta; p.out_f32 = out_f32; p.splits = splits;
     p.dbg = dbg;
+    p.variant = variant;
     gemmp_bf16(p, S(st));
   }, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("pre"), py::arg("aux"), py::arg("dbias"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("ta"),
         py::arg("tb"), py::arg("act"), py::arg("act_bwd"), py::arg("alpha"), py::arg("beta"), py::arg("out_f32"),
-        py::arg("splits"), py::arg("ws"), py::arg("st"), py::arg("dbg") = 0);
+        py::arg("splits"), py::arg("ws"), py::arg("st"), py::arg("dbg") = 0, py::arg("variant") = 0);
   m.def("gemm256_supported", &gemm256_supported);
   m.def("gemm256", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int M, int N, int K,
                       int lda, int ldb, int ldc, bool ta, bool tb, int act, float alpha, float beta, int out_f32,

@@ -521,6 +521,11 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
       n = 256;
     return std::max(8, n);
   }();
+  if (p.variant == 1) {
+    gemmq_launch(p, splits, n_cu, st);
+    if (splits > 1) splitk_reduce(p.workspace, p.C, p.M, p.N, p.ldc, splits, p.beta, p.out_f32, st);
+    return;
+  }
   const int items = ((p.M + TM - 1) / TM) * ((p.N + TN - 1) / TN) * splits;
   dim3 grid(std::min(items, n_cu)), block(NTHREADS);  // persistent: one workgroup per CU
   const int epi = splits > 1 ? kEpiSplit : p.act_bwd ? kEpiDact : (p.bias || p.pre || p.act) ? kEpiBiasAct : kEpiPlain;

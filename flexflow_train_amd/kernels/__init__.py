@@ -502,11 +502,12 @@ def gemmp_supported(a, b, trans_a=False, trans_b=False) -> bool:
 
 
 def gemmp(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, beta=0.0, out=None,
-          out_dtype=None, pre=None, aux=None, act_bwd=False, dbias=None, splits=1, _dbg=0):
+          out_dtype=None, pre=None, aux=None, act_bwd=False, dbias=None, splits=1, _dbg=0, variant=0):
     """Phase-pipelined 256x256 MFMA GEMM (csrc/kernels/gemmp.hip):
     C = epi(alpha * op(a) op(b)); epi = [+bias] [pre := .] [act(.) or, with
     ``act_bwd``, . * act'(aux)] [dbias += colsum] [+ beta * C].  Split-K
-    (``splits`` > 1): fp32 partial slabs + a reduce pass, plain epilogue only."""
+    (``splits`` > 1): fp32 partial slabs + a reduce pass, plain epilogue only.
+    ``variant`` 1 runs the same pipeline on 16x16x32 MFMAs (gemmq.hip)."""
     if not gemmp_supported(a, b, trans_a, trans_b):
         raise ValueError("gemmp: unsupported operands (bf16, 16-B aligned, K % 64, dims % 8)")
     M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
@@ -533,7 +534,8 @@ def gemmp(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, 
         ws = _splitk_ws(a.device, s * M * N)
     ext().gemmp(a.data_ptr(), b.data_ptr(), out.data_ptr(), _p(bias), _p(pre), _p(aux), _p(dbias), M, N, K,
                 a.stride(0), b.stride(0), out.stride(0), bool(trans_a), bool(trans_b), ACT_CODES[act], bool(act_bwd),
-                float(alpha), float(beta), int(out.dtype == torch.float32), s, _p(ws), _stream(), int(_dbg))
+                float(alpha), float(beta), int(out.dtype == torch.float32), s, _p(ws), _stream(), int(_dbg),
+                int(variant))
     STATS["gemmp"] += 1
     return out
 

@@ -260,13 +260,17 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
+@pytest.mark.parametrize("variant", [0, 1], ids=["mfma32x32x16", "mfma16x16x32"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1)])
-def test_gemmp(ta, tb, M, N, Kd, splits):
-    """Phase-pipelined persistent GEMM: plain / beta / split-K, the fused
+def test_gemmp(ta, tb, M, N, Kd, splits, variant):
+    """Phase-pipelined persistent GEMM (gemmp.hip; variant 1 = gemmq.hip on
+    16x16x32 MFMAs): plain / beta / split-K, the fused
     bias+activation+pre-activation epilogue and the activation-gradient +
     bias-gradient epilogue, against fp32 torch."""
+    import functools
+    gemmp = functools.partial(K.gemmp, variant=variant)
     torch.manual_seed(13)
     a = torch.randn(Kd, M, device=DEV, dtype=torch.bfloat16) if ta else torch.randn(M, Kd, device=DEV,
                                                                                      dtype=torch.bfloat16)
@@ -275,21 +279,21 @@ def test_gemmp(ta, tb, M, N, Kd, splits):
     af = a.float().t() if ta else a.float()
     bf = b.float().t() if tb else b.float()
     ref = af @ bf
-    c = K.gemmp(a, b, trans_a=ta, trans_b=tb, splits=splits)
+    c = gemmp(a, b, trans_a=ta, trans_b=tb, splits=splits)
     assert _rel(c, ref) < 1e-2
     c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
-    K.gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
+    gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
     assert _rel(c3, ref + 1) < 1e-2
     if splits == 1:
         bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        c2 = K.gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
+        c2 = gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
         u = ref + bias.float()
         assert _rel(pre, u) < 1e-2
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
         aux = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
         db = torch.full((N,), 0.5, device=DEV)
-        g = K.gemmp(a, b, trans_a=ta, trans_b=tb, act="gelu", aux=aux, act_bwd=True, dbias=db)
+        g = gemmp(a, b, trans_a=ta, trans_b=tb, act="gelu", aux=aux, act_bwd=True, dbias=db)
         x = aux.float().requires_grad_(True)
         torch.nn.functional.gelu(x, approximate="tanh").backward(torch.ones_like(x))
         gr = ref * x.grad

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Sync-cost ablation of the phase-pipelined GEMMs (timing only: with the
+waits or barriers removed the results are garbage).  dbg bits: 1 = no vmcnt
+waits, 2 = no barriers.  Interleaved rounds in one process."""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from flexflow_train_amd import kernels as K  # noqa: E402
+from tools.gemm_ab import operands, timed  # noqa: E402
+
+CASES = [("fwd_qkv", "fwd", 1024, 3072), ("dx_ffn1", "dx", 1024, 4096), ("fwd_ffn2", "fwd", 4096, 1024),
+         ("dw_ffn1", "dw", 1024, 4096)]
+
+
+def main():
+    for name, kind, kin, nout in CASES:
+        a, b, ta, tb = operands(kind, kin, nout, "cuda")
+        M, N = (a.shape[1] if ta else a.shape[0]), (b.shape[0] if tb else b.shape[1])
+        Kd = a.shape[0] if ta else a.shape[1]
+        sp = 4 if kind == "dw" else 1
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        cands = {}
+        for v in (0, 1):
+            for dbg in (0, 1, 2, 3):
+                cands[f"v{v}_d{dbg}"] = lambda v=v, dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out,
+                                                                     splits=sp, variant=v, _dbg=dbg)
+        times = {k: [] for k in cands}
+        for _ in range(5):
+            for k, f in cands.items():
+                times[k].append(timed(f, 10))
+        fl = 2.0 * M * N * Kd
+        res = {"case": name}
+        for k in cands:
+            res[k + "_TF"] = round(fl / statistics.median(times[k]) / 1e9, 1)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
