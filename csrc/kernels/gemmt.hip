@@ -1,0 +1,533 @@
+// One-wave-per-SIMD bf16 GEMM for gfx950 (GemmPParams.variant = 3).
+//
+// Geometry (the shape hipBLASLt's fastest gfx950 kernels use on these
+// problems, MT256x256x64 MI16x16 with an 8 x 8 MFMA wave tile): a 256 x 256
+// output tile per workgroup of 4 waves (2 x 2), a 128 x 128 tile per wave =
+// 8 x 8 v_mfma_f32_16x16x32_bf16 blocks whose accumulators (256 registers)
+// live in AGPRs: with one wave per SIMD the unified register file holds 512
+// per lane.  Per 32-deep k-step a wave reads 8 A + 8 B fragments for 64
+// MFMAs: half the LDS read traffic per MFMA of a 128 x 64 wave tile.
+//
+// K loop, one barrier per 64-deep K-tile, two phases:
+//   A: MFMAs of k-step 0 (fragments F0)      | read F1 (k-step 1 of this tile),
+//                                              write the staged registers of tile
+//                                              t+1 to the other LDS buffer, issue
+//                                              the global loads of tile t+2
+//   -- lgkmcnt(0), barrier --
+//   B: MFMAs of k-step 1 (F1)                | read F0 (k-step 0 of tile t+1)
+// so fragment reads run one phase ahead of their MFMAs and global loads one
+// K-tile ahead of their LDS writes (register staging, guide T14; no LDS-DMA
+// issue cost in the MFMA stream).  WAR: a buffer is rewritten in phase A of
+// tile t+2, after every wave passed the barrier of tile t+1, which follows
+// its last reads of it (lgkmcnt(0) before the barrier).
+//
+// Operand images (bank-conflict-free reads AND writes):
+//   K-contiguous operand [outer][k]: [256 outer][64 k], 128-B rows, 16-B slot
+//     = chunk ^ ((row >> 1) & 7); read by ds_read_b128 (lane -> row lane & 15)
+//   K-outer operand [k][outer]: two halves [64 k][128 outer] (one per wave
+//     row / column), 256-B rows, mfma.h 256-B swizzle; read by two
+//     ds_read_b64_tr_b16 per fragment.
+// Global loads: buffer_load_dwordx4 with per-lane voffsets fixed per tile and
+// the K advance in the scalar soffset.
+//
+// Accumulators hold C^T (mfma(B fragment, A fragment)): D column lane & 15 ->
+// m, D row 4 (lane >> 4) + e -> n: a lane owns 4 consecutive n of one row.
+// Epilogues as gemmp.hip: plain (+ beta C, bf16 / fp32), bias + activation
+// (+ pre-activation), activation-gradient (+ bias-gradient column sums),
+// split-K fp32 slabs.
+#include <type_traits>
+#include <utility>
+
+#include "kernels.h"
+#include "mfma.h"
+
+namespace ffk {
+
+namespace {
+
+constexpr int TM = 256, TN = 256, TK = 64, NTHREADS = 256;
+constexpr int HALF = 16 * 1024;   // 32 KB per operand tile per buffer
+constexpr int BUFT = 4 * HALF;    // A tile + B tile
+constexpr int GROUP = 4;
+typedef float f32x4t __attribute__((ext_vector_type(4)));
+typedef int i32x4t __attribute__((ext_vector_type(4)));
+
+struct GemmTArgs {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  float* ws;
+  const bf16* bias;
+  bf16* pre;
+  const bf16* aux;
+  float* dbias;
+  int M, N, K, lda, ldb, ldc;
+  float alpha, beta;
+  int act, act_bwd, out_f32, splits;
+  unsigned bytesA, bytesB;
+};
+
+// activation code (elementwise.hip numbering) fixed at compile time: a run-time
+// switch here keeps hipcc from unrolling the epilogue, which then indexes the
+// AGPR accumulators dynamically through scratch
+template <int ACT>
+__device__ __forceinline__ float t_act(float x) {
+  if (ACT == 1) return x > 0.f ? x : 0.f;
+  if (ACT == 2) return 1.f / (1.f + __expf(-x));
+  if (ACT == 3) return fast_tanh(x);
+  if (ACT == 4) return gelu_tanh(x);
+  return x;
+}
+template <int ACT>
+__device__ __forceinline__ float t_act_grad(float x) {
+  if (ACT == 1) return x > 0.f ? 1.f : 0.f;
+  if (ACT == 2) {
+    const float s = 1.f / (1.f + __expf(-x));
+    return s * (1.f - s);
+  }
+  if (ACT == 3) {
+    const float t = fast_tanh(x);
+    return 1.f - t * t;
+  }
+  if (ACT == 4) return gelu_tanh_grad(x);
+  return 1.f;
+}
+
+__device__ __forceinline__ int t_slot128(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+__device__ __forceinline__ f32x4t mfma16(bf16x8 a, bf16x8 b, f32x4t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Staging map: chunk i (0..7) of thread tid for one operand tile.
+//  K-contiguous: row = (tid >> 3) + 32 i, 16-B chunk c = tid & 7
+//  K-outer:      flat = tid + 256 i: half h = flat >> 10, k row r = (flat >> 4) & 63, chunk c = flat & 15
+// The per-lane part of the byte offset is chunk 0's (one VGPR per operand);
+// the chunk index and the K advance are wave-uniform and go in soffset.
+// Rows / columns past the operand's edge are not clamped: they read zeros
+// (buffer range check) or in-range bytes of another row, and only feed
+// masked outputs.
+template <bool KOUTER>
+__device__ __forceinline__ unsigned stage_voff(int ld, int outer0, int tid) {
+  if (KOUTER) {
+    const int r = tid >> 4, c = tid & 15;
+    return (static_cast<unsigned>(r) * static_cast<unsigned>(ld) + static_cast<unsigned>(outer0 + c * 8)) * 2u;
+  }
+  const int row = outer0 + (tid >> 3);
+  return (static_cast<unsigned>(row) * static_cast<unsigned>(ld) + static_cast<unsigned>((tid & 7) * 8)) * 2u;
+}
+template <bool KOUTER>
+__device__ __forceinline__ unsigned stage_soff(int ld, int i) {
+  if (KOUTER) return static_cast<unsigned>(16 * (i & 3)) * static_cast<unsigned>(ld) * 2u + (i >> 2) * 256u;
+  return static_cast<unsigned>(32 * i) * static_cast<unsigned>(ld) * 2u;
+}
+template <bool KOUTER>
+__device__ __forceinline__ int stage_lds(int i, int tid) {
+  if (KOUTER) {
+    const int flat = tid + 256 * i;
+    const int h = flat >> 10, r = (flat >> 4) & 63, c = flat & 15;
+    return h * HALF + r * 256 + swz_chunk<256>(r, c) * 16;
+  }
+  const int row = (tid >> 3) + 32 * i, c = tid & 7;
+  return row * 128 + t_slot128(row, c) * 16;
+}
+
+// LDS-DMA staging of one operand tile (32 KB = 32 x 1 KiB wave pieces, 8 per
+// wave).  The DMA writes lane-linearly (base + 16 lane), so each lane's
+// global source is the logical chunk that the image's swizzle stores in its
+// physical slot (guide rule 21).  Piece i of wave w is image KiB j = 8 w + i.
+//  K-contiguous image: KiB j = rows 8j..8j+7; the chunk swizzle depends on i
+//    through bit 2 ((row >> 1) & 7 gains 4 i) -> two per-lane voffsets.
+//  K-outer image: KiB j = half j >> 4 (= w >> 1), rows 4 (j & 15) + lane >> 4;
+//    the swizzle depends on i & 3 -> four per-lane voffsets.
+template <bool KOUTER>
+__device__ __forceinline__ unsigned dma_voff(int ld, int outer0, int i, int wave, int lane) {
+  const int j = wave * 8 + i;
+  if (KOUTER) {
+    const int h = j >> 4, r = 4 * (j & 15) + (lane >> 4);
+    const int c = swz_chunk<256>(r, lane & 15);
+    return (static_cast<unsigned>(r) * static_cast<unsigned>(ld) + static_cast<unsigned>(outer0 + h * 128 + c * 8)) * 2u;
+  }
+  const int row = 8 * j + (lane >> 3);
+  const int c = t_slot128(row, lane & 7);
+  return (static_cast<unsigned>(outer0 + row) * static_cast<unsigned>(ld) + static_cast<unsigned>(c * 8)) * 2u;
+}
+
+__device__ __forceinline__ bf16x8 row16(const unsigned char* img, int o0, int ks, int lane) {
+  const int r = o0 + (lane & 15);
+  return lds_read16(img, r * 128 + (t_slot128(r, ks * 4 + (lane >> 4)) << 4));
+}
+__device__ __forceinline__ bf16x8 tr16(const unsigned char* img, int ks, int o0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int col = o0 + 4 * (i & 3);
+  const int r = ks * 32 + 8 * g + (i >> 2);
+  const int oa = img_off<256>(r, col >> 3) + (col & 7) * 2;
+  const int ob = img_off<256>(r + 4, col >> 3) + (col & 7) * 2;
+  return cat44(lds_tr(img, oa), lds_tr(img, ob));  // intrinsic: no LDS-DMA here to be drained
+}
+
+enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3 };
+
+__device__ __forceinline__ uint2 pack4(const float (&v)[4]) {
+  bf16x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+  return __builtin_bit_cast(uint2, o);
+}
+
+// Store the 8 bf16x4 groups of one row block (blocks nb = 0..7, lane row
+// r = lane >> 4 holding columns 4r..4r+3 of each) as 16-byte stores: for each
+// block pair (2j, 2j+1) one v_permlane16_swap per dword exchanges the odd
+// 16-lane rows of block 2j with the even rows of block 2j+1, after which row
+// r holds 8 consecutive columns, (r >> 1) * 8 .. +8, of block 2j + (r & 1)
+// (guide T21: the store tail is issue-bound; half the instructions).
+__device__ __forceinline__ void store_row16(bf16* C, int64_t row_off, int ncol0, int N, bool mok, const uint2 (&o)[8],
+                                            int lane) {
+  const int r = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto sx = __builtin_amdgcn_permlane16_swap(o[2 * j].x, o[2 * j + 1].x, false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(o[2 * j].y, o[2 * j + 1].y, false, false);
+    const int n = ncol0 + (2 * j + (r & 1)) * 16 + (r >> 1) * 8;
+    if (mok && n < N) *reinterpret_cast<uint4*>(C + row_off + n) = uint4{sx[0], sy[0], sx[1], sy[1]};
+  }
+}
+
+// acc[mb][nb]: row m = m0 + wm*128 + mb*16 + (lane & 15);
+// columns n = n0 + wn*128 + nb*16 + 4 (lane >> 4) + e.
+template <int EPI, int ACT>
+__device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8], int m0, int n0, int split, int wm,
+                                         int wn, int lane) {
+  const int nl = 4 * (lane >> 4);
+  const int ncol0 = n0 + wn * 128;
+  const int nbase = ncol0 + nl;
+  // bf16 results (and pre-activations) go out through the paired 16-B path
+  constexpr bool WIDE = EPI == kEpiBiasAct || EPI == kEpiDact || EPI == kEpiPlain;
+  float csum[8][4];
+  if (EPI == kEpiDact) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) csum[b][c] = 0.f;
+  }
+  const bool wide = WIDE && !(EPI == kEpiPlain && (g.out_f32 || g.beta != 0.f));
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+    const int m_raw = m0 + wm * 128 + mb * 16 + (lane & 15);
+    const bool mok = m_raw < g.M;
+    const int m = mok ? m_raw : g.M - 1;
+    const int64_t roff = static_cast<int64_t>(m) * g.ldc;
+    uint2 ob[8], pb[8];
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int n_raw = nbase + nb * 16;
+      const bool ok = mok && n_raw < g.N;  // N % 8 == 0: a 4-group is all-in or all-out
+      const int n = ok ? n_raw : min(n_raw, g.N - 4);
+      const int64_t off = roff + n;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[mb][nb][e];
+      if (EPI == kEpiSplit) {
+        float* Wp = g.ws + (static_cast<int64_t>(split) * g.M + m) * g.N + n;
+        if (ok) *reinterpret_cast<f32x4t*>(Wp) = f32x4t{v[0], v[1], v[2], v[3]};
+        continue;
+      }
+      if (EPI == kEpiBiasAct) {
+        const bf16x4 bb = g.bias ? *reinterpret_cast<const bf16x4*>(g.bias + n) : bf16x4{};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bf2f(bb[e]);
+        pb[nb] = pack4(v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = t_act<ACT>(v[e]);
+      }
+      if (EPI == kEpiDact) {
+        const bf16x4 xa = *reinterpret_cast<const bf16x4*>(g.aux + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= t_act_grad<ACT>(bf2f(xa[e]));
+      }
+      if (EPI == kEpiPlain && !wide) {
+        if (g.beta != 0.f) {
+          if (g.out_f32) {
+            const f32x4t o = *reinterpret_cast<const f32x4t*>(static_cast<const float*>(g.C) + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += g.beta * o[e];
+          } else {
+            const bf16x4 o = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(g.C) + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += g.beta * bf2f(o[e]);
+          }
+        }
+        if (g.out_f32) {
+          if (ok) *reinterpret_cast<f32x4t*>(static_cast<float*>(g.C) + off) = f32x4t{v[0], v[1], v[2], v[3]};
+        } else if (ok) {
+          *reinterpret_cast<uint2*>(static_cast<bf16*>(g.C) + off) = pack4(v);
+        }
+        continue;
+      }
+      ob[nb] = pack4(v);
+      if (EPI == kEpiDact) {
+        const bf16x4 o = __builtin_bit_cast(bf16x4, ob[nb]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csum[nb][e] += ok ? bf2f(o[e]) : 0.f;  // the stored (rounded) value
+      }
+    }
+    if (WIDE && wide) {
+      store_row16(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, ob, lane);
+      if (EPI == kEpiBiasAct && g.pre) store_row16(g.pre, roff, ncol0, g.N, mok, pb, lane);
+    }
+  }
+  if (EPI == kEpiDact && g.dbias) {
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sm = csum[nb][e];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+        const int n = nbase + nb * 16 + e;
+        if ((lane & 15) == 0 && n < g.N) atomicAdd(g.dbias + n, sm);
+      }
+  }
+}
+
+// STG: 0 = both operands staged through registers; 1 = B by LDS-DMA (issued
+// in phase B, two phases ahead of its first read), A through registers
+template <bool TA, bool TB, int EPI, int ACT, int STG>
+__global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kernel(
+    GemmTArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUFT];  // the ONE LDS object
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- tile (bijective XCD remap + grouped raster, guide T1)
+  const int gm = (g.M + TM - 1) / TM, gn = (g.N + TN - 1) / TN;
+  const int nwg = gm * gn;
+  const int W = nwg * g.splits;
+  const int bid = xcd_remap(blockIdx.x, W);
+  const int split = bid / nwg, t = bid % nwg;
+  const int per_group = GROUP * gn;
+  const int first_m = (t / per_group) * GROUP;
+  const int gsize = min(gm - first_m, GROUP);
+  const int m0 = (first_m + (t % per_group) % gsize) * TM;
+  const int n0 = ((t % per_group) / gsize) * TN;
+  const int L = g.K / TK / g.splits;
+  const int kt0 = split * L;
+
+  // ---- global staging (A: KOUTER = TA, B: KOUTER = !TB)
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.A), static_cast<short>(0), g.bytesA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.B), static_cast<short>(0), g.bytesB, 0x00020000);
+  const unsigned kstepA = TA ? static_cast<unsigned>(TK * g.lda * 2) : TK * 2u;
+  const unsigned kstepB = !TB ? static_cast<unsigned>(TK * g.ldb * 2) : TK * 2u;
+  const unsigned voA = stage_voff<TA>(g.lda, m0, tid);
+  const unsigned voB = stage_voff<!TB>(g.ldb, n0, tid);
+  constexpr int NDV = !TB ? 4 : 2;  // B DMA voffsets (K-outer: by i & 3, K-contiguous: by i & 1)
+  unsigned dvB[NDV];
+#pragma unroll
+  for (int i = 0; i < NDV; ++i) dvB[i] = STG == 1 ? dma_voff<!TB>(g.ldb, n0, i, wave, lane) : 0u;
+  // scalar part of B DMA piece i's offset (rows beyond piece i % NDV's)
+  auto dsoffB = [&](int i) -> unsigned {
+    return !TB ? static_cast<unsigned>(4 * (i - (i & 3))) * static_cast<unsigned>(g.ldb) * 2u
+               : static_cast<unsigned>(8 * (i - (i & 1))) * static_cast<unsigned>(g.ldb) * 2u;
+  };
+  constexpr int NR = STG == 1 ? 8 : 16;
+  i32x4t R[16];
+  (void)NR;
+  auto gload = [&](int kt) {  // issue the register-staged global loads of K-tile kt
+    const unsigned ka = static_cast<unsigned>(kt) * kstepA;
+    const unsigned kb = static_cast<unsigned>(kt) * kstepB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      R[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          rA, voA, __builtin_amdgcn_readfirstlane(ka + stage_soff<TA>(g.lda, i)), 0);
+    if (STG == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        R[8 + i] = __builtin_amdgcn_raw_buffer_load_b128(
+            rB, voB, __builtin_amdgcn_readfirstlane(kb + stage_soff<!TB>(g.ldb, i)), 0);
+    }
+  };
+  auto swrite = [&](unsigned char* buf) {  // R -> LDS image of one K-tile
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<i32x4t*>(buf + stage_lds<TA>(i, tid)) = R[i];
+    if (STG == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) *reinterpret_cast<i32x4t*>(buf + 2 * HALF + stage_lds<!TB>(i, tid)) = R[8 + i];
+    }
+  };
+  auto dmaB = [&](unsigned char* buf, int kt, int i) {  // B DMA piece i of K-tile kt into buf
+    const unsigned kb = static_cast<unsigned>(kt) * kstepB + dsoffB(i);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (__attribute__((address_space(3))) void*)(buf + 2 * HALF +
+                                                                                             (wave * 8 + i) * 1024),
+                                             16, dvB[i % NDV], __builtin_amdgcn_readfirstlane(kb), 0, 0);
+  };
+
+  // ---- fragments
+  auto rdA = [&](const unsigned char* buf, int mb, int ks) -> bf16x8 {
+    return TA ? tr16(buf + wm * HALF, ks, mb * 16, lane) : row16(buf, wm * 128 + mb * 16, ks, lane);
+  };
+  auto rdB = [&](const unsigned char* buf, int nb, int ks) -> bf16x8 {
+    const unsigned char* b = buf + 2 * HALF;
+    return TB ? row16(b, wn * 128 + nb * 16, ks, lane) : tr16(b + wn * HALF, ks, nb * 16, lane);
+  };
+
+  f32x4t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4t{};
+  // fa[mb] is re-read for the next k-step right after its last MFMA; the B
+  // fragments alternate between two named sets (all 8 live through a k-step)
+  bf16x8 fa[8], fbx[8], fby[8];
+
+  // ---- prologue: tile 0 -> buffer 0, tile 1 in flight, k-step 0 fragments
+  gload(kt0);
+  if (STG == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dmaB(smem, kt0, i);
+  }
+  swrite(smem);
+  gload(kt0 + 1);
+  if (STG == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dmaB(smem + BUFT, kt0 + 1, i);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // B of tile 0 landed (A / B of tile 1 in flight)
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[i] = rdA(smem, i, 0);
+    fbx[i] = rdB(smem, i, 0);
+  }
+
+  // LDS read instructions per (A, B) fragment pair: ds_read_b128 = 1, transposed = 2
+  constexpr int NRD = (TA ? 2 : 1) + (TB ? 1 : 2);
+  // One straight-line body per K-tile (no branches: past the last K-tile the
+  // global loads read zeros or unused in-range bytes and land in a buffer
+  // nobody reads).  Program order IS the schedule: each 8-MFMA group (one A
+  // fragment x the 8 B fragments, 128 cycles of matrix work) carries the
+  // re-read of that A fragment and of one B fragment for the next k-step,
+  // and in phase A also two LDS writes of the staged tile and the two global
+  // loads that refill those registers; sched_barrier(0) between groups keeps
+  // hipcc from hoisting all LDS / memory work out of the MFMA stream.
+  for (int kt = 0; kt < L; ++kt) {
+    unsigned char* cur = smem + (kt & 1) * BUFT;
+    unsigned char* nxt = smem + ((kt + 1) & 1) * BUFT;
+    const unsigned ka = static_cast<unsigned>(kt0 + kt + 2) * kstepA;
+    const unsigned kb = static_cast<unsigned>(kt0 + kt + 2) * kstepB;
+    // ---- phase A: k-step 0 (fa, fbx) | read k-step 1 into (fa, fby), stage tile kt+1, load tile kt+2
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
+      fa[mb] = rdA(cur, mb, 1);
+      fby[mb] = rdB(cur, mb, 1);
+      // LDS writes + refills: STG 0: chunks 2mb, 2mb+1 (A chunks for mb < 4,
+      // B after); STG 1: A chunk mb
+#pragma unroll
+      for (int h = 0; h < (STG == 1 ? 1 : 2); ++h) {
+        const int c = STG == 1 ? mb : 2 * mb + h;
+        if (c < 8) {
+          *reinterpret_cast<i32x4t*>(nxt + stage_lds<TA>(c, tid)) = R[c];
+          R[c] = __builtin_amdgcn_raw_buffer_load_b128(rA, voA,
+                                                       __builtin_amdgcn_readfirstlane(ka + stage_soff<TA>(g.lda, c)), 0);
+        } else {
+          *reinterpret_cast<i32x4t*>(nxt + 2 * HALF + stage_lds<!TB>(c - 8, tid)) = R[c];
+          R[c] = __builtin_amdgcn_raw_buffer_load_b128(
+              rB, voB, __builtin_amdgcn_readfirstlane(kb + stage_soff<!TB>(g.ldb, c - 8)), 0);
+        }
+      }
+      // one memory instruction between MFMAs (an MFMA leaves the SIMD's issue
+      // free for 8 of its 16 cycles); the fragment re-reads go last, after
+      // the group's final use of fa[mb]
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if (STG == 0) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (STG == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // B of tile kt+1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // k-step 1 reads + LDS writes done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // ---- phase B: k-step 1 (fa, fby) | read k-step 0 of tile kt+1 into (fa, fbx)
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
+      fa[mb] = rdA(nxt, mb, 0);
+      fbx[mb] = rdB(nxt, mb, 0);
+      if (STG == 1) dmaB(cur, kt0 + kt + 2, mb);  // tile kt's buffer: its reads retired at the barrier
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  epilogue<EPI, ACT>(g, acc, m0, n0, split, wm, wn, lane);
+}
+
+}  // namespace
+
+bool gemmt_act_supported(int act) { return act == 0 || act == 1 || act == 4; }
+
+void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t st) {
+  auto bytes = [](int rows, int ld) {
+    const uint64_t b = static_cast<uint64_t>(rows) * static_cast<uint64_t>(ld) * 2u;
+    return static_cast<unsigned>(b > 0xFFFFFFFFull ? 0xFFFFFFFFull : b);
+  };
+  GemmTArgs g{static_cast<const bf16*>(p.A), static_cast<const bf16*>(p.B), p.C, p.workspace,
+              static_cast<const bf16*>(p.bias), static_cast<bf16*>(p.pre), static_cast<const bf16*>(p.aux), p.dbias,
+              p.M, p.N, p.K, p.lda, p.ldb, p.ldc, p.alpha, p.beta, p.act, p.act_bwd ? 1 : 0, p.out_f32, splits,
+              bytes(p.trans_a ? p.K : p.M, p.lda), bytes(p.trans_b ? p.N : p.K, p.ldb)};
+  const int items = ((p.M + TM - 1) / TM) * ((p.N + TN - 1) / TN) * splits;
+  dim3 grid(items), block(NTHREADS);
+  const int epi = splits > 1 ? kEpiSplit : p.act_bwd ? kEpiDact : (p.bias || p.pre || p.act) ? kEpiBiasAct : kEpiPlain;
+  auto launch = [&](auto ta, auto tb, auto stg) {
+    constexpr bool TA = decltype(ta)::value, TB = decltype(tb)::value;
+    constexpr int S = decltype(stg)::value;
+    switch (epi * 8 + p.act) {
+      case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S>), grid, block, 0, st, g); break;
+      case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiSplit, 0, S>), grid, block, 0, st, g); break;
+      case kEpiBiasAct * 8 + 0:
+        hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 0, S>), grid, block, 0, st, g);
+        break;
+      case kEpiBiasAct * 8 + 1:
+        hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 1, S>), grid, block, 0, st, g);
+        break;
+      case kEpiBiasAct * 8 + 4:
+        hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 4, S>), grid, block, 0, st, g);
+        break;
+      case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiDact, 1, S>), grid, block, 0, st, g); break;
+      case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiDact, 4, S>), grid, block, 0, st, g); break;
+      default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
+    }
+  };
+  using F = std::false_type;
+  using T = std::true_type;
+  auto by_stage = [&](auto ta, auto tb) {
+    if (stage_mode == 1) launch(ta, tb, std::integral_constant<int, 1>{});
+    else launch(ta, tb, std::integral_constant<int, 0>{});
+  };
+  if (!p.trans_a && !p.trans_b) by_stage(F{}, F{});
+  else if (!p.trans_a && p.trans_b) by_stage(F{}, T{});
+  else if (p.trans_a && !p.trans_b) by_stage(T{}, F{});
+  else by_stage(T{}, T{});
+  FFK_LAUNCH_CHECK("gemmt");
+}
+
+}  // namespace ffk

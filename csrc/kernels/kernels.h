@@ -112,11 +112,16 @@ struct GemmPParams {
   float alpha = 1.f, beta = 0.f;
   int out_f32 = 0, splits = 1;
   int dbg = 0;                  // ablation bits for timing experiments (gemmp.hip)
-  int variant = 0;              // 0: 32x32x16 MFMA (gemmp.hip), 1: 16x16x32 MFMA (gemmq.hip)
+  int variant = 0;              // 0: 32x32x16 MFMA (gemmp.hip), 1: 16x16x32 (gemmq.hip), 2: ping-pong (gemmr.hip),
+                                // 3 / 4: one wave per SIMD, 128x128 wave tile, B staged
+                                // through registers / by LDS-DMA (gemmt.hip)
 };
 bool gemmp_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b);
 void gemmp_bf16(const GemmPParams& p, hipStream_t st);
 void gemmq_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
+void gemmr_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
+void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t st);
+bool gemmt_act_supported(int act);
 
 // ---- tensorops.hip: general tensor operators (N-d, <= 6 dims)
 struct NdShape {

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dx,dw")
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--cands", default="", help="comma list of candidate prefixes (blaslt,p,q,r,t)")
     args = ap.parse_args()
     dev = "cuda"
     only = set(args.only.split(","))
@@ -76,10 +77,17 @@ def main():
         Kd = a.shape[0] if ta else a.shape[1]
         ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
         cands = {"blaslt": lambda o: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=o)}
-        splits = [1] if kind != "dw" else [1, 2, 4, 8]
+        splits = [1] if kind != "dw" else [2, 4, 8]
         for sp in splits:
             cands[f"p{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp)
             cands[f"q{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=1)
+            cands[f"r{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=2)
+            cands[f"t{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=3)
+            cands[f"u{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=4)
+        if args.cands:
+            keep = args.cands.split(",")
+            cands = {k: v for k, v in cands.items() if k == "blaslt" and "blaslt" in keep
+                     or k != "blaslt" and k.rstrip("0123456789") in keep}
         outs = {k: torch.empty(M, N, device=dev, dtype=torch.bfloat16) for k in cands}
         err = {}
         for k, f in cands.items():
