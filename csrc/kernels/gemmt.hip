@@ -166,7 +166,10 @@ __device__ __forceinline__ bf16x8 tr16(const unsigned char* img, int ks, int o0,
   return cat44(lds_tr(img, oa), lds_tr(img, ob));  // intrinsic: no LDS-DMA here to be drained
 }
 
-enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3 };
+// kEpiPlain: bf16 C = alpha * AB (16-B paired stores); kEpiGeneral: fp32
+// output and / or beta != 0 (kept apart: its extra live registers in a shared
+// epilogue made the allocator shuttle accumulators through VGPRs in the loop)
+enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3, kEpiGeneral = 4 };
 
 __device__ __forceinline__ uint2 pack4(const float (&v)[4]) {
   bf16x4 o;
@@ -210,7 +213,6 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
 #pragma unroll
       for (int c = 0; c < 4; ++c) csum[b][c] = 0.f;
   }
-  const bool wide = WIDE && !(EPI == kEpiPlain && (g.out_f32 || g.beta != 0.f));
 #pragma unroll
   for (int mb = 0; mb < 8; ++mb) {
     const int m_raw = m0 + wm * 128 + mb * 16 + (lane & 15);
@@ -245,7 +247,7 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] *= t_act_grad<ACT>(bf2f(xa[e]));
       }
-      if (EPI == kEpiPlain && !wide) {
+      if (EPI == kEpiGeneral) {
         if (g.beta != 0.f) {
           if (g.out_f32) {
             const f32x4t o = *reinterpret_cast<const f32x4t*>(static_cast<const float*>(g.C) + off);
@@ -271,7 +273,7 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
         for (int e = 0; e < 4; ++e) csum[nb][e] += ok ? bf2f(o[e]) : 0.f;  // the stored (rounded) value
       }
     }
-    if (WIDE && wide) {
+    if (WIDE) {
       store_row16(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, ob, lane);
       if (EPI == kEpiBiasAct && g.pre) store_row16(g.pre, roff, ncol0, g.N, mok, pb, lane);
     }
@@ -288,6 +290,12 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
         if ((lane & 15) == 0 && n < g.N) atomicAdd(g.dbias + n, sm);
       }
   }
+}
+
+// 16 bytes per lane straight into LDS (kept out of the kernel template: the
+// builtin inside a lambda of a kernel template drops the host launch stub)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
 // STG: 0 = both operands staged through registers; 1 = B by LDS-DMA (issued
@@ -360,9 +368,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   };
   auto dmaB = [&](unsigned char* buf, int kt, int i) {  // B DMA piece i of K-tile kt into buf
     const unsigned kb = static_cast<unsigned>(kt) * kstepB + dsoffB(i);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (__attribute__((address_space(3))) void*)(buf + 2 * HALF +
-                                                                                             (wave * 8 + i) * 1024),
-                                             16, dvB[i % NDV], __builtin_amdgcn_readfirstlane(kb), 0, 0);
+    dma16(rB, buf + 2 * HALF + (wave * 8 + i) * 1024, dvB[i % NDV], __builtin_amdgcn_readfirstlane(kb));
   };
 
   // ---- fragments
@@ -478,7 +484,37 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  // pin the accumulators to AGPRs at the loop exit: otherwise the epilogue's
+  // VALU use of them can tip the allocator into keeping some in VGPRs and
+  // shuttling them (v_accvgpr_read / write) inside the loop
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
   epilogue<EPI, ACT>(g, acc, m0, n0, split, wm, wn, lane);
+}
+
+template <bool TA, bool TB, int S>
+void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
+  switch (epi * 8 + act) {
+    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S>), grid, block, 0, st, g); break;
+    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiSplit, 0, S>), grid, block, 0, st, g); break;
+    case kEpiGeneral * 8:
+      hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiGeneral, 0, S>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 0:
+      hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 0, S>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 1:
+      hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 1, S>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 4:
+      hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 4, S>), grid, block, 0, st, g);
+      break;
+    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiDact, 1, S>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiDact, 4, S>), grid, block, 0, st, g); break;
+    default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
+  }
 }
 
 }  // namespace
@@ -496,37 +532,22 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
               bytes(p.trans_a ? p.K : p.M, p.lda), bytes(p.trans_b ? p.N : p.K, p.ldb)};
   const int items = ((p.M + TM - 1) / TM) * ((p.N + TN - 1) / TN) * splits;
   dim3 grid(items), block(NTHREADS);
-  const int epi = splits > 1 ? kEpiSplit : p.act_bwd ? kEpiDact : (p.bias || p.pre || p.act) ? kEpiBiasAct : kEpiPlain;
-  auto launch = [&](auto ta, auto tb, auto stg) {
-    constexpr bool TA = decltype(ta)::value, TB = decltype(tb)::value;
-    constexpr int S = decltype(stg)::value;
-    switch (epi * 8 + p.act) {
-      case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S>), grid, block, 0, st, g); break;
-      case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiSplit, 0, S>), grid, block, 0, st, g); break;
-      case kEpiBiasAct * 8 + 0:
-        hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 0, S>), grid, block, 0, st, g);
-        break;
-      case kEpiBiasAct * 8 + 1:
-        hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 1, S>), grid, block, 0, st, g);
-        break;
-      case kEpiBiasAct * 8 + 4:
-        hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 4, S>), grid, block, 0, st, g);
-        break;
-      case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiDact, 1, S>), grid, block, 0, st, g); break;
-      case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiDact, 4, S>), grid, block, 0, st, g); break;
-      default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
-    }
-  };
-  using F = std::false_type;
-  using T = std::true_type;
-  auto by_stage = [&](auto ta, auto tb) {
-    if (stage_mode == 1) launch(ta, tb, std::integral_constant<int, 1>{});
-    else launch(ta, tb, std::integral_constant<int, 0>{});
-  };
-  if (!p.trans_a && !p.trans_b) by_stage(F{}, F{});
-  else if (!p.trans_a && p.trans_b) by_stage(F{}, T{});
-  else if (p.trans_a && !p.trans_b) by_stage(T{}, F{});
-  else by_stage(T{}, T{});
+  const int epi = splits > 1                        ? kEpiSplit
+                  : p.act_bwd                       ? kEpiDact
+                  : (p.bias || p.pre || p.act)      ? kEpiBiasAct
+                  : (p.out_f32 || p.beta != 0.f)    ? kEpiGeneral
+                                                    : kEpiPlain;
+  if (stage_mode == 1) {
+    if (!p.trans_a && !p.trans_b) launch_t<false, false, 1>(g, grid, block, epi, p.act, st);
+    else if (!p.trans_a && p.trans_b) launch_t<false, true, 1>(g, grid, block, epi, p.act, st);
+    else if (p.trans_a && !p.trans_b) launch_t<true, false, 1>(g, grid, block, epi, p.act, st);
+    else launch_t<true, true, 1>(g, grid, block, epi, p.act, st);
+  } else {
+    if (!p.trans_a && !p.trans_b) launch_t<false, false, 0>(g, grid, block, epi, p.act, st);
+    else if (!p.trans_a && p.trans_b) launch_t<false, true, 0>(g, grid, block, epi, p.act, st);
+    else if (p.trans_a && !p.trans_b) launch_t<true, false, 0>(g, grid, block, epi, p.act, st);
+    else launch_t<true, true, 0>(g, grid, block, epi, p.act, st);
+  }
   FFK_LAUNCH_CHECK("gemmt");
 }
 

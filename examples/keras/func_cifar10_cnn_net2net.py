@@ -1,4 +1,5 @@
-"""Keras functional CNN on CIFAR-10 (reference: examples/python/keras/func_cifar10_cnn.py)."""
+"""Teacher -> student weight transfer on a functional CIFAR-10 CNN
+(reference: examples/python/keras/func_cifar10_cnn_net2net.py)."""
 from _common import ModelAccuracy, cifar10, epochs, verify
 
 import flexflow.keras.optimizers
@@ -6,11 +7,9 @@ from flexflow.keras.layers import Activation, Conv2D, Dense, Flatten, Input, Max
 from flexflow.keras.models import Model
 
 
-def top_level_task():
-    x_train, y_train = cifar10()
+def build():
     inp = Input(shape=(3, 32, 32), dtype="float32")
-    t = Conv2D(filters=32, input_shape=(3, 32, 32), kernel_size=(3, 3), strides=(1, 1), padding=(1, 1),
-               activation="relu")(inp)
+    t = Conv2D(filters=32, kernel_size=(3, 3), strides=(1, 1), padding=(1, 1), activation="relu")(inp)
     t = Conv2D(filters=32, kernel_size=(3, 3), strides=(1, 1), padding=(1, 1), activation="relu")(t)
     t = MaxPooling2D(pool_size=(2, 2), strides=(2, 2), padding="valid")(t)
     t = Conv2D(filters=64, kernel_size=(3, 3), strides=(1, 1), padding=(1, 1), activation="relu")(t)
@@ -19,14 +18,22 @@ def top_level_task():
     t = Flatten()(t)
     t = Dense(512, activation="relu")(t)
     t = Dense(10)(t)
-    out = Activation("softmax")(t)
-    model = Model(inp, out)
+    model = Model(inp, Activation("softmax")(t))
     model.compile(optimizer=flexflow.keras.optimizers.SGD(learning_rate=0.01), loss="sparse_categorical_crossentropy",
                   metrics=["accuracy", "sparse_categorical_crossentropy"])
-    print(model.summary())
-    model.fit(x_train, y_train, epochs=epochs(80), callbacks=verify(ModelAccuracy.CIFAR10_CNN))
+    return model
+
+
+def top_level_task():
+    x_train, y_train = cifar10()
+    teacher = build()
+    teacher.fit(x_train, y_train, epochs=epochs(40))
+    student = build()
+    for i in (0, 1, 3, 4, 7, 8):   # the conv and dense layers
+        student.get_layer(index=i).set_weights(student.ffmodel, *teacher.get_layer(index=i).get_weights(teacher.ffmodel))
+    student.fit(x_train, y_train, epochs=epochs(40), callbacks=verify(ModelAccuracy.CIFAR10_CNN))
 
 
 if __name__ == "__main__":
-    print("Functional API, cifar10 cnn")
+    print("Functional API, cifar10 cnn teacher student")
     top_level_task()

@@ -178,3 +178,23 @@ def build_arg_parser() -> argparse.ArgumentParser:
     for f in ("-ll:fsize", "-ll:zsize", "-ll:util", "-ll:bgwork", "-ll:csize", "-lg:prof", "-lg:prof_logfile"):
         a(f, dest="_ignored_" + f.strip("-").replace(":", "_"), type=str)
     return p
+
+
+class NetConfig:
+    """Dataset location of the CNN examples (reference flexflow_cffi.py:2400
+    NetConfig: the ``--dataset`` / ``-d`` flag)."""
+
+    def __init__(self, argv: Optional[List[str]] = None):
+        ns, _ = build_arg_parser().parse_known_args(sys.argv[1:] if argv is None else argv)
+        self.dataset_path = ns.dataset_path or ""
+
+
+def flexflow_python_binding() -> str:
+    """The reference selects cffi / pybind11 bindings; this framework's
+    native core is bound with pybind11."""
+    return "pybind11"
+
+
+def flexflow_python_interpreter() -> str:
+    return "native"
+

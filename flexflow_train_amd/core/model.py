@@ -51,6 +51,24 @@ def _act(a) -> str:
     return str(a)
 
 
+def _regularizer(r):
+    """-> ("none" | "l1" | "l2", lambda) from a regularizer object
+    (``.type`` RegularizerMode, ``._lambda``) or a (kind, lambda) pair."""
+    if r is None:
+        return "none", 0.0
+    if isinstance(r, (tuple, list)):
+        kind, lam = r
+        return str(kind).lower(), float(lam)
+    kind = getattr(r, "type", None)
+    name = getattr(kind, "name", str(kind)).upper()
+    lam = float(getattr(r, "_lambda", getattr(r, "lambda_", 0.0)))
+    if name.endswith("L1"):
+        return "l1", lam
+    if name.endswith("L2"):
+        return "l2", lam
+    return "none", 0.0
+
+
 class Tensor:
     def __init__(self, model: "FFModel", vref, name: Optional[str] = None):
         self.model = model
@@ -92,33 +110,64 @@ class Tensor:
 
     # ---- Legion region access (flexflow_cffi.py Tensor.inline_map /
     # attach_numpy_array / get_array ...).  There are no regions here: a
-    # "mapped" tensor is a host numpy view of the current value (inputs: the
-    # pending feed, others: the last computed value), and attaching an array
-    # makes it the next fed batch.
-    def inline_map(self, ffmodel, ffconfig=None):
-        self._mapped = self.get_tensor(ffmodel)
+    # "mapped" tensor is a host numpy view of the current value (inputs and
+    # the label: the pending feed, others: the last computed value), and
+    # attaching an array makes it the next fed batch.  The reference's
+    # spellings (ffconfig), (ffmodel, ffconfig) and (ffconfig, data_type) are
+    # all accepted.
+    def _args(self, args):
+        m, rest = self.model, list(args)
+        if rest and isinstance(rest[0], FFModel):
+            m = rest.pop(0)
+        if rest and isinstance(rest[0], FFConfig):
+            rest.pop(0)
+        return m, rest
+
+    def _feed_key(self):
+        return self.name or f"input_{self.vref.node}"
+
+    def _host_value(self, m):
+        """Current value; an input / label with nothing fed yet gets a zero
+        array that becomes its pending feed (writes into it are seen)."""
+        v = m._get_value(self)
+        if v is not None:
+            return v
+        is_input = any(t is self or t.name == self.name for t in m._inputs) or self.name == "label"
+        if not is_input:
+            return None
+        dims = m._label_dims() if self.vref is None else list(self.dims)
+        dt = DataType.DT_INT32 if self.name == "label" and m._sparse_labels() else self.data_type
+        arr = np.zeros(dims, dtype=_NP_DT[_dt_str(dt)])
+        m._pending_feeds[self._feed_key()] = arr
+        return arr
+
+    def inline_map(self, *args):
+        m, _ = self._args(args)
+        self._mapped = self._host_value(m)
         return self._mapped
 
-    def inline_unmap(self, ffmodel, ffconfig=None):
+    def inline_unmap(self, *args):
         self._mapped = None
 
     def is_mapped(self):
         return getattr(self, "_mapped", None) is not None
 
-    def get_array(self, ffmodel, ffconfig=None, data_type=None):
-        a = self._mapped if self.is_mapped() else self.get_tensor(ffmodel)
+    def get_array(self, *args):
+        m, _ = self._args(args)
+        a = self._mapped if self.is_mapped() else self._host_value(m)
         return None if a is None else np.asarray(a)
 
-    def get_flat_array(self, ffmodel, ffconfig=None, data_type=None):
-        a = self.get_array(ffmodel, ffconfig, data_type)
+    def get_flat_array(self, *args):
+        a = self.get_array(*args)
         return None if a is None else a.reshape(-1)
 
-    def attach_numpy_array(self, ffmodel, ffconfig, np_array):
-        self.set_tensor(ffmodel, np_array)
+    def attach_numpy_array(self, *args):
+        m, rest = self._args(args)
+        self.set_tensor(m, rest[-1])
 
-    def detach_numpy_array(self, ffmodel=None, ffconfig=None):
-        m = ffmodel or self.model
-        m._pending_feeds.pop(self.name or f"input_{self.vref.node}", None)
+    def detach_numpy_array(self, *args):
+        m, _ = self._args(args)
+        m._pending_feeds.pop(self._feed_key(), None)
 
     def __repr__(self):
         return f"Tensor({self.name}, dims={self.dims})"
@@ -394,8 +443,14 @@ class FFModel:
 
     def dense(self, input, out_dim, activation=ActiMode.AC_MODE_NONE, use_bias=True, datatype=None, shared_op=None,
               kernel_initializer=None, bias_initializer=None, kernel_regularizer=None, name=None):
+        """Linear layer.  ``kernel_regularizer`` (an object with ``type`` =
+        RegularizerMode and ``_lambda``, e.g. flexflow.keras.regularizers.L2,
+        or a ("l1" | "l2", lambda) pair) adds lambda * W (L2) or
+        lambda * sign(W) (L1) to the kernel gradient, as the reference's
+        Linear backward does (linear_kernels.cu:258, cublasSgeam dW += lambda W)."""
+        reg, lam = _regularizer(kernel_regularizer)
         return self._add("LINEAR", [input], name, (kernel_initializer, bias_initializer), out_channels=out_dim,
-                         activation=_act(activation), use_bias=use_bias)
+                         activation=_act(activation), use_bias=use_bias, regularizer=reg, regularizer_lambda=lam)
 
     def concat(self, tensors, axis, name=None):
         return self._add("CONCAT", list(tensors), name, axis=axis)
@@ -669,17 +724,19 @@ class FFModel:
     def _input_name(self, t):
         return t.name
 
-    def fit(self, x=None, y=None, batch_size=None, epochs=1):
+    def fit(self, x=None, y=None, batch_size=None, epochs=1, batch_hooks=None):
         """Training loop over data loaders (or arrays).  Prints the
-        reference's ``ELAPSED TIME = ..., THROUGHPUT = ... samples/s``."""
+        reference's ``ELAPSED TIME = ..., THROUGHPUT = ... samples/s``.
+        ``batch_hooks`` = (begin(it), end(it)) callables run around every
+        iteration (the keras frontend's per-batch callbacks)."""
         ex = self.executor
         xs = x if isinstance(x, (list, tuple)) else [x]
         bs = batch_size or self.ffconfig.batch_size
         if getattr(self, "local_backing", None) is not None:
-            return self._fit_local(xs, y, bs, epochs)
+            return self._fit_local(xs, y, bs, epochs, batch_hooks)
         native = self._native_loader(xs, y, bs)
         if native is not None:
-            return self._fit_native(native, epochs)
+            return self._fit_native(native, epochs, batch_hooks)
         loaders = [d if isinstance(d, SingleDataLoader) else SingleDataLoader(self, self._inputs[i], d)
                    for i, d in enumerate(xs)]
         ylo = y if isinstance(y, SingleDataLoader) else SingleDataLoader(self, self._label_tensor, y)
@@ -704,6 +761,8 @@ class FFModel:
                 for l in loaders + [ylo]:
                     l.next_batch()
             for it in range(skip, iters):
+                if batch_hooks:
+                    batch_hooks[0](it)
                 feeds = {self._inputs[i].name: torch.as_tensor(l.next_batch()) for i, l in enumerate(loaders)}
                 labels = torch.as_tensor(ylo.next_batch())
                 if use_graph and not first:
@@ -716,6 +775,8 @@ class FFModel:
                     ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
                 first = False
                 self._after_fit_step(epoch, it, iters)
+                if batch_hooks:
+                    batch_hooks[1](it)
                 # perf_metrics() all-reduces across ranks: every rank calls it, rank 0 prints
                 if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0:
                     pm = ex.perf_metrics()
@@ -814,7 +875,7 @@ class FFModel:
             b.set_weight(n, self.executor.get_parameter(n).numpy())
         self.local_backing = b
 
-    def _fit_local(self, xs, y, bs, epochs):
+    def _fit_local(self, xs, y, bs, epochs, batch_hooks=None):
         b = self.local_backing
         arrays = [np.asarray(d.full if isinstance(d, SingleDataLoader) else d) for d in xs]
         labels = np.asarray(y.full if isinstance(y, SingleDataLoader) else y)
@@ -824,10 +885,14 @@ class FFModel:
         for epoch in range(epochs):
             b.reset_metrics()
             for it in range(iters):
+                if batch_hooks:
+                    batch_hooks[0](it)
                 sl = slice(it * bs, (it + 1) * bs)
                 for n, a in zip(names, arrays):
                     b.set_input(n, a[sl])
                 b.train_step(labels[sl].astype(np.float32))
+                if batch_hooks:
+                    batch_hooks[1](it)
             mm = b.metrics()
             if self.dist.rank == 0 and iters:
                 acc = 100.0 * mm["correct"] / max(mm["samples"], 1)
@@ -841,7 +906,7 @@ class FFModel:
         self.last_throughput = thr
         return thr
 
-    def _fit_native(self, loader, epochs):
+    def _fit_native(self, loader, epochs, batch_hooks=None):
         ex = self.executor
         iters = loader.iters_per_epoch
         num_samples = iters * loader.batch
@@ -858,6 +923,8 @@ class FFModel:
             for epoch in range(start_epoch, epochs):
                 ex.zero_metrics()
                 for it in range(start_it if epoch == start_epoch else 0, iters):
+                    if batch_hooks:
+                        batch_hooks[0](it)
                     feeds, labels, _ = loader.next()
                     if use_graph and not first:
                         if graphed is None:
@@ -867,6 +934,8 @@ class FFModel:
                         ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
                     first = False
                     self._after_fit_step(epoch, it, iters)
+                    if batch_hooks:
+                        batch_hooks[1](it)
                     if self.ffconfig.print_freq and (it + 1) % self.ffconfig.print_freq == 0:
                         pm = ex.perf_metrics()   # a collective: every rank calls it
                         if self.dist.rank == 0:
@@ -918,6 +987,16 @@ class FFModel:
         if v is None:
             return None
         return v
+
+    def _sparse_labels(self) -> bool:
+        lt = self.loss_type
+        return "SPARSE" in str(getattr(lt, "name", lt)).upper()
+
+    def _label_dims(self):
+        bs = self.ffconfig.batch_size
+        if self._sparse_labels() or not self._layers:
+            return [bs, 1]
+        return list(self._layers[-1].get_output_tensor().dims)
 
     def _get_value(self, t: Tensor):
         """Latest value of a tensor as numpy (this rank's piece): a pending

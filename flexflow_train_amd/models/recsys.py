@@ -36,6 +36,38 @@ class DLRMConfig:
     mlp_top: List[int] = dataclasses.field(default_factory=lambda: [64, 64, 2])
     sigmoid_bot: int = -1
     sigmoid_top: int = -2  # index counted from the end: last layer
+    arch_interaction_op: str = "cat"
+    loss_threshold: float = 0.0
+    dataset_path: str = ""
+    data_size: int = -1
+
+    @classmethod
+    def from_args(cls, argv=None, **kw) -> "DLRMConfig":
+        """The reference's DLRM command line (examples/cpp/DLRM/dlrm.cc
+        parse_input_args): --arch-sparse-feature-size N, --arch-embedding-size
+        a-b-c, --embedding-bag-size N, --arch-mlp-bot a-b-c, --arch-mlp-top
+        a-b-c, --loss-threshold F, --sigmoid-top N, --sigmoid-bot N,
+        --arch-interaction-op cat|dot, --dataset PATH, --data-size N, -b N."""
+        import sys
+        argv = sys.argv[1:] if argv is None else list(argv)
+        cfg = cls(**kw)
+        ints = lambda v: [int(x) for x in v.split("-") if x]  # noqa: E731
+        flags = {"--arch-sparse-feature-size": ("sparse_feature_size", int),
+                 "--arch-embedding-size": ("embedding_size", ints), "--embedding-bag-size": ("embedding_bag_size", int),
+                 "--arch-mlp-bot": ("mlp_bot", ints), "--arch-mlp-top": ("mlp_top", ints),
+                 "--loss-threshold": ("loss_threshold", float), "--sigmoid-top": ("sigmoid_top", int),
+                 "--sigmoid-bot": ("sigmoid_bot", int), "--arch-interaction-op": ("arch_interaction_op", str),
+                 "--dataset": ("dataset_path", str), "--data-size": ("data_size", int),
+                 "-b": ("batch_size", int), "--batch-size": ("batch_size", int)}
+        i = 0
+        while i < len(argv):
+            if argv[i] in flags and i + 1 < len(argv):
+                name, conv = flags[argv[i]]
+                setattr(cfg, name, conv(argv[i + 1]))
+                i += 2
+            else:
+                i += 1
+        return cfg
 
 
 def dlrm_large(**kw) -> DLRMConfig:

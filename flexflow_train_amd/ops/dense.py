@@ -100,7 +100,7 @@ class LinearOp(OpImpl):
                   and K.gemmp_supported(g, W, False, True))
             if ok and _dact_fused_wins(g, W, pre2, act_p, db_p is not None):
                 dx = K.gemmp(g, W, trans_b=True, act=act_p, aux=pre2, act_bwd=True,
-                             dbias=db_p.reshape(-1) if db_p is not None else None)
+                             dbias=db_p.reshape(-1) if db_p is not None else None, variant=_dact_variant(act_p))
                 pctx.extra["grad_is_preact"] = True
                 return [dx.reshape(*dy.shape[:-1], W.shape[0])]
         if need_input_grad[0]:
@@ -116,6 +116,13 @@ class LinearOp(OpImpl):
 _DACT_CHOICE = {}
 
 
+def _dact_variant(act: str) -> int:
+    """The fused activation-gradient GEMM runs on gemmt (one wave per SIMD,
+    128x128 wave tiles) for the activations it instantiates, else on gemmp."""
+    from .gemm import _GT_VARIANT
+    return _GT_VARIANT if _GT_VARIANT and act in ("relu", "gelu") else 0
+
+
 def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:
     """Measure once per shape (outside graph capture): the fused input-gradient
     GEMM with the activation-gradient + bias-gradient epilogue (gemmp) against
@@ -129,7 +136,7 @@ def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:
     from .gemm import _time
     db = torch.zeros(W.shape[0], device=g.device, dtype=torch.float32)
     fused = _time(lambda: K.gemmp(g, W, trans_b=True, act=act, aux=pre, act_bwd=True,
-                                  dbias=db if has_bias else None))
+                                  dbias=db if has_bias else None, variant=_dact_variant(act)))
     dx = matmul(g, W, trans_b=True)   # settles the autotuner's pick first
     plain = _time(lambda: (matmul(g, W, trans_b=True),
                            K.colsum_act(dx, pre, act, db if has_bias else None, write_dx=True)))

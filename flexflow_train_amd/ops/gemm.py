@@ -12,8 +12,10 @@ torch.mm / addmm) is the plain library GEMM.  ``FF_GEMM`` selects:
   in the library epilogue), the 128² register-staged MFMA kernel, the
   256² LDS-DMA kernel (csrc/kernels/gemm256.hip) and the phase-pipelined
   persistent 256² kernel (``p:s``, csrc/kernels/gemmp.hip, fused bias /
-  activation / pre-activation epilogue) at several split-K degrees (the
-  long-K weight-gradient GEMMs are where split-K wins);
+  activation / pre-activation epilogue) and the one-wave-per-SIMD 128x128
+  wave-tile kernel (``t:s``, csrc/kernels/gemmt.hip, same epilogues) at
+  several split-K degrees (the long-K weight-gradient GEMMs are where split-K
+  and gemmt win); the 256² LDS-DMA kernel only with FF_GEMM256=1;
 * ``hip``: always the MFMA kernel; ``blas``: always hipBLASLt.
 
 On CPU everything is a torch matmul in the compute dtype.
@@ -155,6 +157,21 @@ def _gp(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
                    splits=splits)
 
 
+# gemmp.hip family variant of the one-wave-per-SIMD kernel (gemmt.hip): 3 =
+# both operands staged through registers, 4 = B by LDS-DMA
+_GT_VARIANT = int(os.environ.get("FF_GEMMT_VARIANT", "3"))
+
+
+def _gt(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
+    return K.gemmp(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
+                   splits=splits, variant=_GT_VARIANT)
+
+
+def _gt_ok(bias, act, out, beta, pre) -> bool:
+    """gemmt instantiates the activation epilogues for none / relu / gelu."""
+    return _gp_ok(bias, act, out, beta, pre) and act in ("none", "relu", "gelu")
+
+
 def _gp_ok(bias, act, out, beta, pre) -> bool:
     """Epilogues gemmp implements: plain (alpha/beta, bf16 or fp32 out) or
     bias/activation/pre-activation into a fresh bf16 output."""
@@ -204,7 +221,7 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
     """name -> callable(a, b, ta, tb, bias, act, out, beta, pre) tried by the autotuner."""
     c = {"hip": _hip, "blas": _blas}
     c.update(_lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre))
-    if os.environ.get("FF_GEMM256", "1") != "0" and K.gemm256_supported(a, b, trans_a, trans_b):
+    if os.environ.get("FF_GEMM256", "0") != "0" and K.gemm256_supported(a, b, trans_a, trans_b):
         M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
         N = b.shape[0] if trans_b else b.shape[1]
         plain = bias is None and act == "none" and pre is None
@@ -224,6 +241,8 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
             splits |= {s for s in (d // 2, d, d * 2) if 1 <= s <= max(1, Kd // 512) and (Kd // 64) % s == 0}
         for s in sorted(splits):
             c[f"p:{s}"] = (lambda s_: (lambda *args: _gp(*args, splits=s_)))(s)
+            if _GT_VARIANT and _gt_ok(bias, act, out, beta, pre):
+                c[f"t:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_)))(s)
     return c
 
 
@@ -283,7 +302,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
         choice = "hip"
-    if choice.startswith("p:") and not K.gemmp_supported(a, b, trans_a, trans_b):
+    if choice[:2] in ("p:", "t:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -303,6 +322,8 @@ def _resolve(name: str):
         return lambda *args: _lt(*args, algo=int(arg))
     if kind == "p":
         return lambda *args: _gp(*args, splits=int(arg))
+    if kind == "t":
+        return lambda *args: _gt(*args, splits=int(arg))
     return lambda *args: _hip256(*args, splits=int(arg))
 
 

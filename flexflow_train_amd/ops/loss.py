@@ -181,8 +181,6 @@ class PerfMetrics:
         pm.mae_loss = v[M_ABSERR] / (n * max(1, out_dim))
         return pm
 
-    def get_accuracy(self) -> float:
-        return 100.0 * self.train_correct / max(1, self.train_all)
 
     def get_throughput(self) -> float:
         return self.train_all / max(1e-9, self.current_time - self.start_time)

@@ -117,6 +117,8 @@ class ParamPiece:
     trainable: bool
     consumer_op: str = ""
     consumer_attrs: dict = dataclasses.field(default_factory=dict)
+    # kernel regularizer of a LINEAR weight: ("l1" | "l2", lambda)
+    regularizer: Optional[Tuple[str, float]] = None
     offset: int = 0
     numel: int = 0
     flat_id: int = 0
@@ -244,6 +246,10 @@ class Executor:
                                logical_shape=tuple(lay.sizes), initializer=init, group=(), trainable=bool(
                                    pcg.create_grad(C.ValueRef(n, 0))),
                                consumer_op=optype[cnode], consumer_attrs=cattrs)
+            reg = str(cattrs.get("regularizer", "none"))
+            if (optype[cnode] == "LINEAR" and reg in ("l1", "l2") and float(cattrs.get("regularizer_lambda", 0.0)) != 0
+                    and [(w.node, w.idx) for w in pcg.layer_weights(cnode)][:1] == [tuple(t)]):
+                piece.regularizer = (reg, float(cattrs["regularizer_lambda"]))
             self.params.append(piece)
             self.param_of_value[t] = piece
             folded.add(n)
@@ -1093,6 +1099,8 @@ class Executor:
             if sync:
                 for p in s.weights:
                     if p.final_step == i and p.trainable:
+                        if p.regularizer is not None:
+                            self._add_regularizer_grad(p)
                         self._param_done(p)
         self._saved = {}
         self._env = {}
@@ -1163,6 +1171,19 @@ class Executor:
             if len(f["group"]) > 1 and self.dist.distributed:
                 self._wg_join()
             self._launch_bucket(f, b)
+
+    def _add_regularizer_grad(self, p: ParamPiece):
+        """Kernel regularizer (reference Linear backward, linear_kernels.cu:258):
+        dW += lambda * W (L2) or lambda * sign(W) (L1).  Added once per step
+        to the summed gradient: each of the |group| replicas adds 1/|group| of
+        it before the all-reduce sums them."""
+        kind, lam = p.regularizer
+        lam = lam / max(1, len(p.group))
+        w = p.master.view(p.grad.shape)
+        if kind == "l2":
+            p.grad.add_(w.to(p.grad.dtype), alpha=lam)
+        else:
+            p.grad.add_(torch.sign(w).to(p.grad.dtype), alpha=lam)
 
     def _debug_sync(self, s, phase: str):
         """sync_debug: wait for the operator's kernels; a fault surfaces here,

@@ -8,7 +8,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXAMPLES = ["native/mnist_mlp.py", "native/cifar10_cnn.py", "native/multi_head_attention.py", "native/bert_proxy.py",
-            "native/dlrm.py", "keras/seq_mnist_mlp.py", "keras/func_cifar10_cnn.py", "pytorch/mnist_mlp_torch.py"]
+            "native/dlrm.py", "pytorch/mnist_mlp_torch.py"]
+# every keras example (reference: examples/python/keras/*.py)
+KERAS = sorted(f for f in os.listdir(os.path.join(ROOT, "examples", "keras"))
+               if f.endswith(".py") and not f.startswith("_") and f != "accuracy.py")
+EXAMPLES += [f"keras/{f}" for f in KERAS]
 
 
 @pytest.mark.parametrize("script", EXAMPLES)

@@ -208,3 +208,39 @@ def test_activation_value_and_gradient_access():
     np.testing.assert_allclose(hv, np.maximum(X @ W + b, 0), rtol=1e-4, atol=1e-5)
     g = h.get_gradients(m)
     assert g.shape == (4, 6) and np.isfinite(g).all() and np.abs(g).sum() > 0
+
+
+@pytest.mark.parametrize("kind", ["l2", "l1"])
+def test_dense_kernel_regularizer(kind):
+    """dense(kernel_regularizer=...) adds lambda*W (L2) / lambda*sign(W) (L1)
+    to the kernel gradient (reference linear_kernels.cu:258); the bias and the
+    other layer are untouched."""
+    import numpy as np
+    from flexflow_train_amd.core import ActiMode, DataType, FFConfig, FFModel, LossType, SGDOptimizer
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((4, 8)).astype(np.float32)
+    Y = np.array([[0], [1], [2], [1]], np.int32)
+    lr, lam = 0.5, 0.1
+
+    def run(reg):
+        cfg = FFConfig()
+        cfg.batch_size = 4
+        m = FFModel(cfg)
+        x = m.create_tensor([4, 8], DataType.DT_FLOAT, name="x")
+        h = m.dense(x, 6, ActiMode.AC_MODE_RELU, kernel_regularizer=reg, name="h")
+        m.softmax(m.dense(h, 3, name="o"))
+        m.compile(optimizer=SGDOptimizer(m, lr=lr), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY)
+        layer = m.get_layer_by_name("h")
+        w0 = layer.get_weight_tensor().get_weights(m).copy()
+        m.fit(x=X, y=Y, epochs=1)
+        return (w0, layer.get_weight_tensor().get_weights(m), layer.get_bias_tensor().get_weights(m),
+                m.get_layer_by_name("o").get_weight_tensor().get_weights(m))
+
+    w0a, wa, ba, oa = run(None)
+    w0b, wb, bb, ob = run((kind, lam))
+    np.testing.assert_array_equal(w0a, w0b)
+    step = lam * (w0a if kind == "l2" else np.sign(w0a))
+    np.testing.assert_allclose(wb, wa - lr * step, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(bb, ba, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(ob, oa, rtol=1e-6, atol=1e-7)
