@@ -77,6 +77,8 @@ class Tensor:
 
     @property
     def dims(self):
+        if self.vref is None:   # the label tensor: no graph value
+            return tuple(getattr(self, "_dims", ()))
         return tuple(self.model.cg.shape(self.vref).dims)
 
     @property
@@ -209,7 +211,14 @@ class Layer:
         return len(self.model.cg.layer_data_inputs(self.node))
 
     def get_input_by_id(self, i):
-        return Tensor(self.model, self.model.cg.layer_data_inputs(self.node)[i])
+        v = self.model.cg.layer_data_inputs(self.node)[i]
+        for t in self.model._inputs:   # a model input: the same tensor object (its feed name)
+            if t.vref.node == v.node and t.vref.idx == v.idx:
+                return t
+        return Tensor(self.model, v)
+
+    def get_input_tensor_by_id(self, i):
+        return self.get_input_by_id(i)
 
     def get_input_tensor(self):
         return self.get_input_by_id(0)
@@ -618,8 +627,9 @@ class FFModel:
             self._init_local_backing(loss_type)
         # label tensor (reference: created in compile, [batch, 1] int32 for sparse CE)
         out_lay = self.executor.value_layout[self.executor.loss_value]
-        if loss_type is not None and normalize_loss_type(loss_type) == "sparse_categorical_crossentropy":
-            ldims = list(out_lay.sizes[:-1]) + [1]
+        if loss_type is not None:
+            sparse = normalize_loss_type(loss_type) == "sparse_categorical_crossentropy"
+            ldims = list(out_lay.sizes[:-1]) + [1] if sparse else list(out_lay.sizes)
             self._label_tensor = Tensor(self, None, "label")
             self._label_tensor._dims = tuple(ldims)
         return self
@@ -993,10 +1003,10 @@ class FFModel:
         return "SPARSE" in str(getattr(lt, "name", lt)).upper()
 
     def _label_dims(self):
-        bs = self.ffconfig.batch_size
-        if self._sparse_labels() or not self._layers:
-            return [bs, 1]
-        return list(self._layers[-1].get_output_tensor().dims)
+        lt = self._label_tensor
+        if lt is not None and getattr(lt, "_dims", None):
+            return list(lt._dims)
+        return [self.ffconfig.batch_size, 1]
 
     def _get_value(self, t: Tensor):
         """Latest value of a tensor as numpy (this rank's piece): a pending
