@@ -140,7 +140,7 @@ class PyTorchModel:
                 _function(em, node)
             elif node.op == "get_attr":
                 raise NotImplementedError(f"get_attr {node.target} (module attributes are not supported)")
-        return outputs[0] if len(outputs) == 1 else outputs
+        return list(outputs)   # a list, as the reference's torch_to_ff / file_to_ff return
 
     def _module(self, em: _Emitter, node, mod: nn.Module):
         ins = _args_nodes(node.args)
@@ -416,7 +416,7 @@ def string_to_ff(lines: Sequence[str], ffmodel, input_tensors: Sequence):
             env[name] = x[int(a[0])]
         else:
             raise NotImplementedError(f".ff op {op}")
-    return out[0] if len(out) == 1 else out
+    return list(out)
 
 
 def copy_weights(ffmodel, torch_weights: Optional[Dict] = None):
