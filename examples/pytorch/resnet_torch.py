@@ -3,11 +3,20 @@ is not installed here) and the export of ResNet-18 to resnet18.ff
 (reference: examples/python/pytorch/resnet_torch.py)."""
 from typing import List, Optional, Type, Union
 
+import os
+import sys
+
 import torch
 import torch.nn as nn
-from _common import ff_path
 
-from flexflow.torch.model import PyTorchModel
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from flexflow.torch.model import PyTorchModel  # noqa: E402
+
+
+def ff_path(name):
+    d = os.environ.get("FF_EXAMPLE_DIR", ".")
+    os.makedirs(d, exist_ok=True)
+    return os.path.join(d, name)
 
 
 def conv3x3(cin, cout, stride=1, groups=1):

@@ -281,6 +281,29 @@ def encode_model(nodes: List[Node], initializers: Dict[str, np.ndarray], inputs:
 
 
 # -------------------------------------------------------------------- importer
+def _fuse_matmul_add(nodes: List[Node], consts, shapes) -> List[Node]:
+    """MatMul(x, W) whose only consumer is Add(., bias) with a constant 1-D
+    bias -> one Gemm(x, W, bias) (the keras2onnx form of a Dense layer)."""
+    users: Dict[str, List[Node]] = {}
+    for n in nodes:
+        for i in n.inputs:
+            users.setdefault(i, []).append(n)
+    out, skip = [], set()
+    for n in nodes:
+        if id(n) in skip:
+            continue
+        if n.op_type == "MatMul" and len(users.get(n.outputs[0], [])) == 1:
+            u = users[n.outputs[0]][0]
+            other = [i for i in u.inputs if i != n.outputs[0]]
+            if (u.op_type == "Add" and len(other) == 1 and
+                    (other[0] in consts and consts[other[0]].ndim == 1 or len(shapes.get(other[0], [])) == 1)):
+                out.append(Node("Gemm", [n.inputs[0], n.inputs[1], other[0]], u.outputs, n.name or u.name, {}))
+                skip.add(id(u))
+                continue
+        out.append(n)
+    return out
+
+
 class ONNXModel:
     def __init__(self, model):
         if isinstance(model, (bytes, bytearray)):
@@ -293,17 +316,30 @@ class ONNXModel:
         self.weights: Dict[str, Tuple[str, np.ndarray]] = {}
 
     def apply(self, ffmodel, input_tensors):
+        """Replay the graph into ``ffmodel``.  ``input_tensors``: a list (the
+        graph's non-initializer inputs in order) or a {input name: tensor}
+        dict as in the reference (``apply(ffmodel, {"input.1": t})``).
+        Returns the output tensor (one output) or the list of them."""
         g = self.graph
-        env: Dict[str, object] = {}
         consts: Dict[str, np.ndarray] = dict(g.initializers)
-        real_inputs = [n for (n, _, _) in g.inputs if n not in consts]
-        for n, t in zip(real_inputs, input_tensors):
-            env[n] = t
+        # parameters exported as graph inputs (export_params=False) are known
+        # by shape only: FlexFlow initialises them itself
+        self.shapes: Dict[str, List[int]] = {n: list(d) for (n, d, _) in g.inputs}
+        if isinstance(input_tensors, dict):
+            env: Dict[str, object] = dict(input_tensors)
+        else:
+            real_inputs = [n for (n, _, _) in g.inputs if n not in consts]
+            env = dict(zip(real_inputs, input_tensors))
         pads: Dict[str, Tuple[str, List[int]]] = {}
-        for node in g.nodes:
+        for node in _fuse_matmul_add(g.nodes, consts, self.shapes):
             self._handle(ffmodel, node, env, consts, pads)
         outs = [env[n] for (n, _, _) in g.outputs]
         return outs[0] if len(outs) == 1 else outs
+
+    def _shape(self, consts, name) -> List[int]:
+        if name in consts:
+            return list(consts[name].shape)
+        return list(self.shapes[name])
 
     def _handle(self, ff, node: Node, env, consts, pads):
         op, a, name = node.op_type, node.attrs, node.name or node.outputs[0]
@@ -349,11 +385,14 @@ class ONNXModel:
             env[o] = ff.pool2d(x, h, w, 1, 1, 0, 0, PoolType.POOL_AVG, name=name)
         elif op == "BatchNormalization":
             env[o] = ff.batch_norm(x, False, name=name)
-            self.weights[name + ".gamma"] = ("copy", const(1))
-            self.weights[name + ".beta"] = ("copy", const(2))
+            if node.inputs[1] in consts:
+                self.weights[name + ".gamma"] = ("copy", const(1))
+            if node.inputs[2] in consts:
+                self.weights[name + ".beta"] = ("copy", const(2))
         elif op == "Conv":
-            w = const(1)
-            k = a.get("kernel_shape", list(w.shape[2:]))
+            w = consts.get(node.inputs[1])
+            wshape = self._shape(consts, node.inputs[1])
+            k = a.get("kernel_shape", wshape[2:])
             s = a.get("strides", [1, 1])
             p = list(a.get("pads", [0, 0, 0, 0]))
             if node.inputs[0] in pads:
@@ -361,23 +400,28 @@ class ONNXModel:
                 pp = pads[node.inputs[0]][1]
                 p = [p[0] + pp[2], p[1] + pp[3]]
             bias = len(node.inputs) > 2
-            env[o] = ff.conv2d(x, w.shape[0], k[0], k[1], s[0], s[1], p[0], p[1], ActiMode.AC_MODE_NONE,
+            env[o] = ff.conv2d(x, wshape[0], k[0], k[1], s[0], s[1], p[0], p[1], ActiMode.AC_MODE_NONE,
                                int(a.get("group", 1)), bias, name=name)
-            self.weights[name + ".kernel"] = ("copy", w)
-            if bias:
+            if w is not None:
+                self.weights[name + ".kernel"] = ("copy", w)
+            if bias and node.inputs[2] in consts:
                 self.weights[name + ".bias"] = ("copy", const(2))
         elif op == "Dropout":
             env[o] = ff.dropout(x, float(a.get("ratio", 0.5)), 0, name=name)
         elif op == "Flatten":
             env[o] = ff.flat(x, name=name)
         elif op in ("Gemm", "MatMul"):
-            w = const(1)
-            if op == "Gemm" and int(a.get("transB", 0)):
-                w = w.T
+            w = consts.get(node.inputs[1])
+            wshape = self._shape(consts, node.inputs[1])
+            tb = op == "Gemm" and int(a.get("transB", 0))
+            if tb:
+                w = None if w is None else w.T
+                wshape = wshape[::-1]
             bias = op == "Gemm" and len(node.inputs) > 2
-            env[o] = ff.dense(x, w.shape[1], ActiMode.AC_MODE_NONE, bias, name=name)
-            self.weights[name + ".kernel"] = ("copy", np.ascontiguousarray(w))
-            if bias:
+            env[o] = ff.dense(x, wshape[1], ActiMode.AC_MODE_NONE, bias, name=name)
+            if w is not None:
+                self.weights[name + ".kernel"] = ("copy", np.ascontiguousarray(w))
+            if bias and node.inputs[2] in consts:
                 self.weights[name + ".bias"] = ("copy", const(2))
         elif op in ("Relu", "Sigmoid", "Tanh", "Identity"):
             fn = {"Relu": ff.relu, "Sigmoid": ff.sigmoid, "Tanh": ff.tanh, "Identity": ff.identity}[op]
@@ -425,3 +469,268 @@ class ONNXModel:
         for pname, (_, arr) in self.weights.items():
             if pname in names:
                 ex.set_parameter(pname, torch.as_tensor(np.asarray(arr, dtype=np.float32)))
+
+
+class ONNXModelKeras(ONNXModel):
+    """A keras-exported ONNX file (reference onnx/model.py ONNXModelKeras:
+    Dense layers as MatMul + Add, channels-first images)."""
+
+    def __init__(self, model, ffconfig=None, ffmodel=None):
+        super().__init__(model)
+        self.ffconfig, self.ffmodel = ffconfig, ffmodel
+
+
+# ------------------------------------------------------------------ exporters
+def _save(data: bytes, path):
+    if path:
+        with open(path, "wb") as f:
+            f.write(data)
+    return data
+
+
+def export_torch(module, example_inputs, path: Optional[str] = None, export_params: bool = True,
+                 input_names: Optional[List[str]] = None) -> bytes:
+    """nn.Module -> ONNX (the ``torch.onnx.export`` role; the ``onnx``
+    package is not available here).  torch.fx traces the module; leaf
+    modules Linear, Conv2d, BatchNorm2d, ReLU, Sigmoid, Tanh, MaxPool2d,
+    AvgPool2d, AdaptiveAvgPool2d(1), Flatten, Softmax, Dropout, Identity and
+    the functions add / mul / sub / cat / flatten / relu / softmax / view /
+    reshape map to ONNX nodes.  Inputs are named ``input.1``, ``input.2``,
+    ... as torch's exporter names them.  ``export_params=False`` lists the
+    parameters as shaped graph inputs instead of initializers."""
+    import operator
+
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+    from torch.fx.passes.shape_prop import ShapeProp
+
+    gm = torch.fx.symbolic_trace(module)
+    ex = tuple(example_inputs) if isinstance(example_inputs, (tuple, list)) else (example_inputs,)
+    was = module.training
+    module.eval()
+    with torch.no_grad():
+        ShapeProp(gm).propagate(*ex)
+    module.train(was)
+    nodes: List[Node] = []
+    inits: Dict[str, np.ndarray] = {}
+    param_inputs: List[Tuple[str, List[int]]] = []
+    inputs: List[Tuple[str, List[int]]] = []
+    outputs: List[Tuple[str, List[int]]] = []
+    names: Dict[object, str] = {}
+
+    def shp(n):
+        return [int(d) for d in n.meta["tensor_meta"].shape]
+
+    def param(pname, t):
+        arr = t.detach().cpu().float().numpy()
+        if export_params:
+            inits[pname] = np.ascontiguousarray(arr)
+        else:
+            param_inputs.append((pname, list(arr.shape)))
+        return pname
+
+    def emit(op, ins, n, **attrs):
+        names[n] = n.name
+        nodes.append(Node(op, ins, [n.name], n.name, attrs))
+
+    def pair(v):
+        return list(v) if isinstance(v, (tuple, list)) else [v, v]
+
+    for n in gm.graph.nodes:
+        if n.op == "placeholder":
+            nm = (input_names or [])[len(inputs)] if input_names and len(inputs) < len(input_names) else \
+                f"input.{len(inputs) + 1}"
+            names[n] = nm
+            inputs.append((nm, shp(n)))
+        elif n.op == "call_module":
+            m = gm.get_submodule(n.target)
+            x = names[n.args[0]]
+            if isinstance(m, nn.Linear):
+                ins = [x, param(f"{n.target}.weight", m.weight)]
+                if m.bias is not None:
+                    ins.append(param(f"{n.target}.bias", m.bias))
+                emit("Gemm", ins, n, transB=1)
+            elif isinstance(m, nn.Conv2d):
+                if m.padding_mode != "zeros" or isinstance(m.padding, str):
+                    raise NotImplementedError("Conv2d: explicit zero padding only")
+                ins = [x, param(f"{n.target}.weight", m.weight)]
+                if m.bias is not None:
+                    ins.append(param(f"{n.target}.bias", m.bias))
+                ph, pw = pair(m.padding)
+                emit("Conv", ins, n, kernel_shape=pair(m.kernel_size), strides=pair(m.stride),
+                     pads=[ph, pw, ph, pw], group=int(m.groups), dilations=pair(m.dilation))
+            elif isinstance(m, nn.BatchNorm2d):
+                ins = [x, param(f"{n.target}.weight", m.weight), param(f"{n.target}.bias", m.bias),
+                       param(f"{n.target}.running_mean", m.running_mean),
+                       param(f"{n.target}.running_var", m.running_var)]
+                emit("BatchNormalization", ins, n, epsilon=float(m.eps), momentum=float(1 - (m.momentum or 0.1)))
+            elif isinstance(m, (nn.ReLU, nn.Sigmoid, nn.Tanh, nn.Identity)):
+                emit({nn.ReLU: "Relu", nn.Sigmoid: "Sigmoid", nn.Tanh: "Tanh", nn.Identity: "Identity"}[type(m)],
+                     [x], n)
+            elif isinstance(m, (nn.MaxPool2d, nn.AvgPool2d)):
+                if m.ceil_mode:
+                    raise NotImplementedError("pooling with ceil_mode")
+                ph, pw = pair(m.padding)
+                emit("MaxPool" if isinstance(m, nn.MaxPool2d) else "AveragePool", [x], n,
+                     kernel_shape=pair(m.kernel_size), strides=pair(m.stride or m.kernel_size), pads=[ph, pw, ph, pw])
+            elif isinstance(m, nn.AdaptiveAvgPool2d):
+                if pair(m.output_size) != [1, 1]:
+                    raise NotImplementedError("AdaptiveAvgPool2d to a size other than 1")
+                emit("GlobalAveragePool", [x], n)
+            elif isinstance(m, nn.Flatten):
+                emit("Flatten", [x], n, axis=int(m.start_dim))
+            elif isinstance(m, nn.Softmax):
+                emit("Softmax", [x], n, axis=int(m.dim if m.dim is not None else -1))
+            elif isinstance(m, nn.Dropout):
+                emit("Dropout", [x], n, ratio=float(m.p))
+            else:
+                raise NotImplementedError(f"export_torch: module {type(m).__name__}")
+        elif n.op in ("call_function", "call_method"):
+            t = n.target
+            a0 = n.args[0] if n.args else None
+            if t in (operator.add, operator.iadd, torch.add, "add", "add_"):
+                emit("Add", [names[a0], names[n.args[1]]], n)
+            elif t in (operator.mul, torch.mul, "mul"):
+                emit("Mul", [names[a0], names[n.args[1]]], n)
+            elif t in (operator.sub, torch.sub, "sub"):
+                emit("Sub", [names[a0], names[n.args[1]]], n)
+            elif t is torch.cat:
+                dim = n.args[1] if len(n.args) > 1 else n.kwargs.get("dim", 0)
+                emit("Concat", [names[v] for v in a0], n, axis=int(dim))
+            elif t in (torch.flatten, "flatten"):
+                emit("Flatten", [names[a0]], n, axis=int(n.args[1] if len(n.args) > 1 else n.kwargs.get("start_dim", 0)))
+            elif t in (torch.relu, F.relu, "relu"):
+                emit("Relu", [names[a0]], n)
+            elif t in (F.softmax, torch.softmax, "softmax"):
+                dim = n.args[1] if len(n.args) > 1 else n.kwargs.get("dim", -1)
+                emit("Softmax", [names[a0]], n, axis=int(dim))
+            elif t in ("view", "reshape", torch.reshape):
+                out = shp(n)
+                cname = f"{n.name}.shape"
+                inits[cname] = np.asarray([0] + out[1:], dtype=np.int64)   # 0: keep the batch dimension
+                emit("Reshape", [names[a0], cname], n)
+            else:
+                raise NotImplementedError(f"export_torch: function {t}")
+        elif n.op == "output":
+            res = n.args[0]
+            for r in (res if isinstance(res, (tuple, list)) else [res]):
+                outputs.append((names[r], shp(r)))
+        else:
+            raise NotImplementedError(f"export_torch: {n.op} {n.target}")
+    return _save(encode_model(nodes, inits, inputs + param_inputs, outputs), path)
+
+
+def export_keras(model, path: Optional[str] = None, export_params: bool = True) -> bytes:
+    """flexflow.keras Model -> ONNX in keras2onnx's form (Dense = MatMul +
+    Add, activations as their own nodes, channels-first images; the
+    ``keras2onnx.convert_keras`` role).  Inputs are named ``input_1``,
+    ``input_2``, ...  Weights come from the compiled model when
+    ``export_params`` (the model must have been compiled)."""
+    from .keras.layers import (Activation, Add, AveragePooling2D, BatchNormalization, Concatenate, Conv2D, Dense,
+                               Dropout, Flatten, InputLayer, MaxPooling2D, Multiply, Permute, Reshape, Subtract)
+    from .keras.models import _graph_order
+
+    ff = model.ffmodel if export_params else None
+    if export_params and ff is None:
+        raise RuntimeError("export_keras: compile the model first (or pass export_params=False)")
+    nodes: List[Node] = []
+    inits: Dict[str, np.ndarray] = {}
+    extra_inputs: List[Tuple[str, List[int]]] = []
+    names: Dict[int, str] = {}
+    acts = {"relu": "Relu", "sigmoid": "Sigmoid", "tanh": "Tanh", "softmax": "Softmax"}
+
+    def dims(t):
+        return [1 if d is None else int(d) for d in t.shape]
+
+    def weights(layer, shapes):
+        if ff is None:
+            ws = [np.zeros(s, np.float32) for s in shapes]
+        else:
+            ws = [np.asarray(w, np.float32) for w in layer.get_weights(ff)]
+        out = []
+        for i, w in enumerate(ws):
+            nm = f"{layer.name}/w{i}"
+            if export_params:
+                inits[nm] = np.ascontiguousarray(w)
+            else:
+                extra_inputs.append((nm, list(w.shape)))
+            out.append(nm)
+        return out
+
+    inputs = []
+    for i, t in enumerate(model.inputs):
+        names[id(t)] = f"input_{i + 1}"
+        inputs.append((names[id(t)], dims(t)))
+    for t in _graph_order(model.outputs):
+        if id(t) in names:
+            continue
+        L = t.layer
+        ins = [names[id(i)] for i in t.inputs]
+        o = f"{L.name}/out{len([1 for n in nodes if n.name.startswith(L.name)])}"
+        act = None
+        if isinstance(L, Dense):
+            fin = t.inputs[0].shape[-1]
+            w = weights(L, [(fin, L.units)] + ([(L.units,)] if L.use_bias else []))
+            mm = o + "/matmul"
+            nodes.append(Node("MatMul", [ins[0], w[0]], [mm if L.use_bias else o], L.name, {}))
+            if L.use_bias:
+                nodes.append(Node("Add", [mm, w[1]], [o], L.name + "/bias", {}))
+            act = L.activation
+        elif isinstance(L, Conv2D):
+            cin = t.inputs[0].shape[1]
+            w = weights(L, [(L.filters, cin // L.groups, *L.k)] + ([(L.filters,)] if L.use_bias else []))
+            ph, pw = L._pad()
+            nodes.append(Node("Conv", [ins[0]] + w, [o], L.name,
+                              {"kernel_shape": list(L.k), "strides": list(L.s), "pads": [ph, pw, ph, pw],
+                               "group": int(L.groups)}))
+            act = L.activation
+        elif isinstance(L, (MaxPooling2D, AveragePooling2D)):
+            nodes.append(Node("MaxPool" if isinstance(L, MaxPooling2D) else "AveragePool", ins, [o], L.name,
+                              {"kernel_shape": list(L.p), "strides": list(L.s),
+                               "pads": [L.pad[0], L.pad[1], L.pad[0], L.pad[1]]}))
+        elif isinstance(L, Flatten):
+            nodes.append(Node("Flatten", ins, [o], L.name, {"axis": 1}))
+        elif isinstance(L, Activation):
+            if L.activation in (None, "linear"):
+                nodes.append(Node("Identity", ins, [o], L.name, {}))
+            else:
+                nodes.append(Node(acts[L.activation], ins, [o], L.name,
+                                  {"axis": -1} if L.activation == "softmax" else {}))
+        elif isinstance(L, Concatenate):
+            nodes.append(Node("Concat", ins, [o], L.name, {"axis": int(L.axis)}))
+        elif isinstance(L, (Add, Subtract, Multiply)):
+            op = {Add: "Add", Subtract: "Sub", Multiply: "Mul"}[type(L)]
+            cur = ins[0]
+            for j, x in enumerate(ins[1:]):
+                nxt = o if j == len(ins) - 2 else f"{o}/{j}"
+                nodes.append(Node(op, [cur, x], [nxt], f"{L.name}/{j}", {}))
+                cur = nxt
+        elif isinstance(L, Dropout):
+            nodes.append(Node("Dropout", ins, [o], L.name, {"ratio": float(L.rate)}))
+        elif isinstance(L, BatchNormalization):
+            c = t.inputs[0].shape[1]
+            w = weights(L, [(c,), (c,)])
+            mean, var = f"{L.name}/mean", f"{L.name}/var"
+            inits[mean], inits[var] = np.zeros(c, np.float32), np.ones(c, np.float32)
+            nodes.append(Node("BatchNormalization", [ins[0], w[0], w[1], mean, var], [o], L.name,
+                              {"epsilon": float(L.epsilon)}))
+        elif isinstance(L, Reshape):
+            cname = f"{L.name}/shape"
+            inits[cname] = np.asarray([0] + list(t.shape[1:]), np.int64)
+            nodes.append(Node("Reshape", [ins[0], cname], [o], L.name, {}))
+        elif isinstance(L, Permute):
+            nodes.append(Node("Transpose", ins, [o], L.name, {"perm": list(L.perm)}))
+        elif isinstance(L, InputLayer):
+            raise ValueError(f"export_keras: {L.name} is not a model input")
+        else:
+            raise NotImplementedError(f"export_keras: layer {type(L).__name__}")
+        if act not in (None, "linear"):
+            pre = o
+            o = pre + "/" + act
+            nodes[-1].outputs = [pre]
+            nodes.append(Node(acts[act], [pre], [o], f"{L.name}/{act}", {"axis": -1} if act == "softmax" else {}))
+        names[id(t)] = o
+    outputs = [(names[id(t)], dims(t)) for t in model.outputs]
+    return _save(encode_model(nodes, inits, inputs + extra_inputs, outputs), path)
+

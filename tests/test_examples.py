@@ -11,14 +11,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the *_torch.py / export_* scripts only write a .ff file
 EXAMPLES = sorted(f"pytorch/{f}" for f in os.listdir(os.path.join(ROOT, "examples", "pytorch"))
                   if f.endswith(".py") and not f.startswith("_"))
+# every ONNX example (reference: examples/python/onnx/*.py); *_pt / *_keras export
+EXAMPLES += sorted(f"onnx/{f}" for f in os.listdir(os.path.join(ROOT, "examples", "onnx"))
+                   if f.endswith(".py") and not f.startswith("_") and f != "accuracy.py")
 EXPORT_ONLY = {"pytorch/cifar10_cnn_torch.py", "pytorch/resnet_torch.py", "pytorch/torch_vision_torch.py",
-               "pytorch/export_regnet_fx.py"}
+               "pytorch/export_regnet_fx.py"} | {e for e in EXAMPLES if e.startswith("onnx/") and
+                                                 (e.endswith("_pt.py") or e.endswith("_keras.py"))}
 # every native example (reference: examples/python/native/*.py)
 EXAMPLES += sorted(f"native/{f}" for f in os.listdir(os.path.join(ROOT, "examples", "native"))
                    if f.endswith(".py") and not f.startswith("_") and f != "accuracy.py")
 # the 229 / 299-pixel CNNs run a couple of tiny batches on the CPU
 HEAVY = {"native/alexnet.py", "native/inception.py", "native/resnet.py", "keras/func_cifar10_alexnet.py",
-         "pytorch/resnet.py", "pytorch/regnet.py", "pytorch/torch_vision.py", "pytorch/resnet152_training.py"}
+         "pytorch/resnet.py", "pytorch/regnet.py", "pytorch/torch_vision.py", "pytorch/resnet152_training.py",
+         "onnx/alexnet.py", "onnx/resnet.py"}
 # every keras example (reference: examples/python/keras/*.py)
 KERAS = sorted(f for f in os.listdir(os.path.join(ROOT, "examples", "keras"))
                if f.endswith(".py") and not f.startswith("_") and f != "accuracy.py")
@@ -35,7 +40,7 @@ def test_example_runs(script, tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     if script in EXPORT_ONLY:
-        assert any(f.endswith(".ff") for f in os.listdir(tmp_path)), r.stdout[-2000:]
+        assert any(f.endswith((".ff", ".onnx")) for f in os.listdir(tmp_path)), r.stdout[-2000:]
     else:
         assert "THROUGHPUT" in r.stdout, r.stdout[-2000:]
 

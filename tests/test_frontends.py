@@ -244,3 +244,66 @@ def test_dense_kernel_regularizer(kind):
     np.testing.assert_allclose(wb, wa - lr * step, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(bb, ba, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(ob, oa, rtol=1e-6, atol=1e-7)
+
+
+def test_onnx_export_torch_roundtrip_matches_torch():
+    """export_torch (fx -> ONNX wire format) -> ONNXModel import -> same
+    forward as the torch module (weights carried as initializers)."""
+    import torch
+    import torch.nn as nn
+    from flexflow.core import DataType, FFConfig, FFModel, LossType, SGDOptimizer
+    from flexflow.onnx.model import ONNXModel, export_torch
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(3, 4, 3, padding=1)
+            self.pool = nn.MaxPool2d(2, 2)
+            self.fc = nn.Linear(4 * 4 * 4, 5)
+
+        def forward(self, x):
+            y = self.pool(torch.relu(self.conv(x)))
+            return torch.softmax(self.fc(torch.flatten(y, 1)), dim=-1)
+
+    torch.manual_seed(0)
+    net = Net().eval()
+    x = torch.randn(4, 3, 8, 8)
+    data = export_torch(net, x)
+    cfg = FFConfig()
+    cfg.batch_size = 4
+    ff = FFModel(cfg)
+    t = ff.create_tensor([4, 3, 8, 8], DataType.DT_FLOAT)
+    om = ONNXModel(data)
+    om.apply(ff, {"input.1": t})
+    ff.compile(optimizer=SGDOptimizer(ff, 0.0), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY)
+    om.copy_weights(ff)
+    out = ff.executor.forward({t.name: x}, training=False)
+    torch.testing.assert_close(out.float(), net(x), rtol=1e-4, atol=1e-5)
+
+
+def test_onnx_export_keras_roundtrip_matches_keras():
+    import numpy as np
+    from flexflow.core import DataType, FFConfig, FFModel, LossType, SGDOptimizer
+    from flexflow.keras.layers import Activation, Conv2D, Dense, Flatten, Input, MaxPooling2D
+    from flexflow.keras.models import Model
+    from flexflow.onnx.model import ONNXModelKeras, export_keras
+
+    inp = Input(shape=(3, 8, 8))
+    t = MaxPooling2D()(Conv2D(4, 3, padding="same", activation="relu")(inp))
+    out = Activation("softmax")(Dense(5)(Dense(6, activation="relu")(Flatten()(t))))
+    km = Model(inp, out)
+    km.compile(optimizer="sgd", loss="sparse_categorical_crossentropy", metrics=["accuracy"], batch_size=4)
+    data = export_keras(km)
+    cfg = FFConfig()
+    cfg.batch_size = 4
+    ff = FFModel(cfg)
+    x = ff.create_tensor([4, 3, 8, 8], DataType.DT_FLOAT)
+    om = ONNXModelKeras(data, cfg, ff)
+    om.apply(ff, {"input_1": x})
+    assert [n.op_type for n in om.graph.nodes].count("MatMul") == 2      # keras2onnx form, fused on import
+    ff.compile(optimizer=SGDOptimizer(ff, 0.0), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY)
+    om.copy_weights(ff)
+    xv = np.random.default_rng(0).standard_normal((4, 3, 8, 8)).astype(np.float32)
+    import torch
+    got = ff.executor.forward({x.name: torch.as_tensor(xv)}, training=False).float().numpy()
+    np.testing.assert_allclose(got, km.predict(xv), rtol=1e-4, atol=1e-5)
