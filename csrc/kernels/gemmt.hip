@@ -65,6 +65,7 @@ struct GemmTArgs {
   float alpha, beta;
   int act, act_bwd, out_f32, splits;
   unsigned bytesA, bytesB;
+  int dbg;   // ablation bits (timing experiments, tools/gemm_ablate.py)
 };
 
 // activation code (elementwise.hip numbering) fixed at compile time: a run-time
@@ -300,7 +301,10 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* l
 
 // STG: 0 = both operands staged through registers; 1 = B by LDS-DMA (issued
 // in phase B, two phases ahead of its first read), A through registers
-template <bool TA, bool TB, int EPI, int ACT, int STG>
+// DBG (timing ablations only, results are garbage): 1 = no global loads in
+// the loop, 2 = no LDS writes in the loop, 4 = no mid-tile barrier, 8 = no
+// epilogue
+template <bool TA, bool TB, int EPI, int ACT, int STG, int DBG = 0>
 __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kernel(
     GemmTArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUFT];  // the ONE LDS object
@@ -440,13 +444,15 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       for (int h = 0; h < (STG == 1 ? 1 : 2); ++h) {
         const int c = STG == 1 ? mb : 2 * mb + h;
         if (c < 8) {
-          *reinterpret_cast<i32x4t*>(nxt + stage_lds<TA>(c, tid)) = R[c];
-          R[c] = __builtin_amdgcn_raw_buffer_load_b128(rA, voA,
-                                                       __builtin_amdgcn_readfirstlane(ka + stage_soff<TA>(g.lda, c)), 0);
+          if (!(DBG & 2)) *reinterpret_cast<i32x4t*>(nxt + stage_lds<TA>(c, tid)) = R[c];
+          if (!(DBG & 1))
+            R[c] = __builtin_amdgcn_raw_buffer_load_b128(
+                rA, voA, __builtin_amdgcn_readfirstlane(ka + stage_soff<TA>(g.lda, c)), 0);
         } else {
-          *reinterpret_cast<i32x4t*>(nxt + 2 * HALF + stage_lds<!TB>(c - 8, tid)) = R[c];
-          R[c] = __builtin_amdgcn_raw_buffer_load_b128(
-              rB, voB, __builtin_amdgcn_readfirstlane(kb + stage_soff<!TB>(g.ldb, c - 8)), 0);
+          if (!(DBG & 2)) *reinterpret_cast<i32x4t*>(nxt + 2 * HALF + stage_lds<!TB>(c - 8, tid)) = R[c];
+          if (!(DBG & 1))
+            R[c] = __builtin_amdgcn_raw_buffer_load_b128(
+                rB, voB, __builtin_amdgcn_readfirstlane(kb + stage_soff<!TB>(g.ldb, c - 8)), 0);
         }
       }
       // one memory instruction between MFMAs (an MFMA leaves the SIMD's issue
@@ -470,7 +476,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     __builtin_amdgcn_sched_barrier(0);
     if (STG == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // B of tile kt+1 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // k-step 1 reads + LDS writes done
-    __builtin_amdgcn_s_barrier();
+    if (!(DBG & 4)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // ---- phase B: k-step 1 (fa, fby) | read k-step 0 of tile kt+1 into (fa, fbx)
 #pragma unroll
@@ -491,11 +497,230 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  epilogue<EPI, ACT>(g, acc, m0, n0, split, wm, wn, lane);
+  if (!(DBG & 8)) epilogue<EPI, ACT>(g, acc, m0, n0, split, wm, wn, lane);
+}
+
+// Persistent form (variant 5): one workgroup per CU walks its work items
+// (tiles x K-splits) b, b + grid, ...; the K-tile stream runs on across item
+// boundaries, so the last two iterations of an item already stage the next
+// item's first two K-tiles and read its first fragments, and the epilogue of
+// item i overlaps the in-flight global loads of item i + 1 (no prologue
+// bubble per tile).  Requires L = K / 64 / splits >= 2.
+template <bool TA, bool TB, int EPI, int ACT>
+__global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_pers_kernel(
+    GemmTArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUFT];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int gm = (g.M + TM - 1) / TM, gn = (g.N + TN - 1) / TN;
+  const int nwg = gm * gn;
+  const int W = nwg * g.splits;
+  const int L = g.K / TK / g.splits;
+  const int per_group = GROUP * gn;
+  // item -> (m0, n0, split); item % 8 is the XCD the workgroup runs on
+  // (gridDim.x is a multiple of 8 or equal to W), so the bijective remap keeps
+  // the tiles that run together on one XCD adjacent in the grouped raster
+  auto geom = [&](int item, int& m0, int& n0, int& split) {
+    const int bid = xcd_remap(item, W);
+    split = bid / nwg;
+    const int t = bid % nwg;
+    const int first_m = (t / per_group) * GROUP;
+    const int gsize = min(gm - first_m, GROUP);
+    m0 = (first_m + (t % per_group) % gsize) * TM;
+    n0 = ((t % per_group) / gsize) * TN;
+  };
+
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.A), static_cast<short>(0), g.bytesA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.B), static_cast<short>(0), g.bytesB, 0x00020000);
+  const unsigned kstepA = TA ? static_cast<unsigned>(TK * g.lda * 2) : TK * 2u;
+  const unsigned kstepB = !TB ? static_cast<unsigned>(TK * g.ldb * 2) : TK * 2u;
+
+  int item = blockIdx.x;
+  int m0, n0, split;
+  geom(item, m0, n0, split);
+  int nitem = item + static_cast<int>(gridDim.x);
+  int m0n = m0, n0n = n0, splitn = split;
+  if (nitem < W) geom(nitem, m0n, n0n, splitn);
+  unsigned voA = stage_voff<TA>(g.lda, m0, tid), voB = stage_voff<!TB>(g.ldb, n0, tid);
+  unsigned voAn = stage_voff<TA>(g.lda, m0n, tid), voBn = stage_voff<!TB>(g.ldb, n0n, tid);
+  int kt0 = split * L, kt0n = splitn * L;
+
+  i32x4t R[16];
+  auto rdA = [&](const unsigned char* buf, int mb, int ks) -> bf16x8 {
+    return TA ? tr16(buf + wm * HALF, ks, mb * 16, lane) : row16(buf, wm * 128 + mb * 16, ks, lane);
+  };
+  auto rdB = [&](const unsigned char* buf, int nb, int ks) -> bf16x8 {
+    const unsigned char* b = buf + 2 * HALF;
+    return TB ? row16(b, wn * 128 + nb * 16, ks, lane) : tr16(b + wn * HALF, ks, nb * 16, lane);
+  };
+
+  f32x4t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4t{};
+  bf16x8 fa[8], fbx[8], fby[8];
+
+  // ---- prologue (first item only): K-tile 0 -> buffer 0, K-tile 1 in flight
+  {
+    const unsigned ka = static_cast<unsigned>(kt0) * kstepA, kb = static_cast<unsigned>(kt0) * kstepB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      R[i] = __builtin_amdgcn_raw_buffer_load_b128(rA, voA, __builtin_amdgcn_readfirstlane(ka + stage_soff<TA>(g.lda, i)),
+                                                   0);
+      R[8 + i] = __builtin_amdgcn_raw_buffer_load_b128(
+          rB, voB, __builtin_amdgcn_readfirstlane(kb + stage_soff<!TB>(g.ldb, i)), 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      *reinterpret_cast<i32x4t*>(smem + stage_lds<TA>(i, tid)) = R[i];
+      *reinterpret_cast<i32x4t*>(smem + 2 * HALF + stage_lds<!TB>(i, tid)) = R[8 + i];
+    }
+    const unsigned ka1 = ka + kstepA, kb1 = kb + kstepB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      R[i] = __builtin_amdgcn_raw_buffer_load_b128(rA, voA,
+                                                   __builtin_amdgcn_readfirstlane(ka1 + stage_soff<TA>(g.lda, i)), 0);
+      R[8 + i] = __builtin_amdgcn_raw_buffer_load_b128(
+          rB, voB, __builtin_amdgcn_readfirstlane(kb1 + stage_soff<!TB>(g.ldb, i)), 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[i] = rdA(smem, i, 0);
+    fbx[i] = rdB(smem, i, 0);
+  }
+
+  constexpr int NRD = (TA ? 2 : 1) + (TB ? 1 : 2);
+  int pos = 0;  // K-tiles this workgroup has consumed: the LDS buffer of K-tile kt is (pos + kt) & 1
+  for (;;) {
+    for (int kt = 0; kt < L; ++kt) {
+      unsigned char* cur = smem + ((pos + kt) & 1) * BUFT;
+      unsigned char* nxt = smem + ((pos + kt + 1) & 1) * BUFT;
+      // the loads issued now are for stream position kt + 2: this item's or the next one's
+      const bool nx = kt + 2 >= L;
+      const unsigned vA = nx ? voAn : voA, vB = nx ? voBn : voB;
+      const unsigned kk = static_cast<unsigned>(nx ? kt0n + kt + 2 - L : kt0 + kt + 2);
+      const unsigned ka = kk * kstepA, kb = kk * kstepB;
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
+        fa[mb] = rdA(cur, mb, 1);
+        fby[mb] = rdB(cur, mb, 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = 2 * mb + h;
+          if (c < 8) {
+            *reinterpret_cast<i32x4t*>(nxt + stage_lds<TA>(c, tid)) = R[c];
+            R[c] = __builtin_amdgcn_raw_buffer_load_b128(rA, vA,
+                                                         __builtin_amdgcn_readfirstlane(ka + stage_soff<TA>(g.lda, c)), 0);
+          } else {
+            *reinterpret_cast<i32x4t*>(nxt + 2 * HALF + stage_lds<!TB>(c - 8, tid)) = R[c];
+            R[c] = __builtin_amdgcn_raw_buffer_load_b128(
+                rB, vB, __builtin_amdgcn_readfirstlane(kb + stage_soff<!TB>(g.ldb, c - 8)), 0);
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
+        fa[mb] = rdA(nxt, mb, 0);
+        fbx[mb] = rdB(nxt, mb, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    epilogue<EPI, ACT>(g, acc, m0, n0, split, wm, wn, lane);
+    if (nitem >= W) break;   // uniform: every wave of the workgroup leaves together
+    pos += L;
+    item = nitem;
+    m0 = m0n, n0 = n0n, split = splitn, voA = voAn, voB = voBn, kt0 = kt0n;
+    nitem = item + static_cast<int>(gridDim.x);
+    if (nitem < W) {
+      geom(nitem, m0n, n0n, splitn);
+      voAn = stage_voff<TA>(g.lda, m0n, tid);
+      voBn = stage_voff<!TB>(g.ldb, n0n, tid);
+      kt0n = splitn * L;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4t{};
+  }
+  // drain the (unused) loads of the stream's last two positions before exit
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool TA, bool TB>
+void launch_pers(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
+  switch (epi * 8 + act) {
+    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiPlain, 0>), grid, block, 0, st, g); break;
+    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiSplit, 0>), grid, block, 0, st, g); break;
+    case kEpiGeneral * 8:
+      hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiGeneral, 0>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 0:
+      hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBiasAct, 0>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 1:
+      hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBiasAct, 1>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 4:
+      hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBiasAct, 4>), grid, block, 0, st, g);
+      break;
+    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiDact, 1>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiDact, 4>), grid, block, 0, st, g); break;
+    default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
+  }
+}
+
+template <bool TA, bool TB>
+void launch_dbg(const GemmTArgs& g, dim3 grid, dim3 block, hipStream_t st) {
+  switch (g.dbg) {
+    case 1: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 1>), grid, block, 0, st, g); break;
+    case 2: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 2>), grid, block, 0, st, g); break;
+    case 3: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 3>), grid, block, 0, st, g); break;
+    case 4: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 4>), grid, block, 0, st, g); break;
+    case 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 8>), grid, block, 0, st, g); break;
+    case 15: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 15>), grid, block, 0, st, g); break;
+    default: throw std::invalid_argument("gemmt: unsupported ablation bits");
+  }
 }
 
 template <bool TA, bool TB, int S>
 void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
+  if constexpr (!TA && S == 0) {
+    if (g.dbg && epi == kEpiPlain) return launch_dbg<TA, TB>(g, grid, block, st);
+  }
   switch (epi * 8 + act) {
     case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S>), grid, block, 0, st, g); break;
     case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiSplit, 0, S>), grid, block, 0, st, g); break;
@@ -529,7 +754,7 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
   GemmTArgs g{static_cast<const bf16*>(p.A), static_cast<const bf16*>(p.B), p.C, p.workspace,
               static_cast<const bf16*>(p.bias), static_cast<bf16*>(p.pre), static_cast<const bf16*>(p.aux), p.dbias,
               p.M, p.N, p.K, p.lda, p.ldb, p.ldc, p.alpha, p.beta, p.act, p.act_bwd ? 1 : 0, p.out_f32, splits,
-              bytes(p.trans_a ? p.K : p.M, p.lda), bytes(p.trans_b ? p.N : p.K, p.ldb)};
+              bytes(p.trans_a ? p.K : p.M, p.lda), bytes(p.trans_b ? p.N : p.K, p.ldb), p.dbg};
   const int items = ((p.M + TM - 1) / TM) * ((p.N + TN - 1) / TN) * splits;
   dim3 grid(items), block(NTHREADS);
   const int epi = splits > 1                        ? kEpiSplit
@@ -537,7 +762,23 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
                   : (p.bias || p.pre || p.act)      ? kEpiBiasAct
                   : (p.out_f32 || p.beta != 0.f)    ? kEpiGeneral
                                                     : kEpiPlain;
-  if (stage_mode == 1) {
+  const int L = p.K / TK / splits;
+  if (stage_mode == 2 && L >= 2) {
+    static int n_cu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                  hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    // a multiple of 8 workgroups (XCD-aware item mapping) unless all items fit
+    const int pg = items <= n_cu ? items : (n_cu / 8) * 8;
+    dim3 pgrid(pg);
+    if (!p.trans_a && !p.trans_b) launch_pers<false, false>(g, pgrid, block, epi, p.act, st);
+    else if (!p.trans_a && p.trans_b) launch_pers<false, true>(g, pgrid, block, epi, p.act, st);
+    else if (p.trans_a && !p.trans_b) launch_pers<true, false>(g, pgrid, block, epi, p.act, st);
+    else launch_pers<true, true>(g, pgrid, block, epi, p.act, st);
+  } else if (stage_mode == 1) {
     if (!p.trans_a && !p.trans_b) launch_t<false, false, 1>(g, grid, block, epi, p.act, st);
     else if (!p.trans_a && p.trans_b) launch_t<false, true, 1>(g, grid, block, epi, p.act, st);
     else if (p.trans_a && !p.trans_b) launch_t<true, false, 1>(g, grid, block, epi, p.act, st);

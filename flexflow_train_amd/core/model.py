@@ -307,6 +307,7 @@ class FFModel:
         self.loss_type = None
         self.metrics: List[str] = []
         self._pending_feeds: Dict[str, np.ndarray] = {}
+        self._constants: Dict[str, np.ndarray] = {}
         self._traces: Dict[int, dict] = {}
         self._active_trace: Optional[dict] = None
         self.ffconfig._models.append(self)
@@ -371,9 +372,23 @@ class FFModel:
         self._inputs.append(t)
         return t
 
-    def create_constant(self, dims, value, data_type=DataType.DT_FLOAT):
-        t = self.create_tensor(dims, data_type, create_grad=False)
-        self._pending_feeds[t.name] = np.full(dims, value, dtype=_NP_DT[_dt_str(data_type)])
+    def create_constant(self, dims, value, data_type=DataType.DT_FLOAT, name=None):
+        """A constant tensor filled with ``value`` (not trainable, never fed)."""
+        return self.create_constant_array(np.full(dims, value, dtype=_NP_DT[_dt_str(data_type)]), name=name)
+
+    def create_constant_array(self, array, name=None):
+        """A constant tensor holding ``array`` (e.g. position buckets or masks
+        folded by a frontend): an executor input that is placed on the device
+        once and never fed by data loaders."""
+        arr = np.ascontiguousarray(array)
+        dt = {np.dtype(np.float32): DataType.DT_FLOAT, np.dtype(np.float64): DataType.DT_FLOAT,
+              np.dtype(np.int32): DataType.DT_INT32, np.dtype(np.int64): DataType.DT_INT64,
+              np.dtype(np.float16): DataType.DT_HALF, np.dtype(np.bool_): DataType.DT_BOOLEAN}[arr.dtype]
+        if arr.dtype == np.float64:
+            arr = arr.astype(np.float32)
+        t = self.create_tensor(list(arr.shape), dt, create_grad=False, name=self._uname(name, "constant"))
+        self._inputs.remove(t)       # not a fed input
+        self._constants[t.name] = arr
         t._constant = True
         return t
 
@@ -622,6 +637,7 @@ class FFModel:
                                  metrics=self.metrics, optimizer=self._optimizer.cfg, output=out_v,
                                  valid_classes=self.valid_classes)
         self.executor.init_parameters()
+        self.executor.constants = dict(self._constants)
         self.local_backing = None
         if self.ffconfig.local_execution:
             self._init_local_backing(loss_type)

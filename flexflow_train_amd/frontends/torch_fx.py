@@ -75,18 +75,39 @@ class PyTorchModel:
         self.input_names = list(input_names or [])
         self.batch_size = batch_size
         self.seq_length = seq_length
-        self.graph = self._trace()
+        # Hugging Face models (and anything torch.fx cannot trace) go through
+        # torch.export + the ATen lowering (torch_export.py) at torch_to_ff
+        # time, with example inputs shaped like the FF input tensors: the
+        # reference's transformers.utils.fx tracer is gone in transformers 5
+        self.graph = None
+        self.trace_error = None
+        if not is_hf_model:
+            try:
+                self.graph = torch.fx.symbolic_trace(self.model)
+            except Exception as e:   # data-dependent control flow etc.
+                self.trace_error = e
         self.modules = dict(self.model.named_modules())
 
-    def _trace(self) -> torch.fx.GraphModule:
-        if self.is_hf_model:
-            from transformers.utils.fx import symbolic_trace as hf_trace  # noqa: WPS433
+    def _export_to_ff(self, ffmodel, input_tensors: Sequence, verbose: bool):
+        from .torch_export import ATenImporter, HFWrapper, _TORCH_DT
 
-            return hf_trace(self.model, input_names=self.input_names or None)
-        return torch.fx.symbolic_trace(self.model)
+        ex = []
+        for t in input_tensors:
+            dt = _TORCH_DT.get(t.data_type, torch.float32)
+            ex.append(torch.ones(list(t.dims), dtype=dt) if not dt.is_floating_point
+                      else torch.randn(list(t.dims), dtype=dt))
+        mod = HFWrapper(self.model, self.input_names) if self.is_hf_model else self.model
+        imp = ATenImporter(mod, ex)
+        outs = imp.to_ff(ffmodel, list(input_tensors))
+        self._importer = imp
+        if verbose:
+            print(imp.ep.graph_module.graph)
+        return outs
 
     # ------------------------------------------------------------------ API
     def torch_to_ff(self, ffmodel, input_tensors: Sequence, verbose: bool = False):
+        if self.graph is None:
+            return self._export_to_ff(ffmodel, input_tensors, verbose)
         em = _Emitter(ffmodel)
         outs = self._lower(em, list(input_tensors))
         self._last_emitter = em
@@ -99,11 +120,20 @@ class PyTorchModel:
     def weights(self) -> Dict[str, dict]:
         """FF layer name -> {weight name: (layout, torch parameter)} for
         ``copy_weights`` (the same names ``torch_to_ff``/``file_to_ff`` use)."""
+        if self.graph is None:
+            imp = getattr(self, "_importer", None)
+            if imp is None:
+                raise RuntimeError("call torch_to_ff first (torch.export path)")
+            return imp.weights
         em = _Emitter(None)
         self._lower(em, None)
         return em.weights
 
     def torch_to_string(self) -> List[str]:
+        if self.graph is None:
+            raise NotImplementedError("the .ff text IR covers torch.fx-traceable modules; import this model with "
+                                      "torch_to_ff (torch.export path)" +
+                                      (f" (fx: {self.trace_error})" if self.trace_error else ""))
         em = _Emitter(None)
         self._lower(em, None)
         return em.lines

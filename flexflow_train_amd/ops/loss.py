@@ -80,12 +80,18 @@ class LossFunction:
                 lf[:, self.valid_cols:] = float("-inf")
             lse = torch.logsumexp(lf, -1)
             lab64 = lab.long()
-            ll = lf.gather(1, lab64.view(-1, 1)).view(-1)
-            metrics[M_LOSS] += (lse - ll).sum()
-            metrics[M_CORRECT] += (lf.argmax(-1) == lab64).float().sum()
-            metrics[M_COUNT] += rows
+            # labels outside [0, C) (e.g. -100 padding) are ignored, as in the
+            # HIP kernel: no loss, no gradient, not counted
+            valid = (lab64 >= 0) & (lab64 < C)
+            safe = torch.where(valid, lab64, torch.zeros_like(lab64))
+            ll = lf.gather(1, safe.view(-1, 1)).view(-1)
+            vf = valid.float()
+            metrics[M_LOSS] += ((lse - ll) * vf).sum()
+            metrics[M_CORRECT] += ((lf.argmax(-1) == lab64).float() * vf).sum()
+            metrics[M_COUNT] += vf.sum()
             p = torch.softmax(lf, -1)
-            p[torch.arange(rows, device=p.device), lab64] -= 1.0
+            p[torch.arange(rows, device=p.device), safe] -= vf
+            p *= vf.view(-1, 1)
             return (p * scale).to(logits.dtype).view(logits.shape)
         if lt == "categorical_crossentropy":
             lf = logits.reshape(rows, C).float()

@@ -152,6 +152,11 @@ def _stable_seed(*parts) -> int:
 
 
 class Executor:
+    # constant inputs: name -> host array (FFModel.create_constant*), and
+    # their device pieces, built on the first forward
+    constants: Dict[str, object] = {}
+    _const_env: Optional[Dict] = None
+
     def __init__(self, pcg, dist_ctx: DistContext, cfg: ExecConfig, views: Optional[Dict[int, Tuple[int, int]]] = None,
                  loss_type=None, metrics: Sequence[str] = (), optimizer=None, output: Optional[Value] = None,
                  label_dtype: Optional[torch.dtype] = None, valid_classes: Optional[int] = None):
@@ -925,6 +930,17 @@ class Executor:
             piece = self._local_piece(name, x)
             if piece is not None:
                 env[self.inputs[name][0]] = piece
+        if self.constants:
+            # constant inputs (FFModel.create_constant*): placed on the device
+            # once, never fed; the same tensors every step (graph-capture safe)
+            if self._const_env is None:
+                self._const_env = {}
+                for name, x in self.constants.items():
+                    piece = self._local_piece(name, torch.as_tensor(x))
+                    if piece is not None:
+                        self._const_env[self.inputs[name][0]] = piece
+            for v, piece in self._const_env.items():
+                env.setdefault(v, piece)
         for p in self.params:
             if p.group:
                 env[p.terminal] = p.compute

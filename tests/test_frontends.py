@@ -307,3 +307,35 @@ def test_onnx_export_keras_roundtrip_matches_keras():
     import torch
     got = ff.executor.forward({x.name: torch.as_tensor(xv)}, training=False).float().numpy()
     np.testing.assert_allclose(got, km.predict(xv), rtol=1e-4, atol=1e-5)
+
+
+def test_hf_mt5_import_matches_torch():
+    """PyTorchModel(is_hf_model=True): a Hugging Face MT5 (encoder-decoder,
+    relative position buckets, RMS norms, gated GELU, padding mask) through
+    torch.export + the ATen lowering gives the module's logits."""
+    import torch
+    transformers = pytest.importorskip("transformers")
+    from flexflow.core import DataType, FFConfig, FFModel, LossType, SGDOptimizer
+    from flexflow.torch.model import PyTorchModel, copy_weights
+
+    cfg = transformers.MT5Config(vocab_size=256, d_model=32, d_kv=8, d_ff=64, num_layers=2, num_decoder_layers=2,
+                                 num_heads=4, relative_attention_num_buckets=8, dropout_rate=0.0)
+    torch.manual_seed(0)
+    m = transformers.MT5ForConditionalGeneration(cfg).eval()
+    B, S = 2, 10
+    ids, dids = torch.randint(0, 256, (B, S)), torch.randint(0, 256, (B, S))
+    mask = torch.ones(B, S, dtype=torch.long)
+    mask[1, 7:] = 0
+    with torch.no_grad():
+        ref = m(input_ids=ids, attention_mask=mask, decoder_input_ids=dids, use_cache=False).logits
+    fc = FFConfig()
+    fc.batch_size = B
+    ff = FFModel(fc)
+    names = ["input_ids", "attention_mask", "decoder_input_ids"]
+    ts = [ff.create_tensor([B, S], DataType.DT_INT64, create_grad=False, name=n) for n in names]
+    outs = PyTorchModel(m, is_hf_model=True, input_names=names).torch_to_ff(ff, ts)
+    assert isinstance(outs, list) and tuple(outs[0].dims) == (B, S, 256)
+    ff.compile(optimizer=SGDOptimizer(ff, 0.0), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY)
+    copy_weights(ff)
+    got = ff.executor.forward(dict(zip(names, (ids, mask, dids))), training=False)
+    torch.testing.assert_close(got.float(), ref, rtol=1e-4, atol=1e-4)
