@@ -29,12 +29,14 @@ def main():
     if a.last:
         rows = rows[-a.last:]
     if a.steps:
-        ends = [i for i, r in enumerate(rows) if re.search(r"adam|sgd", r[0])]
-        # a step's update may be split over several kernels: take the last of each run
-        marks = [i for j, i in enumerate(ends) if j + 1 == len(ends) or ends[j + 1] != i + 1]
-        if len(marks) > a.steps:
-            rows = rows[marks[-a.steps - 1] + 1:marks[-1] + 1]
-        print(f"last {a.steps} steps: {len(rows)} dispatches")
+        # a step ends with the same optimizer-update kernel every time: the
+        # last update kernel of the trace marks the step boundaries
+        upd = [r[0] for r in rows if re.search(r"adam|sgd", r[0])]
+        marks = [i for i, r in enumerate(rows) if upd and r[0] == upd[-1]]
+        n = min(a.steps, len(marks) - 1)
+        if n > 0:
+            rows = rows[marks[-n - 1] + 1:marks[-1] + 1]
+        print(f"last {n} steps: {len(rows)} dispatches")
     span = (rows[-1][2] - rows[0][1]) / 1e6 if rows else 0.0
     tot = collections.Counter()
     cnt = collections.Counter()
