@@ -14,7 +14,7 @@ EXAMPLES = sorted(f"pytorch/{f}" for f in os.listdir(os.path.join(ROOT, "example
 # every ONNX example (reference: examples/python/onnx/*.py); *_pt / *_keras export
 EXAMPLES += sorted(f"onnx/{f}" for f in os.listdir(os.path.join(ROOT, "examples", "onnx"))
                    if f.endswith(".py") and not f.startswith("_") and f != "accuracy.py")
-EXAMPLES += ["pytorch/mt5/mt5_ff.py", "pytorch/mt5/mt5_torch.py"]
+EXAMPLES += ["pytorch/mt5/mt5_ff.py", "pytorch/mt5/mt5_torch.py", "keras/candle_uno/candle_uno.py"]
 EXPORT_ONLY = {"pytorch/cifar10_cnn_torch.py", "pytorch/resnet_torch.py", "pytorch/torch_vision_torch.py",
                "pytorch/export_regnet_fx.py"} | {e for e in EXAMPLES if e.startswith("onnx/") and
                                                  (e.endswith("_pt.py") or e.endswith("_keras.py"))}
