@@ -172,6 +172,7 @@ PYBIND11_MODULE(_ffcore, m) {
 
   py::class_<ComputationGraph>(m, "ComputationGraph")
       .def(py::init<>())
+      .def("set_input_replicated", &ComputationGraph::set_input_replicated, py::arg("node"))
       .def("create_input", &ComputationGraph::create_input, py::arg("shape"), py::arg("create_grad") = true,
            py::arg("name") = "")
       .def("create_weight", &ComputationGraph::create_weight, py::arg("shape"), py::arg("initializer"),

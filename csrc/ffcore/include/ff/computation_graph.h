@@ -52,6 +52,9 @@ class ComputationGraph {
   Graph g;
 
   ValueRef create_input(const TensorShape& shape, bool create_grad = true, const std::string& name = "");
+  // A constant input (no sample dimension): data-parallel strategies replicate
+  // it instead of partitioning its first dimension.
+  void set_input_replicated(int node);
   ValueRef create_weight(const TensorShape& shape, const std::string& initializer, bool create_grad = true,
                          const std::string& name = "");
   // Adds an operator layer; creates its weight layers (with the given or

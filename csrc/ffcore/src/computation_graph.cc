@@ -34,6 +34,12 @@ ValueRef ComputationGraph::create_input(const TensorShape& shape, bool create_gr
   return {id, 0};
 }
 
+void ComputationGraph::set_input_replicated(int node) {
+  auto& n = g.node(node);
+  if (n.label.op.type != OpType::INPUT) throw FFError("set_input_replicated: not an INPUT node");
+  n.label.op.set("replicated", true);
+}
+
 ValueRef ComputationGraph::create_weight(const TensorShape& shape, const std::string& init, bool create_grad,
                                          const std::string& name) {
   OpAttrs a(OpType::WEIGHT);
@@ -562,7 +568,9 @@ ParallelComputationGraph data_parallel_pcg(const ComputationGraph& cg, int degre
     if (t == OpType::INPUT) {
       auto const& s = n.outputs[0].shape;
       ValueRef v = p.add_input(lift_to_parallel(s), n.outputs[0].create_grad, n.label.name);
-      if (degree > 1 && s.num_dims() > 0 && s.dims[0] % degree == 0) v = p.parallel_partition(v, 0, degree);
+      const bool replicated = n.label.op.has("replicated") && n.label.op.b("replicated");
+      if (degree > 1 && !replicated && s.num_dims() > 0 && s.dims[0] % degree == 0)
+        v = p.parallel_partition(v, 0, degree);
       vm[{id, 0}] = v;
       continue;
     }

@@ -300,7 +300,9 @@ Lowering lower_strategy(const ComputationGraph& cg, const StrategyConfig& cfg, i
       auto const& s = n.outputs[0].shape;
       ValueRef v = p.add_input(lift_to_parallel(s), n.outputs[0].create_grad, n.label.name);
       L.cg_to_pcg[id] = v.node;
-      if (c.batch > 1) {
+      // constant inputs (no sample dimension) stay whole on every rank
+      const bool replicated = n.label.op.has("replicated") && n.label.op.b("replicated");
+      if (c.batch > 1 && !replicated) {
         if (s.num_dims() < 1 || s.dims[0] % c.batch) throw FFError("input " + n.label.name + ": batch degree");
         v = p.parallel_partition(v, 0, c.batch);
         ++L.num_parallel_ops;

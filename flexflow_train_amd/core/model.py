@@ -388,6 +388,7 @@ class FFModel:
             arr = arr.astype(np.float32)
         t = self.create_tensor(list(arr.shape), dt, create_grad=False, name=self._uname(name, "constant"))
         self._inputs.remove(t)       # not a fed input
+        self.cg.set_input_replicated(t.vref.node)   # no sample dimension: replicated under data parallelism
         self._constants[t.name] = arr
         t._constant = True
         return t

@@ -179,3 +179,22 @@ def test_cnn_input_channel_parallel_conv(tmp_path):
     write_strategy(M.cnn, 2, {"c2": {"batch": 1, "model": 2, "kind": "row"}}, path)
     out = run_distributed(M.cnn, 2, path, steps=2)
     assert_params_close(out["params"], ref["params"], rtol=1e-4, atol=1e-5)
+
+
+def _const_model(m):
+    """A Linear fed x + a constant row (FFModel.create_constant_array): the
+    constant has no sample dimension and must stay whole on every rank."""
+    import numpy as np
+    import torch
+    from flexflow_train_amd.core import DataType
+    x = m.create_tensor([8, 6], DataType.DT_FLOAT, name="x")
+    c = m.create_constant_array(np.linspace(-1, 1, 6, dtype=np.float32).reshape(1, 6), name="row")
+    m.softmax(m.dense(m.relu(m.add(x, c)), 4, name="fc"))
+    g = torch.Generator().manual_seed(3)
+    return {"x": torch.randn(8, 6, generator=g)}, torch.randint(0, 4, (8, 1), generator=g, dtype=torch.int32)
+
+
+def test_constant_input_replicated_under_data_parallel():
+    single = run_single(_const_model, steps=3)
+    multi = run_distributed(_const_model, world=2, steps=3)
+    assert_params_close(single["params"], multi["params"])
