@@ -185,6 +185,7 @@ __device__ __forceinline__ uint2 pack4(const float (&v)[4]) {
 // 16-lane rows of block 2j with the even rows of block 2j+1, after which row
 // r holds 8 consecutive columns, (r >> 1) * 8 .. +8, of block 2j + (r & 1)
 // (guide T21: the store tail is issue-bound; half the instructions).
+template <bool NT = false>
 __device__ __forceinline__ void store_row16(bf16* C, int64_t row_off, int ncol0, int N, bool mok, const uint2 (&o)[8],
                                             int lane) {
   const int r = lane >> 4;
@@ -193,13 +194,21 @@ __device__ __forceinline__ void store_row16(bf16* C, int64_t row_off, int ncol0,
     const auto sx = __builtin_amdgcn_permlane16_swap(o[2 * j].x, o[2 * j + 1].x, false, false);
     const auto sy = __builtin_amdgcn_permlane16_swap(o[2 * j].y, o[2 * j + 1].y, false, false);
     const int n = ncol0 + (2 * j + (r & 1)) * 16 + (r >> 1) * 8;
-    if (mok && n < N) *reinterpret_cast<uint4*>(C + row_off + n) = uint4{sx[0], sy[0], sx[1], sy[1]};
+    if (mok && n < N) {
+      if (NT) {   // streamed past L2: keep the operands resident
+        const i32x4t v{static_cast<int>(sx[0]), static_cast<int>(sy[0]), static_cast<int>(sx[1]),
+                       static_cast<int>(sy[1])};
+        __builtin_nontemporal_store(v, reinterpret_cast<i32x4t*>(C + row_off + n));
+      } else {
+        *reinterpret_cast<uint4*>(C + row_off + n) = uint4{sx[0], sy[0], sx[1], sy[1]};
+      }
+    }
   }
 }
 
 // acc[mb][nb]: row m = m0 + wm*128 + mb*16 + (lane & 15);
 // columns n = n0 + wn*128 + nb*16 + 4 (lane >> 4) + e.
-template <int EPI, int ACT>
+template <int EPI, int ACT, bool NT = false>
 __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8], int m0, int n0, int split, int wm,
                                          int wn, int lane) {
   const int nl = 4 * (lane >> 4);
@@ -275,8 +284,8 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
       }
     }
     if (WIDE) {
-      store_row16(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, ob, lane);
-      if (EPI == kEpiBiasAct && g.pre) store_row16(g.pre, roff, ncol0, g.N, mok, pb, lane);
+      store_row16<NT>(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, ob, lane);
+      if (EPI == kEpiBiasAct && g.pre) store_row16<NT>(g.pre, roff, ncol0, g.N, mok, pb, lane);
     }
   }
   if (EPI == kEpiDact && g.dbias) {
@@ -497,7 +506,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  if (!(DBG & 8)) epilogue<EPI, ACT>(g, acc, m0, n0, split, wm, wn, lane);
+  if (!(DBG & 8)) epilogue<EPI, ACT, (DBG & 16) != 0>(g, acc, m0, n0, split, wm, wn, lane);
 }
 
 // Persistent form (variant 5): one workgroup per CU walks its work items
@@ -712,6 +721,7 @@ void launch_dbg(const GemmTArgs& g, dim3 grid, dim3 block, hipStream_t st) {
     case 4: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 4>), grid, block, 0, st, g); break;
     case 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 8>), grid, block, 0, st, g); break;
     case 15: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 15>), grid, block, 0, st, g); break;
+    case 16: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 16>), grid, block, 0, st, g); break;
     default: throw std::invalid_argument("gemmt: unsupported ablation bits");
   }
 }

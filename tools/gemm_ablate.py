@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Sync-cost ablation of the phase-pipelined GEMMs (timing only: with the
-waits or barriers removed the results are garbage).  dbg bits: 1 = no vmcnt
-waits, 2 = no barriers.  Interleaved rounds in one process."""
+waits or barriers removed the results are garbage).  gemmp / gemmq (variants
+0 / 1) dbg bits: 1 = no vmcnt waits, 2 = no barriers.  gemmt (variant 3,
+NN / NT only, ``--gemmt``): 1 = no global loads in the loop, 2 = no LDS
+writes (the loads then die too), 4 = no mid-tile barrier, 8 = no epilogue,
+15 = all of them (MFMAs + fragment reads only), 16 = non-temporal epilogue stores.  Interleaved rounds in one
+process:  python tools/gemm_ablate.py [--gemmt]"""
 import json
 import os
 import statistics
@@ -14,7 +18,7 @@ from flexflow_train_amd import kernels as K  # noqa: E402
 from tools.gemm_ab import operands, timed  # noqa: E402
 
 CASES = [("fwd_qkv", "fwd", 1024, 3072), ("dx_ffn1", "dx", 1024, 4096), ("fwd_ffn2", "fwd", 4096, 1024),
-         ("dw_ffn1", "dw", 1024, 4096)]
+         ("dw_ffn1", "dw", 1024, 4096), ("fwd_ffn1", "fwd", 1024, 4096), ("dx_qkv", "dx", 1024, 3072)]
 
 
 def main():
@@ -25,10 +29,18 @@ def main():
         sp = 4 if kind == "dw" else 1
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         cands = {}
-        for v in (0, 1):
-            for dbg in (0, 1, 2, 3):
-                cands[f"v{v}_d{dbg}"] = lambda v=v, dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out,
-                                                                     splits=sp, variant=v, _dbg=dbg)
+        if "--gemmt" in sys.argv:
+            if ta:
+                continue
+            cands["blaslt"] = lambda: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=out)
+            for dbg in (0, 8, 16):
+                cands[f"t_d{dbg}"] = lambda dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out, splits=sp,
+                                                             variant=3, _dbg=dbg)
+        else:
+            for v in (0, 1):
+                for dbg in (0, 1, 2, 3):
+                    cands[f"v{v}_d{dbg}"] = lambda v=v, dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out,
+                                                                         splits=sp, variant=v, _dbg=dbg)
         times = {k: [] for k in cands}
         for _ in range(5):
             for k, f in cands.items():
