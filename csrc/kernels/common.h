@@ -94,17 +94,24 @@ __device__ __forceinline__ float fmax3(float a, float b, float c) {
 __device__ __forceinline__ float fast_tanh(float x) {
   return 1.f - __fdividef(2.f, __expf(2.f * x) + 1.f);
 }
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + fast_tanh(u));
+// tanh-approximated GELU in its sigmoid form: 0.5 (1 + tanh u) = s = 1 / (1 +
+// 2^(-2 u log2 e)), u = k0 (x + k1 x^3): bare v_exp_f32 + v_rcp_f32 and a few
+// FMAs per element (the GEMM epilogues apply it to 256 values per lane, where
+// libm exp / divide fix-ups tripled the VALU work).  x -> -inf: 2^arg = inf,
+// s = 0; x -> +inf: s = 1.
+__device__ __forceinline__ float gelu_sig(float x, float x2) {
+  constexpr float k1 = 0.044715f, c = -2.f * 0.7978845608028654f * 1.4426950408889634f;
+  const float arg = x * __builtin_fmaf(c * k1, x2, c);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(arg));
 }
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_sig(x, x * x); }
+// d/dx [x s(2u)] = s + x s (1 - s) 2 k0 (1 + 3 k1 x^2)
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = fast_tanh(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  constexpr float k0x2 = 2.f * 0.7978845608028654f, k1x3 = 3.f * 0.044715f;
+  const float x2 = x * x;
+  const float s = gelu_sig(x, x2);
+  const float w = x * __builtin_fmaf(k0x2 * k1x3, x2, k0x2);
+  return __builtin_fmaf(w, s - s * s, s);
 }
 
 // Counter-based RNG (splitmix64 finaliser) for dropout: deterministic in

@@ -527,7 +527,7 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
     const uint64_t b_bytes = uint64_t(p.trans_b ? p.N : p.K) * uint64_t(p.ldb) * 2u;
     const bool small = a_bytes < (1ull << 32) && b_bytes < (1ull << 32);
     if (p.variant == 2 && small) gemmr_launch(p, splits, n_cu, st);
-    else if (p.variant >= 3 && small && gemmt_act_supported(p.act))
+    else if (p.variant >= 3 && small && gemmt_supported(p))
       gemmt_launch(p, splits, p.variant - 3, st);
     else gemmq_launch(p, splits, n_cu, st);
     if (splits > 1) splitk_reduce(p.workspace, p.C, p.M, p.N, p.ldc, splits, p.beta, p.out_f32, st);

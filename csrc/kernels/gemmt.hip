@@ -94,6 +94,42 @@ __device__ __forceinline__ float t_act_grad(float x) {
   return 1.f;
 }
 
+typedef float f32x2t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2t __attribute__((ext_vector_type(2)));
+
+// activation (gradient) of an element pair: float2 arithmetic lowers to
+// v_pk_mul / v_pk_fma / v_pk_add (two lanes' worth per VALU issue); only the
+// v_exp / v_rcp transcendentals stay per element
+__device__ __forceinline__ f32x2t gelu_sig2(f32x2t x, f32x2t x2) {
+  constexpr float k1 = 0.044715f, c = -2.f * 0.7978845608028654f * 1.4426950408889634f;
+  const f32x2t arg = x * __builtin_elementwise_fma(x2, f32x2t{c * k1, c * k1}, f32x2t{c, c});
+  const f32x2t d = f32x2t{__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)} + 1.f;
+  return f32x2t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+template <int ACT>
+__device__ __forceinline__ f32x2t t_act2(f32x2t x) {
+  if (ACT == 1) return f32x2t{x.x > 0.f ? x.x : 0.f, x.y > 0.f ? x.y : 0.f};
+  if (ACT == 4) return x * gelu_sig2(x, x * x);
+  return f32x2t{t_act<ACT>(x.x), t_act<ACT>(x.y)};
+}
+// g * act'(x)
+template <int ACT>
+__device__ __forceinline__ f32x2t t_dact2(f32x2t g, f32x2t x) {
+  if (ACT == 1) return f32x2t{x.x > 0.f ? g.x : 0.f, x.y > 0.f ? g.y : 0.f};
+  if (ACT == 4) {
+    constexpr float k0x2 = 2.f * 0.7978845608028654f, k1x3 = 3.f * 0.044715f;
+    const f32x2t x2 = x * x;
+    const f32x2t sg = gelu_sig2(x, x2);
+    const f32x2t w = x * __builtin_elementwise_fma(x2, f32x2t{k0x2 * k1x3, k0x2 * k1x3}, f32x2t{k0x2, k0x2});
+    return g * __builtin_elementwise_fma(w, sg - sg * sg, sg);
+  }
+  return f32x2t{g.x * t_act_grad<ACT>(x.x), g.y * t_act_grad<ACT>(x.y)};
+}
+// bf16 pair (one dword) -> float2: low half << 16, high half masked
+__device__ __forceinline__ f32x2t unpack2(unsigned u) {
+  return f32x2t{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+}
+
 __device__ __forceinline__ int t_slot128(int r, int c) { return c ^ ((r >> 1) & 7); }
 
 __device__ __forceinline__ f32x4t mfma16(bf16x8 a, bf16x8 b, f32x4t c) {
@@ -172,11 +208,13 @@ __device__ __forceinline__ bf16x8 tr16(const unsigned char* img, int ks, int o0,
 // epilogue made the allocator shuttle accumulators through VGPRs in the loop)
 enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3, kEpiGeneral = 4 };
 
-__device__ __forceinline__ uint2 pack4(const float (&v)[4]) {
-  bf16x4 o;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-  return __builtin_bit_cast(uint2, o);
+// one v_cvt_pk_bf16_f32 per pair (per-element casts pack through perm/alignbit)
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2t{a, b}, bf16x2t));
+}
+__device__ __forceinline__ uint2 pack4(const float (&v)[4]) { return uint2{pack2(v[0], v[1]), pack2(v[2], v[3])}; }
+__device__ __forceinline__ unsigned pack2v(f32x2t v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2t));
 }
 
 // Store the 8 bf16x4 groups of one row block (blocks nb = 0..7, lane row
@@ -223,12 +261,52 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
 #pragma unroll
       for (int c = 0; c < 4; ++c) csum[b][c] = 0.f;
   }
+  // bias of this lane's 32 columns, loaded once (not per row block)
+  float bv[8][4];
+  if (EPI == kEpiBiasAct) {
+    if (g.bias) {
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) {
+        const bf16x4 bb = *reinterpret_cast<const bf16x4*>(g.bias + min(nbase + nb * 16, g.N - 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[nb][e] = bf2f(bb[e]);
+      }
+    } else {
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[nb][e] = 0.f;
+    }
+  }
+  // activation-gradient inputs, prefetched one row block ahead
+  uint2 xa[2][8];
+  auto row_of = [&](int mb) {
+    const int m_raw = m0 + wm * 128 + mb * 16 + (lane & 15);
+    return m_raw < g.M ? m_raw : g.M - 1;
+  };
+  if (EPI == kEpiDact) {
+    const int64_t r0 = static_cast<int64_t>(row_of(0)) * g.ldc;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb)
+      xa[0][nb] = *reinterpret_cast<const uint2*>(g.aux + r0 + min(nbase + nb * 16, g.N - 4));
+  }
 #pragma unroll
   for (int mb = 0; mb < 8; ++mb) {
     const int m_raw = m0 + wm * 128 + mb * 16 + (lane & 15);
     const bool mok = m_raw < g.M;
     const int m = mok ? m_raw : g.M - 1;
     const int64_t roff = static_cast<int64_t>(m) * g.ldc;
+    const float mf = mok ? 1.f : 0.f;
+    if (EPI == kEpiDact && mb < 7) {
+      const int64_t r1 = static_cast<int64_t>(row_of(mb + 1)) * g.ldc;
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb)
+        xa[(mb + 1) & 1][nb] = *reinterpret_cast<const uint2*>(g.aux + r1 + min(nbase + nb * 16, g.N - 4));
+    }
+    // re-pin this row block's accumulators: one pin per block here (rather than
+    // all 64 at the loop exit) keeps hipcc from permuting the AGPRs first
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[mb][j]));
     uint2 ob[8], pb[8];
 #pragma unroll
     for (int nb = 0; nb < 8; ++nb) {
@@ -236,26 +314,33 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
       const bool ok = mok && n_raw < g.N;  // N % 8 == 0: a 4-group is all-in or all-out
       const int n = ok ? n_raw : min(n_raw, g.N - 4);
       const int64_t off = roff + n;
+      if (EPI == kEpiBiasAct || EPI == kEpiDact) {  // alpha 1 (gemmt_supported); element pairs
+        f32x2t v[2] = {f32x2t{acc[mb][nb][0], acc[mb][nb][1]}, f32x2t{acc[mb][nb][2], acc[mb][nb][3]}};
+        if (EPI == kEpiBiasAct) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            v[h] += f32x2t{bv[nb][2 * h], bv[nb][2 * h + 1]};
+            (h ? pb[nb].y : pb[nb].x) = pack2v(v[h]);  // the pre-activation
+            v[h] = t_act2<ACT>(v[h]);
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            v[h] = t_dact2<ACT>(v[h], unpack2(h ? xa[mb & 1][nb].y : xa[mb & 1][nb].x));
+            csum[nb][2 * h] += mf * v[h].x;  // masked rows add 0 (fp32 sum of the gradient)
+            csum[nb][2 * h + 1] += mf * v[h].y;
+          }
+        }
+        ob[nb] = uint2{pack2v(v[0]), pack2v(v[1])};
+        continue;
+      }
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[mb][nb][e];
+      for (int e = 0; e < 4; ++e) v[e] = EPI == kEpiPlain ? acc[mb][nb][e] : g.alpha * acc[mb][nb][e];  // plain: alpha 1
       if (EPI == kEpiSplit) {
         float* Wp = g.ws + (static_cast<int64_t>(split) * g.M + m) * g.N + n;
         if (ok) *reinterpret_cast<f32x4t*>(Wp) = f32x4t{v[0], v[1], v[2], v[3]};
         continue;
-      }
-      if (EPI == kEpiBiasAct) {
-        const bf16x4 bb = g.bias ? *reinterpret_cast<const bf16x4*>(g.bias + n) : bf16x4{};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bf2f(bb[e]);
-        pb[nb] = pack4(v);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = t_act<ACT>(v[e]);
-      }
-      if (EPI == kEpiDact) {
-        const bf16x4 xa = *reinterpret_cast<const bf16x4*>(g.aux + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] *= t_act_grad<ACT>(bf2f(xa[e]));
       }
       if (EPI == kEpiGeneral) {
         if (g.beta != 0.f) {
@@ -277,11 +362,6 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
         continue;
       }
       ob[nb] = pack4(v);
-      if (EPI == kEpiDact) {
-        const bf16x4 o = __builtin_bit_cast(bf16x4, ob[nb]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) csum[nb][e] += ok ? bf2f(o[e]) : 0.f;  // the stored (rounded) value
-      }
     }
     if (WIDE) {
       store_row16<NT>(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, ob, lane);
@@ -289,16 +369,30 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
     }
   }
   if (EPI == kEpiDact && g.dbias) {
+    // column sums over the 16 lanes of a row group (lane & 15) as a
+    // reduce-scatter: each xor step halves the live values (30 shuffles, not
+    // 128), leaving lane 2 values: k = 16 b3 + 8 b2 + 4 b1 + 2 b0 + {0, 1}
+    float cv[32];
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb)
+    for (int k = 0; k < 32; ++k) cv[k] = csum[k >> 2][k & 3];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float sm = csum[nb][e];
+    for (int st = 0, c = 32; st < 4; ++st, c >>= 1) {
+      const int o = 8 >> st;
+      const bool hi = (lane & o) != 0;
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
-        const int n = nbase + nb * 16 + e;
-        if ((lane & 15) == 0 && n < g.N) atomicAdd(g.dbias + n, sm);
+      for (int i = 0; i < c / 2; ++i) {
+        const float send = hi ? cv[i] : cv[i + c / 2];
+        const float keep = hi ? cv[i + c / 2] : cv[i];
+        cv[i] = keep + __shfl_xor(send, o, 64);
       }
+    }
+    const int kb = 16 * ((lane >> 3) & 1) + 8 * ((lane >> 2) & 1) + 4 * ((lane >> 1) & 1) + 2 * (lane & 1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = kb + t;
+      const int n = nbase + (k >> 2) * 16 + (k & 3);
+      if (n < g.N) atomicAdd(g.dbias + n, cv[t]);
+    }
   }
 }
 
@@ -505,7 +599,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    for (int j = 0; j < 8; ++j) if (0) asm volatile("" : "+a"(acc[i][j]));
   if (!(DBG & 8)) epilogue<EPI, ACT, (DBG & 16) != 0>(g, acc, m0, n0, split, wm, wn, lane);
 }
 
@@ -754,7 +848,12 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
 
 }  // namespace
 
-bool gemmt_act_supported(int act) { return act == 0 || act == 1 || act == 4; }
+// the bias / activation / activation-gradient and plain bf16 epilogues take
+// alpha = 1 (their callers' only use); other alphas go to gemmq
+bool gemmt_supported(const GemmPParams& p) {
+  const bool fused = p.bias || p.pre || p.act || p.act_bwd;
+  return (p.act == 0 || p.act == 1 || p.act == 4) && (!fused || p.alpha == 1.f);
+}
 
 void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t st) {
   auto bytes = [](int rows, int ld) {
@@ -770,8 +869,8 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
   const int epi = splits > 1                        ? kEpiSplit
                   : p.act_bwd                       ? kEpiDact
                   : (p.bias || p.pre || p.act)      ? kEpiBiasAct
-                  : (p.out_f32 || p.beta != 0.f)    ? kEpiGeneral
-                                                    : kEpiPlain;
+                  : (p.out_f32 || p.beta != 0.f || p.alpha != 1.f) ? kEpiGeneral
+                                                                   : kEpiPlain;
   const int L = p.K / TK / splits;
   if (stage_mode == 2 && L >= 2) {
     static int n_cu = [] {

@@ -121,7 +121,7 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st);
 void gemmq_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
 void gemmr_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
 void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t st);
-bool gemmt_act_supported(int act);
+bool gemmt_supported(const GemmPParams& p);
 
 // ---- tensorops.hip: general tensor operators (N-d, <= 6 dims)
 struct NdShape {

@@ -302,7 +302,10 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
         torch.nn.functional.gelu(x, approximate="tanh").backward(torch.ones_like(x))
         gr = ref * x.grad
         assert _rel(g, gr) < 1e-2
-        assert _rel(db, g.float().sum(0) + 0.5) < 1e-4
+        if variant >= 3:   # gemmt sums the fp32 gradient (before its bf16 rounding)
+            assert _rel(db, gr.sum(0) + 0.5) < 1e-3
+        else:              # the other kernels sum the stored bf16 values
+            assert _rel(db, g.float().sum(0) + 0.5) < 1e-4
 
 
 def test_dropout_and_cast():
