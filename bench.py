@@ -97,8 +97,10 @@ def main():
                           "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
                           "vs_baseline": None, "dtype": "bf16", "data": res["data"], "config": conf}), flush=True)
         if os.environ.get("FF_GEMM_REPORT"):
+            from flexflow_train_amd.ops.dense import dact_report
             from flexflow_train_amd.ops.gemm import report
             print(report(), file=sys.stderr)
+            print(dact_report(), file=sys.stderr)
         if args.profile and res.get("profile"):
             print(json.dumps({"profile_ms_total": res["profile"]}), file=sys.stderr)
 

@@ -244,11 +244,40 @@ __device__ __forceinline__ void store_row16(bf16* C, int64_t row_off, int ncol0,
   }
 }
 
+// LDS-staged C (one 128 x 128 bf16 wave tile = 32 KB, rows of 256 B, 16-B
+// chunk slot = chunk ^ (row & 15)): the row block's paired 16-B groups go to
+// LDS, and the tile leaves as whole rows, 4 rows x 256 contiguous bytes per
+// store instruction (8 full 128-B lines instead of 16 half lines).
+__device__ __forceinline__ void stage_row16(unsigned char* st, int mb, const uint2 (&o)[8], int lane) {
+  const int r = lane >> 4;
+  const int row = mb * 16 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto sx = __builtin_amdgcn_permlane16_swap(o[2 * j].x, o[2 * j + 1].x, false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(o[2 * j].y, o[2 * j + 1].y, false, false);
+    const int chunk = 4 * j + 2 * (r & 1) + (r >> 1);
+    *reinterpret_cast<i32x4t*>(st + row * 256 + ((chunk ^ (row & 15)) << 4)) =
+        i32x4t{static_cast<int>(sx[0]), static_cast<int>(sy[0]), static_cast<int>(sx[1]), static_cast<int>(sy[1])};
+  }
+}
+__device__ __forceinline__ void flush_rows(const unsigned char* st, bf16* C, int mrow0, int ncol0, int M, int N,
+                                           int ldc, int lane) {
+  const int c = lane & 15;
+  const int col = ncol0 + c * 8;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int row = 4 * i + (lane >> 4);
+    const i32x4t v = *reinterpret_cast<const i32x4t*>(st + row * 256 + ((c ^ (row & 15)) << 4));
+    const int m = mrow0 + row;
+    if (m < M && col < N) *reinterpret_cast<i32x4t*>(C + static_cast<int64_t>(m) * ldc + col) = v;
+  }
+}
+
 // acc[mb][nb]: row m = m0 + wm*128 + mb*16 + (lane & 15);
 // columns n = n0 + wn*128 + nb*16 + 4 (lane >> 4) + e.
-template <int EPI, int ACT, bool NT = false>
+template <int EPI, int ACT, bool NT = false, bool STAGE = false>
 __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8], int m0, int n0, int split, int wm,
-                                         int wn, int lane) {
+                                         int wn, int lane, unsigned char* st = nullptr) {
   const int nl = 4 * (lane >> 4);
   const int ncol0 = n0 + wn * 128;
   const int nbase = ncol0 + nl;
@@ -363,10 +392,17 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
       }
       ob[nb] = pack4(v);
     }
-    if (WIDE) {
+    if (WIDE && STAGE) {
+      stage_row16(st, mb, ob, lane);
+      if (EPI == kEpiBiasAct && g.pre) store_row16<NT>(g.pre, roff, ncol0, g.N, mok, pb, lane);
+    } else if (WIDE) {
       store_row16<NT>(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, ob, lane);
       if (EPI == kEpiBiasAct && g.pre) store_row16<NT>(g.pre, roff, ncol0, g.N, mok, pb, lane);
     }
+  }
+  if (WIDE && STAGE) {
+    asm volatile("" ::: "memory");  // LDS is in order within a wave: no wait, no barrier
+    flush_rows(st, static_cast<bf16*>(g.C), m0 + wm * 128, ncol0, g.M, g.N, g.ldc, lane);
   }
   if (EPI == kEpiDact && g.dbias) {
     // column sums over the 16 lanes of a row group (lane & 15) as a
@@ -600,7 +636,10 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) if (0) asm volatile("" : "+a"(acc[i][j]));
-  if (!(DBG & 8)) epilogue<EPI, ACT, (DBG & 16) != 0>(g, acc, m0, n0, split, wm, wn, lane);
+  constexpr bool STAGE_C = (DBG & 32) != 0;
+  if (STAGE_C) __syncthreads();  // every wave is past its last K-loop LDS read
+  if (!(DBG & 8))
+    epilogue<EPI, ACT, (DBG & 16) != 0, STAGE_C>(g, acc, m0, n0, split, wm, wn, lane, smem + wave * 32768);
 }
 
 // Persistent form (variant 5): one workgroup per CU walks its work items
@@ -816,6 +855,7 @@ void launch_dbg(const GemmTArgs& g, dim3 grid, dim3 block, hipStream_t st) {
     case 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 8>), grid, block, 0, st, g); break;
     case 15: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 15>), grid, block, 0, st, g); break;
     case 16: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 16>), grid, block, 0, st, g); break;
+    case 32: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 32>), grid, block, 0, st, g); break;
     default: throw std::invalid_argument("gemmt: unsupported ablation bits");
   }
 }

@@ -114,6 +114,7 @@ class LinearOp(OpImpl):
 
 
 _DACT_CHOICE = {}
+_DACT_TIMES = {}
 
 
 def _dact_variant(act: str) -> int:
@@ -141,7 +142,16 @@ def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:
     plain = _time(lambda: (matmul(g, W, trans_b=True),
                            K.colsum_act(dx, pre, act, db if has_bias else None, write_dx=True)))
     _DACT_CHOICE[key] = fused < plain
+    _DACT_TIMES[key] = (fused, plain)
     return _DACT_CHOICE[key]
+
+
+def dact_report() -> str:
+    """One line per input-gradient GEMM that could fuse the activation
+    gradient: fused (gemmt / gemmp epilogue) vs plain GEMM + colsum_act, ms."""
+    return "\n".join(f"dact g{list(k[0])} W{list(k[1])} act={k[2]} bias={int(k[3])} -> "
+                     f"{'fused' if _DACT_CHOICE.get(k) else 'plain'}  fused:{f:.3f} plain:{p:.3f}"
+                     for k, (f, p) in _DACT_TIMES.items())
 
 
 @register("BATCHMATMUL", "MATMUL")

@@ -4,7 +4,8 @@ waits or barriers removed the results are garbage).  gemmp / gemmq (variants
 0 / 1) dbg bits: 1 = no vmcnt waits, 2 = no barriers.  gemmt (variant 3,
 NN / NT only, ``--gemmt``): 1 = no global loads in the loop, 2 = no LDS
 writes (the loads then die too), 4 = no mid-tile barrier, 8 = no epilogue,
-15 = all of them (MFMAs + fragment reads only), 16 = non-temporal epilogue stores.  Interleaved rounds in one
+15 = all of them (MFMAs + fragment reads only), 16 = non-temporal epilogue stores, 32 = C staged through
+LDS and stored as whole rows (a correct result: its error is reported).  Interleaved rounds in one
 process:  python tools/gemm_ablate.py [--gemmt]"""
 import json
 import os
@@ -33,7 +34,7 @@ def main():
             if ta:
                 continue
             cands["blaslt"] = lambda: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=out)
-            for dbg in (0, 8, 16):
+            for dbg in [int(x) for x in os.environ.get("GEMMT_DBG", "0,8,32").split(",")]:
                 cands[f"t_d{dbg}"] = lambda dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out, splits=sp,
                                                              variant=3, _dbg=dbg)
         else:
@@ -41,12 +42,19 @@ def main():
                 for dbg in (0, 1, 2, 3):
                     cands[f"v{v}_d{dbg}"] = lambda v=v, dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out,
                                                                          splits=sp, variant=v, _dbg=dbg)
+        errs = {}
+        if "--gemmt" in sys.argv:
+            ref = ((a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float()))
+            for k in ("t_d0", "t_d32"):
+                if k in cands:
+                    cands[k]()
+                    errs[k + "_err"] = round(((out.float() - ref).norm() / ref.norm()).item(), 5)
         times = {k: [] for k in cands}
         for _ in range(5):
             for k, f in cands.items():
                 times[k].append(timed(f, 10))
         fl = 2.0 * M * N * Kd
-        res = {"case": name}
+        res = {"case": name, **errs}
         for k in cands:
             res[k + "_TF"] = round(fl / statistics.median(times[k]) / 1e9, 1)
         print(json.dumps(res), flush=True)
