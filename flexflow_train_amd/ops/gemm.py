@@ -237,8 +237,10 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
         N = b.shape[0] if trans_b else b.shape[1]
         splits = {1}
         if bias is None and act == "none" and pre is None:
+            # powers of two around the grid-filling degree (K-tiles must split evenly)
             d = K.default_splits(M, N, Kd)
-            splits |= {s for s in (d // 2, d, d * 2) if 1 <= s <= max(1, Kd // 512) and (Kd // 64) % s == 0}
+            splits |= {s for s in (2, 4, 8, 16, 32)
+                       if d / 3 <= s <= 2 * d and s <= max(1, Kd // 512) and (Kd // 64) % s == 0}
         for s in sorted(splits):
             c[f"p:{s}"] = (lambda s_: (lambda *args: _gp(*args, splits=s_)))(s)
             if _GT_VARIANT and _gt_ok(bias, act, out, beta, pre):
