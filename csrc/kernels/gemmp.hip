@@ -521,7 +521,7 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
       n = 256;
     return std::max(8, n);
   }();
-  if (p.variant >= 1 && p.variant <= 5) {
+  if (p.variant >= 1 && p.variant <= 6) {
     // gemmr addresses its operands with 32-bit buffer offsets
     const uint64_t a_bytes = uint64_t(p.trans_a ? p.K : p.M) * uint64_t(p.lda) * 2u;
     const uint64_t b_bytes = uint64_t(p.trans_b ? p.N : p.K) * uint64_t(p.ldb) * 2u;

@@ -194,13 +194,26 @@ __device__ __forceinline__ bf16x8 row16(const unsigned char* img, int o0, int ks
   const int r = o0 + (lane & 15);
   return lds_read16(img, r * 128 + (t_slot128(r, ks * 4 + (lane >> 4)) << 4));
 }
+// ds_read_b64_tr_b16 hidden from the compiler's wait-count pass: with LDS-DMA
+// in flight it treats the intrinsic as a possible reader of the DMA target and
+// drains vmcnt(0) before every one (8 full drains per K-tile).  The caller
+// waits lgkmcnt itself before the first MFMA that consumes these registers.
+__device__ __forceinline__ bf16x4 lds_tr_asm(const unsigned char* base, int off) {
+  bf16x4 r;
+  const unsigned a = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
+      (const __attribute__((address_space(3))) unsigned char*)(base + off)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+template <bool ASM = false>
 __device__ __forceinline__ bf16x8 tr16(const unsigned char* img, int ks, int o0, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int col = o0 + 4 * (i & 3);
   const int r = ks * 32 + 8 * g + (i >> 2);
   const int oa = img_off<256>(r, col >> 3) + (col & 7) * 2;
   const int ob = img_off<256>(r + 4, col >> 3) + (col & 7) * 2;
-  return cat44(lds_tr(img, oa), lds_tr(img, ob));  // intrinsic: no LDS-DMA here to be drained
+  if (ASM) return cat44(lds_tr_asm(img, oa), lds_tr_asm(img, ob));
+  return cat44(lds_tr(img, oa), lds_tr(img, ob));
 }
 
 // kEpiPlain: bf16 C = alpha * AB (16-B paired stores); kEpiGeneral: fp32
@@ -439,7 +452,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* l
 }
 
 // STG: 0 = both operands staged through registers; 1 = B by LDS-DMA (issued
-// in phase B, two phases ahead of its first read), A through registers
+// in phase B, two phases ahead of its first read), A through registers; 2 =
+// both by LDS-DMA (no staging registers, no ds_write in the loop)
 // DBG (timing ablations only, results are garbage): 1 = no global loads in
 // the loop, 2 = no LDS writes in the loop, 4 = no mid-tile barrier, 8 = no
 // epilogue
@@ -478,7 +492,15 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   constexpr int NDV = !TB ? 4 : 2;  // B DMA voffsets (K-outer: by i & 3, K-contiguous: by i & 1)
   unsigned dvB[NDV];
 #pragma unroll
-  for (int i = 0; i < NDV; ++i) dvB[i] = STG == 1 ? dma_voff<!TB>(g.ldb, n0, i, wave, lane) : 0u;
+  for (int i = 0; i < NDV; ++i) dvB[i] = STG >= 1 ? dma_voff<!TB>(g.ldb, n0, i, wave, lane) : 0u;
+  constexpr int NDA = TA ? 4 : 2;   // A DMA voffsets (STG 2)
+  unsigned dvA[NDA];
+#pragma unroll
+  for (int i = 0; i < NDA; ++i) dvA[i] = STG == 2 ? dma_voff<TA>(g.lda, m0, i, wave, lane) : 0u;
+  auto dsoffA = [&](int i) -> unsigned {
+    return TA ? static_cast<unsigned>(4 * (i - (i & 3))) * static_cast<unsigned>(g.lda) * 2u
+              : static_cast<unsigned>(8 * (i - (i & 1))) * static_cast<unsigned>(g.lda) * 2u;
+  };
   // scalar part of B DMA piece i's offset (rows beyond piece i % NDV's)
   auto dsoffB = [&](int i) -> unsigned {
     return !TB ? static_cast<unsigned>(4 * (i - (i & 3))) * static_cast<unsigned>(g.ldb) * 2u
@@ -490,6 +512,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   auto gload = [&](int kt) {  // issue the register-staged global loads of K-tile kt
     const unsigned ka = static_cast<unsigned>(kt) * kstepA;
     const unsigned kb = static_cast<unsigned>(kt) * kstepB;
+    if (STG == 2) return;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       R[i] = __builtin_amdgcn_raw_buffer_load_b128(
@@ -502,6 +525,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     }
   };
   auto swrite = [&](unsigned char* buf) {  // R -> LDS image of one K-tile
+    if (STG == 2) return;
 #pragma unroll
     for (int i = 0; i < 8; ++i) *reinterpret_cast<i32x4t*>(buf + stage_lds<TA>(i, tid)) = R[i];
     if (STG == 0) {
@@ -513,14 +537,18 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     const unsigned kb = static_cast<unsigned>(kt) * kstepB + dsoffB(i);
     dma16(rB, buf + 2 * HALF + (wave * 8 + i) * 1024, dvB[i % NDV], __builtin_amdgcn_readfirstlane(kb));
   };
+  auto dmaA = [&](unsigned char* buf, int kt, int i) {  // A DMA piece i of K-tile kt into buf (STG 2)
+    const unsigned ka = static_cast<unsigned>(kt) * kstepA + dsoffA(i);
+    dma16(rA, buf + (wave * 8 + i) * 1024, dvA[i % NDA], __builtin_amdgcn_readfirstlane(ka));
+  };
 
   // ---- fragments
   auto rdA = [&](const unsigned char* buf, int mb, int ks) -> bf16x8 {
-    return TA ? tr16(buf + wm * HALF, ks, mb * 16, lane) : row16(buf, wm * 128 + mb * 16, ks, lane);
+    return TA ? tr16<STG >= 1>(buf + wm * HALF, ks, mb * 16, lane) : row16(buf, wm * 128 + mb * 16, ks, lane);
   };
   auto rdB = [&](const unsigned char* buf, int nb, int ks) -> bf16x8 {
     const unsigned char* b = buf + 2 * HALF;
-    return TB ? row16(b, wn * 128 + nb * 16, ks, lane) : tr16(b + wn * HALF, ks, nb * 16, lane);
+    return TB ? row16(b, wn * 128 + nb * 16, ks, lane) : tr16<STG >= 1>(b + wn * HALF, ks, nb * 16, lane);
   };
 
   f32x4t acc[8][8];
@@ -534,9 +562,12 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
 
   // ---- prologue: tile 0 -> buffer 0, tile 1 in flight, k-step 0 fragments
   gload(kt0);
-  if (STG == 1) {
+  if (STG >= 1) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dmaB(smem, kt0, i);
+    for (int i = 0; i < 8; ++i) {
+      if (STG == 2) dmaA(smem, kt0, i);
+      dmaB(smem, kt0, i);
+    }
   }
   swrite(smem);
   gload(kt0 + 1);
@@ -544,6 +575,14 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
     for (int i = 0; i < 8; ++i) dmaB(smem + BUFT, kt0 + 1, i);
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // B of tile 0 landed (A / B of tile 1 in flight)
+  }
+  if (STG == 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      dmaA(smem + BUFT, kt0 + 1, i);
+      dmaB(smem + BUFT, kt0 + 1, i);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (tile 1 in flight)
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -569,6 +608,9 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     unsigned char* nxt = smem + ((kt + 1) & 1) * BUFT;
     const unsigned ka = static_cast<unsigned>(kt0 + kt + 2) * kstepA;
     const unsigned kb = static_cast<unsigned>(kt0 + kt + 2) * kstepB;
+    // asm-issued transposed reads (STG 1) are invisible to the compiler's
+    // counters: the k-step 0 fragments of the previous phase B land here
+    if (STG >= 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // ---- phase A: k-step 0 (fa, fbx) | read k-step 1 into (fa, fby), stage tile kt+1, load tile kt+2
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb) {
@@ -580,7 +622,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       // LDS writes + refills: STG 0: chunks 2mb, 2mb+1 (A chunks for mb < 4,
       // B after); STG 1: A chunk mb
 #pragma unroll
-      for (int h = 0; h < (STG == 1 ? 1 : 2); ++h) {
+      for (int h = 0; h < (STG == 2 ? 0 : STG == 1 ? 1 : 2); ++h) {
         const int c = STG == 1 ? mb : 2 * mb + h;
         if (c < 8) {
           if (!(DBG & 2)) *reinterpret_cast<i32x4t*>(nxt + stage_lds<TA>(c, tid)) = R[c];
@@ -597,11 +639,16 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       // one memory instruction between MFMAs (an MFMA leaves the SIMD's issue
       // free for 8 of its 16 cycles); the fragment re-reads go last, after
       // the group's final use of fa[mb]
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      if (STG == 0) {
+      if (STG == 2) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      if (STG == 2) {
+      } else if (STG == 0) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -614,6 +661,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     }
     __builtin_amdgcn_sched_barrier(0);
     if (STG == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // B of tile kt+1 landed
+    if (STG == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (nothing newer in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // k-step 1 reads + LDS writes done
     if (!(DBG & 4)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -625,7 +673,8 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
       fa[mb] = rdA(nxt, mb, 0);
       fbx[mb] = rdB(nxt, mb, 0);
-      if (STG == 1) dmaB(cur, kt0 + kt + 2, mb);  // tile kt's buffer: its reads retired at the barrier
+      if (STG == 2) dmaA(cur, kt0 + kt + 2, mb);
+      if (STG >= 1) dmaB(cur, kt0 + kt + 2, mb);  // tile kt's buffer: its reads retired at the barrier
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -927,7 +976,10 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
     else if (!p.trans_a && p.trans_b) launch_pers<false, true>(g, pgrid, block, epi, p.act, st);
     else if (p.trans_a && !p.trans_b) launch_pers<true, false>(g, pgrid, block, epi, p.act, st);
     else launch_pers<true, true>(g, pgrid, block, epi, p.act, st);
-  } else if (stage_mode == 1) {
+  } else if (stage_mode == 3 && !p.trans_a) {   // both operands by LDS-DMA (NN / NT)
+    if (!p.trans_b) launch_t<false, false, 2>(g, grid, block, epi, p.act, st);
+    else launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
+  } else if (stage_mode == 1 || stage_mode == 3) {
     if (!p.trans_a && !p.trans_b) launch_t<false, false, 1>(g, grid, block, epi, p.act, st);
     else if (!p.trans_a && p.trans_b) launch_t<false, true, 1>(g, grid, block, epi, p.act, st);
     else if (p.trans_a && !p.trans_b) launch_t<true, false, 1>(g, grid, block, epi, p.act, st);

@@ -112,7 +112,7 @@ struct GemmPParams {
   float alpha = 1.f, beta = 0.f;
   int out_f32 = 0, splits = 1;
   int dbg = 0;                  // ablation bits for timing experiments (gemmp.hip)
-  int variant = 0;              // 0: 32x32x16 MFMA (gemmp.hip), 1: 16x16x32 (gemmq.hip), 2: ping-pong (gemmr.hip), 5: persistent gemmt,
+  int variant = 0;              // 0: 32x32x16 MFMA (gemmp.hip), 1: 16x16x32 (gemmq.hip), 2: ping-pong (gemmr.hip), 5: persistent gemmt, 6: gemmt with both operands by LDS-DMA,
                                 // 3 / 4: one wave per SIMD, 128x128 wave tile, B staged
                                 // through registers / by LDS-DMA (gemmt.hip)
 };

@@ -119,9 +119,12 @@ _DACT_TIMES = {}
 
 def _dact_variant(act: str) -> int:
     """The fused activation-gradient GEMM runs on gemmt (one wave per SIMD,
-    128x128 wave tiles) for the activations it instantiates, else on gemmp."""
-    from .gemm import _GT_VARIANT
-    return _GT_VARIANT if _GT_VARIANT and act in ("relu", "gelu") else 0
+    128x128 wave tiles, operands staged by LDS-DMA) for the activations it
+    instantiates, else on gemmp."""
+    from .gemm import _GT_DMA, _GT_VARIANT
+    if not _GT_VARIANT or act not in ("relu", "gelu"):
+        return 0
+    return 6 if _GT_DMA else _GT_VARIANT   # both operands by LDS-DMA (the dact GEMM is NT)
 
 
 def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:

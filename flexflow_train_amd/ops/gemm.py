@@ -13,7 +13,8 @@ torch.mm / addmm) is the plain library GEMM.  ``FF_GEMM`` selects:
   256² LDS-DMA kernel (csrc/kernels/gemm256.hip) and the phase-pipelined
   persistent 256² kernel (``p:s``, csrc/kernels/gemmp.hip, fused bias /
   activation / pre-activation epilogue) and the one-wave-per-SIMD 128x128
-  wave-tile kernel (``t:s``, csrc/kernels/gemmt.hip, same epilogues) at
+  wave-tile kernel (``t:s``, csrc/kernels/gemmt.hip, same epilogues; ``u:s``
+  is the same kernel with B staged by LDS-DMA, ``w:s`` with both) at
   several split-K degrees (the long-K weight-gradient GEMMs are where split-K
   and gemmt win); the 256² LDS-DMA kernel only with FF_GEMM256=1;
 * ``hip``: always the MFMA kernel; ``blas``: always hipBLASLt.
@@ -157,14 +158,19 @@ def _gp(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
                    splits=splits)
 
 
-# gemmp.hip family variant of the one-wave-per-SIMD kernel (gemmt.hip): 3 =
-# both operands staged through registers, 4 = B by LDS-DMA
+# gemmp.hip family variants of the one-wave-per-SIMD kernel (gemmt.hip): 3 =
+# both operands staged through registers ("t:" candidates), 4 = B by LDS-DMA
+# ("u:", 4-8 % faster on most forward / input-gradient shapes), 6 = both by
+# LDS-DMA ("w:", NN / NT only: forward GEMMs at hipBLASLt parity;
+# profiles/gemm_ab_gemmt_dma_r3.jsonl, gemm_ab_gemmt_dma2_r3.jsonl); 0
+# disables all three
 _GT_VARIANT = int(os.environ.get("FF_GEMMT_VARIANT", "3"))
+_GT_DMA = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_DMA", "1") != "0"
 
 
-def _gt(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
+def _gt(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1, variant=None):
     return K.gemmp(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
-                   splits=splits, variant=_GT_VARIANT)
+                   splits=splits, variant=_GT_VARIANT if variant is None else variant)
 
 
 def _gt_ok(bias, act, out, beta, pre) -> bool:
@@ -245,6 +251,10 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
             c[f"p:{s}"] = (lambda s_: (lambda *args: _gp(*args, splits=s_)))(s)
             if _GT_VARIANT and _gt_ok(bias, act, out, beta, pre):
                 c[f"t:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_)))(s)
+                if _GT_DMA:
+                    c[f"u:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=4)))(s)
+                    if not trans_a:
+                        c[f"w:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=6)))(s)
     return c
 
 
@@ -304,7 +314,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
         choice = "hip"
-    if choice[:2] in ("p:", "t:") and not K.gemmp_supported(a, b, trans_a, trans_b):
+    if choice[:2] in ("p:", "t:", "u:", "w:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -326,6 +336,10 @@ def _resolve(name: str):
         return lambda *args: _gp(*args, splits=int(arg))
     if kind == "t":
         return lambda *args: _gt(*args, splits=int(arg))
+    if kind == "u":
+        return lambda *args: _gt(*args, splits=int(arg), variant=4)
+    if kind == "w":
+        return lambda *args: _gt(*args, splits=int(arg), variant=6)
     return lambda *args: _hip256(*args, splits=int(arg))
 
 

@@ -260,8 +260,8 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5], ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128",
-                                                           "wave128dma", "wave128pers"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6], ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128",
+                                                              "wave128dma", "wave128pers", "wave128dma2"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1),
@@ -269,8 +269,8 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
                                             (4096, 4352, 128, 1), (2048, 2048, 1024, 8)])
 def test_gemmp(ta, tb, M, N, Kd, splits, variant):
     """Phase-pipelined persistent GEMM (gemmp.hip; variant 1 = gemmq.hip on
-    16x16x32 MFMAs, variant 2 = gemmr.hip ping-pong schedule, 3-5 = gemmt.hip
-    one wave per SIMD: register / LDS-DMA staging, persistent): plain / beta / split-K, the fused
+    16x16x32 MFMAs, variant 2 = gemmr.hip ping-pong schedule, 3-6 = gemmt.hip
+    one wave per SIMD: register / B by LDS-DMA staging, persistent, both by LDS-DMA): plain / beta / split-K, the fused
     bias+activation+pre-activation epilogue and the activation-gradient +
     bias-gradient epilogue, against fp32 torch."""
     import functools

@@ -85,6 +85,7 @@ def main():
             cands[f"t{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=3)
             cands[f"u{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=4)
             cands[f"v{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=5)
+            cands[f"w{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=6)
         if args.cands:
             keep = args.cands.split(",")
             cands = {k: v for k, v in cands.items() if k == "blaslt" and "blaslt" in keep
