@@ -976,10 +976,12 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
     else if (!p.trans_a && p.trans_b) launch_pers<false, true>(g, pgrid, block, epi, p.act, st);
     else if (p.trans_a && !p.trans_b) launch_pers<true, false>(g, pgrid, block, epi, p.act, st);
     else launch_pers<true, true>(g, pgrid, block, epi, p.act, st);
-  } else if (stage_mode == 3 && !p.trans_a) {   // both operands by LDS-DMA (NN / NT)
-    if (!p.trans_b) launch_t<false, false, 2>(g, grid, block, epi, p.act, st);
-    else launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
-  } else if (stage_mode == 1 || stage_mode == 3) {
+  } else if (stage_mode == 3) {   // both operands by LDS-DMA
+    if (!p.trans_a && !p.trans_b) launch_t<false, false, 2>(g, grid, block, epi, p.act, st);
+    else if (!p.trans_a && p.trans_b) launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
+    else if (p.trans_a && !p.trans_b) launch_t<true, false, 2>(g, grid, block, epi, p.act, st);
+    else launch_t<true, true, 2>(g, grid, block, epi, p.act, st);
+  } else if (stage_mode == 1) {
     if (!p.trans_a && !p.trans_b) launch_t<false, false, 1>(g, grid, block, epi, p.act, st);
     else if (!p.trans_a && p.trans_b) launch_t<false, true, 1>(g, grid, block, epi, p.act, st);
     else if (p.trans_a && !p.trans_b) launch_t<true, false, 1>(g, grid, block, epi, p.act, st);

@@ -161,9 +161,10 @@ def _gp(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
 # gemmp.hip family variants of the one-wave-per-SIMD kernel (gemmt.hip): 3 =
 # both operands staged through registers ("t:" candidates), 4 = B by LDS-DMA
 # ("u:", 4-8 % faster on most forward / input-gradient shapes), 6 = both by
-# LDS-DMA ("w:", NN / NT only: forward GEMMs at hipBLASLt parity;
-# profiles/gemm_ab_gemmt_dma_r3.jsonl, gemm_ab_gemmt_dma2_r3.jsonl); 0
-# disables all three
+# LDS-DMA ("w:": forward GEMMs at hipBLASLt parity, weight gradients 7-10 %
+# past register staging; profiles/gemm_ab_gemmt_dma_r3.jsonl,
+# gemm_ab_gemmt_dma2_r3.jsonl, gemm_ab_gemmt_dma2_dw_r3.jsonl); 0 disables all
+# three
 _GT_VARIANT = int(os.environ.get("FF_GEMMT_VARIANT", "3"))
 _GT_DMA = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_DMA", "1") != "0"
 
@@ -253,8 +254,7 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
                 c[f"t:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_)))(s)
                 if _GT_DMA:
                     c[f"u:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=4)))(s)
-                    if not trans_a:
-                        c[f"w:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=6)))(s)
+                    c[f"w:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=6)))(s)
     return c
 
 
