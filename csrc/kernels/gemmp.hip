@@ -503,7 +503,16 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
     throw std::invalid_argument("gemmp: the activation-gradient epilogue needs aux and an activation");
   const int nk = p.K / TK;
   int splits = std::max(1, std::min(p.splits, nk));
-  while (nk % splits) --splits;  // every work item streams the same number of K-tiles
+  // gemmr / gemmt address their operands with 32-bit buffer offsets
+  const uint64_t a_bytes = uint64_t(p.trans_a ? p.K : p.M) * uint64_t(p.lda) * 2u;
+  const uint64_t b_bytes = uint64_t(p.trans_b ? p.N : p.K) * uint64_t(p.ldb) * 2u;
+  const bool small = a_bytes < (1ull << 32) && b_bytes < (1ull << 32);
+  // the non-persistent gemmt spreads the remainder K-tiles over the first
+  // splits (QKV dW: 48 tiles x 5 splits = 240 workgroups); every other
+  // kernel streams the same number of K-tiles per work item
+  const bool uneven = (p.variant == 3 || p.variant == 4 || p.variant == 6) && small && gemmt_supported(p);
+  if (!uneven)
+    while (nk % splits) --splits;
   if (splits > 1) {
     if (p.bias || p.pre || p.act || p.dbias)
       throw std::invalid_argument("gemmp: split-K has no bias / activation / dbias epilogue");
@@ -522,10 +531,6 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
     return std::max(8, n);
   }();
   if (p.variant >= 1 && p.variant <= 6) {
-    // gemmr addresses its operands with 32-bit buffer offsets
-    const uint64_t a_bytes = uint64_t(p.trans_a ? p.K : p.M) * uint64_t(p.lda) * 2u;
-    const uint64_t b_bytes = uint64_t(p.trans_b ? p.N : p.K) * uint64_t(p.ldb) * 2u;
-    const bool small = a_bytes < (1ull << 32) && b_bytes < (1ull << 32);
     if (p.variant == 2 && small) gemmr_launch(p, splits, n_cu, st);
     else if (p.variant >= 3 && small && gemmt_supported(p))
       gemmt_launch(p, splits, p.variant - 3, st);

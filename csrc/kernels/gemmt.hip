@@ -477,8 +477,10 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   const int gsize = min(gm - first_m, GROUP);
   const int m0 = (first_m + (t % per_group) % gsize) * TM;
   const int n0 = ((t % per_group) / gsize) * TN;
-  const int L = g.K / TK / g.splits;
-  const int kt0 = split * L;
+  // K-tiles of this split: the remainder goes one each to the first splits
+  const int KT = g.K / TK, Lb = KT / g.splits, rem = KT % g.splits;
+  const int L = Lb + (split < rem ? 1 : 0);
+  const int kt0 = split * Lb + min(split, rem);
 
   // ---- global staging (A: KOUTER = TA, B: KOUTER = !TB)
   const __amdgpu_buffer_rsrc_t rA =
@@ -961,7 +963,7 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
                   : (p.out_f32 || p.beta != 0.f || p.alpha != 1.f) ? kEpiGeneral
                                                                    : kEpiPlain;
   const int L = p.K / TK / splits;
-  if (stage_mode == 2 && L >= 2) {
+  if (stage_mode == 2 && L >= 2 && (p.K / TK) % splits == 0) {
     static int n_cu = [] {
       int dev = 0, n = 0;
       if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=

@@ -242,14 +242,19 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
             bias, act, out, beta, pre):
         M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
         N = b.shape[0] if trans_b else b.shape[1]
-        splits = {1}
+        splits, tsplits = {1}, {1}
         if bias is None and act == "none" and pre is None:
-            # powers of two around the grid-filling degree (K-tiles must split evenly)
+            # powers of two around the grid-filling degree (gemmp: K-tiles must
+            # split evenly); gemmt also takes uneven splits, so it adds the
+            # degrees that fill one or two waves of workgroups exactly
             d = K.default_splits(M, N, Kd)
-            splits |= {s for s in (2, 4, 8, 16, 32)
-                       if d / 3 <= s <= 2 * d and s <= max(1, Kd // 512) and (Kd // 64) % s == 0}
+            pow2 = {s for s in (2, 4, 8, 16, 32) if d / 3 <= s <= 2 * d and s <= max(1, Kd // 512)}
+            splits |= {s for s in pow2 if (Kd // 64) % s == 0}
+            tiles = ((M + 255) // 256) * ((N + 255) // 256)
+            tsplits |= pow2 | {s for s in (round(256 / tiles), round(512 / tiles)) if 2 <= s <= max(1, Kd // 512)}
         for s in sorted(splits):
             c[f"p:{s}"] = (lambda s_: (lambda *args: _gp(*args, splits=s_)))(s)
+        for s in sorted(tsplits):
             if _GT_VARIANT and _gt_ok(bias, act, out, beta, pre):
                 c[f"t:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_)))(s)
                 if _GT_DMA:

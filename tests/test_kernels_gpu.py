@@ -266,7 +266,9 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1),
                                             # more work items than CUs: the persistent kernels loop
-                                            (4096, 4352, 128, 1), (2048, 2048, 1024, 8)])
+                                            (4096, 4352, 128, 1), (2048, 2048, 1024, 8),
+                                            # 17 K-tiles over 5 splits: gemmt's uneven split (4,4,3,3,3)
+                                            (512, 768, 1088, 5)])
 def test_gemmp(ta, tb, M, N, Kd, splits, variant):
     """Phase-pipelined persistent GEMM (gemmp.hip; variant 1 = gemmq.hip on
     16x16x32 MFMAs, variant 2 = gemmr.hip ping-pong schedule, 3-6 = gemmt.hip
