@@ -48,6 +48,7 @@ struct AttnParams {
   float* lse;    // [B, H, Sq] log2-domain
   float* delta;  // [B, H, Sq]
   float *dbq, *dbk, *dbv;  // optional [H*D] projection-bias gradients (column sums of dq / dk / dv)
+  int64_t db_ld;           // > 0: dbq / dbk / dbv are per-32-row partial slabs with this row stride
   int B, H, Sq, Sk;
   float scale;       // softmax scale (1/sqrt(D) by default)
   float scale_log2;  // scale * log2(e)
@@ -118,6 +119,48 @@ struct TileLoader {
     }
   }
 };
+
+// Bias-gradient partials of a wave's 32-row output tile, without atomics: the
+// column sums over the 32 rows of each lane half as a reduce-scatter (each xor
+// step halves the live values: 31 shuffles for D = 64 instead of 160), then
+// one plain store per value into this wave's row of a partial slab (every
+// (row block, column) is written by exactly one wave; the host sums the
+// slab's rows).  Lane keeps k = (lane & 31) * NV / 32 + t, k = 16 dt + r.
+// m ? a : b for m = all ones / zero, one v_bfi_b32
+__device__ __forceinline__ float bfi_sel(unsigned m, float a, float b) {
+  float r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+template <int DT>
+__device__ __forceinline__ void bias_partial(const f32x16 (&acc)[DT], float mul, float* row, int lane) {
+  constexpr int NV = 16 * DT;
+  float v[NV];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[dt * 16 + r] = acc[dt][r];
+#pragma unroll
+  for (int st = 0; st < 5; ++st) {
+    const int o = 16 >> st, c = NV >> st;
+    const unsigned m = (lane & o) ? ~0u : 0u;
+#pragma unroll
+    for (int i = 0; i < c / 2; ++i) {
+      // bitwise selects in asm: as C selects hipcc turned the whole pass
+      // into dynamically indexed array reads (cmp / cndmask chains over all
+      // 32 values, 13k instructions, the kernels ran 2x slower)
+      const float send = bfi_sel(m, v[i], v[i + c / 2]);
+      const float keep = bfi_sel(m, v[i + c / 2], v[i]);
+      v[i] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  const int h = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < NV / 32; ++t) {
+    const int k = (lane & 31) * (NV / 32) + t, dt = k >> 4, r = k & 15;
+    row[dt * 32 + 8 * (r >> 2) + 4 * h + (r & 3)] = v[t] * mul;
+  }
+}
 
 // ===========================================================================
 // Forward
@@ -395,7 +438,13 @@ __global__ __launch_bounds__(256, (D == 64 ? 3 : 1)) void attn_bwd_dq_kernel(Att
     }
     __syncthreads();
   }
-  if (P.dbq) bias_colsum<DT>(dq, P.scale, P.dbq + hh * D, lane);
+  if (P.dbq && P.db_ld) {
+    if (qw < P.Sq)  // waves wholly past the sequence own no slab row
+      bias_partial<DT>(dq, P.scale, P.dbq + (static_cast<int64_t>(b) * ((P.Sq + 31) / 32) + qw / 32) * P.db_ld + hh * D,
+                     lane);
+  } else if (P.dbq) {
+    bias_colsum<DT>(dq, P.scale, P.dbq + hh * D, lane);
+  }
   if (q_ok) {
     bf16* row = P.dq + b * P.dq_sb + static_cast<int64_t>(q) * P.dq_ss + hh * P.dq_sh;
 #pragma unroll
@@ -571,8 +620,15 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
   }
 #pragma unroll
   for (int j = 0; j < NKT; ++j) {
-    if (P.dbk) bias_colsum<DT>(dk[j], P.scale, P.dbk + hh * D, lane);
-    if (P.dbv) bias_colsum<DT>(dv[j], 1.f, P.dbv + hh * D, lane);
+    if (P.db_ld) {
+      if (kw + 32 * j >= P.Sk) continue;
+      const int64_t roff = (static_cast<int64_t>(b) * ((P.Sk + 31) / 32) + (kw + 32 * j) / 32) * P.db_ld + hh * D;
+      if (P.dbk) bias_partial<DT>(dk[j], P.scale, P.dbk + roff, lane);
+      if (P.dbv) bias_partial<DT>(dv[j], 1.f, P.dbv + roff, lane);
+    } else {
+      if (P.dbk) bias_colsum<DT>(dk[j], P.scale, P.dbk + hh * D, lane);
+      if (P.dbv) bias_colsum<DT>(dv[j], 1.f, P.dbv + hh * D, lane);
+    }
   }
 #pragma unroll
   for (int j = 0; j < NKT; ++j) {
@@ -619,6 +675,7 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
   P.dbq = t.dbq;
   P.dbk = t.dbk;
   P.dbv = t.dbv;
+  P.db_ld = t.db_ld;
   P.B = B; P.H = H; P.Sq = Sq; P.Sk = Sk;
   P.scale = scale;
   P.scale_log2 = scale * 1.4426950408889634f;

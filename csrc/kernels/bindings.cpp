@@ -107,7 +107,7 @@ PYBIND11_MODULE(_ffkernels, m) {
   m.def("attention_bwd", [](py::tuple q, py::tuple k, py::tuple v, py::tuple o, py::tuple dout, py::tuple dq,
                             py::tuple dk, py::tuple dv, uintptr_t lse, uintptr_t delta, int B, int H, int Sq, int Sk,
                             int D, float scale, bool causal, uintptr_t st, uintptr_t dbq, uintptr_t dbk,
-                            uintptr_t dbv) {
+                            uintptr_t dbv, int64_t db_ld) {
     AttnTensors t;
     t.q = tview(q);
     t.k = tview(k);
@@ -122,11 +122,12 @@ PYBIND11_MODULE(_ffkernels, m) {
     t.dbq = F(dbq);
     t.dbk = F(dbk);
     t.dbv = F(dbv);
+    t.db_ld = db_ld;
     attention_bwd(t, B, H, Sq, Sk, D, scale, causal, S(st));
   }, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"), py::arg("dq"), py::arg("dk"),
         py::arg("dv"), py::arg("lse"), py::arg("delta"), py::arg("B"), py::arg("H"), py::arg("Sq"), py::arg("Sk"),
         py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("st"), py::arg("dbq") = 0, py::arg("dbk") = 0,
-        py::arg("dbv") = 0);
+        py::arg("dbv") = 0, py::arg("db_ld") = 0);
   m.def("gemm", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int M, int N, int K,
                    int lda, int ldb, int ldc, bool ta, bool tb, int act, float alpha, float beta, int out_f32,
                    uintptr_t st) {

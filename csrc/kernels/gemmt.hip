@@ -219,7 +219,8 @@ __device__ __forceinline__ bf16x8 tr16(const unsigned char* img, int ks, int o0,
 // kEpiPlain: bf16 C = alpha * AB (16-B paired stores); kEpiGeneral: fp32
 // output and / or beta != 0 (kept apart: its extra live registers in a shared
 // epilogue made the allocator shuttle accumulators through VGPRs in the loop)
-enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3, kEpiGeneral = 4 };
+// kEpiBias: bf16 C = AB + bias (no activation, no pre-activation copy)
+enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3, kEpiGeneral = 4, kEpiBias = 5 };
 
 // one v_cvt_pk_bf16_f32 per pair (per-element casts pack through perm/alignbit)
 __device__ __forceinline__ unsigned pack2(float a, float b) {
@@ -295,7 +296,7 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
   const int ncol0 = n0 + wn * 128;
   const int nbase = ncol0 + nl;
   // bf16 results (and pre-activations) go out through the paired 16-B path
-  constexpr bool WIDE = EPI == kEpiBiasAct || EPI == kEpiDact || EPI == kEpiPlain;
+  constexpr bool WIDE = EPI == kEpiBiasAct || EPI == kEpiDact || EPI == kEpiPlain || EPI == kEpiBias;
   float csum[8][4];
   if (EPI == kEpiDact) {
 #pragma unroll
@@ -305,7 +306,7 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
   }
   // bias of this lane's 32 columns, loaded once (not per row block)
   float bv[8][4];
-  if (EPI == kEpiBiasAct) {
+  if (EPI == kEpiBiasAct || EPI == kEpiBias) {
     if (g.bias) {
 #pragma unroll
       for (int nb = 0; nb < 8; ++nb) {
@@ -356,9 +357,12 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
       const bool ok = mok && n_raw < g.N;  // N % 8 == 0: a 4-group is all-in or all-out
       const int n = ok ? n_raw : min(n_raw, g.N - 4);
       const int64_t off = roff + n;
-      if (EPI == kEpiBiasAct || EPI == kEpiDact) {  // alpha 1 (gemmt_supported); element pairs
+      if (EPI == kEpiBiasAct || EPI == kEpiDact || EPI == kEpiBias) {  // alpha 1 (gemmt_supported); pairs
         f32x2t v[2] = {f32x2t{acc[mb][nb][0], acc[mb][nb][1]}, f32x2t{acc[mb][nb][2], acc[mb][nb][3]}};
-        if (EPI == kEpiBiasAct) {
+        if (EPI == kEpiBias) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) v[h] += f32x2t{bv[nb][2 * h], bv[nb][2 * h + 1]};
+        } else if (EPI == kEpiBiasAct) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             v[h] += f32x2t{bv[nb][2 * h], bv[nb][2 * h + 1]};
@@ -884,6 +888,9 @@ void launch_pers(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hi
     case kEpiBiasAct * 8 + 0:
       hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBiasAct, 0>), grid, block, 0, st, g);
       break;
+    case kEpiBias * 8:
+      hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBias, 0>), grid, block, 0, st, g);
+      break;
     case kEpiBiasAct * 8 + 1:
       hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBiasAct, 1>), grid, block, 0, st, g);
       break;
@@ -925,6 +932,7 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
     case kEpiBiasAct * 8 + 0:
       hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 0, S>), grid, block, 0, st, g);
       break;
+    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBias, 0, S>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 1:
       hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 1, S>), grid, block, 0, st, g);
       break;
@@ -959,6 +967,7 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
   dim3 grid(items), block(NTHREADS);
   const int epi = splits > 1                        ? kEpiSplit
                   : p.act_bwd                       ? kEpiDact
+                  : (p.bias && !p.pre && !p.act)    ? kEpiBias
                   : (p.bias || p.pre || p.act)      ? kEpiBiasAct
                   : (p.out_f32 || p.beta != 0.f || p.alpha != 1.f) ? kEpiGeneral
                                                                    : kEpiPlain;

@@ -68,6 +68,10 @@ struct AttnTensors {
   float* dbq = nullptr;
   float* dbk = nullptr;
   float* dbv = nullptr;
+  // > 0: dbq / dbk / dbv point at per-32-row partial slabs (row stride db_ld
+  // floats; dq rows b * ceil(Sq/32) + q/32, dk / dv rows b * ceil(Sk/32) +
+  // k/32, columns h * D + d) written without atomics; the caller sums rows
+  int64_t db_ld = 0;
 };
 void attention_fwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, float scale, bool causal,
                    hipStream_t st);

@@ -369,10 +369,13 @@ def attention_fwd(q, k, v, causal=False, scale=None, out=None):
     return out, lse
 
 
-def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None, dbias=None):
+def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None, dbias=None, dbias_atomic=False):
     """Flash-attention backward into dq / dk / dv.  ``dbias`` = optional
-    (dbq, dbk, dbv) fp32 [H*D] projection-bias gradients: the kernels add the
-    column sums of dq / dk / dv (over batch and sequence) in their epilogues."""
+    (dbq, dbk, dbv) fp32 [H*D] projection-bias gradients, accumulated with the
+    column sums of dq / dk / dv (over batch and sequence) computed in the
+    kernels' epilogues: by default each wave stores its 32-row partial into a
+    slab that one reduction then adds (no atomics); ``dbias_atomic`` uses
+    per-column fp32 atomics instead (round 2's form, 2x slower kernels)."""
     B, Sq, H, D = q.shape
     Sk = k.shape[1]
     for name, t, shp in (("o", o, (B, Sq, H, D)), ("do", do, (B, Sq, H, D)), ("dq", dq, (B, Sq, H, D)),
@@ -383,14 +386,28 @@ def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None, dbi
         raise ValueError("attention_bwd: bad lse")
     delta = torch.empty(B, H, Sq, device=q.device, dtype=torch.float32)
     sc = float(scale) if scale is not None else 1.0 / math.sqrt(D)
-    dbs = [0, 0, 0]
+    dbs, ld, slab = [0, 0, 0], 0, None
+    HD = H * D
     if dbias is not None:
+        for t in dbias:
+            if t is not None:
+                _check(t, "dbias", torch.float32, HD)
+        if dbias_atomic:
+            dbs = [t.data_ptr() if t is not None else 0 for t in dbias]
+        else:
+            nq, nk = (Sq + 31) // 32, (Sk + 31) // 32
+            slab = torch.empty(B * max(nq, nk), 3 * HD, device=q.device, dtype=torch.float32)
+            ld = 3 * HD
+            dbs = [slab.data_ptr() + 4 * i * HD if t is not None else 0 for i, t in enumerate(dbias)]
+    ext().attention_bwd(_view4(q), _view4(k), _view4(v), _view4(o), _view4(do), _view4(dq), _view4(dk), _view4(dv),
+                        lse.data_ptr(), delta.data_ptr(), B, H, Sq, Sk, D, sc, bool(causal), _stream(), *dbs, ld)
+    if slab is not None:
+        # every (row block, column) of the slab was written once; rows past a
+        # tensor's own row-block count (Sq != Sk) are not part of its sum
+        rows = (B * nq, B * nk, B * nk)
         for i, t in enumerate(dbias):
             if t is not None:
-                _check(t, "dbias", torch.float32, H * D)
-                dbs[i] = t.data_ptr()
-    ext().attention_bwd(_view4(q), _view4(k), _view4(v), _view4(o), _view4(do), _view4(dq), _view4(dk), _view4(dv),
-                        lse.data_ptr(), delta.data_ptr(), B, H, Sq, Sk, D, sc, bool(causal), _stream(), *dbs)
+                t.add_(slab[:rows[i], i * HD:(i + 1) * HD].sum(0))
     STATS["attention_bwd"] += 1
 
 

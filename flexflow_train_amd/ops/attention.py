@@ -29,11 +29,15 @@ from ..parallel import sequence as SP
 from .base import OpContext, OpImpl, acc_grad, register
 from .gemm import matmul, wgrad_matmul
 
-# q/k/v projection-bias gradients accumulated inside the attention backward
-# kernels (one atomic per column per wave) instead of one column-sum pass over
-# dQKV.  Off by default: at BERT-large shapes the atomics onto H*D addresses
-# made dK/dV 117 -> 220 us and dQ 76 -> 150 us per call, far more than the
-# ~25 us column-sum pass they replace (profiles/ab_attn_dbias_r2.txt).
+# q/k/v projection-bias gradients from the attention backward kernels'
+# epilogues instead of a separate column-sum pass over dQKV
+# (FF_ATTN_FUSED_DBIAS=1).  Round 2 did this with one fp32 atomic per column
+# per wave onto H*D addresses, which made dK/dV 117 -> 220 us and dQ 76 -> 150
+# us (profiles/ab_attn_dbias_r2.txt).  Round 3: each wave stores its 32-row
+# partial sums into a slab row (a reduce-scatter, no atomics) and one
+# reduction adds the slab; measured even with the 25 us pass it replaces
+# (BERT-large 723-727 vs 728 samples/s, profiles/ab_attn_dbias_slab_r3.txt),
+# so the pass stays the default.
 _FUSED_DBIAS = os.environ.get("FF_ATTN_FUSED_DBIAS", "0") == "1"
 
 

@@ -180,10 +180,11 @@ def _ref_attn(q, k, v, causal):
     return (p @ vf).transpose(1, 2)
 
 
+@pytest.mark.parametrize("dbias_atomic", [False, True], ids=["slab", "atomic"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("S", [512, 320])
-def test_attention_fwd_bwd(causal, D, S):
+def test_attention_fwd_bwd(causal, D, S, dbias_atomic):
     torch.manual_seed(6)
     B, H = 2, 4
     qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
@@ -196,7 +197,8 @@ def test_attention_fwd_bwd(causal, D, S):
     ref.backward(do.float())
     dqkv = torch.empty_like(qkv)
     dbias = [torch.full((H * D,), 0.25, device=DEV) for _ in range(3)]
-    K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal, dbias=dbias)
+    K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal, dbias=dbias,
+                    dbias_atomic=dbias_atomic)
     assert _rel(dqkv[:, :, 2], vf.grad) < 3e-2, "dV"
     assert _rel(dqkv[:, :, 1], kf.grad) < 3e-2, "dK"
     assert _rel(dqkv[:, :, 0], qf.grad) < 3e-2, "dQ"
@@ -295,6 +297,7 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         c2 = gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
         u = ref + bias.float()
+        assert _rel(gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias), u) < 1e-2   # bias only
         assert _rel(pre, u) < 1e-2
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
         aux = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)

@@ -1,0 +1,2 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && FF_ATTN_FUSED_DBIAS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_bert -o bert -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 3 > $GRAFT_REPO_ROOT/gpurun_out/prof_bert.log 2>&1

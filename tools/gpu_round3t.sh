@@ -1,0 +1,3 @@
+set -o pipefail
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.log 2>&1
