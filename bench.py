@@ -47,8 +47,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: 32 (BERT), 256 (ResNet-50), "
-                                                                   "1024 (DLRM), 8 (GPT-3 medium)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: 64 (BERT), 256 (ResNet-50), "
+                                                                   "1024 (DLRM), 16 (GPT-3 medium); sized for "
+                                                                   "288 GB of HBM per GPU (profiles/batch_sweep_r3.txt)")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--model", default="bert-large",
                     choices=["bert-large", "bert-base", "resnet50", "dlrm", "gpt3-medium"])
@@ -162,7 +163,7 @@ def _run_bert(args, world, rank, only_dp: bool):
     from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
     from flexflow_train_amd.ops.gemm import choices as gemm_choices
 
-    bpg = args.batch_per_gpu or 32
+    bpg = args.batch_per_gpu or 64
     global_batch = bpg * world
     mk = bert_large if args.model == "bert-large" else bert_base
     kw = dict(batch_size=global_batch, sequence_length=args.seq)
@@ -260,7 +261,7 @@ _ZOO = {
     "resnet50": ("resnet50", 256, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
     "dlrm": ("dlrm", 1024, dict(embedding_size=[1000000] * 8, sparse_feature_size=64, mlp_bot=[64, 512, 512, 64],
                                 mlp_top=[576, 1024, 1024, 1024, 1]), "sgd", {"tables": "8x1M", "sparse": 64}),
-    "gpt3-medium": ("gpt", 8, dict(hidden_size=1024, num_layers=24, num_heads=16, sequence_length=2048),
+    "gpt3-medium": ("gpt", 16, dict(hidden_size=1024, num_layers=24, num_heads=16, sequence_length=2048),
                     "adamw", {"seq_len": 2048, "layers": 24, "hidden": 1024}),
 }
 

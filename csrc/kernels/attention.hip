@@ -346,8 +346,12 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams P) {
 // dQ: query block resident (4 waves x 32 rows), loop over 64-key tiles.
 //   S^T = K Q^T ; P^T = exp2(S^T*c - lse) ; dP^T = V dO^T ;
 //   dS^T = P^T (dP^T - delta) ; dQ^T += K^T dS^T ; dQ = scale * dQ
+// D = 64: 3 waves per SIMD (168 VGPRs) non-causal; causal needs the mask
+// registers on top and spilled at 168 — a scratch reload inside the loop is a
+// VMEM op, and its vmcnt wait drained the next K / V tile's prefetch every
+// iteration — so the causal form runs 2 waves per SIMD without spills
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, (D == 64 ? 3 : 1)) void attn_bwd_dq_kernel(AttnParams P) {
+__global__ __launch_bounds__(256, (D == 64 ? (CAUSAL ? 2 : 3) : 1)) void attn_bwd_dq_kernel(AttnParams P) {
   constexpr int KS = D / 16, DT = D / 32, KV = 64;
   constexpr int TILE_BYTES = KV * D * 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];
@@ -466,8 +470,9 @@ __global__ __launch_bounds__(256, (D == 64 ? 3 : 1)) void attn_bwd_dq_kernel(Att
 // NKT = 2 (64 keys per wave): every Q / dO fragment read from LDS feeds two
 // key subtiles, halving LDS traffic per MFMA; slower in practice (register
 // pressure -> 1 wave/SIMD), kept behind FFK_ATTN_BWD_NKT=2 for experiments.
-template <int D, bool CAUSAL, int NKT>
+template <int D, bool CAUSAL, int NKT, bool PF = false>
 __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_dkdv_kernel(AttnParams P) {
+  static_assert(!PF || NKT == 1, "PF prefetch is written for one key subtile per wave");
   constexpr int KS = D / 16, DT = D / 32, QT = 64, KW = 32 * NKT;
   constexpr int TILE_BYTES = QT * D * 2;
   constexpr int STAGE = 2 * TILE_BYTES + 2 * QT * 4;  // Q, dO, lse, delta
@@ -508,25 +513,46 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
   const int t0 = CAUSAL ? (k_blk / QT) : 0;
 
   TileLoader<D, QT> ql, dl;
-  auto load_scalars = [&](unsigned char* stage, int q0) {
-    float* ls = reinterpret_cast<float*>(stage + 2 * TILE_BYTES);
-    float* ds = ls + QT;
-    if (threadIdx.x < QT) {
-      const int qq = q0 + threadIdx.x;
-      // row constants, pre-shaped to seed the S and dP accumulators (guide:
-      // "row constants as the initial accumulator"): S' = Q K^T - lse / c,
-      // dP' = dO V^T - delta, so p = exp2(c S') and dS = p dP' need no subtraction
-      ls[threadIdx.x] = qq < P.Sq ? -P.lse[static_cast<int64_t>(bh) * P.Sq + qq] * P.inv_scale_log2 : -INFINITY;
-      ds[threadIdx.x] = qq < P.Sq ? -P.delta[static_cast<int64_t>(bh) * P.Sq + qq] : 0.f;
+  // row constants of a query tile, pre-shaped to seed the S and dP
+  // accumulators (guide: "row constants as the initial accumulator"):
+  // S' = Q K^T - lse / c, dP' = dO V^T - delta, so p = exp2(c S') and
+  // dS = p dP' need no subtraction.  Fetched into registers with the tile's
+  // Q / dO loads (a whole tile ahead) and parked in LDS after the compute:
+  // loading them at the park point exposed one global-load latency per tile
+  // to all four waves through the barrier that follows.
+  // The raw values are kept until the park point and only then shaped: any
+  // arithmetic on them at the fetch makes the compiler wait for the load
+  // there, and vmcnt retires in order, so that wait would also drain the
+  // Q / dO tile loads issued just before.
+  float nls = 0.f, nds = 0.f;
+  bool nok = false;
+  auto fetch_scalars = [&](int q0) {
+    const int qq = q0 + threadIdx.x;
+    nok = threadIdx.x < QT && qq < P.Sq;
+    if (nok) {
+      nls = P.lse[static_cast<int64_t>(bh) * P.Sq + qq];
+      nds = P.delta[static_cast<int64_t>(bh) * P.Sq + qq];
     }
   };
-  if (t0 < n_q_tiles) {
-    ql.load(P.q, b, hh, t0 * QT, P.Sq);
-    dl.load(P.dout, b, hh, t0 * QT, P.Sq);
-    ql.store(smem);
-    dl.store(smem + TILE_BYTES);
-    load_scalars(smem, t0 * QT);
-  }
+  auto park_scalars = [&](unsigned char* stage) {
+    float* ls = reinterpret_cast<float*>(stage + 2 * TILE_BYTES);
+    if (threadIdx.x < QT) {
+      ls[threadIdx.x] = nok ? -nls * P.inv_scale_log2 : -INFINITY;
+      ls[QT + threadIdx.x] = nok ? -nds : 0.f;
+    }
+  };
+  // unconditional (rows past Sq load as zeros without touching memory): with
+  // an `if (t0 < n_q_tiles)` around it the compiler kept a CFG path from the
+  // K / V fragment loads above into the loop that skipped this block's
+  // vmcnt(0), so the first MFMA of EVERY iteration waited on vmcnt — and
+  // vmcnt retires in order, so that wait drained the next tile's prefetch
+  // right after issuing it (one exposed global-load latency per tile)
+  ql.load(P.q, b, hh, t0 * QT, P.Sq);
+  dl.load(P.dout, b, hh, t0 * QT, P.Sq);
+  fetch_scalars(t0 * QT);
+  ql.store(smem);
+  dl.store(smem + TILE_BYTES);
+  park_scalars(smem);
   __syncthreads();
 
   for (int t = t0; t < n_q_tiles; ++t) {
@@ -540,6 +566,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
     if (has_next) {
       ql.load(P.q, b, hh, q0 + QT, P.Sq);
       dl.load(P.dout, b, hh, q0 + QT, P.Sq);
+      fetch_scalars(q0 + QT);
     }
     const bool wave_active = !CAUSAL || (q0 + QT - 1 >= kw);
     const bool need_mask = (q0 + QT > P.Sq) || (CAUSAL && q0 < kw + KW - 1) || (kw + KW - 1 >= P.Sk);
@@ -547,6 +574,21 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         f32x16 s[NKT], dp[NKT];
+        // PF: every LDS fragment of this 32-query subtile is requested before
+        // the MFMAs that consume it — the row fragments of S / dP ahead of
+        // the first product, the transposed fragments of dV / dK under the
+        // S / dP products and the exp2 pass — instead of one read pair per
+        // MFMA pair, each waiting out the LDS latency (FFK_ATTN_BWD_PF)
+        [[maybe_unused]] bf16x8 qa_pf[PF ? KS : 1], da_pf[PF ? KS : 1];
+        [[maybe_unused]] bf16x8 tda_pf[PF ? 2 : 1][PF ? DT : 1], tqa_pf[PF ? 2 : 1][PF ? DT : 1];
+        if constexpr (PF) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const int off = lds_off<D>(qt * 32 + (lane & 31), 2 * ks + h);
+            qa_pf[ks] = lds_read16(Qt, off);
+            da_pf[ks] = lds_read16(Dt, off);
+          }
+        }
 #pragma unroll
         for (int j = 0; j < NKT; ++j)
 #pragma unroll
@@ -556,14 +598,29 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
             dp[j][r] = ds[ql_];
           }
         prio_hi(P);
+        if constexpr (PF) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int off = lds_off<D>(qt * 32 + (lane & 31), 2 * ks + h);
-          const bf16x8 qa = lds_read16(Qt, off), da = lds_read16(Dt, off);
+          for (int ks = 0; ks < KS; ++ks) {
+            s[0] = mfma32(qa_pf[ks], kf[0][ks], s[0]);
+            dp[0] = mfma32(da_pf[ks], vf[0][ks], dp[0]);
+          }
 #pragma unroll
-          for (int j = 0; j < NKT; ++j) {
-            s[j] = mfma32(qa, kf[j][ks], s[j]);
-            dp[j] = mfma32(da, vf[j][ks], dp[j]);
+          for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              tda_pf[st][dt] = tr_frag<D>(Dt, qt * 32 + 16 * st, dt, lane);
+              tqa_pf[st][dt] = tr_frag<D>(Qt, qt * 32 + 16 * st, dt, lane);
+            }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const int off = lds_off<D>(qt * 32 + (lane & 31), 2 * ks + h);
+            const bf16x8 qa = lds_read16(Qt, off), da = lds_read16(Dt, off);
+#pragma unroll
+            for (int j = 0; j < NKT; ++j) {
+              s[j] = mfma32(qa, kf[j][ks], s[j]);
+              dp[j] = mfma32(da, vf[j][ks], dp[j]);
+            }
           }
         }
         prio_lo(P);
@@ -598,8 +655,14 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
           }
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
-            const bf16x8 da = tr_frag<D>(Dt, qt * 32 + 16 * st, dt, lane);
-            const bf16x8 qa = tr_frag<D>(Qt, qt * 32 + 16 * st, dt, lane);
+            bf16x8 da, qa;
+            if constexpr (PF) {
+              da = tda_pf[st][dt];
+              qa = tqa_pf[st][dt];
+            } else {
+              da = tr_frag<D>(Dt, qt * 32 + 16 * st, dt, lane);
+              qa = tr_frag<D>(Qt, qt * 32 + 16 * st, dt, lane);
+            }
 #pragma unroll
             for (int j = 0; j < NKT; ++j) {
               dv[j][dt] = mfma32(da, pf[j], dv[j][dt]);
@@ -614,7 +677,7 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
       unsigned char* nxt = smem + ((t + 1 - t0) & 1) * STAGE;
       ql.store(nxt);
       dl.store(nxt + TILE_BYTES);
-      load_scalars(nxt, q0 + QT);
+      park_scalars(nxt);
     }
     __syncthreads();
   }
@@ -714,6 +777,16 @@ static void launch_dkdv(int nkt, dim3 grid, dim3 block, hipStream_t st, const At
       hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 2>), grid, block, 0, st, P);
       return;
     }
+  }
+  // default on: GPT causal shape 0.341 -> 0.333 ms, BERT within noise
+  // (profiles/ab_attn_bwd_pf_r3.txt); FFK_ATTN_BWD_PF=0 for the per-pair reads
+  static const int pf = [] {
+    const char* e = getenv("FFK_ATTN_BWD_PF");
+    return e ? atoi(e) : 1;
+  }();
+  if (pf) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 1, true>), grid, block, 0, st, P);
+    return;
   }
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 1>), grid, block, 0, st, P);
 }
