@@ -40,6 +40,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+if os.environ.get("FF_PKG_ROOT"):  # same-box A/B against a snapshot of the package (tools/gpu_*.sh)
+    sys.path.insert(0, os.path.abspath(os.environ["FF_PKG_ROOT"]))
 
 
 def main():
