@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   const int stride = gridDim.x * 4;
   for (int row0 = blockIdx.x * 4 + wave; row0 < M; row0 += 2 * stride) {
     const int rows[2] = {row0, row0 + stride};
-    float dv[2][C][8], sv[2][C][8];
+    float dv[2][C][8], sv[2][C][8], rv[2][C][8];
     float mean[2], rstd[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -227,6 +227,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       for (int c = 0; c < C; ++c) {
         Vec8<T>::load(dy + base + c * 512 + lane * 8, dv[k][c]);
         Vec8<T>::load(s + base + c * 512 + lane * 8, sv[k][c]);
+        // the residual-stream gradient is loaded with the row, not at the
+        // store after the two row reductions (a dependent HBM latency per
+        // row pair in a latency-bound kernel)
+        if (dres) Vec8<T>::load(dres + base + c * 512 + lane * 8, rv[k][c]);
       }
       if (!ok)
 #pragma unroll
@@ -265,10 +269,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         for (int i = 0; i < 8; ++i)
           o[i] = rstd[k] * (dv[k][c][i] * gm[c][i] - sum_g[k] - sv[k][c][i] * sum_gx[k]);
         if (dres) {
-          float r[8];
-          Vec8<T>::load(dres + base + c * 512 + lane * 8, r);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += r[i];
+          for (int i = 0; i < 8; ++i) o[i] += rv[k][c][i];
         }
         Vec8<T>::store(dx + base + c * 512 + lane * 8, o);
         if (ws_dx) {
