@@ -784,8 +784,8 @@ static void launch_dkdv(int nkt, dim3 grid, dim3 block, hipStream_t st, const At
     const char* e = getenv("FFK_ATTN_BWD_PF");
     return e ? atoi(e) : 1;
   }();
-  if (pf) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 1, true>), grid, block, 0, st, P);
+  if (pf && D == 64) {  // at D = 128 (one wave / SIMD) the prefetch registers spill
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 1, D == 64>), grid, block, 0, st, P);
     return;
   }
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, 1>), grid, block, 0, st, P);
