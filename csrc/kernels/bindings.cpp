@@ -83,6 +83,29 @@ PYBIND11_MODULE(_ffkernels, m) {
                        float momentum, float wd, int nesterov, float gs, uintptr_t st) {
     sgd_step(F(w), P(g), gdt, F(mom), P(wb), n, lr, momentum, wd, nesterov, gs, S(st));
   });
+  // tables: [(master, grad, grad_bf16, compute, idx, idx64, n_idx, rows, dim, scratch_off), ...]
+  m.def("sparse_sgd_rows", [](const std::vector<py::tuple>& tables, uintptr_t scratch, float step, uintptr_t st) {
+    SparseSgdArgs a{};
+    if (tables.size() > static_cast<size_t>(kMaxSparseTables))
+      throw std::invalid_argument("sparse_sgd_rows: too many tables");
+    a.nt = static_cast<int>(tables.size());
+    for (size_t i = 0; i < tables.size(); ++i) {
+      const py::tuple& t = tables[i];
+      if (t.size() != 10) throw std::invalid_argument("sparse_sgd_rows: table tuple must have 10 fields");
+      SparseSgdTable& d = a.t[i];
+      d.master = F(t[0].cast<uintptr_t>());
+      d.grad = P(t[1].cast<uintptr_t>());
+      d.grad_bf16 = t[2].cast<int>();
+      d.compute = P(t[3].cast<uintptr_t>());
+      d.idx = P(t[4].cast<uintptr_t>());
+      d.idx64 = t[5].cast<int>();
+      d.n_idx = t[6].cast<int64_t>();
+      d.rows = t[7].cast<int64_t>();
+      d.dim = t[8].cast<int>();
+      d.scratch_off = t[9].cast<int64_t>();
+    }
+    sparse_sgd_rows(a, F(scratch), step, S(st));
+  });
   m.def("sum_squares", [](uintptr_t x, int64_t n, uintptr_t out, uintptr_t st) {
     sum_squares(F(x), n, F(out), S(st));
   });

@@ -47,6 +47,22 @@ void adam_step(float* w, const void* g, int grad_dtype, float* m, float* v, void
 void sgd_step(float* w, const void* g, int grad_dtype, float* mom, void* w_bf16, int64_t n, float lr,
               float momentum, float weight_decay, int nesterov, float grad_scale, hipStream_t st);
 void sum_squares(const float* x, int64_t n, float* out, hipStream_t st);
+// row-sparse SGD over up to kMaxSparseTables embedding tables (two launches)
+constexpr int kMaxSparseTables = 16;
+struct SparseSgdTable {
+  float* master;       // [rows, dim] fp32
+  void* grad;          // [rows, dim] fp32 or bf16 (grad_bf16)
+  void* compute;       // optional [rows, dim] bf16 copy
+  const void* idx;     // [n_idx] int32 or int64 (idx64)
+  int64_t n_idx, rows, scratch_off;
+  int dim, grad_bf16, idx64;
+};
+struct SparseSgdArgs {
+  SparseSgdTable t[kMaxSparseTables];
+  int nt;
+};
+void sparse_sgd_rows(const SparseSgdArgs& a, float* scratch, float step, hipStream_t st);
+
 
 // ---- embedding.hip  (mode: 0 none, 1 sum, 2 avg)
 void embedding_fwd(int dtype, int index_bits, const void* idx, const void* W, void* out, int64_t B, int L, int D,

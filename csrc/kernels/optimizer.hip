@@ -179,6 +179,60 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+
+// ---------------------------------------------------------------------------
+// Row-sparse SGD over embedding tables (plain SGD: untouched rows have zero
+// gradient, so only the rows the step looked up change).  All tables of a
+// flat go in one launch pair instead of ~11 framework kernels per table:
+//   gather:  scratch[i] = master[r_i] - step * grad[r_i]       (reads only)
+//   scatter: master[r_i] = scratch[i]; compute[r_i] = bf16(..); grad[r_i] = 0
+// r_i = clamp(idx[i], 0, rows - 1).  A row looked up twice gets the same
+// value written twice (both gathers saw the pre-update row), which is why the
+// update is split across two launches: a single pass could read a row
+// another thread already updated or whose gradient it already cleared.
+template <typename GT, typename IT>
+__device__ __forceinline__ void sparse_rows_phase(const SparseSgdTable& t, float* scratch, float step, int phase) {
+  const int dim4 = t.dim >> 2;
+  const int64_t items = t.n_idx * dim4;
+  for (int64_t w = blockIdx.x * 256 + threadIdx.x; w < items; w += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t i = w / dim4;
+    const int c = static_cast<int>(w - i * dim4) * 4;
+    int64_t r = static_cast<int64_t>(static_cast<const IT*>(t.idx)[i]);
+    r = r < 0 ? 0 : (r >= t.rows ? t.rows - 1 : r);
+    const int64_t off = r * t.dim + c;
+    f32x4* sv = reinterpret_cast<f32x4*>(scratch + t.scratch_off + i * t.dim + c);
+    if (phase == 0) {
+      f32x4 W = *reinterpret_cast<const f32x4*>(t.master + off);
+      const f32x4 G = load_grad4<GT>(static_cast<const GT*>(t.grad) + off, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) W[k] -= step * G[k];
+      *sv = W;
+    } else {
+      const f32x4 W = *sv;
+      *reinterpret_cast<f32x4*>(t.master + off) = W;
+      if (t.compute) {
+        bf16x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = f2bf(W[k]);
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(t.compute) + off) = o;
+      }
+      if constexpr (sizeof(GT) == 4) *reinterpret_cast<f32x4*>(static_cast<float*>(t.grad) + off) = f32x4{};
+      else *reinterpret_cast<u16x4*>(static_cast<bf16*>(t.grad) + off) = u16x4{};
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sparse_sgd_kernel(SparseSgdArgs a, float* scratch, float step, int phase) {
+  const SparseSgdTable& t = a.t[blockIdx.y];
+  if (t.grad_bf16) {
+    if (t.idx64) sparse_rows_phase<bf16, int64_t>(t, scratch, step, phase);
+    else sparse_rows_phase<bf16, int32_t>(t, scratch, step, phase);
+  } else {
+    if (t.idx64) sparse_rows_phase<float, int64_t>(t, scratch, step, phase);
+    else sparse_rows_phase<float, int32_t>(t, scratch, step, phase);
+  }
+}
+
 static void need4(int64_t n, const char* w) {
   if (n % 4 != 0) throw std::invalid_argument(std::string(w) + ": flat buffer length must be a multiple of 4");
 }
@@ -225,6 +279,23 @@ void sgd_step(float* w, const void* g, int grad_dtype, float* mom, void* w_bf16,
     hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid), dim3(256), 0, st, w, static_cast<const float*>(g), mom,
                        static_cast<bf16*>(w_bf16), n / 4, lr, momentum, weight_decay, nesterov, grad_scale);
   FFK_LAUNCH_CHECK("sgd");
+}
+
+
+void sparse_sgd_rows(const SparseSgdArgs& a, float* scratch, float step, hipStream_t st) {
+  if (a.nt <= 0) return;
+  if (a.nt > kMaxSparseTables) throw std::invalid_argument("sparse_sgd: too many tables in one launch");
+  int64_t most = 0;
+  for (int i = 0; i < a.nt; ++i) {
+    const SparseSgdTable& t = a.t[i];
+    if (t.dim % 4 || t.rows <= 0) throw std::invalid_argument("sparse_sgd: row width must be a multiple of 4");
+    most = std::max(most, t.n_idx * (t.dim / 4));
+  }
+  if (most == 0) return;
+  const dim3 grid(static_cast<unsigned>(std::min<int64_t>((most + 255) / 256, 1024)), static_cast<unsigned>(a.nt));
+  hipLaunchKernelGGL(sparse_sgd_kernel, grid, dim3(256), 0, st, a, scratch, step, 0);
+  hipLaunchKernelGGL(sparse_sgd_kernel, grid, dim3(256), 0, st, a, scratch, step, 1);
+  FFK_LAUNCH_CHECK("sparse_sgd");
 }
 
 void sum_squares(const float* x, int64_t n, float* out, hipStream_t st) {

@@ -282,6 +282,36 @@ def sgd_step(w, g, mom, w_bf16, lr, momentum, weight_decay, nesterov, grad_scale
     STATS["sgd_step"] += 1
 
 
+def sparse_sgd_rows(tables, step: float) -> bool:
+    """Row-sparse SGD over embedding tables, two launches for all of them
+    (csrc/kernels/optimizer.hip sparse_sgd_kernel).  ``tables``: list of
+    (master [rows, dim] fp32, grad [rows, dim] fp32|bf16, compute [rows, dim]
+    bf16 or None, idx 1-D int32|int64).  master[r] -= step * grad[r];
+    compute[r] = bf16(master[r]); grad[r] = 0 for every looked-up row r
+    (clamped into range).  Returns False (nothing launched) when a table does
+    not meet the kernel's layout: the caller then takes the framework path."""
+    if not tables or len(tables) > 16:
+        return False
+    desc, off = [], 0
+    for m, g, c, idx in tables:
+        rows, dim = m.shape
+        ok = (m.dtype == torch.float32 and m.is_contiguous() and g.shape == m.shape and g.is_contiguous()
+              and g.dtype in (torch.float32, torch.bfloat16) and dim % 4 == 0 and idx.dim() == 1
+              and idx.dtype in (torch.int32, torch.int64) and idx.is_contiguous() and idx.is_cuda
+              and m.data_ptr() % 16 == 0 and g.data_ptr() % (16 if g.dtype == torch.float32 else 8) == 0
+              and (c is None or (c.dtype == torch.bfloat16 and c.shape == m.shape and c.is_contiguous()
+                                 and c.data_ptr() % 8 == 0)))
+        if not ok:
+            return False
+        desc.append((m.data_ptr(), g.data_ptr(), int(g.dtype == torch.bfloat16), 0 if c is None else c.data_ptr(),
+                     idx.data_ptr(), int(idx.dtype == torch.int64), idx.numel(), rows, dim, off))
+        off += idx.numel() * dim
+    scratch = torch.empty(max(off, 4), dtype=torch.float32, device=tables[0][0].device)
+    ext().sparse_sgd_rows(desc, _p(scratch), float(step), _stream())
+    STATS["sparse_sgd"] += 1
+    return True
+
+
 def sum_squares(x, out):
     _check(x, "x", torch.float32)
     _check(out, "out", torch.float32)

@@ -1327,12 +1327,26 @@ class Executor:
         value the dense update gives it -- capture-safe, no boolean mask)."""
         lr = f["opt"].cfg.lr if lr is None else lr
         f["opt"].step_num += 1
+        todo = []
         for p in f["params"]:
             if not p.trainable:
                 continue
             rows = self.steps[p.final_step].ctx.extra.pop("touched_rows", None)
-            if not rows:
-                continue
+            if rows:
+                todo.append((p, rows))
+        from .. import kernels as K
+        if todo and todo[0][0].master.is_cuda and K.available():
+            # every table of the flat in one native launch pair (the framework
+            # path below is ~11 kernels per table)
+            tabs = []
+            for p, rows in todo:
+                n = p.grad.shape[0]
+                idx = rows[0] if len(rows) == 1 else torch.cat([r.to(torch.long) for r in rows])
+                c = None if p.compute is p.master else p.compute.view(n, -1)
+                tabs.append((p.master.view(n, -1), p.grad.view(n, -1), c, idx.reshape(-1)))
+            if K.sparse_sgd_rows(tabs, lr * scale):
+                return
+        for p, rows in todo:
             n = p.grad.shape[0]
             idx = torch.cat([r.to(torch.long) for r in rows]).clamp_(0, n - 1)
             m2, g2 = p.master.view(n, -1), p.grad.view(n, -1)

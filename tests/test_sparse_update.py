@@ -114,7 +114,11 @@ def _gpu_pair(steps_eager=2, replays=3, rows=4096, dim=64, batch=256, bag=4):
 
 @pytest.mark.gpu
 def test_sparse_matches_dense_gpu_eager_and_graphed():
+    from flexflow_train_amd import kernels as K
+
+    n0 = K.STATS["sparse_sgd"]
     out = _gpu_pair()
+    assert K.STATS["sparse_sgd"] > n0, "the native row-sparse SGD did not run"
     ex_s = out[True][0]
     assert any(f["sparse"] for f in ex_s.flats), "embedding table not on the sparse path"
     assert ex_s.cfg.device.type == "cuda"
@@ -127,3 +131,37 @@ def test_sparse_matches_dense_gpu_eager_and_graphed():
     f = next(f for f in ex_s.flats if f["sparse"])
     p = f["params"][0]
     torch.testing.assert_close(p.compute.float(), p.master.to(torch.bfloat16).float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("idt", [torch.int32, torch.int64])
+def test_sparse_sgd_rows_kernel(gdt, idt):
+    """The native two-launch row update against the framework formula: two
+    tables of different widths, repeated ids and ids outside the table."""
+    from flexflow_train_amd import kernels as K
+
+    dev = "cuda"
+    g = torch.Generator(device="cpu").manual_seed(5)
+    tabs, refs = [], []
+    for rows, dim, n in ((1000, 64, 700), (37, 16, 90)):
+        m = torch.randn(rows, dim, generator=g).to(dev)
+        gr = torch.randn(rows, dim, generator=g).to(dev, gdt)
+        c = m.to(torch.bfloat16)
+        idx = torch.randint(-3, rows + 5, (n,), generator=g)
+        idx[:10] = idx[10:20]
+        idx = idx.to(dev, idt)
+        r = idx.long().clamp(0, rows - 1)
+        want = m.clone()
+        want[r] = m[r] - 0.05 * gr[r].float()
+        wg = gr.clone()
+        wg[r] = 0
+        tabs.append((m, gr, c, idx))
+        refs.append((want, wg))
+    n0 = K.STATS["sparse_sgd"]
+    assert K.sparse_sgd_rows(tabs, 0.05)
+    assert K.STATS["sparse_sgd"] == n0 + 1
+    for (m, gr, c, _), (want, wg) in zip(tabs, refs):
+        torch.testing.assert_close(m, want, rtol=1e-6, atol=1e-6)  # the kernel may fuse the multiply-add
+        torch.testing.assert_close(c, m.to(torch.bfloat16), rtol=0, atol=0)
+        torch.testing.assert_close(gr, wg, rtol=0, atol=0)
