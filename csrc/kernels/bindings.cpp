@@ -153,9 +153,13 @@ PYBIND11_MODULE(_ffkernels, m) {
         py::arg("dbv") = 0, py::arg("db_ld") = 0);
   m.def("gemm", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int M, int N, int K,
                    int lda, int ldb, int ldc, bool ta, bool tb, int act, float alpha, float beta, int out_f32,
-                   uintptr_t st) {
-    gemm_bf16_ex(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32, S(st));
-  });
+                   uintptr_t st, int splits, uintptr_t ws) {
+    gemm_bf16_ex(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, out_f32, S(st),
+                 splits, F(ws));
+  }, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("pre"), py::arg("M"), py::arg("N"),
+     py::arg("K"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("ta"), py::arg("tb"), py::arg("act"),
+     py::arg("alpha"), py::arg("beta"), py::arg("out_f32"), py::arg("st"), py::arg("splits") = 1,
+     py::arg("ws") = 0);
   // ---- tensorops
   auto shape = [](const std::vector<int64_t>& v) {
     if (v.size() > 6) throw std::invalid_argument("tensorops: at most 6 dims");

@@ -43,6 +43,8 @@ struct GemmArgs {
   float alpha, beta;
   int act;
   int out_f32;
+  float* ws;   // split-K: fp32 partial slabs [splits][M][N] (epilogue applied by splitk_epi_kernel)
+  int splits;
 };
 
 __device__ __forceinline__ float apply_act(int act, float x) {
@@ -119,15 +121,19 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
-  const int nk = (g.K + BK - 1) / BK;
-  sa.load(g.A, g.lda, m0, g.M, 0, g.K);
-  sb.load(g.B, g.ldb, n0, g.N, 0, g.K);
+  // split-K: split blockIdx.y takes an (uneven) contiguous range of K-tiles
+  const int nk_all = (g.K + BK - 1) / BK;
+  const int sbase = nk_all / g.splits, srem = nk_all % g.splits, sp = blockIdx.y;
+  const int kt0 = sp * sbase + min(sp, srem);
+  const int nk = kt0 + sbase + (sp < srem ? 1 : 0);
+  sa.load(g.A, g.lda, m0, g.M, kt0 * BK, g.K);
+  sb.load(g.B, g.ldb, n0, g.N, kt0 * BK, g.K);
   sa.store(smem);
   sb.store(smem + IMG_BYTES);
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* Ai = smem + (kt & 1) * 2 * IMG_BYTES;
+  for (int kt = kt0; kt < nk; ++kt) {
+    const unsigned char* Ai = smem + ((kt - kt0) & 1) * 2 * IMG_BYTES;
     const unsigned char* Bi = Ai + IMG_BYTES;
     const bool has_next = kt + 1 < nk;
     if (has_next) {
@@ -150,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         for (int mt = 0; mt < 2; ++mt) acc[nt][mt] = mfma32(bf[nt], af[mt], acc[nt][mt]);
     }
     if (has_next) {
-      unsigned char* nxt = smem + ((kt + 1) & 1) * 2 * IMG_BYTES;
+      unsigned char* nxt = smem + ((kt + 1 - kt0) & 1) * 2 * IMG_BYTES;
       sa.store(nxt);
       sb.store(nxt + IMG_BYTES);
     }
@@ -159,6 +165,26 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 
   // ---- epilogue: acc[nt][mt] holds C^T; lane = m, registers = n
   const int h = lane >> 5;
+  if (g.splits > 1) {  // raw alpha * partial into this split's slab (N % 4 == 0, host-checked)
+    float* slab = g.ws + static_cast<int64_t>(sp) * g.M * g.N;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int m = m0 + wm * 64 + mt * 32 + (lane & 31);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int n = n0 + wn * 64 + nt * 32 + 8 * g4 + 4 * h;
+          if (n >= g.N) continue;
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = g.alpha * acc[nt][mt][4 * g4 + e];
+          *reinterpret_cast<f32x4*>(slab + static_cast<int64_t>(m) * g.N + n) = o;
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int m = m0 + wm * 64 + mt * 32 + (lane & 31);
@@ -226,12 +252,66 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   }
 }
 
+// Split-K finish with the full gemm epilogue: v = sum_s ws[s] + bias;
+// pre := v; v = act(v); C = v + beta * C.  Four columns per thread.
+__global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs g) {
+  const int64_t n4 = static_cast<int64_t>(g.M) * g.N / 4;
+  const int64_t slab = static_cast<int64_t>(g.M) * g.N;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t e0 = i * 4;
+    const int m = static_cast<int>(e0 / g.N), n = static_cast<int>(e0 % g.N);
+    f32x4 v = *reinterpret_cast<const f32x4*>(g.ws + e0);
+    for (int z = 1; z < g.splits; ++z) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(g.ws + z * slab + e0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += t[e];
+    }
+    if (g.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += bf2f(g.bias[n + e]);
+    }
+    const int64_t off = static_cast<int64_t>(m) * g.ldc + n;
+    if (g.pre) {
+      bf16x4 pv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pv[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x4*>(g.pre + off) = pv;
+    }
+    if (g.act) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = apply_act(g.act, v[e]);
+    }
+    if (g.out_f32) {
+      float* C = static_cast<float*>(g.C) + off;
+      f32x4 o;
+      if (g.beta != 0.f) o = *reinterpret_cast<f32x4*>(C);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = v[e] + (g.beta != 0.f ? g.beta * o[e] : 0.f);
+      *reinterpret_cast<f32x4*>(C) = o;
+    } else {
+      bf16* C = static_cast<bf16*>(g.C) + off;
+      if (g.beta != 0.f) {
+        const bf16x4 old = *reinterpret_cast<bf16x4*>(C);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += g.beta * bf2f(old[e]);
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x4*>(C) = o;
+    }
+  }
+}
+
 }  // namespace
 
 void gemm_bf16_ex(const void* A, const void* B, void* C, const void* bias, void* pre, int M, int N, int K, int lda,
                   int ldb, int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
-                  hipStream_t st) {
+                  hipStream_t st, int splits, float* ws) {
   if (M <= 0 || N <= 0 || K <= 0) return;
+  splits = std::max(1, std::min(splits, (K + BK - 1) / BK));
+  if (splits > 1 && (!ws || N % 4 || ldc % 4 || (reinterpret_cast<uintptr_t>(ws) & 15)))
+    throw std::invalid_argument("gemm: split-K needs a 16-byte aligned fp32 workspace and N % 4 == 0");
   // 16-byte global loads require 8-element aligned leading dims and
   // contiguous extents (checked here, on the host, before any launch).
   if (lda % 8 || ldb % 8) throw std::invalid_argument("gemm: lda/ldb must be multiples of 8");
@@ -243,14 +323,20 @@ void gemm_bf16_ex(const void* A, const void* B, void* C, const void* bias, void*
     throw std::invalid_argument("gemm: operands must be 16-byte aligned");
   if (ldc % 4 || (reinterpret_cast<uintptr_t>(C) & 7)) throw std::invalid_argument("gemm: C must be 8-byte aligned, ldc%4==0");
   GemmArgs g{static_cast<const bf16*>(A), static_cast<const bf16*>(B), C, static_cast<const bf16*>(bias),
-             static_cast<bf16*>(pre), M, N, K, lda, ldb, ldc, alpha, beta, act, out_f32};
+             static_cast<bf16*>(pre), M, N, K, lda, ldb, ldc, alpha, beta, act, out_f32, ws, splits};
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  dim3 grid(nwg), block(256);
+  dim3 grid(nwg, splits), block(256);
   if (!trans_a && !trans_b) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, st, g);
   else if (!trans_a && trans_b) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, block, 0, st, g);
   else if (trans_a && !trans_b) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, st, g);
   else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, st, g);
   FFK_LAUNCH_CHECK("gemm_bf16");
+  if (splits > 1) {
+    const int64_t n4 = static_cast<int64_t>(M) * N / 4;
+    const int rgrid = static_cast<int>(std::min<int64_t>((n4 + 255) / 256, 2048));
+    hipLaunchKernelGGL(splitk_epi_kernel, dim3(rgrid), dim3(256), 0, st, g);
+    FFK_LAUNCH_CHECK("gemm_bf16 split-K epilogue");
+  }
 }
 
 void gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,

@@ -100,9 +100,11 @@ void gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, i
                int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
                hipStream_t st);
 // Same, additionally storing the pre-activation (bf16, ldc) when `pre` != null.
+// splits > 1: split-K over blockIdx.y into `ws` ([splits][M][N] fp32), then one
+// pass applying the epilogue (small-M GEMMs that cannot fill 256 CUs).
 void gemm_bf16_ex(const void* A, const void* B, void* C, const void* bias, void* pre, int M, int N, int K, int lda,
                   int ldb, int ldc, bool trans_a, bool trans_b, int act, float alpha, float beta, int out_f32,
-                  hipStream_t st);
+                  hipStream_t st, int splits = 1, float* ws = nullptr);
 
 // ---- gemm256.hip: 256x256 tiles, LDS-DMA staging, split-K (fp32 partials
 // in `workspace` [splits][M][N] + reduce pass); needs K % 64 == 0.

@@ -442,10 +442,12 @@ def attention_bwd(q, k, v, o, lse, do, dq, dk, dv, causal=False, scale=None, dbi
 
 
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, beta=0.0, out=None,
-         out_dtype=None, pre=None):
+         out_dtype=None, pre=None, splits=1):
     """C = act(alpha * op(a) @ op(b) + bias) + beta * C with the MFMA GEMM.
 
     a: [M, K] (or [K, M] if trans_a), b: [K, N] (or [N, K] if trans_b), bf16.
+    ``splits`` > 1: split-K into an fp32 workspace, then one epilogue pass
+    (GEMMs whose 128x128 tiles cannot fill the chip, e.g. DLRM's MLPs).
     """
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise ValueError("gemm: operands must be bf16")
@@ -464,10 +466,16 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, b
         _check(bias, "bias", torch.bfloat16, N)
     if pre is not None:
         _check(pre, "pre", torch.bfloat16, M * N)
+    splits = max(1, min(int(splits), (K + 63) // 64))
+    if splits > 1 and (N % 4 or out.stride(0) % 4):
+        splits = 1
+    ws = _splitk_ws(a.device, splits * M * N) if splits > 1 else None
     ext().gemm(a.data_ptr(), b.data_ptr(), out.data_ptr(), _p(bias), _p(pre), M, N, K, a.stride(0), b.stride(0),
                out.stride(0), bool(trans_a), bool(trans_b), ACT_CODES[act], float(alpha), float(beta),
-               int(out.dtype == torch.float32), _stream())
+               int(out.dtype == torch.float32), _stream(), splits, _p(ws))
     STATS["gemm"] += 1
+    if splits > 1:
+        STATS["gemm_splitk"] += 1
     return out
 
 

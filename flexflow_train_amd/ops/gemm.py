@@ -24,7 +24,7 @@ On CPU everything is a torch matmul in the compute dtype.
 from __future__ import annotations
 
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -144,8 +144,20 @@ def _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre):
     return A @ B
 
 
-def _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre):
-    return K.gemm(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre)
+def _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
+    return K.gemm(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
+                  splits=splits)
+
+
+def _hip_splits(M: int, N: int, Kd: int) -> List[int]:
+    """Split-K degrees for the 128x128-tile kernel when its grid leaves most
+    of the 256 CUs idle (small-batch MLPs: a 1024x1024 output is 64 tiles):
+    the degrees that bring the grid to about one or two workgroups per CU,
+    keeping >= 2 K-tiles of 64 per split."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    if tiles >= 192 or N % 4:
+        return []
+    return sorted({s for s in (2, 4, 8, 16) if s * tiles <= 640 and Kd // 64 >= 2 * s})
 
 
 def _hip256(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
@@ -227,6 +239,10 @@ def _lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre):
 def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
     """name -> callable(a, b, ta, tb, bias, act, out, beta, pre) tried by the autotuner."""
     c = {"hip": _hip, "blas": _blas}
+    M_, Kd_ = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N_ = b.shape[0] if trans_b else b.shape[1]
+    for s in _hip_splits(M_, N_, Kd_):
+        c[f"hip:{s}"] = (lambda s_: (lambda *args: _hip(*args, splits=s_)))(s)
     c.update(_lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre))
     if os.environ.get("FF_GEMM256", "0") != "0" and K.gemm256_supported(a, b, trans_a, trans_b):
         M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
@@ -263,8 +279,44 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
     return c
 
 
+_TIME_STREAM: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _time_graphed(fn, iters: int) -> float:
+    """Mean device time of ``fn`` from a replayed hipGraph of ``iters`` calls:
+    eager back-to-back calls of a GEMM this small time the host launch path
+    (pybind + Python), not the kernel, which the training step — itself one
+    graph — never pays.  The candidate is first run eagerly on the timing
+    stream so any per-stream workspace it caches is allocated outside the
+    capture."""
+    dev = torch.cuda.current_device()
+    ts = _TIME_STREAM.setdefault(dev, torch.cuda.Stream())
+    ts.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(ts):
+        fn()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=ts):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    best = float("inf")
+    for _ in range(2):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(ts):
+            s.record()
+            g.replay()
+            e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / iters)
+    torch.cuda.current_stream().wait_stream(ts)
+    return best
+
+
 def _time(fn, iters=5, rounds=2) -> float:
-    """min over rounds of the mean time of ``iters`` back-to-back calls."""
+    """min over rounds of the mean time of ``iters`` back-to-back calls;
+    below ~50 us per call (launch-bound when issued eagerly) the candidate is
+    re-timed from a replayed graph."""
     fn()
     best = float("inf")
     for _ in range(rounds):
@@ -276,6 +328,12 @@ def _time(fn, iters=5, rounds=2) -> float:
         e.record()
         e.synchronize()
         best = min(best, s.elapsed_time(e) / iters)
+    if best < 0.05 and os.environ.get("FF_AUTOTUNE_GRAPH", "1") != "0" and \
+            not torch.cuda.is_current_stream_capturing():
+        try:
+            best = _time_graphed(fn, max(iters, 10))
+        except Exception:  # a candidate that cannot be captured keeps its eager time
+            torch.cuda.synchronize()
     return best
 
 
@@ -335,6 +393,8 @@ def _resolve(name: str):
     if name == "blas":
         return _blas
     kind, _, arg = name.partition(":")
+    if kind == "hip":
+        return lambda *args: _hip(*args, splits=int(arg))
     if kind == "lt":
         return lambda *args: _lt(*args, algo=int(arg))
     if kind == "p":

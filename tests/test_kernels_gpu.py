@@ -237,6 +237,33 @@ def test_gemm(ta, tb, M, N, Kd):
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd,splits", [(1024, 1024, 1024, 4), (304, 136, 200, 3), (1024, 512, 960, 8)])
+def test_gemm_splitk(ta, tb, M, N, Kd, splits):
+    """128x128-tile GEMM split over K (uneven K-tile ranges, ragged M / N / K
+    edges) with the epilogue (bias, pre-activation, activation, beta) applied
+    by the reduction pass."""
+    torch.manual_seed(11)
+    a = torch.randn(Kd, M, device=DEV, dtype=torch.bfloat16) if ta else torch.randn(M, Kd, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    b = torch.randn(N, Kd, device=DEV, dtype=torch.bfloat16) if tb else torch.randn(Kd, N, device=DEV,
+                                                                                     dtype=torch.bfloat16)
+    ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
+    n0 = K.STATS["gemm_splitk"]
+    c = K.gemm(a, b, trans_a=ta, trans_b=tb, splits=splits)
+    assert K.STATS["gemm_splitk"] == n0 + 1
+    assert _rel(c, ref) < 1e-2
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    c2 = K.gemm(a, b, trans_a=ta, trans_b=tb, bias=bias, act="relu", pre=pre, splits=splits)
+    u = ref + bias.float()
+    assert _rel(pre, u) < 1e-2
+    assert _rel(c2, torch.relu(u)) < 1e-2
+    c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
+    K.gemm(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
+    assert _rel(c3, ref + 1) < 1e-2
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3)])
 def test_gemm256(ta, tb, M, N, Kd, splits):
