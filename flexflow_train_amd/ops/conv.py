@@ -52,8 +52,8 @@ def _pick(key, cands):
         if len(cands) == 1 or torch.cuda.is_current_stream_capturing() or _MODE != "auto":
             c = "gemm" if (_MODE == "gemm" and "gemm" in cands) else "native"
         else:
-            from .gemm import _time
-            times = {name: _time(fn, iters=3) for name, fn in cands.items()}
+            from .gemm import _time_all
+            times = _time_all(cands, iters=3)
             c = min(times, key=times.get)
         _CHOICE[key] = c
     return c

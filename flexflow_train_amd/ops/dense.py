@@ -137,13 +137,15 @@ def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:
         return hit
     if torch.cuda.is_current_stream_capturing():
         return False
-    from .gemm import _time
+    from .gemm import _time_all
     db = torch.zeros(W.shape[0], device=g.device, dtype=torch.float32)
-    fused = _time(lambda: K.gemmp(g, W, trans_b=True, act=act, aux=pre, act_bwd=True,
-                                  dbias=db if has_bias else None, variant=_dact_variant(act)))
     dx = matmul(g, W, trans_b=True)   # settles the autotuner's pick first
-    plain = _time(lambda: (matmul(g, W, trans_b=True),
-                           K.colsum_act(dx, pre, act, db if has_bias else None, write_dx=True)))
+    t = _time_all({
+        "fused": lambda: K.gemmp(g, W, trans_b=True, act=act, aux=pre, act_bwd=True,
+                                 dbias=db if has_bias else None, variant=_dact_variant(act)),
+        "plain": lambda: (matmul(g, W, trans_b=True),
+                          K.colsum_act(dx, pre, act, db if has_bias else None, write_dx=True))})
+    fused, plain = t["fused"], t["plain"]
     _DACT_CHOICE[key] = fused < plain
     _DACT_TIMES[key] = (fused, plain)
     return _DACT_CHOICE[key]
