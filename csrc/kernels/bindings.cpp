@@ -106,6 +106,20 @@ PYBIND11_MODULE(_ffkernels, m) {
     }
     sparse_sgd_rows(a, F(scratch), step, S(st));
   });
+  // pieces: [(ptr, len, off), ...] along the axis of `big` ([outer, total, inner])
+  m.def("slice_copy_multi", [](int dt, uintptr_t big, const std::vector<py::tuple>& pieces, int64_t outer,
+                               int64_t inner, int64_t total, int to_slice, uintptr_t st) {
+    SlicePieces p{};
+    if (pieces.size() > static_cast<size_t>(kMaxSlicePieces))
+      throw std::invalid_argument("slice_copy_multi: too many pieces");
+    p.n = static_cast<int>(pieces.size());
+    for (size_t k = 0; k < pieces.size(); ++k) {
+      p.ptr[k] = P(pieces[k][0].cast<uintptr_t>());
+      p.len[k] = pieces[k][1].cast<int64_t>();
+      p.off[k] = pieces[k][2].cast<int64_t>();
+    }
+    slice_copy_multi(dt, P(big), p, outer, inner, total, to_slice, S(st));
+  });
   m.def("sum_squares", [](uintptr_t x, int64_t n, uintptr_t out, uintptr_t st) {
     sum_squares(F(x), n, F(out), S(st));
   });

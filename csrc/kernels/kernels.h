@@ -164,6 +164,15 @@ void sum_to(int dtype, const float* full, void* out, const NdShape& s, const NdS
             hipStream_t st);
 void permute_nd(int dtype, const void* x, void* y, const NdShape& out_shape, const NdStrides& in_strides_permuted,
                 hipStream_t st);
+constexpr int kMaxSlicePieces = 16;
+struct SlicePieces {
+  void* ptr[kMaxSlicePieces];
+  int64_t len[kMaxSlicePieces], off[kMaxSlicePieces];
+  int n;
+};
+// all pieces of a concat (to_slice = 0) or split (1) along one axis in one launch
+void slice_copy_multi(int dtype, void* big, const SlicePieces& p, int64_t outer, int64_t inner, int64_t total,
+                      int to_slice, hipStream_t st);
 void slice_copy(int dtype, const void* x, void* y, int64_t outer, int64_t len, int64_t inner, int64_t total,
                 int64_t off, int to_slice, int accumulate, hipStream_t st);
 void reverse_axis(int dtype, const void* x, void* y, int64_t outer, int64_t len, int64_t inner, hipStream_t st);

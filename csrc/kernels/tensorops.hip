@@ -487,6 +487,39 @@ void permute_nd(int dtype, const void* x, void* y, const NdShape& out_shape, con
   FFK_LAUNCH_CHECK("permute");
 }
 
+// Every piece of a concat / split in one launch (blockIdx.y = piece): a
+// DLRM interaction concatenates 9 feature blocks forward and splits them
+// back in the backward pass, 18 tiny launches per step as single copies.
+template <typename T>
+__global__ __launch_bounds__(256) void slice_copy_multi_kernel(SlicePieces p, T* __restrict__ big, int64_t outer,
+                                                               int64_t inner, int64_t total, int to_slice) {
+  const int k = blockIdx.y;
+  T* sl = static_cast<T*>(p.ptr[k]);
+  const int64_t len = p.len[k], off = p.off[k];
+  const int64_t n = outer * len * inner;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t in = i % inner, j = (i / inner) % len, o = i / (inner * len);
+    const int64_t b = (o * total + off + j) * inner + in;
+    if (to_slice) sl[i] = big[b];
+    else big[b] = sl[i];
+  }
+}
+
+void slice_copy_multi(int dtype, void* big, const SlicePieces& p, int64_t outer, int64_t inner, int64_t total,
+                      int to_slice, hipStream_t st) {
+  if (p.n <= 0) return;
+  if (p.n > kMaxSlicePieces) throw std::invalid_argument("slice_copy_multi: too many pieces");
+  int64_t most = 0;
+  for (int k = 0; k < p.n; ++k) most = std::max(most, outer * p.len[k] * inner);
+  if (most == 0) return;
+  by_dtype(dtype, "slice_copy_multi", [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(slice_copy_multi_kernel<T>, dim3(grid1(most), p.n), dim3(256), 0, st, p, static_cast<T*>(big),
+                       outer, inner, total, to_slice);
+  });
+  FFK_LAUNCH_CHECK("slice_copy_multi");
+}
+
 void slice_copy(int dtype, const void* x, void* y, int64_t outer, int64_t len, int64_t inner, int64_t total,
                 int64_t off, int to_slice, int accumulate, hipStream_t st) {
   const int64_t n = outer * len * inner;

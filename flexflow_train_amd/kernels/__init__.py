@@ -684,25 +684,29 @@ def concat(xs, axis):
     total = sum(int(x.shape[axis]) for x in xs)
     shape[axis] = total
     y = torch.empty(shape, device=xs[0].device, dtype=xs[0].dtype)
-    off = 0
+    off, pieces = 0, []
     for x in xs:
         ln = int(x.shape[axis])
-        ext().slice_copy(_dt(x), x.data_ptr(), y.data_ptr(), outer, ln, inner, total, off, 0, 0, _stream())
+        pieces.append((x.data_ptr(), ln, off))
         off += ln
+    for i in range(0, len(pieces), 16):   # one launch per 16 pieces
+        ext().slice_copy_multi(_dt(y), y.data_ptr(), pieces[i:i + 16], outer, inner, total, 0, _stream())
     STATS["concat"] += 1
     return y
 
 
 def split(x, sizes, axis):
     outer, total, inner, axis = _oli(list(x.shape), axis)
-    outs, off = [], 0
+    outs, off, pieces = [], 0, []
     for ln in sizes:
         shape = list(x.shape)
         shape[axis] = ln
         y = torch.empty(shape, device=x.device, dtype=x.dtype)
-        ext().slice_copy(_dt(x), x.data_ptr(), y.data_ptr(), outer, ln, inner, total, off, 1, 0, _stream())
+        pieces.append((y.data_ptr(), int(ln), off))
         outs.append(y)
         off += ln
+    for i in range(0, len(pieces), 16):
+        ext().slice_copy_multi(_dt(x), x.data_ptr(), pieces[i:i + 16], outer, inner, total, 1, _stream())
     STATS["split"] += 1
     return outs
 

@@ -116,6 +116,24 @@ def test_concat_split_reverse(dtype, axis):
 
 
 @gpu
+@pytest.mark.parametrize("axis", [0, 1])
+def test_concat_split_many_pieces(axis):
+    """More pieces than one launch carries (16): chunked multi-piece copies,
+    pieces of different lengths (DLRM's interaction concat has 9)."""
+    K = _K()
+    xs = []
+    for i in range(21):
+        shp = [6, 8]
+        shp[axis] = 1 + i % 4
+        xs.append(torch.randn(shp, device="cuda").to(torch.bfloat16))
+    y = K.concat(xs, axis)
+    assert torch.equal(y, torch.cat(xs, axis))
+    sizes = [int(x.shape[axis]) for x in xs]
+    for a, b in zip(K.split(y, sizes, axis), torch.split(y, sizes, axis)):
+        assert torch.equal(a, b.contiguous())
+
+
+@gpu
 @pytest.mark.parametrize("dtype", DT)
 @pytest.mark.parametrize("dim", [0, 1, 2])
 @pytest.mark.parametrize("ibits", [torch.int32, torch.int64])
