@@ -279,6 +279,10 @@ def _run_zoo(args, world, rank, only_dp: bool):
     from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
 
     zname, bpg, over, opt, extra = _ZOO[args.model]
+    if args.model == "dlrm" and world == 1:
+        # its 10-20 us MLP GEMM candidates are ranked from replayed graphs
+        # (ops/gemm.py _time_all; eager timing measures the launch path)
+        os.environ.setdefault("FF_AUTOTUNE_GRAPH", "1")
     bpg = args.batch_per_gpu or bpg
     global_batch = bpg * world
     cfg = FFConfig()
