@@ -4,6 +4,13 @@
     python bench.py --gpus N --steps K --warmup W
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+With --gpus N > 1 and no launcher environment (no WORLD_SIZE), bench.py is its
+own launcher: the parent process -- which never touches HIP -- starts N
+ranks through torch.distributed.run on 127.0.0.1 and exits with their status.
+Every rank then checks that the process group really has N members (and is
+RCCL, backend "nccl", on a GPU) and exits non-zero otherwise, so an N-GPU
+number can never silently be a 1-GPU one.
+
 Metric / config from BASELINE.json: "samples/sec (whole node) + speedup-over-
 DP after search, BERT-large 8xMI355X".  The model is BERT-large (24 layers,
 hidden 1024, 16 heads, FFN 4096, seq 512, vocab 30522 padded to 30528) with
@@ -28,7 +35,7 @@ Other BASELINE.json configs run through the same contract with --model:
                top 576-1024-1024-1024-1), per-GPU batch 1024, plain SGD lr 0.01
                (the reference's dlrm.cc:171; row-sparse table update)
   gpt3-medium  GPT-3 medium (24 layers, hidden 1024, 16 heads, seq 2048,
-               vocab 50257), per-GPU batch 8, AdamW
+               vocab 50257), per-GPU batch 16, AdamW
 """
 import argparse
 import collections
@@ -40,7 +47,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-if os.environ.get("FF_PKG_ROOT"):  # same-box A/B against a snapshot of the package (tools/gpu_*.sh)
+if os.environ.get("FF_PKG_ROOT"):  # same-box A/B against a snapshot of the package (profiles/scripts/*.sh)
     sys.path.insert(0, os.path.abspath(os.environ["FF_PKG_ROOT"]))
 
 
@@ -70,13 +77,17 @@ def main():
     args = ap.parse_args()
 
     os.environ["FF_GEMM"] = args.gemm
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     runner = _run_bert if args.model in ("bert-large", "bert-base") else _run_zoo
 
     res = runner(args, world, rank, only_dp=args.strategy == "dp")
+    dist_world, backend = _check_world(res["ex"], args.gpus)
     speed = {}
     if world > 1 and args.strategy == "search":
         pred = res["search"].get("predicted_speedup_over_dp")
@@ -98,7 +109,8 @@ def main():
         print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(res["value"], 2),
                           "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
-                          "vs_baseline": None, "dtype": "bf16", "data": res["data"], "config": conf}), flush=True)
+                          "vs_baseline": None, "dtype": "bf16", "data": res["data"], "config": conf,
+                          "world_size": dist_world, "backend": backend}), flush=True)
         if os.environ.get("FF_GEMM_REPORT"):
             from flexflow_train_amd.ops.dense import dact_report
             from flexflow_train_amd.ops.gemm import report
@@ -106,6 +118,41 @@ def main():
             print(dact_report(), file=sys.stderr)
         if args.profile and res.get("profile"):
             print(json.dumps({"profile_ms_total": res["profile"]}), file=sys.stderr)
+
+
+def _self_launch(n: int) -> int:
+    """Parent of an N-rank run started without a launcher: one rank per GPU
+    through torch.distributed.run (the same command the driver uses), as
+    child processes -- this process imports no GPU library, so no HIP state
+    exists here that a child could inherit."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def _check_world(ex, want: int):
+    """(world size, backend) of the process group the step ran on; exits
+    non-zero when it is not ``want`` ranks, or not RCCL on a GPU."""
+    world = ex.dist.world
+    backend = ex.dist.backend
+    if want > 1:
+        import torch.distributed as dist
+        ok = dist.is_initialized() and dist.get_world_size() == want
+        if ok and ex.cfg.device.type == "cuda" and backend != "nccl":
+            ok = False
+        if not ok:
+            print(f"error: expected a {want}-rank process group (RCCL on GPU), got world={world} "
+                  f"backend={backend}", file=sys.stderr)
+            sys.exit(3)
+    return world, backend
 
 
 def _release(res):
@@ -279,10 +326,6 @@ def _run_zoo(args, world, rank, only_dp: bool):
     from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
 
     zname, bpg, over, opt, extra = _ZOO[args.model]
-    if args.model == "dlrm" and world == 1:
-        # its 10-20 us MLP GEMM candidates are ranked from replayed graphs
-        # (ops/gemm.py _time_all; eager timing measures the launch path)
-        os.environ.setdefault("FF_AUTOTUNE_GRAPH", "1")
     bpg = args.batch_per_gpu or bpg
     global_batch = bpg * world
     cfg = FFConfig()

@@ -274,7 +274,18 @@ void register_ext_bindings(py::module_& m) {
         auto s = substitution_from_legacy_rule(c.rules.at(i));
         if (!s) return py::none();
         return py::cast(*s);
+      })
+      .def("conversion_failure", [](const LegacyRuleCollection& c, size_t i) {
+        std::string why;
+        auto s = substitution_from_legacy_rule(c.rules.at(i), &why);
+        return s ? std::string() : why;
       });
+  m.def("load_substitutions", [](const std::string& s) {
+    std::vector<std::string> skipped;
+    auto subs = load_substitutions(Json::parse(s), &skipped);
+    return py::make_tuple(subs, skipped);
+  });
+  m.def("substitution_from_json", [](const std::string& s) { return Substitution::from_json(Json::parse(s)); });
   m.def("load_legacy_rules", [](const std::string& s) { return load_legacy_rules(Json::parse(s)); });
 
   // ---- model zoo (C++ CG builders)

@@ -8,6 +8,9 @@
 // Node ids are stable ints (deleted ids are never reused) so that a rewrite
 // (substitution) leaves untouched nodes addressable.
 #pragma once
+#include <algorithm>
+#include <queue>
+#include <memory>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -103,14 +106,14 @@ class DataflowGraph {
   int add_node(NodeLabel label, std::vector<ValueRef> inputs, std::vector<TensorLabel> outputs) {
     for (auto const& v : inputs) check_value(v);
     int id = next_id_++;
-    nodes_[id] = Node{std::move(label), std::move(inputs), std::move(outputs)};
+    nodes_[id] = std::make_shared<Node>(Node{std::move(label), std::move(inputs), std::move(outputs)});
     return id;
   }
   // Used by deserialisation / rewrites that must preserve ids.
   void add_node_with_id(int id, NodeLabel label, std::vector<ValueRef> inputs,
                         std::vector<TensorLabel> outputs) {
     if (nodes_.count(id)) throw FFError("duplicate node id " + std::to_string(id));
-    nodes_[id] = Node{std::move(label), std::move(inputs), std::move(outputs)};
+    nodes_[id] = std::make_shared<Node>(Node{std::move(label), std::move(inputs), std::move(outputs)});
     next_id_ = std::max(next_id_, id + 1);
   }
   void remove_node(int id) { nodes_.erase(id); }
@@ -118,17 +121,21 @@ class DataflowGraph {
   const Node& node(int id) const {
     auto it = nodes_.find(id);
     if (it == nodes_.end()) throw FFError("no node " + std::to_string(id));
-    return it->second;
+    return *it->second;
   }
+  // Nodes are shared between copies of a graph (a search copies a graph for
+  // every candidate rewrite and changes a handful of nodes): mutable access
+  // unshares the one node first.
   Node& node(int id) {
     auto it = nodes_.find(id);
     if (it == nodes_.end()) throw FFError("no node " + std::to_string(id));
-    return it->second;
+    return unshare(it->second);
   }
   const TensorLabel& tensor(ValueRef v) const { return node(v.node).outputs.at(v.idx); }
   TensorLabel& tensor(ValueRef v) { return node(v.node).outputs.at(v.idx); }
   std::vector<int> node_ids() const {
     std::vector<int> r;
+    r.reserve(nodes_.size());
     for (auto const& kv : nodes_) r.push_back(kv.first);
     return r;
   }
@@ -139,39 +146,94 @@ class DataflowGraph {
     DiGraph g;
     for (auto const& kv : nodes_) {
       g.add_node(kv.first);
-      for (auto const& v : kv.second.inputs) g.add_edge(v.node, kv.first);
+      for (auto const& v : kv.second->inputs) g.add_edge(v.node, kv.first);
     }
     return g;
   }
-  std::vector<int> topo_order() const { return topological_order(digraph()); }
+  // Kahn's algorithm, smallest ready id first (the order of
+  // topological_order(digraph()), without building the DiGraph).
+  std::vector<int> topo_order() const {
+    const int n = next_id_;
+    // distinct predecessors per node, as CSR arrays (no per-node allocation)
+    std::vector<int> indeg(n, -1), off(n + 1, 0), edges_from, edges_to;
+    edges_from.reserve(nodes_.size() * 2);
+    edges_to.reserve(nodes_.size() * 2);
+    int preds[64];
+    for (auto const& kv : nodes_) {
+      auto const& in = kv.second->inputs;
+      int k = 0;
+      std::vector<int> big;
+      int* pp = preds;
+      if (in.size() > 64) {
+        big.resize(in.size());
+        pp = big.data();
+      }
+      for (auto const& v : in) pp[k++] = v.node;
+      std::sort(pp, pp + k);
+      k = static_cast<int>(std::unique(pp, pp + k) - pp);
+      indeg[kv.first] = k;
+      for (int i = 0; i < k; ++i) {
+        int p = pp[i];
+        if (p < 0 || p >= n || !nodes_.count(p)) throw FFError("dangling value reference " + std::to_string(p));
+        edges_from.push_back(p);
+        edges_to.push_back(kv.first);
+        ++off[p + 1];
+      }
+    }
+    for (int i = 0; i < n; ++i) off[i + 1] += off[i];
+    std::vector<int> succ(edges_to.size()), fill(off.begin(), off.end() - 1);
+    for (size_t e = 0; e < edges_to.size(); ++e) succ[fill[edges_from[e]]++] = edges_to[e];
+    std::priority_queue<int, std::vector<int>, std::greater<int>> q;
+    for (auto const& kv : nodes_)
+      if (indeg[kv.first] == 0) q.push(kv.first);
+    std::vector<int> order;
+    order.reserve(nodes_.size());
+    while (!q.empty()) {
+      int x = q.top();
+      q.pop();
+      order.push_back(x);
+      for (int e = off[x]; e < off[x + 1]; ++e)
+        if (--indeg[succ[e]] == 0) q.push(succ[e]);
+    }
+    if (order.size() != nodes_.size()) throw FFError("graph has a cycle");
+    return order;
+  }
 
   // All (consumer node, input slot) pairs reading value v.
   std::vector<std::pair<int, int>> uses(ValueRef v) const {
     std::vector<std::pair<int, int>> r;
     for (auto const& kv : nodes_)
-      for (size_t i = 0; i < kv.second.inputs.size(); ++i)
-        if (kv.second.inputs[i] == v) r.push_back({kv.first, static_cast<int>(i)});
+      for (size_t i = 0; i < kv.second->inputs.size(); ++i)
+        if (kv.second->inputs[i] == v) r.push_back({kv.first, static_cast<int>(i)});
     return r;
   }
   std::vector<ValueRef> all_values() const {
     std::vector<ValueRef> r;
     for (auto const& kv : nodes_)
-      for (size_t i = 0; i < kv.second.outputs.size(); ++i) r.push_back({kv.first, static_cast<int>(i)});
+      for (size_t i = 0; i < kv.second->outputs.size(); ++i) r.push_back({kv.first, static_cast<int>(i)});
     return r;
   }
   void replace_uses(ValueRef from, ValueRef to) {
-    for (auto& kv : nodes_)
-      for (auto& v : kv.second.inputs)
+    for (auto& kv : nodes_) {
+      bool hit = false;
+      for (auto const& v : kv.second->inputs) hit = hit || v == from;
+      if (!hit) continue;
+      for (auto& v : unshare(kv.second).inputs)
         if (v == from) v = to;
+    }
   }
 
  private:
+  static Node& unshare(std::shared_ptr<Node>& p) {
+    if (p.use_count() > 1) p = std::make_shared<Node>(*p);
+    return *p;
+  }
   void check_value(const ValueRef& v) const {
     auto it = nodes_.find(v.node);
-    if (it == nodes_.end() || v.idx < 0 || v.idx >= static_cast<int>(it->second.outputs.size()))
+    if (it == nodes_.end() || v.idx < 0 || v.idx >= static_cast<int>(it->second->outputs.size()))
       throw FFError("dangling value reference " + std::to_string(v.node) + ":" + std::to_string(v.idx));
   }
-  std::map<int, Node> nodes_;
+  std::map<int, std::shared_ptr<Node>> nodes_;
   int next_id_ = 0;
 };
 

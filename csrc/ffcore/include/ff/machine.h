@@ -16,6 +16,8 @@
 // canonical layouts use.  Collectives are priced with a ring / direct model
 // over the per-GPU xGMI bandwidth, calibratable from measured RCCL numbers.
 #pragma once
+#include <mutex>
+#include <unordered_map>
 #include <map>
 #include <string>
 #include <vector>
@@ -138,8 +140,19 @@ class ProfileTable {
 class CostModel {
  public:
   explicit CostModel(MachineSpecification spec) : spec_(std::move(spec)) {}
+  CostModel(const CostModel& o) : spec_(o.spec_), profiles_(o.profiles_) {}
+  CostModel& operator=(const CostModel& o) {
+    spec_ = o.spec_;
+    profiles_ = o.profiles_;
+    clear_memo();
+    return *this;
+  }
   const MachineSpecification& spec() const { return spec_; }
-  ProfileTable& profiles() { return profiles_; }
+  // mutable access to the measured table invalidates the memoised costs
+  ProfileTable& profiles() {
+    clear_memo();
+    return profiles_;
+  }
 
   // Compute cost of one piece (per-device) of an operator.
   OpCost op_cost(const OpAttrs& op, const std::vector<ParallelTensorShape>& inputs,
@@ -153,9 +166,22 @@ class CostModel {
   static std::string signature(const OpAttrs& op, const std::vector<TensorShape>& pieces);
 
  private:
+  OpCost op_cost_uncached(const OpAttrs& op, const std::vector<ParallelTensorShape>& inputs,
+                          const std::vector<ParallelTensorShape>& weights,
+                          const std::vector<ParallelTensorShape>& outputs, int block_size) const;
+  OpCost parallel_op_cost_uncached(const OpAttrs& op, const ParallelTensorShape& in, const ParallelTensorShape& out,
+                                   int block_size) const;
+  void clear_memo() const {
+    std::lock_guard<std::mutex> lk(memo_mu_);
+    memo_.clear();
+  }
   double gemm_time(double flops, double bytes, double eff_hint) const;
   MachineSpecification spec_;
   ProfileTable profiles_;
+  // (op, parallel shapes, block) -> cost: a search re-costs the same
+  // operators in thousands of candidate graphs that differ in a few nodes
+  mutable std::unordered_map<size_t, OpCost> memo_;
+  mutable std::mutex memo_mu_;
 };
 
 }  // namespace ff

@@ -35,6 +35,14 @@ struct SearchConfig {
   uint64_t seed = 0x5eed;
   double time_limit = 60.0;     // seconds
   bool use_machine_mapping = false;  // Unity cost: DP machine mapping (else simulator)
+  // graph_optimize: Unity best-first pops (-1: `budget`, the reference's
+  // single --budget drives the whole search, unity_algorithm.cc:37-90) and
+  // the share of time_limit MCMC may use before Unity starts
+  int unity_budget = -1;
+  double mcmc_time_share = 0.5;
+  // rule set added to the built-in parallelization rules (legacy TASO corpus
+  // JSON or a substitution-set JSON, load_substitutions); "" = none
+  std::string substitution_path;
   SearchSpaceOptions space;
   SimConfig sim;
 };
@@ -51,8 +59,14 @@ struct SearchResult {
   int accepted = 0;
   double elapsed = 0;
   Json trace;                            // [[iteration, best cost], ...]
+  int rules = 0;                         // Unity: rules tried (built-in + rule set)
+  int rule_set_rules = 0;                // Unity: of which from the rule set
+  std::vector<std::string> best_rules;   // Unity: rewrites from the initial PCG to the best one
   Json to_json(const ComputationGraph* cg = nullptr) const;
 };
+
+// The rule set behind SearchConfig::substitution_path (loaded once per path).
+const std::vector<Substitution>& cached_substitutions(const std::string& path);
 
 // Cost of a lowered strategy with the simulator (inf if invalid).
 double evaluate_strategy(const ComputationGraph& cg, const StrategyConfig& s, const CostModel& cm,

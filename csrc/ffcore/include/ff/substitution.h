@@ -40,7 +40,11 @@ struct PatternValue {
 };
 
 struct AttrConstraint {
-  enum Kind { EQUAL = 0, DIVISIBLE_BY = 1 } kind = EQUAL;
+  // DIM_FROM_END: an axis attribute counted from the last dimension of the
+  // operator's first data input (value -1 = last dim), compared after
+  // normalising the attribute against that input's rank -- the legacy TASO
+  // rules number dims innermost-first and never state the rank
+  enum Kind { EQUAL = 0, DIVISIBLE_BY = 1, DIM_FROM_END = 2 } kind = EQUAL;
   std::string key;
   AttrValue value;
 };
@@ -49,7 +53,9 @@ struct OperatorPattern {
   std::optional<OpType> type;
   std::vector<AttrConstraint> attrs;
   int num_data_inputs = -1;  // -1: any
-  bool satisfied_by(const OpAttrs& op) const;
+  int num_outputs = -1;      // -1: any
+  // rank: of the operator's first data input (-1 unknown: DIM_FROM_END fails)
+  bool satisfied_by(const OpAttrs& op, int rank = -1) const;
 };
 
 struct PCGPattern {
@@ -87,10 +93,35 @@ struct Substitution {
   std::vector<OutputOperator> out_nodes;
   std::vector<PatternValue> output_mapping;  // per pattern output: output value (node<0: pattern input)
   Json to_json() const;
+  static Substitution from_json(const Json& j);  // inverse of to_json
+};
+
+// A rule set file: either the legacy TASO corpus ({"rule": [...]}, every
+// convertible rule) or a list of Substitution::to_json() objects
+// ({"substitutions": [...]}); `skipped` receives the legacy rules that could
+// not be converted (name + reason).
+std::vector<Substitution> load_substitutions(const Json& j, std::vector<std::string>* skipped = nullptr);
+std::vector<Substitution> load_substitutions_file(const std::string& path, std::vector<std::string>* skipped = nullptr);
+
+// Per-PCG lookup tables every pattern match reads (data nodes by operator
+// type, data inputs, input rank, value users): built once per PCG, shared
+// by all the rules tried on it (the Unity search tries every rule on every
+// popped state).
+struct PatternMatchIndex {
+  explicit PatternMatchIndex(const ParallelComputationGraph& pcg);
+  std::vector<int> data_nodes;                             // topological order
+  std::map<OpType, std::vector<int>> by_type;
+  std::vector<char> weight_path;                           // by node id
+  std::vector<int> rank;                                   // rank of the first data input (-1 none)
+  std::vector<std::vector<ValueRef>> din;                  // data inputs by node id
+  std::vector<std::vector<std::vector<std::pair<int, int>>>> users;  // [node][output] -> (user, slot)
+  const std::vector<std::pair<int, int>>& users_of(const ValueRef& v) const;
 };
 
 std::vector<PCGPatternMatch> find_pattern_matches(const PCGPattern& p, const ParallelComputationGraph& pcg,
                                                   size_t max_matches = 1u << 20);
+std::vector<PCGPatternMatch> find_pattern_matches(const PCGPattern& p, const ParallelComputationGraph& pcg,
+                                                  const PatternMatchIndex& ix, size_t max_matches = 1u << 20);
 // nullopt if the rewritten graph fails shape inference.
 std::optional<ParallelComputationGraph> apply_substitution(const ParallelComputationGraph& pcg,
                                                            const Substitution& s, const PCGPatternMatch& m);
@@ -128,8 +159,15 @@ struct LegacyRuleCollection {
 };
 LegacyRuleCollection load_legacy_rules(const Json& j);
 std::string legacy_rule_to_dot(const LegacyRule& r);
-// Converts rules whose weight handling is expressible with implicit weights
-// (weights never rewritten); nullopt otherwise.
-std::optional<Substitution> substitution_from_legacy_rule(const LegacyRule& r);
+// Converts a legacy rule.  Weights are implicit here (a PCG operator's
+// weights take the parallel shape its data inputs imply, re-created on
+// apply), so the legacy rule's weight-side parallel operators (Replicate /
+// Partition / Combine chains that end in a Linear's weight slot) are implied
+// by the data side and dropped.  Dims are innermost-first in the legacy
+// format and become DIM_FROM_END constraints / negative axes.  nullopt (with
+// `why`) for a rule that still cannot be expressed.
+std::optional<Substitution> substitution_from_legacy_rule(const LegacyRule& r, std::string* why = nullptr);
+// The same equivalence read right to left (dst becomes the pattern).
+LegacyRule reverse_legacy_rule(const LegacyRule& r);
 
 }  // namespace ff

@@ -495,8 +495,9 @@ std::string ParallelComputationGraph::as_dot() const {
 }
 
 size_t ParallelComputationGraph::structural_hash() const {
-  std::map<int, size_t> h;
+  std::vector<size_t> h(g.next_id(), 0);
   std::vector<size_t> all;
+  all.reserve(g.num_nodes());
   for (int id : g.topo_order()) {
     auto const& n = g.node(id);
     size_t x = n.label.op.hash();

@@ -292,6 +292,43 @@ double CostModel::gemm_time(double flops, double bytes, double eff_hint) const {
 OpCost CostModel::op_cost(const OpAttrs& op, const std::vector<ParallelTensorShape>& inputs,
                           const std::vector<ParallelTensorShape>& weights,
                           const std::vector<ParallelTensorShape>& outputs, int block_size) const {
+  size_t k = hash_combine(op.hash(), 0x0c057);
+  for (auto const* v : {&inputs, &weights, &outputs}) {
+    k = hash_combine(k, v->size());
+    for (auto const& t : *v) k = hash_combine(k, std::hash<ParallelTensorShape>()(t));
+  }
+  k = hash_combine(k, static_cast<size_t>(block_size));
+  {
+    std::lock_guard<std::mutex> lk(memo_mu_);
+    auto it = memo_.find(k);
+    if (it != memo_.end()) return it->second;
+  }
+  OpCost c = op_cost_uncached(op, inputs, weights, outputs, block_size);
+  std::lock_guard<std::mutex> lk(memo_mu_);
+  memo_.emplace(k, c);
+  return c;
+}
+
+OpCost CostModel::parallel_op_cost(const OpAttrs& op, const ParallelTensorShape& in, const ParallelTensorShape& out,
+                                   int block_size) const {
+  size_t k = hash_combine(op.hash(), 0x9a7a11e1);
+  k = hash_combine(k, std::hash<ParallelTensorShape>()(in));
+  k = hash_combine(k, std::hash<ParallelTensorShape>()(out));
+  k = hash_combine(k, static_cast<size_t>(block_size));
+  {
+    std::lock_guard<std::mutex> lk(memo_mu_);
+    auto it = memo_.find(k);
+    if (it != memo_.end()) return it->second;
+  }
+  OpCost c = parallel_op_cost_uncached(op, in, out, block_size);
+  std::lock_guard<std::mutex> lk(memo_mu_);
+  memo_.emplace(k, c);
+  return c;
+}
+
+OpCost CostModel::op_cost_uncached(const OpAttrs& op, const std::vector<ParallelTensorShape>& inputs,
+                                   const std::vector<ParallelTensorShape>& weights,
+                                   const std::vector<ParallelTensorShape>& outputs, int block_size) const {
   (void)block_size;
   OpCost c;
   std::vector<TensorShape> ip, wp, op_;
@@ -376,8 +413,8 @@ OpCost CostModel::op_cost(const OpAttrs& op, const std::vector<ParallelTensorSha
   return c;
 }
 
-OpCost CostModel::parallel_op_cost(const OpAttrs& op, const ParallelTensorShape& in, const ParallelTensorShape& out,
-                                   int block_size) const {
+OpCost CostModel::parallel_op_cost_uncached(const OpAttrs& op, const ParallelTensorShape& in,
+                                            const ParallelTensorShape& out, int block_size) const {
   (void)block_size;
   OpCost c;
   const double in_b = static_cast<double>(in.piece_shape().size_bytes());

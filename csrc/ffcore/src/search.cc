@@ -1,8 +1,11 @@
 #include "ff/search.h"
 
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
+#include <mutex>
 #include <queue>
 #include <random>
 #include <unordered_set>
@@ -26,6 +29,13 @@ Json SearchResult::to_json(const ComputationGraph* cg) const {
   j["accepted"] = accepted;
   j["elapsed"] = elapsed;
   j["trace"] = trace;
+  if (rules) {
+    j["rules"] = static_cast<int64_t>(rules);
+    j["rule_set_rules"] = static_cast<int64_t>(rule_set_rules);
+    Json br = Json::array();
+    for (auto const& n : best_rules) br.push_back(n);
+    j["best_rules"] = br;
+  }
   if (cg && !strategy.empty()) j["strategy"] = strategy_to_json(*cg, strategy);
   Json v = Json::object();
   for (auto const& kv : views) v[std::to_string(kv.first)] = Json(std::vector<int64_t>{kv.second.start, kv.second.size});
@@ -163,7 +173,15 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   };
   auto rules = generate_parallelization_substitutions(initial, cfg.world);
   rules.insert(rules.end(), extra_rules.begin(), extra_rules.end());
+  if (!cfg.substitution_path.empty()) {
+    auto const& rs = cached_substitutions(cfg.substitution_path);
+    rules.insert(rules.end(), rs.begin(), rs.end());
+    R.rule_set_rules = static_cast<int>(rs.size());
+  }
+  R.rules = static_cast<int>(rules.size());
   std::vector<ParallelComputationGraph> states;
+  std::vector<std::pair<int, int>> parent;   // state -> (parent state, rule index)
+  parent.push_back({-1, -1});
   std::vector<std::map<int, DeviceBlock>> state_views;
   std::priority_queue<State, std::vector<State>, std::greater<State>> pq;
   std::unordered_set<size_t> seen;
@@ -178,6 +196,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   R.evaluated = 1;
   R.trace.push_back(Json(std::vector<double>{0.0, best_cost}));
   int it = 0;
+  double prof[5] = {0, 0, 0, 0, 0};
   for (; it < cfg.budget && !pq.empty(); ++it) {
     if (now_s() - t0 > cfg.time_limit) break;
     State s = pq.top();
@@ -190,21 +209,34 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
       continue;
     }
     const ParallelComputationGraph cur = states[s.id];
-    for (auto const& rule : rules) {
+    const PatternMatchIndex ix(cur);
+    for (size_t ri = 0; ri < rules.size(); ++ri) {
+      auto const& rule = rules[ri];
       if (now_s() - t0 > cfg.time_limit) break;
-      auto matches = find_pattern_matches(rule.pattern, cur, 4096);
+      double tm = now_s();
+      auto matches = find_pattern_matches(rule.pattern, cur, ix, 4096);
+      prof[4] += now_s() - tm;
       for (auto const& m : matches) {
+        double ta = now_s();
         auto next = apply_substitution(cur, rule, m);
+        prof[0] += now_s() - ta;
         if (!next) continue;
+        ta = now_s();
         if (next->num_operator_nodes() > cfg.max_num_ops) continue;
         if (!fits_world(*next, cfg.world)) continue;
+        prof[1] += now_s() - ta;
+        ta = now_s();
         size_t h = next->structural_hash();
+        prof[2] += now_s() - ta;
         if (!seen.insert(h).second) continue;
         std::map<int, DeviceBlock> v;
+        ta = now_s();
         double c = cost_of(*next, &v);
+        prof[3] += now_s() - ta;
         ++R.evaluated;
         if (!std::isfinite(c) || c > cfg.threshold) continue;
         states.push_back(std::move(*next));
+        parent.push_back({s.id, static_cast<int>(ri)});
         state_views.push_back(std::move(v));
         pq.push({c, static_cast<int>(states.size()) - 1});
         if (c < best_cost) {
@@ -215,25 +247,41 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
       }
     }
   }
+  if (getenv("FF_SEARCH_PROFILE"))
+    fprintf(stderr, "unity: apply %.2fs checks %.2fs hash %.2fs cost %.2fs match %.2fs total %.2fs\n", prof[0], prof[1],
+            prof[2], prof[3], prof[4], now_s() - t0);
   R.iterations = it;
   R.pcg = states[best];
   R.views = state_views[best];
   R.cost = best_cost;
+  for (int k = best; k >= 0 && parent[k].second >= 0; k = parent[k].first)
+    R.best_rules.insert(R.best_rules.begin(), rules[parent[k].second].name);
   R.elapsed = now_s() - t0;
   return R;
+}
+
+const std::vector<Substitution>& cached_substitutions(const std::string& path) {
+  static std::mutex mu;
+  static std::map<std::string, std::vector<Substitution>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(path);
+  if (it == cache.end()) it = cache.emplace(path, load_substitutions_file(path)).first;
+  return it->second;
 }
 
 SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, const SearchConfig& cfg) {
   const double t0 = now_s();
   SearchConfig mc = cfg;
-  mc.time_limit = cfg.time_limit * 0.7;
+  mc.time_limit = cfg.time_limit * cfg.mcmc_time_share;
   auto m = mcmc_search(cg, cm, mc);
   SearchConfig uc = cfg;
   uc.time_limit = std::max(0.0, cfg.time_limit - (now_s() - t0));
-  uc.budget = std::max(1, cfg.budget / 50);
+  uc.budget = cfg.unity_budget >= 0 ? cfg.unity_budget : cfg.budget;
   SearchResult best = m;
-  if (uc.time_limit > 0.5) {
+  if (uc.time_limit > 0.05 && uc.budget > 0) {
     auto u = unity_search(m.pcg, cm, uc);
+    best.rules = u.rules;
+    best.rule_set_rules = u.rule_set_rules;
     if (u.cost < best.cost * 0.999) {
       u.data_parallel_cost = m.data_parallel_cost;
       u.strategy.clear();
@@ -279,6 +327,9 @@ SearchConfig search_config_from_json(const Json& j) {
   if (j.contains("seed")) c.seed = static_cast<uint64_t>(j.at("seed").as_int());
   gd("time_limit", c.time_limit);
   gb("use_machine_mapping", c.use_machine_mapping);
+  gi("unity_budget", c.unity_budget);
+  gd("mcmc_time_share", c.mcmc_time_share);
+  if (j.contains("substitution_path")) c.substitution_path = j.at("substitution_path").as_string();
   gb("enable_parameter_parallel", c.space.enable_parameter_parallel);
   gb("enable_attribute_parallel", c.space.enable_attribute_parallel);
   gb("allow_partial_world", c.space.allow_partial_world);

@@ -310,6 +310,12 @@ void gemm_bf16_ex(const void* A, const void* B, void* C, const void* bias, void*
                   hipStream_t st, int splits, float* ws) {
   if (M <= 0 || N <= 0 || K <= 0) return;
   splits = std::max(1, std::min(splits, (K + BK - 1) / BK));
+  // the split-K epilogue stores 4 columns per thread: f32x4 (16 B) into an
+  // fp32 C, bf16x4 (8 B) into a bf16 C and into the pre-activation; an
+  // output view that is not aligned for that runs the single-pass kernel
+  if (splits > 1 && (((reinterpret_cast<uintptr_t>(C) & (out_f32 ? 15 : 7)) != 0) ||
+                     (pre && (reinterpret_cast<uintptr_t>(pre) & 7) != 0)))
+    splits = 1;
   if (splits > 1 && (!ws || N % 4 || ldc % 4 || (reinterpret_cast<uintptr_t>(ws) & 15)))
     throw std::invalid_argument("gemm: split-K needs a 16-byte aligned fp32 workspace and N % 4 == 0");
   // 16-byte global loads require 8-element aligned leading dims and

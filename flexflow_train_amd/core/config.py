@@ -30,6 +30,7 @@ class FFConfig:
     profiling: bool = False
     perform_fusion: bool = True
     search_budget: int = -1
+    search_time_limit: float = 60.0    # seconds for the whole strategy search (MCMC + Unity)
     search_alpha: float = 1.2
     search_overlap_backward_update: bool = True
     only_data_parallel: bool = False
@@ -42,6 +43,10 @@ class FFConfig:
     export_strategy_task_graph_file: str = ""
     include_costs_dot_graph: bool = False
     export_strategy_computation_graph_file: str = ""
+    # Unity rule set added to the built-in parallelization / fusion rules:
+    # "" = the bundled TASO corpus (flexflow_train_amd/data/taso_rules.json,
+    # docs/TASO_RULES.md), "none" = no rule set, else a legacy corpus JSON
+    # (reference substitutions/*.json) or a substitution-set JSON
     substitution_json_path: str = ""
     machine_model_version: int = 0
     machine_model_file: str = ""
@@ -129,6 +134,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("-p", "--print-freq", dest="print_freq", type=int)
     a("-d", "--dataset", dest="dataset_path", type=str)
     a("--budget", "--search-budget", dest="search_budget", type=int)
+    a("--search-time-limit", dest="search_time_limit", type=float)
     a("--alpha", "--search-alpha", dest="search_alpha", type=float)
     a("--simulator-workspace-size", dest="simulator_work_space_size", type=int)
     a("--import", "--import-strategy", dest="import_strategy_file", type=str)

@@ -619,8 +619,13 @@ class FFModel:
         self.pcg, self.views, self.search_report = strat.build_pcg(self.cg, self.ffconfig, world)
         if self.ffconfig.export_strategy_file:
             strat.export_strategy(self.ffconfig.export_strategy_file, self.pcg, self.views, self.search_report)
-        dt = self.ffconfig.compute_dtype if cuda else ("float" if self.ffconfig.compute_dtype == "bfloat16"
-                                                         else self.ffconfig.compute_dtype)
+        # "bfloat16" is the GPU default and means fp32 on the CPU; a CPU run
+        # computes in bf16 only when asked by name ("bfloat16-cpu")
+        dt = self.ffconfig.compute_dtype
+        if dt == "bfloat16-cpu":
+            dt = "bfloat16"
+        elif not cuda and dt == "bfloat16":
+            dt = "float"
         cdt = {"bfloat16": torch.bfloat16, "float": torch.float32, "float32": torch.float32,
                "half": torch.float16}[dt]
         cfg = ExecConfig(compute_dtype=cdt, device=device, seed=self.ffconfig.seed,
@@ -835,11 +840,16 @@ class FFModel:
             return 0, 0
         # check the progress record BEFORE restoring anything: a checkpoint of
         # a differently-sized epoch is not resumed (no weights, no step count)
-        prog = read_checkpoint_meta(path).get("progress") or {}
+        cmeta = read_checkpoint_meta(path)
+        prog = cmeta.get("progress") or {}
         if prog.get("iters_per_epoch") != iters:
             import warnings
             warnings.warn(f"{path}: recorded {prog.get('iters_per_epoch')} iterations per epoch, this fit() runs "
                           f"{iters}; not resuming from it (training starts from the current weights)")
+            # new checkpoints must sort after the stale one: otherwise the
+            # keep-newest rotation deletes them and latest_checkpoint() keeps
+            # returning the mismatched directory
+            self.executor.step_num = max(self.executor.step_num, int(cmeta.get("step", 0)))
             return 0, 0
         meta = load_checkpoint(self, path)
         epoch, it = int(prog["epoch"]), int(prog["iter"])

@@ -52,10 +52,9 @@ def _pick(key, cands):
         if len(cands) == 1 or torch.cuda.is_current_stream_capturing() or _MODE != "auto":
             c = "gemm" if (_MODE == "gemm" and "gemm" in cands) else "native"
         else:
-            # eager clock: graph-timing the conv candidates stalled a ResNet-50
-            # run on the GPU box (tools/gpu_r3s2q.sh); GEMM decisions only
+            # eager clock (these convolutions run for hundreds of microseconds)
             from .gemm import _time
-            times = {name: _time(fn, iters=3, graph=False) for name, fn in cands.items()}
+            times = {name: _time(fn, iters=3) for name, fn in cands.items()}
             c = min(times, key=times.get)
         _CHOICE[key] = c
     return c

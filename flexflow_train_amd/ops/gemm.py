@@ -280,23 +280,77 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
 
 
 _TIME_STREAM: Dict[int, "torch.cuda.Stream"] = {}
+_TRACE = os.environ.get("FF_AUTOTUNE_TRACE", "0") == "1"
+_SLEEP_PER_MS: Dict[int, float] = {}   # device -> torch.cuda._sleep cycles per millisecond
+
+
+def _gpu_busy(ms: float):
+    """Enqueue ~``ms`` of device-side busy wait on the current stream, so the
+    host can queue the calls being timed behind it and the device then runs
+    them back to back (no host launch gaps inside the timed interval)."""
+    dev = torch.cuda.current_device()
+    rate = _SLEEP_PER_MS.get(dev)
+    if rate is None:
+        cyc = 1_000_000
+        torch.cuda._sleep(cyc)   # first call: module load
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        torch.cuda._sleep(cyc)
+        e.record()
+        e.synchronize()
+        rate = _SLEEP_PER_MS[dev] = cyc / max(1e-3, s.elapsed_time(e))
+    torch.cuda._sleep(max(1, int(ms * rate)))
+
+
+def _time_queued(fn, iters: int, rounds: int = 2) -> float:
+    """Mean device time per call of ``fn``: ``iters`` calls queued behind a
+    device busy-wait and bracketed by events.  Eager back-to-back calls of a
+    10-20 us GEMM time the host launch path (pybind + Python), which the
+    training step -- itself one hipGraph -- never pays; this clock sees only
+    the kernels, without capturing anything (the graph clock below is the
+    research alternative).  If the host needed longer to queue the calls
+    than the busy-wait lasted, the round is repeated with a longer wait."""
+    import time as _time_mod
+    fn()
+    best = float("inf")
+    busy = 1.0
+    r = 0
+    while r < rounds:
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        _gpu_busy(busy)
+        t0 = _time_mod.perf_counter()
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        host_ms = (_time_mod.perf_counter() - t0) * 1e3
+        e.synchronize()
+        if host_ms > 0.8 * busy and busy < 64:
+            busy = max(2 * busy, 2 * host_ms)   # the queue may have drained: redo this round
+            continue
+        best = min(best, s.elapsed_time(e) / iters)
+        r += 1
+    return best
 
 
 def _time_graphed(fn, iters: int) -> float:
-    """Mean device time of ``fn`` from a replayed hipGraph of ``iters`` calls:
-    eager back-to-back calls of a GEMM this small time the host launch path
-    (pybind + Python), not the kernel, which the training step — itself one
-    graph — never pays.  The candidate is first run eagerly on the timing
-    stream so any per-stream workspace it caches is allocated outside the
-    capture."""
+    """Mean device time of ``fn`` from a replayed hipGraph of ``iters`` calls
+    (FF_AUTOTUNE_GRAPH=1 only; see docs/PERF.md 'autotuner graph clock' for
+    the replay that never completed).  The candidate is first run eagerly on
+    the timing stream so any per-stream workspace it caches is allocated
+    outside the capture."""
     dev = torch.cuda.current_device()
     ts = _TIME_STREAM.setdefault(dev, torch.cuda.Stream())
+    sync = os.environ.get("FF_AUTOTUNE_GRAPH_SYNC", "1") == "1"
+    if sync:
+        torch.cuda.synchronize()
     ts.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(ts):
         fn()
-    # capture_begin / capture_end directly: the torch.cuda.graph context
-    # manager empties the allocator cache before every capture, which
-    # reshuffled the memory layout of the step being tuned (BERT-large -1 %)
+    if sync:
+        torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(ts):
         g.capture_begin()
@@ -305,6 +359,8 @@ def _time_graphed(fn, iters: int) -> float:
                 fn()
         finally:
             g.capture_end()
+    if sync:
+        torch.cuda.synchronize()
     g.replay()
     best = float("inf")
     for _ in range(2):
@@ -321,27 +377,29 @@ def _time_graphed(fn, iters: int) -> float:
 
 
 def _time_all(fns: Dict[str, Callable[[], Any]], iters=5) -> Dict[str, float]:
-    """Time every candidate the same way: eagerly, and (FF_AUTOTUNE_GRAPH=1)
-    when the fastest one is under ~50 us per call (where eager back-to-back
-    issue is launch-bound) all of them again from replayed graphs — one clock
-    for the comparison.  Opt-in: inside the BERT smoke step's backward a
-    replay of the timing graph never completed (event wait, faulthandler
-    trace in tools/gpu_r3s2t.sh); bench.py turns it on for DLRM, where it
-    was validated and pays (small MLP GEMMs)."""
-    times = {name: _time(fn, iters=iters, graph=False) for name, fn in fns.items()}
-    if (times and min(times.values()) < 0.05 and os.environ.get("FF_AUTOTUNE_GRAPH", "0") == "1"
-            and not torch.cuda.is_current_stream_capturing()):
+    """Time every candidate the same way: eagerly, and when the fastest one
+    is under ~50 us per call (where eager back-to-back issue is launch-bound)
+    all of them again with the queued clock (``_time_queued``), or with the
+    replayed-graph clock under FF_AUTOTUNE_GRAPH=1 -- one clock for the
+    comparison."""
+    times = {name: _time(fn, iters=iters) for name, fn in fns.items()}
+    if times and min(times.values()) < 0.05 and not torch.cuda.is_current_stream_capturing():
+        graph = os.environ.get("FF_AUTOTUNE_GRAPH", "0") == "1"
         try:
-            times = {name: _time_graphed(fn, max(iters, 10)) for name, fn in fns.items()}
+            out = {}
+            for name, fn in fns.items():
+                if _TRACE:
+                    import sys
+                    print(f"[autotune] {'graph' if graph else 'queued'} clock: {name}", file=sys.stderr, flush=True)
+                out[name] = _time_graphed(fn, max(iters, 10)) if graph else _time_queued(fn, max(iters, 10))
+            times = out
         except Exception:  # a candidate that cannot be captured: keep the eager clock for all
             torch.cuda.synchronize()
     return times
 
 
-def _time(fn, iters=5, rounds=2, graph=True) -> float:
-    """min over rounds of the mean time of ``iters`` back-to-back calls;
-    below ~30 us per call (launch-bound when issued eagerly) the candidate is
-    re-timed from a replayed graph (``_time_all`` for a fair comparison)."""
+def _time(fn, iters=5, rounds=2) -> float:
+    """min over rounds of the mean time of ``iters`` back-to-back calls."""
     fn()
     best = float("inf")
     for _ in range(rounds):
@@ -353,12 +411,6 @@ def _time(fn, iters=5, rounds=2, graph=True) -> float:
         e.record()
         e.synchronize()
         best = min(best, s.elapsed_time(e) / iters)
-    if graph and best < 0.03 and os.environ.get("FF_AUTOTUNE_GRAPH", "0") == "1" and \
-            not torch.cuda.is_current_stream_capturing():
-        try:
-            best = _time_graphed(fn, max(iters, 10))
-        except Exception:  # a candidate that cannot be captured keeps its eager time
-            torch.cuda.synchronize()
     return best
 
 

@@ -42,10 +42,17 @@ from .layout import Box, Layout, intersect, rel_slices
 class DistContext:
     """Process-group bookkeeping for one rank."""
 
-    def __init__(self, rank: int = 0, world: int = 1, device: Optional[torch.device] = None):
+    def __init__(self, rank: int = 0, world: int = 1, device: Optional[torch.device] = None,
+                 force_collectives: bool = False):
         self.rank = rank
         self.world = world
         self.device = device or torch.device("cpu")
+        # FF_DIST_WORLD1=1: a one-rank process group whose collectives are
+        # still issued (single-member groups included), so the whole RCCL
+        # path -- communicator creation, bucketed gradient all-reduce /
+        # reduce-scatter / all-gather, all-to-all redistribution and the
+        # graph segments cut at every collective -- runs on a single GPU
+        self.force_collectives = force_collectives
         self._groups: Dict[Tuple[int, ...], object] = {}
         self.stats = {"all_reduce": 0, "all_gather": 0, "all_to_all": 0, "p2p": 0, "local": 0, "bytes": 0}
         # runtime/graphs.SegmentRecorder while a distributed step is being
@@ -61,7 +68,13 @@ class DistContext:
     def from_env(cls, device: Optional[torch.device] = None, backend: Optional[str] = None) -> "DistContext":
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
-        if world > 1 and not dist.is_initialized():
+        force = os.environ.get("FF_DIST_WORLD1", "0") == "1"
+        if (world > 1 or force) and not dist.is_initialized():
+            if world == 1:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", str(_free_port()))
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
             backend = backend or os.environ.get("FF_DIST_BACKEND") or None
             if backend is None:
                 backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
@@ -79,11 +92,19 @@ class DistContext:
             dist.init_process_group(backend=backend, **kw)
         if dist.is_initialized():
             rank, world = dist.get_rank(), dist.get_world_size()
-        return cls(rank, world, device)
+        return cls(rank, world, device, force_collectives=force and dist.is_initialized())
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1 and dist.is_initialized()
+        return (self.world > 1 or self.force_collectives) and dist.is_initialized()
+
+    @property
+    def backend(self) -> str:
+        return str(dist.get_backend()) if dist.is_initialized() else "none"
+
+    def syncs(self, ranks: Sequence[int]) -> bool:
+        """True when a collective over ``ranks`` is actually issued."""
+        return self.distributed and (len(ranks) > 1 or (self.force_collectives and len(ranks) == 1))
 
     def group(self, ranks: Sequence[int]):
         """Sub-communicator for ``ranks``; MUST be called in the same order on
@@ -100,7 +121,7 @@ class DistContext:
             dist.barrier()
 
     def all_reduce_(self, t: torch.Tensor, ranks: Sequence[int], async_op: bool = False):
-        if len(ranks) <= 1 or not self.distributed:
+        if not self.syncs(ranks):
             return None
         self.stats["all_reduce"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
@@ -112,7 +133,7 @@ class DistContext:
         len(ranks) equal chunks) on the i-th rank of sorted(ranks) holds the
         sum.  RCCL runs it in place (output = input + rank * chunk); gloo has
         no reduce-scatter, so the CPU path all-reduces (a superset)."""
-        if len(ranks) <= 1 or not self.distributed:
+        if not self.syncs(ranks):
             return None
         self.stats["reduce_scatter"] = self.stats.get("reduce_scatter", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
@@ -128,7 +149,7 @@ class DistContext:
     def reduce_(self, t: torch.Tensor, ranks: Sequence[int], dst: int, async_op: bool = False):
         """Sum ``t`` over ``ranks`` into rank ``dst`` (parameter-server gradient
         gather, the reference's ParamSync::PS, optimizer_kernel.cu:43-70)."""
-        if len(ranks) <= 1 or not self.distributed:
+        if not self.syncs(ranks):
             return None
         self.stats["reduce"] = self.stats.get("reduce", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
@@ -136,7 +157,7 @@ class DistContext:
         return self._issue(lambda: dist.reduce(t, dst=dst, group=grp, async_op=async_op), async_op)
 
     def broadcast_(self, t: torch.Tensor, ranks: Sequence[int], src: int, async_op: bool = False):
-        if len(ranks) <= 1 or not self.distributed:
+        if not self.syncs(ranks):
             return None
         self.stats["broadcast"] = self.stats.get("broadcast", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
@@ -146,7 +167,7 @@ class DistContext:
     def all_gather_(self, t: torch.Tensor, ranks: Sequence[int]):
         """In-place all-gather of the equal chunks of the 1-D ``t`` (chunk i
         comes from the i-th rank of sorted(ranks))."""
-        if len(ranks) <= 1 or not self.distributed:
+        if not self.syncs(ranks):
             return
         n = len(ranks)
         i = sorted(ranks).index(self.rank)
@@ -167,6 +188,13 @@ class DistContext:
         t = torch.tensor([v], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 # ---------------------------------------------------------------------------

@@ -152,17 +152,16 @@ def _stable_seed(*parts) -> int:
 
 
 class Executor:
-    # constant inputs: name -> host array (FFModel.create_constant*), and
-    # their device pieces, built on the first forward
-    constants: Dict[str, object] = {}
-    _const_env: Optional[Dict] = None
-
     def __init__(self, pcg, dist_ctx: DistContext, cfg: ExecConfig, views: Optional[Dict[int, Tuple[int, int]]] = None,
                  loss_type=None, metrics: Sequence[str] = (), optimizer=None, output: Optional[Value] = None,
                  label_dtype: Optional[torch.dtype] = None, valid_classes: Optional[int] = None):
         self.pcg = pcg
         self.dist = dist_ctx
         self.cfg = cfg
+        # constant inputs: name -> host array (FFModel.create_constant*), and
+        # their device pieces, built on the first forward (per executor)
+        self.constants: Dict[str, object] = {}
+        self._const_env: Optional[Dict] = None
         self.views = dict(views or {})
         self.world = dist_ctx.world
         self.rank = dist_ctx.rank
@@ -624,7 +623,8 @@ class Executor:
             groups.setdefault((p.group, str(p.grad_dtype), p.sparse), []).append(p)
         self.flats = []
         for fid, ((g, gdt, sparse), plist) in enumerate(sorted(groups.items(), key=lambda kv: kv[0])):
-            zero = self.cfg.shard_optimizer and len(g) > 1
+            multi = len(g) > 1 or (self.dist.force_collectives and len(g) == 1)
+            zero = self.cfg.shard_optimizer and multi
             esize = torch.tensor([], dtype=plist[0].grad_dtype).element_size()
             # buckets: contiguous param ranges, finalised in backward order
             buckets, cur, cur_bytes = [], [], 0
@@ -668,7 +668,7 @@ class Executor:
                 opt = FlatOptimizer(self.optimizer_cfg, master, grad, compute)
             self.flats.append({"group": g, "params": plist, "master": master, "grad": grad, "compute": compute,
                                "buckets": binfo, "opt": opt, "zero": zero, "sparse": sparse,
-                               "ps": (not zero) and self.cfg.param_sync == "ps" and len(g) > 1})
+                               "ps": (not zero) and self.cfg.param_sync == "ps" and multi})
         for p in self.params:
             if p.sparse and 0 <= p.final_step < len(self.steps):
                 self.steps[p.final_step].ctx.extra["track_rows"] = True
@@ -689,7 +689,7 @@ class Executor:
                     all_groups.add(tuple(sorted(lay.rank_of(dataclasses.replace(c, b=b)) for b in range(lay.b_deg))))
             all_groups |= self._sp_groups
             for g in sorted(all_groups):
-                if len(g) > 1:
+                if self.dist.syncs(g):
                     self.dist.group(g)
             for s in self.steps:
                 if s.kind == "comm":
@@ -1184,7 +1184,7 @@ class Executor:
             self._wg_join()
             self._update_bucket(f, b)
         elif b["pending"] == 0 and self.cfg.overlap_grad_sync:
-            if len(f["group"]) > 1 and self.dist.distributed:
+            if self.dist.syncs(f["group"]):
                 self._wg_join()
             self._launch_bucket(f, b)
 
@@ -1195,7 +1195,10 @@ class Executor:
         it before the all-reduce sums them."""
         kind, lam = p.regularizer
         lam = lam / max(1, len(p.group))
-        w = p.master.view(p.grad.shape)
+        # the compute copy is whole on every replica (bf16: all-gathered after
+        # each sharded update; fp32: it IS the master, all-gathered likewise);
+        # under ZeRO a bf16 run keeps only this rank's shard of the master current
+        w = p.compute.view(p.grad.shape)
         if kind == "l2":
             p.grad.add_(w.to(p.grad.dtype), alpha=lam)
         else:
@@ -1237,7 +1240,7 @@ class Executor:
         wg[2].clear()
 
     def _launch_bucket(self, f, b):
-        if len(f["group"]) > 1 and self.dist.distributed and not b.get("launched"):
+        if self.dist.syncs(f["group"]) and not b.get("launched"):
             if f["zero"]:
                 # sharded optimizer: each rank only needs the sum of its shard
                 w = self.dist.reduce_scatter_(f["grad"][b["lo"]:b["hi"]], f["group"], async_op=True)
@@ -1408,7 +1411,7 @@ class Executor:
             return []
         out = []
         for f in self.flats:
-            if f["zero"] or f["ps"] or f["sparse"] or (len(f["group"]) > 1 and self.dist.distributed):
+            if f["zero"] or f["ps"] or f["sparse"] or (self.dist.syncs(f["group"])):
                 continue
             if isinstance(f["opt"], FlatOptimizer) and f["opt"].range_capable():
                 out.append(f)

@@ -18,10 +18,27 @@ and their ratio (``predicted_speedup_over_dp``), the reference's headline
 from __future__ import annotations
 
 import json
+import os
 from typing import Dict, Tuple
 
 from .. import _ffcore as C
 from . import native
+
+
+DEFAULT_RULES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "taso_rules.json")
+
+
+def substitution_path(ffconfig) -> str:
+    """The Unity rule-set file FFConfig asks for ("" -> the bundled TASO
+    corpus, "none" -> no rule set)."""
+    p = getattr(ffconfig, "substitution_json_path", "") or ""
+    if p.lower() == "none":
+        return ""
+    if not p:
+        return DEFAULT_RULES if os.path.exists(DEFAULT_RULES) else ""
+    if not os.path.exists(p):
+        raise FileNotFoundError(f"--substitution-json {p}: no such file")
+    return p
 
 
 def _search_local(cg, ffconfig, world: int):
@@ -36,6 +53,10 @@ def _search_local(cg, ffconfig, world: int):
         "enable_attribute_parallel": bool(ffconfig.enable_attribute_parallel),
         "seed": int(ffconfig.seed) & 0x7FFFFFFF,
         "sim": native.sim_config(ffconfig, world),
+        # Unity expands as many states as the reference's single --budget
+        # (unity_algorithm.cc:37-90), over the built-in rules + the rule set
+        "unity_budget": budget,
+        "substitution_path": substitution_path(ffconfig),
     }
     algo = ffconfig.search_algorithm
     if algo == "mcmc":

@@ -36,6 +36,15 @@ def save_checkpoint(model, path: str, progress: Optional[dict] = None):
     complete checkpoint.  ``progress``: training-loop position (fit resume)."""
     ex = model.executor if hasattr(model, "executor") else model
     os.makedirs(path, exist_ok=True)
+    if ex.rank == 0:
+        # rewriting an existing directory: it stops counting as complete
+        # before any shard is replaced, so a crash mid-save cannot leave old
+        # meta.json beside a mix of old and new shards
+        try:
+            os.remove(os.path.join(path, "meta.json"))
+        except FileNotFoundError:
+            pass
+    ex.dist.barrier()
     st = ex.state_dict()
     tmp = os.path.join(path, f"rank{ex.rank}.pt.tmp")
     torch.save(st, tmp)

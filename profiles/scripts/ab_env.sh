@@ -1,5 +1,5 @@
 # A/B of one environment toggle on the same box:
-#   bash tools/ab_env.sh VAR "bench args" out_name [value_a value_b]
+#   bash profiles/scripts/ab_env.sh VAR "bench args" out_name [value_a value_b]
 # Runs bench.py with VAR=a and VAR=b twice each (interleaved), lines into gpurun_out/<out_name>.txt
 set -o pipefail
 VAR=$1; ARGS=$2; OUT=gpurun_out/$3.txt

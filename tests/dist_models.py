@@ -17,6 +17,17 @@ def mlp(m):
     return {"x": torch.randn(16, 32, generator=g)}, torch.randint(0, 8, (16,), generator=g)
 
 
+def mlp_l2(m):
+    """MLP whose first Dense carries an L2 kernel regularizer."""
+    x = m.create_tensor([16, 32], DataType.DT_FLOAT, name="x")
+    t = m.dense(x, 64, ActiMode.AC_MODE_RELU, kernel_regularizer=("l2", 0.5), name="fc0")
+    t = m.dense(t, 48, kernel_regularizer=("l1", 0.05), name="fc1")
+    t = m.dense(t, 8, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(9)
+    return {"x": torch.randn(16, 32, generator=g)}, torch.randint(0, 8, (16,), generator=g)
+
+
 def attention(m):
     B, S, E = 4, 8, 32
     x = m.create_tensor([B, S, E], DataType.DT_FLOAT, name="x")

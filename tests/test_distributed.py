@@ -130,6 +130,18 @@ def test_sharded_optimizer_matches(world):
     assert out["stats"].get("reduce_scatter", 0) > 0
 
 
+def test_sharded_optimizer_regularizer_bf16():
+    """ZeRO with bf16 compute and L1/L2 kernel regularizers: only this rank's
+    shard of the fp32 master is current, so lambda*W must come from the
+    (whole, all-gathered) compute copy -- same trajectory as the unsharded
+    2-rank run at the same precision."""
+    over = {"compute_dtype": "bfloat16-cpu", "bucket_mb": 0}
+    ref = run_distributed(M.mlp_l2, 2, steps=4, optimizer="adam", cfg_over=over)
+    out = run_distributed(M.mlp_l2, 2, steps=4, optimizer="adam", cfg_over=dict(over, shard_optimizer=True))
+    assert out["stats"].get("reduce_scatter", 0) > 0
+    assert_params_close(out["params"], ref["params"], rtol=1e-2, atol=1e-3)
+
+
 def test_recompile_switches_strategy(tmp_path):
     """RecompileState: after 2 DP steps switch to a tensor-parallel strategy
     (alter = import a strategy file) and continue; the result matches 4

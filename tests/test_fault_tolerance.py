@@ -93,7 +93,8 @@ def test_pruning_counts_only_complete_checkpoints(tmp_path):
 
 def test_resume_with_other_epoch_size_restores_nothing(tmp_path):
     """A checkpoint recorded with a different iterations-per-epoch is not
-    resumed: neither its weights nor its step counter are loaded."""
+    resumed: its weights are not loaded, and the step counter continues past
+    its step so later checkpoints sort after it."""
     import json
     d = str(tmp_path / "ckpt")
     _fit(d, 4, True)
@@ -105,9 +106,29 @@ def test_resume_with_other_epoch_size_restores_nothing(tmp_path):
     ref, steps = _fit(None, 0, True)
     with pytest.warns(UserWarning, match="not resuming"):
         got, steps2 = _fit(d, 0, True)
-    assert steps2 == steps
+    assert steps2 == 12 + steps
     for n in ref:
         torch.testing.assert_close(got[n], ref[n], rtol=0, atol=0)
+
+
+def test_saves_after_a_non_resumed_start_survive(tmp_path):
+    """After a mismatched checkpoint is skipped, the run's own checkpoints are
+    numbered after it, survive the keep-newest rotation, and are what a
+    restart resumes from."""
+    import json
+    from flexflow_train_amd.utils.checkpoint import latest_checkpoint, read_checkpoint_meta
+    d = str(tmp_path / "ckpt")
+    _fit(d, 4, True)
+    meta_f = os.path.join(d, "step-12", "meta.json")
+    meta = json.load(open(meta_f))
+    meta["progress"]["iters_per_epoch"] = 99
+    json.dump(meta, open(meta_f, "w"))
+    with pytest.warns(UserWarning, match="not resuming"):
+        _fit(d, 4, True)                     # steps 13..24, checkpoints at 16, 20, 24
+    assert sorted(os.listdir(d)) == ["step-20", "step-24"]
+    last = latest_checkpoint(d)
+    assert last.endswith("step-24")
+    assert read_checkpoint_meta(last)["progress"]["iters_per_epoch"] == N // B
 
 
 def _rank(rank, world, port, d, fault, out):
