@@ -279,7 +279,6 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
     return c
 
 
-_TIME_STREAM: Dict[int, "torch.cuda.Stream"] = {}
 _TRACE = os.environ.get("FF_AUTOTUNE_TRACE", "0") == "1"
 _SLEEP_PER_MS: Dict[int, float] = {}   # device -> torch.cuda._sleep cycles per millisecond
 
@@ -308,9 +307,13 @@ def _time_queued(fn, iters: int, rounds: int = 2) -> float:
     device busy-wait and bracketed by events.  Eager back-to-back calls of a
     10-20 us GEMM time the host launch path (pybind + Python), which the
     training step -- itself one hipGraph -- never pays; this clock sees only
-    the kernels, without capturing anything (the graph clock below is the
-    research alternative).  If the host needed longer to queue the calls
-    than the busy-wait lasted, the round is repeated with a longer wait."""
+    the kernels, without capturing anything.  It replaces round 3's clock
+    that replayed each candidate from a captured hipGraph: one such replay
+    (torch's in-place hipBLASLt accumulate, captured inside the smoke step's
+    backward) never completed, while the same capture / replay outside a
+    training step completes (docs/PERF.md 'Autotuner clock').  If the host
+    needed longer to queue the calls than the busy-wait lasted, the round is
+    repeated with a longer wait."""
     import time as _time_mod
     fn()
     best = float("inf")
@@ -335,66 +338,20 @@ def _time_queued(fn, iters: int, rounds: int = 2) -> float:
     return best
 
 
-def _time_graphed(fn, iters: int) -> float:
-    """Mean device time of ``fn`` from a replayed hipGraph of ``iters`` calls
-    (FF_AUTOTUNE_GRAPH=1 only; see docs/PERF.md 'autotuner graph clock' for
-    the replay that never completed).  The candidate is first run eagerly on
-    the timing stream so any per-stream workspace it caches is allocated
-    outside the capture."""
-    dev = torch.cuda.current_device()
-    ts = _TIME_STREAM.setdefault(dev, torch.cuda.Stream())
-    sync = os.environ.get("FF_AUTOTUNE_GRAPH_SYNC", "1") == "1"
-    if sync:
-        torch.cuda.synchronize()
-    ts.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(ts):
-        fn()
-    if sync:
-        torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(ts):
-        g.capture_begin()
-        try:
-            for _ in range(iters):
-                fn()
-        finally:
-            g.capture_end()
-    if sync:
-        torch.cuda.synchronize()
-    g.replay()
-    best = float("inf")
-    for _ in range(2):
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(ts):
-            s.record()
-            g.replay()
-            e.record()
-        e.synchronize()
-        best = min(best, s.elapsed_time(e) / iters)
-    torch.cuda.current_stream().wait_stream(ts)
-    return best
-
-
 def _time_all(fns: Dict[str, Callable[[], Any]], iters=5) -> Dict[str, float]:
     """Time every candidate the same way: eagerly, and when the fastest one
     is under ~50 us per call (where eager back-to-back issue is launch-bound)
-    all of them again with the queued clock (``_time_queued``), or with the
-    replayed-graph clock under FF_AUTOTUNE_GRAPH=1 -- one clock for the
-    comparison."""
+    all of them again with the queued clock (``_time_queued``) -- one clock
+    for the comparison."""
     times = {name: _time(fn, iters=iters) for name, fn in fns.items()}
     if times and min(times.values()) < 0.05 and not torch.cuda.is_current_stream_capturing():
-        graph = os.environ.get("FF_AUTOTUNE_GRAPH", "0") == "1"
-        try:
-            out = {}
-            for name, fn in fns.items():
-                if _TRACE:
-                    import sys
-                    print(f"[autotune] {'graph' if graph else 'queued'} clock: {name}", file=sys.stderr, flush=True)
-                out[name] = _time_graphed(fn, max(iters, 10)) if graph else _time_queued(fn, max(iters, 10))
-            times = out
-        except Exception:  # a candidate that cannot be captured: keep the eager clock for all
-            torch.cuda.synchronize()
+        out = {}
+        for name, fn in fns.items():
+            if _TRACE:
+                import sys
+                print(f"[autotune] queued clock: {name}", file=sys.stderr, flush=True)
+            out[name] = _time_queued(fn, max(iters, 10))
+        times = out
     return times
 
 
