@@ -2,6 +2,8 @@
 // simulator, machine mapping, substitutions and strategy search.
 // Structured results cross the boundary as JSON strings (parsed by
 // flexflow_train_amd.search.native); graphs stay native objects.
+#include <limits>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -21,15 +23,85 @@ namespace ff {
 
 namespace {
 
-std::map<int, DeviceBlock> views_from_py(const std::map<int, std::pair<int, int>>& v) {
-  std::map<int, DeviceBlock> r;
-  for (auto const& kv : v) r[kv.first] = DeviceBlock{kv.second.first, kv.second.second};
-  return r;
+std::map<int, std::vector<int>> views_to_py(const std::map<int, Placement>& v) {
+  return std::map<int, std::vector<int>>(v.begin(), v.end());
 }
 
-std::map<int, std::pair<int, int>> views_to_py(const std::map<int, DeviceBlock>& v) {
-  std::map<int, std::pair<int, int>> r;
-  for (auto const& kv : v) r[kv.first] = {kv.second.start, kv.second.size};
+// ---- the generic machine-mapping DP over a JSON-described problem with a
+// table cost estimator (the reference's make_fake_cost_estimator cases,
+// lib/compiler/test/src/compiler/machine_mapping/get_optimal_machine_mapping.cc)
+BinaryTreePath path_from(const std::string& s) {
+  BinaryTreePath p;
+  for (char c : s)
+    if (c == 'L' || c == 'R') p.push_back(c == 'R');
+  return p;
+}
+std::string path_to(const BinaryTreePath& p) {
+  std::string s;
+  for (int x : p) s += x ? 'R' : 'L';
+  return s;
+}
+
+int tree_from_json(MMProblemTree& t, const Json& j) {
+  if (j.contains("leaf")) {
+    UnmappedOpKey k;
+    k.id = j.at("leaf").as_string();
+    if (j.contains("task_space")) {
+      std::vector<int64_t> ts;
+      for (auto const& x : j.at("task_space").as_array()) ts.push_back(x.as_int());
+      ParallelTensorShape o;
+      for (size_t i = 0; i + 2 < ts.size(); ++i) o.shard_dims.push_back({ts[i], static_cast<int>(ts[i])});
+      o.sum_degree = ts.size() >= 2 ? static_cast<int>(ts[ts.size() - 2]) : 1;
+      o.discard_copy_degree = ts.empty() ? 1 : static_cast<int>(ts.back());
+      k.outputs.push_back(o);
+    }
+    return t.add_leaf(k);
+  }
+  int l = tree_from_json(t, j.at("left"));
+  int r = tree_from_json(t, j.at("right"));
+  if (j.at("kind").as_string() == "parallel") return t.add_parallel(l, r);
+  std::vector<AbstractedSingleTensorMovement> mv;
+  if (j.contains("movement"))
+    for (auto const& m : j.at("movement").as_array()) {
+      AbstractedSingleTensorMovement a;
+      for (auto const& x : m.at("src").as_array()) a.src.insert(path_from(x.as_string()));
+      for (auto const& x : m.at("dst").as_array()) a.dst.insert(path_from(x.as_string()));
+      mv.push_back(a);
+    }
+  return t.add_series(mv, l, r);
+}
+
+struct TableEstimator : MMCostEstimator {
+  std::map<std::string, double> ops, moves;
+  double default_op = std::numeric_limits<double>::infinity();
+  double default_move = std::numeric_limits<double>::infinity();
+  double estimate_op(const UnmappedOpKey& k, const MachineView& v) const override {
+    auto it = ops.find(k.id + "@" + v.str());
+    return it == ops.end() ? default_op : it->second;
+  }
+  static std::string move_key(const std::vector<SingleTensorMovement>& m) {
+    std::string s;
+    for (auto const& x : m) {
+      s += "[";
+      for (auto const& v : x.src) s += v.str() + ",";
+      s += "->";
+      for (auto const& v : x.dst) s += v.str() + ",";
+      s += "]";
+    }
+    return s;
+  }
+  double estimate_movement(const std::vector<SingleTensorMovement>& m) const override {
+    auto it = moves.find(move_key(m));
+    return it == moves.end() ? default_move : it->second;
+  }
+};
+
+MachineResource resource_from(const Json& j) {
+  MachineResource r;
+  if (j.contains("node_offset")) r.node_offset = static_cast<int>(j.at("node_offset").as_int());
+  if (j.contains("gpu_offset")) r.gpu_offset = static_cast<int>(j.at("gpu_offset").as_int());
+  r.num_nodes = static_cast<int>(j.at("num_nodes").as_int());
+  r.gpus_per_node = static_cast<int>(j.at("gpus_per_node").as_int());
   return r;
 }
 
@@ -215,12 +287,37 @@ void register_ext_bindings(py::module_& m) {
 
   // ---- simulator
   m.def("simulate", [](const ParallelComputationGraph& p, const CostModel& cm, const std::string& sim_cfg,
-                       const std::map<int, std::pair<int, int>>& views, bool dot) {
-    Simulator S(cm, sim_config_from_json(sim_cfg.empty() ? Json::object() : Json::parse(sim_cfg)));
-    auto r = S.simulate(p, views_from_py(views), dot);
-    return py::make_tuple(r.to_json().dump(), dot ? S.task_graph_dot(r) : std::string());
+                       const std::map<int, std::vector<int>>& views, bool dot, const NetworkModel* net) {
+    SimConfig c = sim_config_from_json(sim_cfg.empty() ? Json::object() : Json::parse(sim_cfg));
+    c.network = net;
+    Simulator S(cm, c);
+    auto r = S.simulate(p, std::map<int, Placement>(views.begin(), views.end()), dot);
+    Json j = r.to_json();
+    if (dot) {
+      Json tl = Json::array();
+      for (auto const& t : r.tasks) {
+        Json x = Json::object();
+        x["type"] = static_cast<int64_t>(t.type);
+        x["name"] = t.name;
+        x["devices"] = Json(std::vector<int64_t>(t.devices.begin(), t.devices.end()));
+        x["src"] = static_cast<int64_t>(t.src);
+        x["dst"] = static_cast<int64_t>(t.dst);
+        x["bytes"] = t.bytes;
+        x["links"] = Json(std::vector<int64_t>(t.links.begin(), t.links.end()));
+        x["start"] = t.start_time;
+        x["end"] = t.end_time;
+        x["deps"] = Json(std::vector<int64_t>(t.deps.begin(), t.deps.end()));
+        tl.push_back(x);
+      }
+      j["tasks"] = tl;
+    }
+    return py::make_tuple(j.dump(), dot ? S.task_graph_dot(r) : std::string());
   }, py::arg("pcg"), py::arg("cost_model"), py::arg("sim_config") = "",
-        py::arg("views") = std::map<int, std::pair<int, int>>{}, py::arg("dot") = false);
+        py::arg("views") = std::map<int, std::vector<int>>{}, py::arg("dot") = false,
+        py::arg("network") = static_cast<const NetworkModel*>(nullptr));
+  m.def("region_transfers", [](const ParallelTensorShape& t, const std::vector<int>& src, const std::vector<int>& dst) {
+    return region_transfers(t, src, dst);
+  });
   m.def("evaluate_strategy", [](const ComputationGraph& cg, const std::string& strategy, const CostModel& cm,
                                 const std::string& sim_cfg, int world) {
     SimResult r;
@@ -231,14 +328,94 @@ void register_ext_bindings(py::module_& m) {
   });
 
   // ---- machine mapping
-  m.def("machine_mapping", [](const ParallelComputationGraph& p, const CostModel& cm, int world, bool sub_blocks) {
-    MachineMappingContext ctx;
-    ctx.cost = &cm;
-    ctx.allow_sub_blocks = sub_blocks;
-    MachineMapper mm(p, ctx);
-    auto r = mm.solve(DeviceBlock{0, world});
-    return py::make_tuple(r.runtime, r.feasible, views_to_py(r.views));
-  }, py::arg("pcg"), py::arg("cost_model"), py::arg("world"), py::arg("allow_sub_blocks") = true);
+  m.def("machine_mapping", [](const ParallelComputationGraph& p, const CostModel& cm, int world, bool contiguous) {
+    MachineMappingOptions o;
+    o.contiguous_only = contiguous;
+    MachineMappingResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = get_optimal_machine_mapping(p, cm, world, o);
+    }
+    return py::make_tuple(r.runtime, r.feasible, views_to_py(r.views), r.to_json().dump());
+  }, py::arg("pcg"), py::arg("cost_model"), py::arg("world"), py::arg("contiguous_only") = false);
+  m.def("machine_mapping_problem_tree", [](const ParallelComputationGraph& p) {
+    auto prob = get_machine_mapping_problem_tree(p);
+    Json j = Json::object();
+    j["num_entries"] = static_cast<int64_t>(prob.tree.e.size());
+    int series = 0, parallel = 0, moves = 0;
+    for (auto const& e : prob.tree.e) {
+      series += e.kind == MMProblemTree::SERIES;
+      parallel += e.kind == MMProblemTree::PARALLEL;
+      moves += static_cast<int>(e.movement.size());
+    }
+    j["series"] = static_cast<int64_t>(series);
+    j["parallel"] = static_cast<int64_t>(parallel);
+    j["movements"] = static_cast<int64_t>(moves);
+    Json leaves = Json::object();
+    for (auto const& kv : prob.node_of_path) leaves[path_to(kv.first)] = static_cast<int64_t>(kv.second);
+    j["leaves"] = leaves;
+    return j.dump();
+  });
+  // generic DP on a JSON problem + table costs (tests: the reference cases)
+  m.def("machine_mapping_dp", [](const std::string& problem, const std::string& table, const std::string& allowed,
+                                 const std::string& resources) {
+    MMProblemTree t;
+    t.root = tree_from_json(t, Json::parse(problem));
+    TableEstimator est;
+    Json tj = Json::parse(table);
+    for (auto const& x : tj.at("ops").as_array())
+      est.ops.emplace(x.at("leaf").as_string() + "@" + MachineView::from_json(x.at("view")).str(), x.at("cost").as_double());
+    for (auto const& x : tj.at("movements").as_array()) {
+      std::vector<SingleTensorMovement> mv;
+      for (auto const& y : x.at("tensors").as_array()) {
+        SingleTensorMovement s;
+        for (auto const& v : y.at("src").as_array()) s.src.push_back(MachineView::from_json(v));
+        for (auto const& v : y.at("dst").as_array()) s.dst.push_back(MachineView::from_json(v));
+        mv.push_back(s);
+      }
+      est.moves.emplace(TableEstimator::move_key(mv), x.at("cost").as_double());  // first wins (unordered_map init)
+    }
+    std::vector<std::pair<MachineResource, std::vector<MachineView>>> allow;
+    const Json aj = Json::parse(allowed);
+    for (auto const& x : aj.as_array()) {
+      std::vector<MachineView> vs;
+      for (auto const& v : x.at("views").as_array()) vs.push_back(MachineView::from_json(v));
+      allow.push_back({resource_from(x.at("resource")), vs});
+    }
+    MMContext ctx;
+    ctx.cost = &est;
+    ctx.allowed_views = [&](const UnmappedOpKey&, const MachineResource& r) {
+      for (auto const& a : allow)
+        if (a.first.num_nodes == r.num_nodes && a.first.gpus_per_node == r.gpus_per_node) return a.second;
+      return std::vector<MachineView>{};
+    };
+    MMCache cache;
+    auto r = get_optimal_machine_mapping(cache, ctx, t, resource_from(Json::parse(resources)));
+    if (!r) return std::string("null");
+    Json j = Json::object();
+    j["runtime"] = r->runtime;
+    Json m = Json::object();
+    for (auto const& kv : r->mapping) m[path_to(kv.first)] = kv.second.to_json();
+    j["mapping"] = m;
+    j["cache_entries"] = static_cast<int64_t>(cache.results.size());
+    return j.dump();
+  });
+  m.def("machine_resource_splits", [](const std::string& resource) {
+    Json out = Json::array();
+    for (auto const& sp : get_machine_resource_splits(resource_from(Json::parse(resource)))) {
+      Json x = Json::array();
+      for (auto const* r : {&sp.first, &sp.second}) {
+        Json y = Json::object();
+        y["node_offset"] = static_cast<int64_t>(r->node_offset);
+        y["num_nodes"] = static_cast<int64_t>(r->num_nodes);
+        y["gpu_offset"] = static_cast<int64_t>(r->gpu_offset);
+        y["gpus_per_node"] = static_cast<int64_t>(r->gpus_per_node);
+        x.push_back(y);
+      }
+      out.push_back(x);
+    }
+    return out.dump();
+  });
 
   // ---- substitutions
   py::class_<Substitution>(m, "Substitution")

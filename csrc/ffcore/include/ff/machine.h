@@ -76,9 +76,20 @@ struct MachineView {
   MachineSpaceCoordinate start;
   std::vector<MachineViewDimension> dims;
   bool operator==(const MachineView& o) const { return start == o.start && dims == o.dims; }
+  bool operator!=(const MachineView& o) const { return !(*this == o); }
+  bool operator<(const MachineView& o) const;
+  std::string str() const;
   Json to_json() const;
   static MachineView from_json(const Json& j);
 };
+
+// The devices an operator (or a tensor) occupies, in task linear order:
+// entry lin * reps + r holds task coordinate unravel(lin) (row-major over
+// [shard degrees..., sum, copy]), redundant replica r.  A contiguous device
+// block [start, start + size) is the placement {start, ..., start + size - 1}.
+using Placement = std::vector<int>;
+
+extern const double kMovementInfeasible;
 
 // Task space of an operator = the degrees of its output [shard..., sum, copy].
 std::vector<int> operator_task_space(const ParallelTensorShape& out);
@@ -106,6 +117,10 @@ struct DeviceBlock {
 MachineView block_machine_view(const std::vector<int>& ts, const DeviceBlock& b, const MachineSpecification& spec);
 // Power-of-two splits of a block into two disjoint halves-or-quarters.
 std::vector<std::pair<DeviceBlock, DeviceBlock>> get_resource_splits(const DeviceBlock& b);
+Placement block_placement(const DeviceBlock& b);
+Placement block_placement(int start, int size);
+// the devices of a view, in task linear order (= get_device_ids)
+Placement view_placement(const std::vector<int>& task_space, const MachineView& v, const MachineSpecification& spec);
 
 // ---------------------------------------------------------------------------
 // Cost model
@@ -163,6 +178,12 @@ class CostModel {
                           int block_size) const;
   // Moving a tensor between two device blocks of the same layout.
   double movement_cost(const ParallelTensorShape& t, const DeviceBlock& src, const DeviceBlock& dst) const;
+  // Moving a tensor between two placements (region intersection: piece i is
+  // held by every device of entries [i*reps, (i+1)*reps) on each side; a
+  // consumer device that does not hold its piece receives it from a holder;
+  // transfers between distinct device pairs run concurrently over their
+  // own xGMI links, inter-node pairs over the NIC).
+  double movement_cost(const ParallelTensorShape& t, const Placement& src, const Placement& dst) const;
   static std::string signature(const OpAttrs& op, const std::vector<TensorShape>& pieces);
 
  private:

@@ -51,7 +51,7 @@ struct SearchResult {
   std::string algorithm;
   ParallelComputationGraph pcg;
   StrategyConfig strategy;               // MCMC only
-  std::map<int, DeviceBlock> views;      // PCG node -> block (empty: whole world)
+  std::map<int, Placement> views;        // PCG node -> devices (empty: whole world)
   double cost = 0;                       // simulated seconds / iteration
   double data_parallel_cost = 0;
   int iterations = 0;

@@ -1,12 +1,25 @@
 // Event-driven simulator of one training iteration of a PCG on a machine.
 //
 // Parity: lib/runtime/src/simulator.cc Simulator::simulate_runtime (:816-1243)
-// — per-op forward/backward tasks (:823-841), transfer tasks for data
-// dependencies between different device sets (:843-901), weight-gradient
-// synchronization overlapped with backward (:914-955), list scheduling with
-// per-device serialization (:1020-1085), the NCCL all-reduce pass
-// (:1087-1215) and the framebuffer memory penalty (:1216-1242); dot export
-// of the task graph (--taskgraph).
+// and LogicalTaskgraphBasedSimulator (:1245-1870):
+//  * per-operator forward / backward tasks on the devices of the operator's
+//    placement (each device's compute lane runs its partition; :823-841);
+//  * data dependencies between operators on different device sets become
+//    transfer tasks sized by the intersection of the producer's and the
+//    consumer's pieces (region intersection, :843-899), from a holder of the
+//    piece to every consumer device that lacks it; with a NetworkModel the
+//    transfer is routed and occupies every link of its route
+//    (route_transfer, :1482-1683), else its device pair's xGMI link;
+//  * weight-gradient synchronization: NCCL mode = bucketed all-reduces on
+//    each device's communication lane, serialized per device and overlapped
+//    with the rest of the backward pass (the NCCL pass, :1087-1215; with a
+//    NetworkModel the all-reduce is priced by its ring expansion over the
+//    routed links, expand_allreduce :1684-1795); parameter-server mode =
+//    gradients reduced into the group leader, the update on the leader, the
+//    weights broadcast back (barrier / update / final tasks, :957-1019);
+//  * list scheduling in each rank's issue order with per-device (and
+//    per-link) serialization (:1020-1085);
+//  * framebuffer memory penalty (:1216-1242); dot export (--taskgraph).
 //
 // MI355X model: each device has a compute lane (one HIP stream: kernels and
 // the inline RCCL collectives of parallel ops) and a communication lane (the
@@ -23,6 +36,8 @@
 
 namespace ff {
 
+class NetworkModel;
+
 struct SimConfig {
   int world = 1;                      // devices used by the executor
   bool overlap_grad_sync = true;
@@ -32,30 +47,40 @@ struct SimConfig {
   double memory_penalty_per_mb = 1e-3;   // seconds per MB over capacity (reference: 1 ms / MB)
   double comm_compute_slowdown = 0.05;   // compute slowdown while a collective overlaps
   bool bf16_weight_grads = true;
+  bool parameter_server = false;         // ParamSync::PS instead of all-reduce
+  const NetworkModel* network = nullptr; // routed transfers / collectives (LogicalTaskgraph mode)
 };
 
 struct SimTask {
-  enum Type { FORWARD = 0, BACKWARD = 1, COMM = 2, UPDATE = 3, ALLREDUCE = 4 };
+  enum Type { FORWARD = 0, BACKWARD = 1, COMM = 2, UPDATE = 3, ALLREDUCE = 4, XFER = 5, REDUCE = 6, BCAST = 7,
+              BARRIER = 8 };
   Type type = FORWARD;
   int node = -1;
   std::string name;
-  int dev_start = 0, dev_size = 1;
+  int dev_start = 0, dev_size = 1;  // range covering `devices` (reports)
+  std::vector<int> devices;         // lanes the task occupies
+  std::vector<int> links;           // routed transfers: network link ids
+  int src = -1, dst = -1;           // XFER endpoints
+  double bytes = 0;
   double run_time = 0, ready_time = 0, start_time = 0, end_time = 0;
   std::vector<int> deps;
-  double xfer = 0;  // extra transfer latency added on the incoming edge
+  double xfer = 0;
 };
 
 struct SimResult {
   double iteration_time = 0;   // seconds
   double forward_time = 0;     // critical-path forward end
   double backward_end = 0;
-  double sync_time = 0;        // summed all-reduce time
+  double sync_time = 0;        // summed all-reduce / PS time
   double exposed_sync = 0;     // iteration_time - backward_end - update
   double update_time = 0;
   double comm_time = 0;        // summed parallel-op communication
+  double xfer_time = 0;        // summed region-intersection transfer time
+  double xfer_bytes = 0;
   double peak_memory = 0;      // max bytes on one device
   double memory_penalty = 0;
   int num_tasks = 0;
+  int num_xfers = 0;
   std::vector<SimTask> tasks;  // only filled when keep_tasks
   Json to_json() const;
 };
@@ -64,8 +89,9 @@ class Simulator {
  public:
   Simulator(const CostModel& cm, SimConfig cfg) : cm_(cm), cfg_(std::move(cfg)) {}
   const SimConfig& config() const { return cfg_; }
-  // views: PCG node -> device block (defaults to the whole world)
-  SimResult simulate(const ParallelComputationGraph& pcg, const std::map<int, DeviceBlock>& views = {},
+  // views: PCG node -> placement (device list in task order; default: the
+  // whole world, devices 0..world-1)
+  SimResult simulate(const ParallelComputationGraph& pcg, const std::map<int, Placement>& views = {},
                      bool keep_tasks = false) const;
   std::string task_graph_dot(const SimResult& r) const;
 
@@ -82,5 +108,9 @@ std::map<int, NodeRole> classify_nodes(const ParallelComputationGraph& pcg);
 OpCost pcg_node_cost(const CostModel& cm, const ParallelComputationGraph& pcg, int node, int block_size);
 // The PCG data-flow DAG restricted to COMPUTE/PARALLEL/INPUT nodes.
 DiGraph data_path_digraph(const ParallelComputationGraph& pcg);
+// Region intersection of one tensor between two placements: (src device,
+// dst device, bytes) for every consumer device that lacks its piece.
+std::vector<std::tuple<int, int, double>> region_transfers(const ParallelTensorShape& t, const Placement& src,
+                                                           const Placement& dst);
 
 }  // namespace ff

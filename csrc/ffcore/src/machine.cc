@@ -95,6 +95,8 @@ MachineView MachineView::from_json(const Json& j) {
   return v;
 }
 
+const double kMovementInfeasible = 1e30;
+
 std::vector<int> operator_task_space(const ParallelTensorShape& out) {
   std::vector<int> ts = out.shard_degrees();
   ts.push_back(out.sum_degree);
@@ -211,6 +213,37 @@ MachineView block_machine_view(const std::vector<int>& ts, const DeviceBlock& b,
   const int R = b.size / T;
   for (size_t i = 0; i < ts.size(); ++i) v.dims.push_back({R, ProjectionType::INTRA_NODE});
   return v;
+}
+
+bool MachineView::operator<(const MachineView& o) const {
+  if (start.node_idx != o.start.node_idx) return start.node_idx < o.start.node_idx;
+  if (start.device_idx != o.start.device_idx) return start.device_idx < o.start.device_idx;
+  if (dims.size() != o.dims.size()) return dims.size() < o.dims.size();
+  for (size_t i = 0; i < dims.size(); ++i) {
+    if (dims[i].stride != o.dims[i].stride) return dims[i].stride < o.dims[i].stride;
+    if (dims[i].projection != o.dims[i].projection) return dims[i].projection < o.dims[i].projection;
+  }
+  return false;
+}
+
+std::string MachineView::str() const {
+  std::string s = "(" + std::to_string(start.node_idx) + "," + std::to_string(start.device_idx) + ")[";
+  for (size_t i = 0; i < dims.size(); ++i) {
+    if (i) s += ",";
+    s += std::to_string(dims[i].stride) + (dims[i].projection == ProjectionType::INTER_NODE ? "N" : "D");
+  }
+  return s + "]";
+}
+
+Placement block_placement(int start, int size) {
+  Placement p(size);
+  for (int i = 0; i < size; ++i) p[i] = start + i;
+  return p;
+}
+Placement block_placement(const DeviceBlock& b) { return block_placement(b.start, b.size); }
+
+Placement view_placement(const std::vector<int>& ts, const MachineView& v, const MachineSpecification& spec) {
+  return get_device_ids(ts, v, spec);
 }
 
 std::vector<std::pair<DeviceBlock, DeviceBlock>> get_resource_splits(const DeviceBlock& b) {
@@ -455,6 +488,38 @@ OpCost CostModel::parallel_op_cost_uncached(const OpAttrs& op, const ParallelTen
   }
   c.memory = out_b;
   return c;
+}
+
+double CostModel::movement_cost(const ParallelTensorShape& t, const Placement& src, const Placement& dst) const {
+  if (src == dst || src.empty() || dst.empty()) return 0;
+  const int T = std::max(1, t.total_parallel_degree());
+  if (static_cast<int>(src.size()) % T || static_cast<int>(dst.size()) % T) return kMovementInfeasible;
+  const int rs = static_cast<int>(src.size()) / T, rd = static_cast<int>(dst.size()) / T;
+  const double piece = static_cast<double>(t.piece_shape().size_bytes());
+  std::map<std::pair<int, int>, double> pair_bytes;
+  std::map<int, double> in_bytes;
+  for (int i = 0; i < T; ++i) {
+    for (int r = 0; r < rd; ++r) {
+      const int d = dst[i * rd + r];
+      bool held = false;
+      for (int q = 0; q < rs && !held; ++q) held = src[i * rs + q] == d;
+      if (held) continue;
+      const int s = src[i * rs + (r % rs)];  // spread readers over the holders
+      pair_bytes[{s, d}] += piece;
+      in_bytes[d] += piece;
+    }
+  }
+  if (pair_bytes.empty()) return 0;
+  const int gpn = std::max(1, spec_.num_gpus_per_node);
+  double t_max = 0;
+  for (auto const& kv : pair_bytes) {
+    const bool inter = kv.first.first / gpn != kv.first.second / gpn;
+    const double bw = inter ? spec_.inter_node_bandwidth : spec_.xgmi_link_bandwidth;
+    t_max = std::max(t_max, kv.second / bw);
+  }
+  for (auto const& kv : in_bytes)
+    t_max = std::max(t_max, kv.second / (std::max(1, spec_.xgmi_links) * spec_.xgmi_link_bandwidth));
+  return t_max + spec_.collective_latency;
 }
 
 double CostModel::movement_cost(const ParallelTensorShape& t, const DeviceBlock& src, const DeviceBlock& dst) const {

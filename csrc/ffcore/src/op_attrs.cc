@@ -1172,7 +1172,8 @@ OpSpec fused_parallel_spec() {
   s.required = {"ops"};  // JSON array of parallel OpAttrs
   s.pout = [](const OpAttrs& a, const PShapes& in) {
     auto cur = in;
-    for (auto const& j : Json::parse(a.s("ops")).as_array()) {
+    const Json ops_j = Json::parse(a.s("ops"));
+    for (auto const& j : ops_j.as_array()) {
       OpAttrs sub = normalize_attrs(OpAttrs::from_json(j));
       cur = infer_parallel_output_shapes(sub, cur);
     }

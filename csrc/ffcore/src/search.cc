@@ -38,7 +38,7 @@ Json SearchResult::to_json(const ComputationGraph* cg) const {
   }
   if (cg && !strategy.empty()) j["strategy"] = strategy_to_json(*cg, strategy);
   Json v = Json::object();
-  for (auto const& kv : views) v[std::to_string(kv.first)] = Json(std::vector<int64_t>{kv.second.start, kv.second.size});
+  for (auto const& kv : views) v[std::to_string(kv.first)] = Json(std::vector<int64_t>(kv.second.begin(), kv.second.end()));
   j["views"] = v;
   return j;
 }
@@ -158,7 +158,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   SimConfig sim = cfg.sim;
   sim.world = cfg.world;
   Simulator S(cm, sim);
-  auto cost_of = [&](const ParallelComputationGraph& g, std::map<int, DeviceBlock>* views) -> double {
+  auto cost_of = [&](const ParallelComputationGraph& g, std::map<int, Placement>* views) -> double {
     try {
       if (cfg.use_machine_mapping) {
         auto m = get_optimal_machine_mapping(g, cm, cfg.world);
@@ -182,7 +182,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   std::vector<ParallelComputationGraph> states;
   std::vector<std::pair<int, int>> parent;   // state -> (parent state, rule index)
   parent.push_back({-1, -1});
-  std::vector<std::map<int, DeviceBlock>> state_views;
+  std::vector<std::map<int, Placement>> state_views;
   std::priority_queue<State, std::vector<State>, std::greater<State>> pq;
   std::unordered_set<size_t> seen;
   states.push_back(initial);
@@ -229,7 +229,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
         size_t h = next->structural_hash();
         prof[2] += now_s() - ta;
         if (!seen.insert(h).second) continue;
-        std::map<int, DeviceBlock> v;
+        std::map<int, Placement> v;
         ta = now_s();
         double c = cost_of(*next, &v);
         prof[3] += now_s() - ta;
@@ -309,6 +309,7 @@ SimConfig sim_config_from_json(const Json& j) {
   gd("memory_penalty_per_mb", c.memory_penalty_per_mb);
   gd("comm_compute_slowdown", c.comm_compute_slowdown);
   gb("bf16_weight_grads", c.bf16_weight_grads);
+  gb("parameter_server", c.parameter_server);
   return c;
 }
 

@@ -8,10 +8,13 @@ A ``Layout`` places the pieces of a ParallelTensorShape on ranks:
 * ``reps`` = implicit redundant replicas when the total degree T is smaller
   than the device block (the same piece computed redundantly).
 
-Placement (the MachineView of the op that produces the tensor): the block of
-ranks ``[start, start + block)``; within it rank ``start + lin*reps + rep``
-holds task coordinate ``unravel(lin, degrees + [a, b])`` (row-major, copy axis
-innermost, implicit replicas innermost of all).  With this canonical
+Placement (the MachineView of the op that produces the tensor): a device
+list (``devices``; the contiguous block ``[start, start + block)`` when it is
+None); entry ``lin*reps + rep`` of it holds task coordinate
+``unravel(lin, degrees + [a, b])`` (row-major, copy axis innermost, implicit
+replicas innermost of all).  Device lists come from the machine-mapping DP's
+MachineViews (strided views included: ``get_device_ids`` lists a view's
+devices in exactly this task order).  With this canonical
 placement the Unity/Megatron patterns line up without data movement:
 DP x TP puts TP groups on consecutive ranks, Replicate after Reduction is a
 no-op, a column-parallel Linear's output shard lives where its input copy
@@ -56,8 +59,17 @@ class Layout:
     # TP group's weight shards on consecutive ranks, exactly where the
     # matching activation pieces live.
     copy_outer: bool = False
+    # explicit placement (device per entry); None: [start, start + block)
+    devices: Optional[Tuple[int, ...]] = None
 
     def __post_init__(self):
+        if self.devices is not None:
+            devs = tuple(int(d) for d in self.devices)
+            object.__setattr__(self, "devices", devs)
+            object.__setattr__(self, "block", len(devs))
+            object.__setattr__(self, "start", devs[0] if devs else 0)
+            if len(set(devs)) != len(devs):
+                raise ValueError(f"layout: placement repeats a device {devs}")
         if len(self.sizes) != len(self.degrees):
             raise ValueError("layout: rank mismatch")
         for s, d in zip(self.sizes, self.degrees):
@@ -91,11 +103,22 @@ class Layout:
         return dataclasses.replace(self, summed="b" if self.summed == "a" else "a")
 
     def with_block(self, block: int, start: int = 0) -> "Layout":
-        return dataclasses.replace(self, block=block, start=start)
+        return dataclasses.replace(self, block=block, start=start, devices=None)
+
+    def with_devices(self, devices: Sequence[int]) -> "Layout":
+        return dataclasses.replace(self, devices=tuple(devices))
 
     # ---- placement
+    def _index(self, rank: int) -> int:
+        if self.devices is None:
+            return rank - self.start
+        try:
+            return self.devices.index(rank)
+        except ValueError:
+            return -1
+
     def coord(self, rank: int) -> Optional[Coord]:
-        idx = rank - self.start
+        idx = self._index(rank)
         if idx < 0 or idx >= self.block:
             return None
         lin, rep = divmod(idx, self.reps)
@@ -123,9 +146,12 @@ class Layout:
         lin = 0
         for d, v in zip(dims, vals):
             lin = lin * d + v
-        return self.start + lin * self.reps + coord.rep
+        idx = lin * self.reps + coord.rep
+        return self.start + idx if self.devices is None else self.devices[idx]
 
     def ranks(self) -> List[int]:
+        if self.devices is not None:
+            return list(self.devices)
         return list(range(self.start, self.start + self.block))
 
     def summed_index(self, c: Coord) -> int:
@@ -159,11 +185,39 @@ class Layout:
         yield from rec(0, [])
 
 
-def layout_from_pshape(pshape, block: int, start: int = 0) -> Layout:
-    """Layout of a C++ ParallelTensorShape (flexflow_train_amd._ffcore)."""
+def layout_from_pshape(pshape, block: int = 0, start: int = 0, devices: Optional[Sequence[int]] = None) -> Layout:
+    """Layout of a C++ ParallelTensorShape (flexflow_train_amd._ffcore) on the
+    block [start, start + block) or on an explicit device list."""
     sizes = tuple(int(d.size) for d in pshape.shard_dims)
     degs = tuple(int(d.degree) for d in pshape.shard_dims)
+    if devices is not None:
+        devices = tuple(int(d) for d in devices)
+        if devices == tuple(range(devices[0], devices[0] + len(devices))):
+            return Layout(sizes, degs, int(pshape.sum_degree), int(pshape.discard_copy_degree), len(devices),
+                          devices[0])
+        return Layout(sizes, degs, int(pshape.sum_degree), int(pshape.discard_copy_degree), len(devices),
+                      devices[0], devices=devices)
     return Layout(sizes, degs, int(pshape.sum_degree), int(pshape.discard_copy_degree), block, start)
+
+
+def placement(view, world: int) -> Tuple[int, ...]:
+    """Normalise a machine view to a device tuple: a device list / tuple as
+    is, a ``{"start": s, "block": b}`` dict (or ``("block", s, b)``) as the
+    block, None as the whole world."""
+    if view is None:
+        return tuple(range(world))
+    if isinstance(view, dict):
+        if "devices" in view:
+            return tuple(int(d) for d in view["devices"])
+        return tuple(range(int(view["start"]), int(view["start"]) + int(view["block"])))
+    if len(view) == 3 and view[0] == "block":
+        return tuple(range(int(view[1]), int(view[1]) + int(view[2])))
+    return tuple(int(d) for d in view)
+
+
+def block(start: int, size: int) -> Tuple[int, ...]:
+    """The contiguous device block [start, start + size) as a placement."""
+    return tuple(range(start, start + size))
 
 
 def intersect(b1: Box, b2: Box) -> Optional[Box]:

@@ -37,7 +37,7 @@ from .. import ops as _ops_pkg  # noqa: F401  (registers operator impls)
 from ..ops import base as opbase
 from ..ops.loss import N_SLOTS, LossFunction, PerfMetrics
 from ..parallel.comm import DistContext, Redistributor
-from ..parallel.layout import Layout, layout_from_pshape
+from ..parallel.layout import Layout, layout_from_pshape, placement
 from ..parallel.sequence import SeqGroup
 from ..ops.moe import ExpertGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig, ShardedOptimizer
@@ -152,7 +152,7 @@ def _stable_seed(*parts) -> int:
 
 
 class Executor:
-    def __init__(self, pcg, dist_ctx: DistContext, cfg: ExecConfig, views: Optional[Dict[int, Tuple[int, int]]] = None,
+    def __init__(self, pcg, dist_ctx: DistContext, cfg: ExecConfig, views: Optional[Dict[int, Sequence[int]]] = None,
                  loss_type=None, metrics: Sequence[str] = (), optimizer=None, output: Optional[Value] = None,
                  label_dtype: Optional[torch.dtype] = None, valid_classes: Optional[int] = None):
         self.pcg = pcg
@@ -162,8 +162,10 @@ class Executor:
         # their device pieces, built on the first forward (per executor)
         self.constants: Dict[str, object] = {}
         self._const_env: Optional[Dict] = None
-        self.views = dict(views or {})
         self.world = dist_ctx.world
+        # PCG node -> placement (device tuple in task order, search/machine
+        # mapping); nodes without one run on every rank
+        self.views = {int(k): placement(v, self.world) for k, v in (views or {}).items()}
         self.rank = dist_ctx.rank
         self.redist = Redistributor(dist_ctx)
         self.metrics_names = list(metrics)
@@ -189,12 +191,13 @@ class Executor:
         self._overlap_lr = None
 
     # ------------------------------------------------------------------ build
-    def _view(self, node: int) -> Tuple[int, int]:
-        return self.views.get(node, (0, self.world))
+    def _view(self, node: int) -> Tuple[int, ...]:
+        v = self.views.get(node)
+        return v if v is not None else tuple(range(self.world))
 
     def _layout(self, v: Value, node_for_view: Optional[int] = None) -> Layout:
-        start, block = self._view(v[0] if node_for_view is None else node_for_view)
-        return layout_from_pshape(self.pcg.shape(C.ValueRef(v[0], v[1])), block, start)
+        devs = self._view(v[0] if node_for_view is None else node_for_view)
+        return layout_from_pshape(self.pcg.shape(C.ValueRef(v[0], v[1])), devices=devs)
 
     def _build(self, output: Optional[Value]):
         pcg = self.pcg
@@ -297,18 +300,18 @@ class Executor:
             ins = inputs_of[n]
             if t in _PAR_OPS:
                 src = self.value_layout[ins[0]]
-                start, block = self._view(n)
-                dst = layout_from_pshape(pcg.shape(C.ValueRef(n, 0)), block, start)
+                devs = self._view(n)
+                dst = layout_from_pshape(pcg.shape(C.ValueRef(n, 0)), devices=devs)
                 self.steps.append(Step("comm", n, t, [ins[0]], [(n, 0)], src=src, dst=dst, name=names[n]))
                 self.value_layout[(n, 0)] = dst
                 continue
             nw = C.num_weights(pcg.layer_op(n))
             data_ins, w_ins = ins[:len(ins) - nw], ins[len(ins) - nw:]
-            start, block = self._view(n)
+            devs = self._view(n)
             # implicit view changes for data inputs
             real_ins = []
             for v in data_ins:
-                want = layout_from_pshape(pcg.shape(C.ValueRef(*v)), block, start)
+                want = layout_from_pshape(pcg.shape(C.ValueRef(*v)), devices=devs)
                 have = self.value_layout[v]
                 if have != want:
                     nv = (-(len(self.steps) + 1) * 1000 - v[0], v[1])  # synthetic value id
@@ -324,7 +327,7 @@ class Executor:
                 wpieces.append(self.param_of_value[v])
             outs = [(n, i) for i in range(nout[n])]
             for o in outs:
-                self.value_layout[o] = layout_from_pshape(pcg.shape(C.ValueRef(*o)), block, start)
+                self.value_layout[o] = layout_from_pshape(pcg.shape(C.ValueRef(*o)), devices=devs)
             olay = self.value_layout[outs[0]]
             coord = olay.coord(self.rank)
             in0 = pcg.shape(C.ValueRef(*data_ins[0])) if data_ins else None

@@ -197,18 +197,29 @@ def _records_for_layers(cg, ops: List[dict]) -> Dict[int, dict]:
     return out
 
 
-def _view(op: dict, world: int, name: str) -> Optional[Tuple[int, int]]:
-    ids = list(op.get("device_ids", ()))
+def _view(op: dict, world: int, name: str) -> Optional[Tuple[int, ...]]:
+    """The record's device ids as a placement (partition order = the task
+    order: the innermost dim varies fastest in both); None = every rank."""
+    ids = [int(d) for d in op.get("device_ids", ())]
     if not ids:
         return None
-    if max(ids) >= world:
+    if max(ids) >= world or min(ids) < 0:
         raise ValueError(f"strategy record '{name}' uses device {max(ids)} but only {world} ranks run")
-    lo = min(ids)
-    if sorted(ids) != list(range(lo, lo + len(ids))):
-        raise ValueError(f"strategy record '{name}': devices {ids} are not a contiguous block")
-    if lo == 0 and len(ids) == world:
+    if len(set(ids)) != len(ids):
+        raise ValueError(f"strategy record '{name}': devices {ids} repeat")
+    if ids == list(range(world)):
         return None
-    return (lo, len(ids))
+    return tuple(ids)
+
+
+def task_devices(view, total: int) -> List[int]:
+    """``total`` device ids of a placement in task order (one per partition;
+    implicit replicas dropped), every rank's first ``total`` when None."""
+    if view is None:
+        return list(range(total))
+    devs = list(view)
+    reps = max(1, len(devs) // max(1, total))
+    return devs[::reps][:total]
 
 
 def to_pcg(cg, ops: List[dict], world: int):
@@ -222,7 +233,7 @@ def to_pcg(cg, ops: List[dict], world: int):
         if key not in strat:
             raise ValueError(f"layer {name_of[n]!r} has no strategy entry")
         key_of[n] = key
-    views_cg: Dict[int, Tuple[int, int]] = {}
+    views_cg: Dict[int, Tuple[int, ...]] = {}
     for n, op in recs.items():
         dims = [int(d) for d in op.get("dims", ())] or [1]
         sample = dims[-1]
@@ -249,7 +260,7 @@ def to_pcg(cg, ops: List[dict], world: int):
     return pcg, views, report
 
 
-def from_pcg(pcg, views: Dict[int, Tuple[int, int]]) -> List[dict]:
+def from_pcg(pcg, views: Dict[int, Tuple[int, ...]]) -> List[dict]:
     """Per-op legacy records of a lowered strategy (dims innermost-first)."""
     ops = []
     for n in pcg.topo_order():
@@ -259,8 +270,7 @@ def from_pcg(pcg, views: Dict[int, Tuple[int, int]]) -> List[dict]:
         ps = pcg.shape(C.ValueRef(n, 0))
         deg = list(ps.shard_degrees())
         total = ps.total_parallel_degree()
-        start, block = views.get(n, (0, None))
         ops.append({"name": pcg.layer_name(n) or f"{op.op_type.lower()}{n}", "device_type": "GPU",
-                    "dims": list(reversed(deg)), "device_ids": list(range(start, start + (block or total))),
+                    "dims": list(reversed(deg)), "device_ids": task_devices(views.get(n), total),
                     "memory_types": []})
     return ops

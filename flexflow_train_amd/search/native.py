@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 from .. import _ffcore as C
 
@@ -87,19 +87,28 @@ def sim_config(ffconfig=None, world: int = 1) -> dict:
     return cfg
 
 
-def simulate(pcg, cm, world: int, views: Optional[Dict[int, Tuple[int, int]]] = None, dot: bool = False,
-             **sim_kw):
+def simulate(pcg, cm, world: int, views: Optional[Dict[int, Sequence[int]]] = None, dot: bool = False,
+             network=None, **sim_kw):
+    """Simulated iteration; ``views``: PCG node -> placement (device list in
+    task order); ``network``: a NetworkModel for routed transfers /
+    collectives; ``dot``: also the task list and its dot graph."""
     cfg = {"world": world, **sim_kw}
-    res, dot_s = C.simulate(pcg, cm, json.dumps(cfg), dict(views or {}), dot)
+    res, dot_s = C.simulate(pcg, cm, json.dumps(cfg), {int(k): [int(d) for d in v] for k, v in (views or {}).items()},
+                            dot, network)
     out = json.loads(res)
     if dot:
         out["dot"] = dot_s
     return out
 
 
-def machine_mapping(pcg, cm, world: int, allow_sub_blocks: bool = True):
-    runtime, feasible, views = C.machine_mapping(pcg, cm, world, allow_sub_blocks)
-    return {"runtime": runtime, "feasible": feasible, "views": {int(k): tuple(v) for k, v in views.items()}}
+def machine_mapping(pcg, cm, world: int, contiguous_only: bool = False):
+    """The machine-mapping DP (csrc/ffcore/src/mapping.cc): runtime, and per
+    PCG node its placement (device tuple) and MachineView."""
+    runtime, feasible, views, rep = C.machine_mapping(pcg, cm, world, contiguous_only)
+    rep = json.loads(rep)
+    return {"runtime": runtime, "feasible": feasible, "views": {int(k): tuple(v) for k, v in views.items()},
+            "machine_views": {int(k): v for k, v in rep.get("machine_views", {}).items()},
+            "cache_entries": rep.get("cache_entries", 0)}
 
 
 def sp_decomposition(graph, strict: bool = False):

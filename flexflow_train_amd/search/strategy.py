@@ -8,11 +8,13 @@ lib/runtime/src/model.cc compile, examples/cpp/DLRM/strategies/*.pb).
 
 Strategy file (JSON, "ffmi355x.strategy.v1"):
   {"world": N, "pcg": <ParallelComputationGraph v1 JSON>,
-   "views": {"<node>": [start, block]},
+   "placements": {"<node>": [device, ...]},      (task order; round <= 3 files:
+   "views": {"<node>": [start, block]}, still read)
    "ops": [{"name", "op_type", "device_type": "GPU", "degrees": [...],
             "sum_degree", "discard_copy_degree", "device_ids": [...]}]}
 The "ops" list mirrors the reference's per-op FFProtoBuf::Strategy records
-(keyed by op name) and is informational; the PCG + views are authoritative.
+(keyed by op name) and is informational; the PCG + placements are
+authoritative.
 A ``.pb`` path reads / writes the reference's protobuf strategy format itself
 (legacy_strategy.py), e.g. examples/cpp/DLRM/strategies/*.pb.
 """
@@ -23,6 +25,7 @@ import os
 from typing import Dict, Tuple
 
 from .. import _ffcore as C
+from ..parallel.layout import block as _block
 from ..utils.logging import get_logger
 from . import legacy_strategy as legacy
 
@@ -70,7 +73,7 @@ def build_pcg(cg, ffconfig, world: int):
     return pcg, views, report
 
 
-def export_strategy(path: str, pcg, views: Dict[int, Tuple[int, int]], report=None):
+def export_strategy(path: str, pcg, views: Dict[int, Tuple[int, ...]], report=None):
     if path.endswith(".pb"):
         # the reference's protobuf format (per-op degrees + device ids)
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
@@ -83,14 +86,14 @@ def export_strategy(path: str, pcg, views: Dict[int, Tuple[int, int]], report=No
         if op.op_type in ("INPUT", "WEIGHT") or pcg.is_weight_path(n):
             continue
         ps = pcg.shape(C.ValueRef(n, 0))
-        start, block = views.get(n, (0, None))
         total = ps.total_parallel_degree()
         ops.append({"name": pcg.layer_name(n), "op_type": op.op_type, "device_type": "GPU",
                     "degrees": list(ps.shard_degrees()), "sum_degree": ps.sum_degree,
                     "discard_copy_degree": ps.discard_copy_degree,
-                    "device_ids": list(range(start, start + (block or total)))})
+                    "device_ids": legacy.task_devices(views.get(n), total)})
     doc = {"format": "ffmi355x.strategy.v1", "world": (report or {}).get("world"),
-           "pcg": json.loads(pcg.to_json()), "views": {str(k): list(v) for k, v in views.items()}, "ops": ops}
+           "pcg": json.loads(pcg.to_json()), "placements": {str(k): list(v) for k, v in views.items()},
+           "ops": ops}
     if report:
         doc["search"] = {k: v for k, v in report.items() if k != "cg_to_pcg"}
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
@@ -106,5 +109,8 @@ def import_strategy(path: str, world: int):
     if doc.get("world") not in (None, world):
         raise ValueError(f"{path}: strategy is for {doc['world']} ranks, running on {world}")
     pcg = C.ParallelComputationGraph.from_json(json.dumps(doc["pcg"]))
-    views = {int(k): tuple(v) for k, v in doc.get("views", {}).items()}
+    if "placements" in doc:
+        views = {int(k): tuple(int(d) for d in v) for k, v in doc["placements"].items()}
+    else:  # round <= 3 files: contiguous blocks [start, block]
+        views = {int(k): _block(int(v[0]), int(v[1])) for k, v in doc.get("views", {}).items()}
     return pcg, views

@@ -80,5 +80,5 @@ def search(cg, ffconfig, world: int):
     if distributed:
         dist.broadcast_object_list(payload, src=0)
     pcg = C.ParallelComputationGraph.from_json(payload[0])
-    views: Dict[int, Tuple[int, int]] = {int(k): tuple(v) for k, v in payload[1].items()}
+    views: Dict[int, Tuple[int, ...]] = {int(k): tuple(v) for k, v in payload[1].items()}
     return pcg, views, payload[2]

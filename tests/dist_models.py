@@ -142,3 +142,17 @@ def dlrm_small(m):
     feeds = {f"sparse{i}": torch.randint(0, V, (B, 2), generator=g, dtype=torch.int32) for i in range(T)}
     feeds["dense"] = torch.randn(B, 6, generator=g)
     return feeds, torch.randint(0, 4, (B,), generator=g)
+
+
+def towers(m):
+    """Two independent Linear towers over one input, summed (inter-operator
+    placement: each tower may run on its own devices)."""
+    x = m.create_tensor([8, 16], DataType.DT_FLOAT, name="x")
+    a = m.dense(x, 32, ActiMode.AC_MODE_RELU, name="a0")
+    a = m.dense(a, 12, name="a1")
+    b = m.dense(x, 32, ActiMode.AC_MODE_RELU, name="b0")
+    b = m.dense(b, 12, name="b1")
+    t = m.add(a, b, name="sum")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(3)
+    return {"x": torch.randn(8, 16, generator=g)}, torch.randint(0, 12, (8,), generator=g)

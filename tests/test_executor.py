@@ -125,13 +125,18 @@ def test_strategy_export_import_roundtrip(tmp_path):
     M.mlp(m)
     pcg = C.data_parallel_pcg(m.cg, 4)
     path = str(tmp_path / "s.json")
-    export_strategy(path, pcg, {3: (0, 4)}, {"world": 4})
+    export_strategy(path, pcg, {3: (0, 1, 2, 3)}, {"world": 4})
     p2, views = import_strategy(path, 4)
-    assert p2.structural_hash() == pcg.structural_hash() and views == {3: (0, 4)}
+    assert p2.structural_hash() == pcg.structural_hash() and views == {3: (0, 1, 2, 3)}
     doc = json.load(open(path))
     assert doc["ops"] and all("device_ids" in o for o in doc["ops"])
     with pytest.raises(ValueError):
         import_strategy(path, 2)
+    # round <= 3 files carried contiguous blocks [start, block]
+    doc.pop("placements")
+    doc["views"] = {"3": [0, 4]}
+    json.dump(doc, open(path, "w"))
+    assert import_strategy(path, 4)[1] == {3: (0, 1, 2, 3)}
 
 
 def test_tracing_chrome_export(tmp_path):

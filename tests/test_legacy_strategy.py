@@ -42,7 +42,7 @@ def test_lower_reference_dlrm_strategy():
     pcg, views, rep = L.to_pcg(m.cg, ops, 8)
     assert rep["matched_layers"] >= 8 + 1
     tables = [n for n in pcg.topo_order() if pcg.layer_op(n).op_type == "EMBEDDING"]
-    assert sorted(views[n] for n in tables) == [(i, 1) for i in range(8)]
+    assert sorted(views[n] for n in tables) == [(i,) for i in range(8)]
     for n in tables:   # each table whole on its device (degree 1)
         assert pcg.shape(C.ValueRef(n, 0)).total_parallel_degree() == 1
     with pytest.raises(ValueError):

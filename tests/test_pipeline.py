@@ -76,7 +76,7 @@ def _stage_strategy(path):
     views = {}
     for n in pcg.topo_order():
         name = pcg.layer_name(n).split(".")[0]
-        views[n] = (0, 1) if name in ("x", "fc0", "fc1") else (1, 1)
+        views[n] = (0,) if name in ("x", "fc0", "fc1") else (1,)
     export_strategy(path, pcg, views, {"world": 2, "source": "test"})
 
 

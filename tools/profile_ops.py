@@ -3,8 +3,9 @@
 and write the measured cost table the C++ cost model loads
 (FF_PROFILE_TABLE / FFConfig.profile_table_file).
 
-    python tools/profile_ops.py --model bert-large --world 8 --batch-per-gpu 32 \
+    python tools/profile_ops.py --model bert-large --world 8 --batch-per-gpu 64 \
         --out profiles/op_costs_bert_large_mi355x.json
+    python tools/profile_ops.py --model gpt3-medium | resnet50 | dlrm ...   (bench.py's configs)
 
 Strategies profiled: data parallel, and for every model-parallel degree m
 dividing the world the uniform column / row / head-parallel variants (each
@@ -45,17 +46,24 @@ def uniform_strategies(cg, world):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="bert-large")
+    ap.add_argument("--model", default="bert-large",
+                    choices=["bert-large", "bert-base", "gpt3-medium", "resnet50", "dlrm"])
     ap.add_argument("--world", type=int, default=8)
-    ap.add_argument("--batch-per-gpu", type=int, default=32)
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: bench.py's per-GPU batch")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
-    from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
-
-    mk = bert_large if args.model == "bert-large" else bert_base
     m = FFModel(FFConfig())
-    build_bert(m, mk(batch_size=args.batch_per_gpu * args.world, sequence_length=args.seq))
+    if args.model in ("bert-large", "bert-base"):
+        from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert
+        mk = bert_large if args.model == "bert-large" else bert_base
+        build_bert(m, mk(batch_size=(args.batch_per_gpu or 64) * args.world, sequence_length=args.seq))
+    else:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        from flexflow_train_amd import models as Z
+        zname, bpg, over, _, _ = bench._ZOO[args.model]
+        Z.build(zname, m, batch_size=(args.batch_per_gpu or bpg) * args.world, **over)
     pcgs = []
     for s in uniform_strategies(m.cg, args.world):
         try:
