@@ -60,6 +60,12 @@ class LocalTrainingBacking {
   void set_weight(const std::string& name, const std::vector<float>& data);
   std::vector<float> get_weight(const std::string& name) const;
   std::vector<float> get_output() const;  // the graph's (last layer's) output
+  ValueRef output() const { return output_; }
+  // the slot of any graph tensor (or its gradient); nullptr if none is kept
+  HostTensor* slot(const ValueRef& v, bool grad = false);
+  LocalOptimizer& optimizer() { return opt_; }
+  // runs one operator layer's forward on the current slot contents
+  void forward_layer(int node);
 
   void forward();
   // loss + metrics on the output, then the full backward pass

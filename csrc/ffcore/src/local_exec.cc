@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <functional>
 #include <numeric>
 #include <random>
 
@@ -403,6 +404,563 @@ void bmm_bwd(Ctx& c) {
   }
 }
 
+// ---- math unaries (exp, sin, cos, rsqrt, sqrt, log, pow, elu)
+float math_f(const OpAttrs& op, float x) {
+  switch (op.type) {
+    case OpType::EXP: return std::exp(x);
+    case OpType::SIN: return std::sin(x);
+    case OpType::COS: return std::cos(x);
+    case OpType::RSQRT: return 1.f / std::sqrt(x);
+    case OpType::SQRT: return std::sqrt(x);
+    case OpType::LOG: return std::log(x);
+    case OpType::POW: return std::pow(x, static_cast<float>(op.f("exponent")));
+    case OpType::ELU: return x > 0.f ? x : std::exp(x) - 1.f;
+    default: return x;
+  }
+}
+float math_d(const OpAttrs& op, float x) {
+  switch (op.type) {
+    case OpType::EXP: return std::exp(x);
+    case OpType::SIN: return std::cos(x);
+    case OpType::COS: return -std::sin(x);
+    case OpType::RSQRT: return -0.5f / (x * std::sqrt(x));
+    case OpType::SQRT: return 0.5f / std::sqrt(x);
+    case OpType::LOG: return 1.f / x;
+    case OpType::POW: {
+      const float e = static_cast<float>(op.f("exponent"));
+      return e * std::pow(x, e - 1.f);
+    }
+    case OpType::ELU: return x > 0.f ? 1.f : std::exp(x);
+    default: return 1.f;
+  }
+}
+void math_fwd(Ctx& c) {
+  const auto& x = c.in[0]->v;
+  auto& y = c.out[0]->v;
+  for (size_t i = 0; i < x.size(); ++i) y[i] = math_f(*c.op, x[i]);
+}
+void math_bwd(Ctx& c) {
+  if (!c.d_in[0]) return;
+  const auto& x = c.in[0]->v;
+  const auto& g = c.d_out[0]->v;
+  for (size_t i = 0; i < x.size(); ++i) c.d_in[0]->v[i] += g[i] * math_d(*c.op, x[i]);
+}
+
+std::vector<int64_t> strides_of(const std::vector<int64_t>& d) {
+  std::vector<int64_t> s(d.size(), 1);
+  for (int i = static_cast<int>(d.size()) - 2; i >= 0; --i) s[i] = s[i + 1] * d[i + 1];
+  return s;
+}
+int norm_dim(int64_t d, size_t nd) { return static_cast<int>(d < 0 ? d + static_cast<int64_t>(nd) : d); }
+
+// ---- transpose: y[i_0..] = x[perm-indexed]
+void transpose_map(const Ctx& c, const std::function<void(int64_t, int64_t)>& f) {
+  const auto& xd = c.in[0]->dims;
+  const auto& p = c.op->ints("perm");
+  const auto xs = strides_of(xd);
+  const auto& yd = c.out[0]->dims;
+  const int nd = static_cast<int>(yd.size());
+  std::vector<int64_t> idx(nd, 0);
+  const int64_t n = c.out[0]->numel();
+  for (int64_t o = 0; o < n; ++o) {
+    int64_t src = 0;
+    for (int k = 0; k < nd; ++k) src += idx[k] * xs[norm_dim(p[k], xd.size())];
+    f(o, src);
+    for (int k = nd - 1; k >= 0; --k) {
+      if (++idx[k] < yd[k]) break;
+      idx[k] = 0;
+    }
+  }
+}
+void transpose_fwd(Ctx& c) { transpose_map(c, [&](int64_t o, int64_t s) { c.out[0]->v[o] = c.in[0]->v[s]; }); }
+void transpose_bwd(Ctx& c) {
+  if (c.d_in[0]) transpose_map(c, [&](int64_t o, int64_t s) { c.d_in[0]->v[s] += c.d_out[0]->v[o]; });
+}
+
+// ---- reverse along one axis (an involution: the backward is the same map)
+void reverse_map(const Ctx& c, const std::function<void(int64_t, int64_t)>& f) {
+  const auto& d = c.in[0]->dims;
+  const int ax = norm_dim(c.op->i("axis"), d.size());
+  int64_t outer = 1, inner = 1;
+  for (int k = 0; k < ax; ++k) outer *= d[k];
+  for (size_t k = ax + 1; k < d.size(); ++k) inner *= d[k];
+  const int64_t L = d[ax];
+  for (int64_t o = 0; o < outer; ++o)
+    for (int64_t l = 0; l < L; ++l)
+      for (int64_t i = 0; i < inner; ++i) f((o * L + l) * inner + i, (o * L + (L - 1 - l)) * inner + i);
+}
+void reverse_fwd(Ctx& c) { reverse_map(c, [&](int64_t o, int64_t s) { c.out[0]->v[o] = c.in[0]->v[s]; }); }
+void reverse_bwd(Ctx& c) {
+  if (c.d_in[0]) reverse_map(c, [&](int64_t o, int64_t s) { c.d_in[0]->v[s] += c.d_out[0]->v[o]; });
+}
+
+// ---- split along an axis
+void split_fwd(Ctx& c) {
+  const auto& d = c.in[0]->dims;
+  const int ax = norm_dim(c.op->i("axis"), d.size());
+  int64_t outer = 1, inner = 1;
+  for (int k = 0; k < ax; ++k) outer *= d[k];
+  for (size_t k = ax + 1; k < d.size(); ++k) inner *= d[k];
+  int64_t off = 0;
+  for (size_t j = 0; j < c.out.size(); ++j) {
+    const int64_t L = c.out[j]->dims[ax];
+    for (int64_t o = 0; o < outer; ++o)
+      std::copy_n(c.in[0]->v.begin() + (o * d[ax] + off) * inner, L * inner, c.out[j]->v.begin() + o * L * inner);
+    off += L;
+  }
+}
+void split_bwd(Ctx& c) {
+  if (!c.d_in[0]) return;
+  const auto& d = c.in[0]->dims;
+  const int ax = norm_dim(c.op->i("axis"), d.size());
+  int64_t outer = 1, inner = 1;
+  for (int k = 0; k < ax; ++k) outer *= d[k];
+  for (size_t k = ax + 1; k < d.size(); ++k) inner *= d[k];
+  int64_t off = 0;
+  for (size_t j = 0; j < c.out.size(); ++j) {
+    const int64_t L = c.out[j]->dims[ax];
+    if (c.d_out[j])
+      for (int64_t o = 0; o < outer; ++o)
+        for (int64_t e = 0; e < L * inner; ++e)
+          c.d_in[0]->v[(o * d[ax] + off) * inner + e] += c.d_out[j]->v[o * L * inner + e];
+    off += L;
+  }
+}
+
+// ---- reduce sum / mean over axes
+void reduce_map(const Ctx& c, const std::function<void(int64_t, int64_t)>& f) {
+  const auto& d = c.in[0]->dims;
+  std::vector<bool> red(d.size(), false);
+  for (auto a : c.op->ints("axes")) red[norm_dim(a, d.size())] = true;
+  std::vector<int64_t> od;
+  for (size_t k = 0; k < d.size(); ++k) od.push_back(red[k] ? 1 : d[k]);
+  const auto os = strides_of(od);
+  std::vector<int64_t> idx(d.size(), 0);
+  const int64_t n = c.in[0]->numel();
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t o = 0;
+    for (size_t k = 0; k < d.size(); ++k) o += (red[k] ? 0 : idx[k]) * os[k];
+    f(i, o);
+    for (int k = static_cast<int>(d.size()) - 1; k >= 0; --k) {
+      if (++idx[k] < d[k]) break;
+      idx[k] = 0;
+    }
+  }
+}
+double reduce_scale(const Ctx& c) {
+  if (c.op->type != OpType::MEAN && c.op->type != OpType::REDUCE_MEAN) return 1.0;
+  return static_cast<double>(c.out[0]->numel()) / static_cast<double>(std::max<int64_t>(1, c.in[0]->numel()));
+}
+void reduce_fwd(Ctx& c) {
+  std::fill(c.out[0]->v.begin(), c.out[0]->v.end(), 0.f);
+  reduce_map(c, [&](int64_t i, int64_t o) { c.out[0]->v[o] += c.in[0]->v[i]; });
+  const float k = static_cast<float>(reduce_scale(c));
+  if (k != 1.f)
+    for (auto& e : c.out[0]->v) e *= k;
+}
+void reduce_bwd(Ctx& c) {
+  if (!c.d_in[0]) return;
+  const float k = static_cast<float>(reduce_scale(c));
+  reduce_map(c, [&](int64_t i, int64_t o) { c.d_in[0]->v[i] += k * c.d_out[0]->v[o]; });
+}
+
+// ---- gather along `dim` (index has the input's rank)
+void gather_map(const Ctx& c, const std::function<void(int64_t, int64_t)>& f) {
+  const auto& xd = c.in[0]->dims;
+  const auto& id = c.in[1]->dims;
+  const int dim = norm_dim(c.op->i("dim"), xd.size());
+  const auto xs = strides_of(xd);
+  std::vector<int64_t> idx(id.size(), 0);
+  const int64_t n = c.in[1]->numel();
+  for (int64_t o = 0; o < n; ++o) {
+    int64_t src = 0;
+    for (size_t k = 0; k < id.size(); ++k) {
+      int64_t v = static_cast<int>(k) == dim ? static_cast<int64_t>(c.in[1]->v[o]) : idx[k];
+      v = std::min<int64_t>(std::max<int64_t>(v, 0), xd[k] - 1);
+      src += v * xs[k];
+    }
+    f(o, src);
+    for (int k = static_cast<int>(id.size()) - 1; k >= 0; --k) {
+      if (++idx[k] < id[k]) break;
+      idx[k] = 0;
+    }
+  }
+}
+void gather_fwd(Ctx& c) { gather_map(c, [&](int64_t o, int64_t s) { c.out[0]->v[o] = c.in[0]->v[s]; }); }
+void gather_bwd(Ctx& c) {
+  if (c.d_in[0]) gather_map(c, [&](int64_t o, int64_t s) { c.d_in[0]->v[s] += c.d_out[0]->v[o]; });
+}
+
+// ---- conv2d, NCHW, weight [O, C/g, KH, KW] (direct convolution)
+struct ConvGeom {
+  int64_t N, C, H, W, O, OH, OW, KH, KW, SH, SW, PH, PW, G;
+};
+ConvGeom conv_geom(const Ctx& c) {
+  const auto& x = c.in[0]->dims;
+  const auto& y = c.out[0]->dims;
+  return {x[0], x[1], x[2], x[3], y[1], y[2], y[3], c.op->i("kernel_h"), c.op->i("kernel_w"), c.op->i("stride_h"),
+          c.op->i("stride_w"), c.op->i("padding_h"), c.op->i("padding_w"), c.op->i("groups")};
+}
+template <typename F>
+void conv_loop(const ConvGeom& g, F&& f) {
+  const int64_t cpg = g.C / g.G, opg = g.O / g.G;
+  for (int64_t n = 0; n < g.N; ++n)
+    for (int64_t o = 0; o < g.O; ++o) {
+      const int64_t grp = o / opg;
+      for (int64_t oh = 0; oh < g.OH; ++oh)
+        for (int64_t ow = 0; ow < g.OW; ++ow) {
+          const int64_t yi = ((n * g.O + o) * g.OH + oh) * g.OW + ow;
+          for (int64_t ci = 0; ci < cpg; ++ci)
+            for (int64_t kh = 0; kh < g.KH; ++kh) {
+              const int64_t ih = oh * g.SH - g.PH + kh;
+              if (ih < 0 || ih >= g.H) continue;
+              for (int64_t kw = 0; kw < g.KW; ++kw) {
+                const int64_t iw = ow * g.SW - g.PW + kw;
+                if (iw < 0 || iw >= g.W) continue;
+                const int64_t xi = ((n * g.C + grp * cpg + ci) * g.H + ih) * g.W + iw;
+                const int64_t wi = ((o * cpg + ci) * g.KH + kh) * g.KW + kw;
+                f(yi, xi, wi);
+              }
+            }
+        }
+    }
+}
+void conv2d_fwd(Ctx& c) {
+  const auto g = conv_geom(c);
+  auto& y = c.out[0]->v;
+  std::fill(y.begin(), y.end(), 0.f);
+  const auto& x = c.in[0]->v;
+  const auto& w = c.w[0]->v;
+  conv_loop(g, [&](int64_t yi, int64_t xi, int64_t wi) { y[yi] += x[xi] * w[wi]; });
+  if (c.w.size() > 1)
+    for (int64_t i = 0; i < static_cast<int64_t>(y.size()); ++i) y[i] += c.w[1]->v[(i / (g.OH * g.OW)) % g.O];
+  const Activation a = activation_from_string(c.op->s("activation"));
+  if (a != Activation::NONE) {
+    c.saved->assign(1, *c.out[0]);
+    for (auto& e : y) e = act_f(a, e);
+  }
+}
+void conv2d_bwd(Ctx& c) {
+  const auto g = conv_geom(c);
+  std::vector<float> gy = c.d_out[0]->v;
+  const Activation a = activation_from_string(c.op->s("activation"));
+  if (a != Activation::NONE)
+    for (size_t i = 0; i < gy.size(); ++i) gy[i] *= act_d(a, (*c.saved)[0].v[i]);
+  const auto& x = c.in[0]->v;
+  const auto& w = c.w[0]->v;
+  conv_loop(g, [&](int64_t yi, int64_t xi, int64_t wi) {
+    if (c.d_w[0]) c.d_w[0]->v[wi] += gy[yi] * x[xi];
+    if (c.d_in[0]) c.d_in[0]->v[xi] += gy[yi] * w[wi];
+  });
+  if (c.w.size() > 1 && c.d_w[1])
+    for (int64_t i = 0; i < static_cast<int64_t>(gy.size()); ++i) c.d_w[1]->v[(i / (g.OH * g.OW)) % g.O] += gy[i];
+}
+
+// ---- pool2d (max / avg, padding excluded from the average)
+void pool2d_fwd(Ctx& c) {
+  const auto& xd = c.in[0]->dims;
+  const auto& yd = c.out[0]->dims;
+  const int64_t KH = c.op->i("kernel_h"), KW = c.op->i("kernel_w"), SH = c.op->i("stride_h"),
+                SW = c.op->i("stride_w"), PH = c.op->i("padding_h"), PW = c.op->i("padding_w");
+  const bool mx = c.op->s("pool_type") == "max";
+  HostTensor arg;
+  arg.resize(yd);
+  for (int64_t nc = 0; nc < yd[0] * yd[1]; ++nc)
+    for (int64_t oh = 0; oh < yd[2]; ++oh)
+      for (int64_t ow = 0; ow < yd[3]; ++ow) {
+        float acc = mx ? -INFINITY : 0.f;
+        int64_t best = -1, cnt = 0;
+        for (int64_t kh = 0; kh < KH; ++kh)
+          for (int64_t kw = 0; kw < KW; ++kw) {
+            const int64_t ih = oh * SH - PH + kh, iw = ow * SW - PW + kw;
+            if (ih < 0 || ih >= xd[2] || iw < 0 || iw >= xd[3]) continue;
+            const int64_t xi = (nc * xd[2] + ih) * xd[3] + iw;
+            const float v = c.in[0]->v[xi];
+            if (mx) {
+              if (v > acc) acc = v, best = xi;
+            } else {
+              acc += v;
+              ++cnt;
+            }
+          }
+        const int64_t yi = (nc * yd[2] + oh) * yd[3] + ow;
+        c.out[0]->v[yi] = mx ? acc : acc / static_cast<float>(std::max<int64_t>(1, cnt));
+        arg.v[yi] = static_cast<float>(mx ? best : cnt);
+      }
+  c.saved->assign(1, arg);
+  const Activation a = activation_from_string(c.op->s("activation"));
+  if (a != Activation::NONE) {
+    c.saved->push_back(*c.out[0]);
+    for (auto& e : c.out[0]->v) e = act_f(a, e);
+  }
+}
+void pool2d_bwd(Ctx& c) {
+  if (!c.d_in[0]) return;
+  const auto& xd = c.in[0]->dims;
+  const auto& yd = c.out[0]->dims;
+  const int64_t KH = c.op->i("kernel_h"), KW = c.op->i("kernel_w"), SH = c.op->i("stride_h"),
+                SW = c.op->i("stride_w"), PH = c.op->i("padding_h"), PW = c.op->i("padding_w");
+  const bool mx = c.op->s("pool_type") == "max";
+  const auto& arg = (*c.saved)[0].v;
+  const Activation a = activation_from_string(c.op->s("activation"));
+  for (int64_t nc = 0; nc < yd[0] * yd[1]; ++nc)
+    for (int64_t oh = 0; oh < yd[2]; ++oh)
+      for (int64_t ow = 0; ow < yd[3]; ++ow) {
+        const int64_t yi = (nc * yd[2] + oh) * yd[3] + ow;
+        float g = c.d_out[0]->v[yi];
+        if (a != Activation::NONE) g *= act_d(a, (*c.saved)[1].v[yi]);
+        if (mx) {
+          if (arg[yi] >= 0) c.d_in[0]->v[static_cast<int64_t>(arg[yi])] += g;
+          continue;
+        }
+        const float share = g / std::max(1.f, arg[yi]);
+        for (int64_t kh = 0; kh < KH; ++kh)
+          for (int64_t kw = 0; kw < KW; ++kw) {
+            const int64_t ih = oh * SH - PH + kh, iw = ow * SW - PW + kw;
+            if (ih < 0 || ih >= xd[2] || iw < 0 || iw >= xd[3]) continue;
+            c.d_in[0]->v[(nc * xd[2] + ih) * xd[3] + iw] += share;
+          }
+      }
+}
+
+// ---- batch norm (training statistics over N and the spatial dims, channel dim 1)
+void bn_geom(const Ctx& c, int64_t& N, int64_t& C, int64_t& S) {
+  const auto& d = c.in[0]->dims;
+  N = d[0];
+  C = d[1];
+  S = 1;
+  for (size_t k = 2; k < d.size(); ++k) S *= d[k];
+}
+void batchnorm_fwd(Ctx& c) {
+  int64_t N, C, S;
+  bn_geom(c, N, C, S);
+  const float eps = static_cast<float>(c.op->f("eps"));
+  HostTensor stat;
+  stat.resize({2, C});  // mean, inverse std
+  const auto& x = c.in[0]->v;
+  auto& y = c.out[0]->v;
+  const double cnt = static_cast<double>(N * S);
+  for (int64_t ch = 0; ch < C; ++ch) {
+    double m = 0, v = 0;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t s = 0; s < S; ++s) m += x[(n * C + ch) * S + s];
+    m /= cnt;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t s = 0; s < S; ++s) {
+        const double dd = x[(n * C + ch) * S + s] - m;
+        v += dd * dd;
+      }
+    v /= cnt;
+    const float inv = 1.f / std::sqrt(static_cast<float>(v) + eps);
+    stat.v[ch] = static_cast<float>(m);
+    stat.v[C + ch] = inv;
+    const float gm = c.w.empty() ? 1.f : c.w[0]->v[ch], bt = c.w.size() > 1 ? c.w[1]->v[ch] : 0.f;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t s = 0; s < S; ++s) {
+        const int64_t i = (n * C + ch) * S + s;
+        float o = (x[i] - stat.v[ch]) * inv * gm + bt;
+        if (c.op->b("relu") && o < 0.f) o = 0.f;
+        y[i] = o;
+      }
+  }
+  c.saved->assign(1, stat);
+}
+void batchnorm_bwd(Ctx& c) {
+  int64_t N, C, S;
+  bn_geom(c, N, C, S);
+  const auto& x = c.in[0]->v;
+  const auto& y = c.out[0]->v;
+  const auto& st = (*c.saved)[0].v;
+  const double cnt = static_cast<double>(N * S);
+  for (int64_t ch = 0; ch < C; ++ch) {
+    const float m = st[ch], inv = st[C + ch];
+    const float gm = c.w.empty() ? 1.f : c.w[0]->v[ch];
+    double sg = 0, sgx = 0;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t s = 0; s < S; ++s) {
+        const int64_t i = (n * C + ch) * S + s;
+        float g = c.d_out[0]->v[i];
+        if (c.op->b("relu") && y[i] <= 0.f) g = 0.f;
+        const float xh = (x[i] - m) * inv;
+        sg += g;
+        sgx += g * xh;
+      }
+    if (c.d_w.size() > 0 && c.d_w[0]) c.d_w[0]->v[ch] += static_cast<float>(sgx);
+    if (c.d_w.size() > 1 && c.d_w[1]) c.d_w[1]->v[ch] += static_cast<float>(sg);
+    if (!c.d_in[0]) continue;
+    for (int64_t n = 0; n < N; ++n)
+      for (int64_t s = 0; s < S; ++s) {
+        const int64_t i = (n * C + ch) * S + s;
+        float g = c.d_out[0]->v[i];
+        if (c.op->b("relu") && y[i] <= 0.f) g = 0.f;
+        const float xh = (x[i] - m) * inv;
+        c.d_in[0]->v[i] += static_cast<float>(gm * inv * (g - sg / cnt - xh * sgx / cnt));
+      }
+  }
+}
+
+// ---- multi-head attention with the logical weight layout of op_attrs mha_spec:
+// weight [P, H], per head column: Wq [Eq, k] | Wk [Ek, k] | Wv [Ev, v] | Wo [v, E]
+// (row-major blocks); input bias [2k + v, H] (q | k | v); output bias [E].
+struct MhaGeom {
+  int64_t B, Sq, Sk, Eq, Ek, Ev, E, H, kd, vd;
+  int64_t off_q() const { return 0; }
+  int64_t off_k() const { return Eq * kd; }
+  int64_t off_v() const { return Eq * kd + Ek * kd; }
+  int64_t off_o() const { return Eq * kd + Ek * kd + Ev * vd; }
+};
+MhaGeom mha_geom(const Ctx& c) {
+  MhaGeom g;
+  g.B = c.in[0]->dims[0];
+  g.Sq = c.in[0]->dims[1];
+  g.Sk = c.in[1]->dims[1];
+  g.Eq = c.in[0]->dims[2];
+  g.Ek = c.in[1]->dims[2];
+  g.Ev = c.in[2]->dims[2];
+  g.E = c.op->i("embed_dim");
+  g.H = c.op->i("num_heads");
+  g.kd = c.op->i("kdim") > 0 ? c.op->i("kdim") : g.E / g.H;
+  g.vd = c.op->i("vdim") > 0 ? c.op->i("vdim") : g.E / g.H;
+  return g;
+}
+// dense [rows, cols] block of head h out of the [P, H] weight (or its gradient)
+std::vector<float> head_block(const HostTensor& W, int64_t H, int64_t h, int64_t off, int64_t rows, int64_t cols) {
+  std::vector<float> m(rows * cols);
+  for (int64_t i = 0; i < rows * cols; ++i) m[i] = W.v[(off + i) * H + h];
+  return m;
+}
+void head_block_add(HostTensor* W, int64_t H, int64_t h, int64_t off, const std::vector<float>& m) {
+  if (!W) return;
+  for (size_t i = 0; i < m.size(); ++i) W->v[(off + static_cast<int64_t>(i)) * H + h] += m[i];
+}
+void mha_fwd(Ctx& c) {
+  const auto g = mha_geom(c);
+  const bool bias = c.w.size() > 1, causal = c.op->b("causal");
+  const float scale = 1.f / std::sqrt(static_cast<float>(g.kd));
+  auto& y = c.out[0]->v;
+  std::fill(y.begin(), y.end(), 0.f);
+  c.saved->assign(5, HostTensor{});
+  auto& Qs = (*c.saved)[0].v;
+  auto& Ks = (*c.saved)[1].v;
+  auto& Vs = (*c.saved)[2].v;
+  auto& Ps = (*c.saved)[3].v;
+  auto& Os = (*c.saved)[4].v;
+  Qs.assign(g.B * g.H * g.Sq * g.kd, 0.f);
+  Ks.assign(g.B * g.H * g.Sk * g.kd, 0.f);
+  Vs.assign(g.B * g.H * g.Sk * g.vd, 0.f);
+  Ps.assign(g.B * g.H * g.Sq * g.Sk, 0.f);
+  Os.assign(g.B * g.H * g.Sq * g.vd, 0.f);
+  for (int64_t h = 0; h < g.H; ++h) {
+    const auto Wq = head_block(*c.w[0], g.H, h, g.off_q(), g.Eq, g.kd);
+    const auto Wk = head_block(*c.w[0], g.H, h, g.off_k(), g.Ek, g.kd);
+    const auto Wv = head_block(*c.w[0], g.H, h, g.off_v(), g.Ev, g.vd);
+    const auto Wo = head_block(*c.w[0], g.H, h, g.off_o(), g.vd, g.E);
+    for (int64_t b = 0; b < g.B; ++b) {
+      const int64_t bh = b * g.H + h;
+      float* Q = Qs.data() + bh * g.Sq * g.kd;
+      float* K = Ks.data() + bh * g.Sk * g.kd;
+      float* V = Vs.data() + bh * g.Sk * g.vd;
+      float* P = Ps.data() + bh * g.Sq * g.Sk;
+      float* O = Os.data() + bh * g.Sq * g.vd;
+      matmul(c.in[0]->v.data() + b * g.Sq * g.Eq, Wq.data(), Q, g.Sq, g.kd, g.Eq, false, false, false);
+      matmul(c.in[1]->v.data() + b * g.Sk * g.Ek, Wk.data(), K, g.Sk, g.kd, g.Ek, false, false, false);
+      matmul(c.in[2]->v.data() + b * g.Sk * g.Ev, Wv.data(), V, g.Sk, g.vd, g.Ev, false, false, false);
+      if (bias) {
+        const auto& bi = c.w[1]->v;  // [2k + v, H]
+        for (int64_t s = 0; s < g.Sq; ++s)
+          for (int64_t j = 0; j < g.kd; ++j) Q[s * g.kd + j] += bi[j * g.H + h];
+        for (int64_t s = 0; s < g.Sk; ++s) {
+          for (int64_t j = 0; j < g.kd; ++j) K[s * g.kd + j] += bi[(g.kd + j) * g.H + h];
+          for (int64_t j = 0; j < g.vd; ++j) V[s * g.vd + j] += bi[(2 * g.kd + j) * g.H + h];
+        }
+      }
+      matmul(Q, K, P, g.Sq, g.Sk, g.kd, false, true, false);
+      for (int64_t i = 0; i < g.Sq; ++i) {
+        float* r = P + i * g.Sk;
+        float m = -INFINITY;
+        for (int64_t j = 0; j < g.Sk; ++j) {
+          r[j] = (causal && j > i) ? -INFINITY : r[j] * scale;
+          m = std::max(m, r[j]);
+        }
+        double sum = 0;
+        for (int64_t j = 0; j < g.Sk; ++j) sum += (r[j] = r[j] == -INFINITY ? 0.f : std::exp(r[j] - m));
+        for (int64_t j = 0; j < g.Sk; ++j) r[j] = static_cast<float>(r[j] / sum);
+      }
+      matmul(P, V, O, g.Sq, g.vd, g.Sk, false, false, false);
+      matmul(O, Wo.data(), y.data() + b * g.Sq * g.E, g.Sq, g.E, g.vd, false, false, true);
+    }
+  }
+  if (c.w.size() > 2)
+    for (int64_t r = 0; r < g.B * g.Sq; ++r)
+      for (int64_t e = 0; e < g.E; ++e) y[r * g.E + e] += c.w[2]->v[e];
+}
+void mha_bwd(Ctx& c) {
+  const auto g = mha_geom(c);
+  const bool bias = c.w.size() > 1;
+  const float scale = 1.f / std::sqrt(static_cast<float>(g.kd));
+  const auto& gy = c.d_out[0]->v;
+  const auto& Qs = (*c.saved)[0].v;
+  const auto& Ks = (*c.saved)[1].v;
+  const auto& Vs = (*c.saved)[2].v;
+  const auto& Ps = (*c.saved)[3].v;
+  const auto& Os = (*c.saved)[4].v;
+  HostTensor* dW = c.d_w[0];
+  HostTensor* dbi = bias && c.d_w.size() > 1 ? c.d_w[1] : nullptr;
+  if (c.w.size() > 2 && c.d_w.size() > 2 && c.d_w[2])
+    for (int64_t r = 0; r < g.B * g.Sq; ++r)
+      for (int64_t e = 0; e < g.E; ++e) c.d_w[2]->v[e] += gy[r * g.E + e];
+  std::vector<float> dO(g.Sq * g.vd), dP(g.Sq * g.Sk), dQ(g.Sq * g.kd), dK(g.Sk * g.kd), dV(g.Sk * g.vd);
+  for (int64_t h = 0; h < g.H; ++h) {
+    const auto Wq = head_block(*c.w[0], g.H, h, g.off_q(), g.Eq, g.kd);
+    const auto Wk = head_block(*c.w[0], g.H, h, g.off_k(), g.Ek, g.kd);
+    const auto Wv = head_block(*c.w[0], g.H, h, g.off_v(), g.Ev, g.vd);
+    const auto Wo = head_block(*c.w[0], g.H, h, g.off_o(), g.vd, g.E);
+    std::vector<float> dWq(Wq.size(), 0.f), dWk(Wk.size(), 0.f), dWv(Wv.size(), 0.f), dWo(Wo.size(), 0.f);
+    for (int64_t b = 0; b < g.B; ++b) {
+      const int64_t bh = b * g.H + h;
+      const float* Q = Qs.data() + bh * g.Sq * g.kd;
+      const float* K = Ks.data() + bh * g.Sk * g.kd;
+      const float* V = Vs.data() + bh * g.Sk * g.vd;
+      const float* P = Ps.data() + bh * g.Sq * g.Sk;
+      const float* O = Os.data() + bh * g.Sq * g.vd;
+      const float* G = gy.data() + b * g.Sq * g.E;
+      matmul(O, G, dWo.data(), g.vd, g.E, g.Sq, true, false, true);
+      matmul(G, Wo.data(), dO.data(), g.Sq, g.vd, g.E, false, true, false);
+      matmul(dO.data(), V, dP.data(), g.Sq, g.Sk, g.vd, false, true, false);
+      matmul(P, dO.data(), dV.data(), g.Sk, g.vd, g.Sq, true, false, false);
+      for (int64_t i = 0; i < g.Sq; ++i) {  // softmax backward, then the 1/sqrt(k) scale
+        double dot = 0;
+        for (int64_t j = 0; j < g.Sk; ++j) dot += P[i * g.Sk + j] * dP[i * g.Sk + j];
+        for (int64_t j = 0; j < g.Sk; ++j)
+          dP[i * g.Sk + j] = P[i * g.Sk + j] * (dP[i * g.Sk + j] - static_cast<float>(dot)) * scale;
+      }
+      matmul(dP.data(), K, dQ.data(), g.Sq, g.kd, g.Sk, false, false, false);
+      matmul(dP.data(), Q, dK.data(), g.Sk, g.kd, g.Sq, true, false, false);
+      const float* xq = c.in[0]->v.data() + b * g.Sq * g.Eq;
+      const float* xk = c.in[1]->v.data() + b * g.Sk * g.Ek;
+      const float* xv = c.in[2]->v.data() + b * g.Sk * g.Ev;
+      matmul(xq, dQ.data(), dWq.data(), g.Eq, g.kd, g.Sq, true, false, true);
+      matmul(xk, dK.data(), dWk.data(), g.Ek, g.kd, g.Sk, true, false, true);
+      matmul(xv, dV.data(), dWv.data(), g.Ev, g.vd, g.Sk, true, false, true);
+      if (c.d_in[0]) matmul(dQ.data(), Wq.data(), c.d_in[0]->v.data() + b * g.Sq * g.Eq, g.Sq, g.Eq, g.kd, false, true, true);
+      if (c.d_in[1]) matmul(dK.data(), Wk.data(), c.d_in[1]->v.data() + b * g.Sk * g.Ek, g.Sk, g.Ek, g.kd, false, true, true);
+      if (c.d_in[2]) matmul(dV.data(), Wv.data(), c.d_in[2]->v.data() + b * g.Sk * g.Ev, g.Sk, g.Ev, g.vd, false, true, true);
+      if (dbi) {
+        for (int64_t s = 0; s < g.Sq; ++s)
+          for (int64_t j = 0; j < g.kd; ++j) dbi->v[j * g.H + h] += dQ[s * g.kd + j];
+        for (int64_t s = 0; s < g.Sk; ++s) {
+          for (int64_t j = 0; j < g.kd; ++j) dbi->v[(g.kd + j) * g.H + h] += dK[s * g.kd + j];
+          for (int64_t j = 0; j < g.vd; ++j) dbi->v[(2 * g.kd + j) * g.H + h] += dV[s * g.vd + j];
+        }
+      }
+    }
+    head_block_add(dW, g.H, h, g.off_q(), dWq);
+    head_block_add(dW, g.H, h, g.off_k(), dWk);
+    head_block_add(dW, g.H, h, g.off_v(), dWv);
+    head_block_add(dW, g.H, h, g.off_o(), dWo);
+  }
+}
+
 double elapsed_ms(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -425,6 +983,18 @@ const std::map<OpType, LocalTrainingBacking::OpImpl>& LocalTrainingBacking::regi
     m[OpType::EMBEDDING] = {embedding_fwd, embedding_bwd};
     m[OpType::CONCAT] = {concat_fwd, concat_bwd};
     m[OpType::BATCHMATMUL] = {bmm_fwd, bmm_bwd};
+    for (auto t : {OpType::EXP, OpType::SIN, OpType::COS, OpType::RSQRT, OpType::SQRT, OpType::LOG, OpType::POW,
+                   OpType::ELU})
+      m[t] = {math_fwd, math_bwd};
+    m[OpType::TRANSPOSE] = {transpose_fwd, transpose_bwd};
+    m[OpType::REVERSE] = {reverse_fwd, reverse_bwd};
+    m[OpType::SPLIT] = {split_fwd, split_bwd};
+    for (auto t : {OpType::REDUCE_SUM, OpType::REDUCE_MEAN, OpType::MEAN}) m[t] = {reduce_fwd, reduce_bwd};
+    m[OpType::GATHER] = {gather_fwd, gather_bwd};
+    m[OpType::CONV2D] = {conv2d_fwd, conv2d_bwd};
+    m[OpType::POOL2D] = {pool2d_fwd, pool2d_bwd};
+    m[OpType::BATCHNORM] = {batchnorm_fwd, batchnorm_bwd};
+    m[OpType::MULTIHEAD_ATTENTION] = {mha_fwd, mha_bwd};
     return m;
   }();
   return r;
@@ -545,22 +1115,31 @@ std::vector<float> LocalTrainingBacking::get_weight(const std::string& name) con
 }
 std::vector<float> LocalTrainingBacking::get_output() const { return val_.at(output_).v; }
 
+HostTensor* LocalTrainingBacking::slot(const ValueRef& v, bool grad) {
+  auto& m = grad ? grad_ : val_;
+  auto it = m.find(v);
+  return it == m.end() ? nullptr : &it->second;
+}
+
+void LocalTrainingBacking::forward_layer(int n) {
+  const auto& node = cg_.g.node(n);
+  auto it = registry().find(node.label.op.type);
+  if (it == registry().end()) throw FFError("local execution: layer " + node.label.name + " is not an operator");
+  OpCtx c;
+  c.op = &node.label.op;
+  for (auto const& v : cg_.layer_data_inputs(n)) c.in.push_back(&val_[v]);
+  for (auto const& v : cg_.layer_weights(n)) c.w.push_back(&val_[v]);
+  for (size_t i = 0; i < node.outputs.size(); ++i) c.out.push_back(&val_[{n, static_cast<int>(i)}]);
+  c.saved = &saved_[n];
+  c.training = true;
+  c.seed = seed_ * 7919ull + static_cast<uint64_t>(n) * 104729ull + static_cast<uint64_t>(step_);
+  const auto t0 = std::chrono::steady_clock::now();
+  it->second.fwd(c);
+  times_[n].first += elapsed_ms(t0);
+}
+
 void LocalTrainingBacking::forward() {
-  const auto& reg = registry();
-  for (int n : order_) {
-    const auto& node = cg_.g.node(n);
-    OpCtx c;
-    c.op = &node.label.op;
-    for (auto const& v : cg_.layer_data_inputs(n)) c.in.push_back(&val_[v]);
-    for (auto const& v : cg_.layer_weights(n)) c.w.push_back(&val_[v]);
-    for (size_t i = 0; i < node.outputs.size(); ++i) c.out.push_back(&val_[{n, static_cast<int>(i)}]);
-    c.saved = &saved_[n];
-    c.training = true;
-    c.seed = seed_ * 7919ull + static_cast<uint64_t>(n) * 104729ull + static_cast<uint64_t>(step_);
-    const auto t0 = std::chrono::steady_clock::now();
-    reg.at(node.label.op.type).fwd(c);
-    times_[n].first += elapsed_ms(t0);
-  }
+  for (int n : order_) forward_layer(n);
 }
 
 void LocalTrainingBacking::backward(const std::vector<float>& labels) {

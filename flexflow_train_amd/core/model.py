@@ -632,7 +632,8 @@ class FFModel:
                          profiling=self.ffconfig.profiling, fuse_add_layernorm=self.ffconfig.perform_fusion,
                          shard_optimizer=bool(self.ffconfig.shard_optimizer),
                          param_sync=_param_sync_str(self.ffconfig.parameter_sync),
-                         bucket_bytes=int(self.ffconfig.bucket_mb) << 20)
+                         bucket_bytes=int(self.ffconfig.bucket_mb) << 20,
+                         inplace=bool(self.ffconfig.enable_inplace_optimizations))
         if self.ffconfig.softmax_identity_backward:
             cfg.softmax_identity_backward = True
         out_v = None

@@ -71,10 +71,32 @@ def _torch_unary(op, ctx, x):
     raise NotImplementedError(op)
 
 
+_INPLACE_ACT = {"RELU": torch.relu_, "SIGMOID": torch.sigmoid_, "TANH": torch.tanh_, "EXP": torch.exp_}
+
+
+def _act_grad_from_output(op, y, dy):
+    yf = y.float()
+    if op == "RELU":
+        d = (yf > 0).float()
+    elif op == "SIGMOID":
+        d = yf * (1 - yf)
+    elif op == "TANH":
+        d = 1 - yf * yf
+    else:  # EXP
+        d = yf
+    return (dy.float() * d).to(dy.dtype)
+
+
 @register("RELU", "SIGMOID", "TANH", "GELU", "ELU", "EXP")
 class ActivationOp(OpImpl):
     def forward(self, ctx, inputs, weights):
         x = inputs[0]
+        if ctx.extra.get("inplace_ok") and ctx.op_type in _INPLACE_ACT:
+            # --enable-inplace-optimizations: the output overwrites the input,
+            # the backward runs from the output
+            with torch.no_grad():
+                y = _INPLACE_ACT[ctx.op_type](x)
+            return [y], ("out", y)
         if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.numel() % 8 == 0
                 and x.is_contiguous() and K.available()
                 and not (ctx.op_type == "GELU" and ctx.a("approximate", "tanh") != "tanh")):
@@ -88,6 +110,8 @@ class ActivationOp(OpImpl):
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
         kind, x = saved
         dy = grad_outputs[0]
+        if kind == "out":
+            return [_act_grad_from_output(ctx.op_type, x, dy)]
         if kind == "hip" and dy.is_contiguous():
             return [K.act_bwd(dy, x, _HIP_ACTS[ctx.op_type], float(ctx.a("alpha", 1.0)))]
         xf = x.detach().float().requires_grad_(True)
@@ -115,14 +139,29 @@ class UnaryOp(AutogradOp):
     def compute(self, ctx, inputs, weights):
         return [_torch_unary(ctx.op_type, ctx, inputs[0])]
 
+    _INPLACE = {"SCALAR_MULTIPLY": torch.Tensor.mul_, "SCALAR_ADD": torch.Tensor.add_,
+                "SCALAR_SUB": torch.Tensor.sub_, "SCALAR_TRUE_DIV": torch.Tensor.div_}
+
     def forward(self, ctx, inputs, weights):
         x = inputs[0]
+        if ctx.extra.get("inplace_ok") and ctx.op_type in self._INPLACE:
+            s = self._scalar(ctx)
+            with torch.no_grad():
+                y = self._INPLACE[ctx.op_type](x, s)
+            return [y], ("inplace", s)
         if ctx.op_type in K.UNARY_CODES and K.tensorop_ok(x):
             s = self._scalar(ctx)
             return [K.unary(x, ctx.op_type, s)], ("hip", x, s)
         return super().forward(ctx, inputs, weights)
 
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        if saved[0] == "inplace":
+            s, g = saved[1], grad_outputs[0]
+            if not need_input_grad[0]:
+                return [None]
+            if ctx.op_type == "SCALAR_MULTIPLY":
+                return [g * s]
+            return [g / s if ctx.op_type == "SCALAR_TRUE_DIV" else g]
         if saved[0] == "hip":
             _, x, s = saved
             g = grad_outputs[0]

@@ -82,6 +82,10 @@ class ExecConfig:
     # operator's forward and backward and re-raise a device fault naming the
     # operator that launched it.  Not usable inside a hipGraph capture.
     sync_debug: bool = dataclasses.field(default_factory=lambda: os.environ.get("FF_SYNC_DEBUG", "0") != "0")
+    # --enable-inplace-optimizations: element-wise activations / scalar ops
+    # whose input has no other reader overwrite that input instead of
+    # allocating an output (_plan_inplace)
+    inplace: bool = False
     # row-sparse SGD update of embedding tables (plain SGD only; exact)
     sparse_embedding_update: bool = True
     # "counter": every rank generates only its own piece from a counter-based
@@ -129,6 +133,10 @@ class ParamPiece:
     master: Optional[torch.Tensor] = None
     compute: Optional[torch.Tensor] = None
     grad: Optional[torch.Tensor] = None
+
+
+_INPLACE_OPS = frozenset({"RELU", "SIGMOID", "TANH", "EXP", "SCALAR_MULTIPLY", "SCALAR_ADD", "SCALAR_SUB",
+                          "SCALAR_TRUE_DIV"})
 
 
 @dataclasses.dataclass
@@ -401,8 +409,63 @@ class Executor:
             for s in self.steps:
                 if s.kind == "compute" and s.op_type == "SOFTMAX":
                     s.ctx.extra["identity_backward"] = True
+        self._inplace_prod: Dict[int, int] = {}
+        if self.cfg.inplace:
+            self._plan_inplace()
         self._mark_requires_grad()
         self._assign_params_to_buffers()
+
+    def _plan_inplace(self):
+        """--enable-inplace-optimizations (reference FFModel::compile:
+        Op::can_inplace_output / do_inplace_output, model.cc).  An element-wise
+        activation (RELU / SIGMOID / TANH / EXP: backward from the output) or
+        scalar op (backward needs no activation) whose input is read by
+        nothing else writes its output over the input: no allocation, half
+        the activation memory of the pair.  Static conditions here: one
+        reader, not a fed input / constant / parameter, not the loss or
+        output value, same layout in and out.  The storage check at run time
+        (_inplace_ok) covers the dynamic ones: the producer kept the tensor
+        for its own backward, or it is a view of a live tensor."""
+        uses: Dict[Value, int] = {}
+        for st in self.steps:
+            for v in st.inputs:
+                uses[v] = uses.get(v, 0) + 1
+        fed = {v[0] for v in self.inputs.values()}
+        terminals = {p.terminal for p in self.params if p.group}
+        prod = {o: i for i, st in enumerate(self.steps) for o in st.outputs}
+        for i, st in enumerate(self.steps):
+            if st.kind != "compute" or st.op_type not in _INPLACE_OPS or len(st.inputs) != 1:
+                continue
+            v = st.inputs[0]
+            j = prod.get(v)
+            if (j is None or self.steps[j].kind != "compute" or uses.get(v, 0) != 1 or v in fed or v in terminals
+                    or v in (self.loss_value, self.output_value)
+                    or self.value_layout.get(v) != self.value_layout.get(st.outputs[0])):
+                continue
+            st.ctx.extra["inplace"] = True
+            self._inplace_prod[i] = j
+
+    def _inplace_ok(self, i: int, s: Step, x: Optional[torch.Tensor]) -> bool:
+        if x is None or s.inputs[0] in self.retain or not x.is_floating_point():
+            return False
+        ptr = x.untyped_storage().data_ptr()
+        j = self._inplace_prod[i]
+        # what may still be read: the producer's saved tensors, its other
+        # outputs and its inputs (x may be a view of one: FLAT / RESHAPE)
+        prod = self.steps[j]
+        held = [self._saved.get(j)] + [self._env_out.get(o) for o in prod.outputs if o != s.inputs[0]] + \
+            [self._env_out.get(v) for v in prod.inputs]
+        stack = list(held)
+        while stack:
+            t = stack.pop()
+            if isinstance(t, torch.Tensor):
+                if t.untyped_storage().data_ptr() == ptr:
+                    return False
+            elif isinstance(t, (tuple, list)):
+                stack.extend(t)
+            elif isinstance(t, dict):
+                stack.extend(t.values())
+        return True
 
     def _fuse_add_layernorm(self):
         by_out = {o: s for s in self.steps for o in s.outputs}
@@ -964,6 +1027,9 @@ class Executor:
             s.ctx.step = self.step_num
             ins = [env[v] for v in s.inputs]
             ws = [p.compute for p in s.weights]
+            if i in self._inplace_prod:
+                self._env_out = env
+                s.ctx.extra["inplace_ok"] = self._inplace_ok(i, s, ins[0])
             impl = opbase.get_impl(s.op_type)
             t0 = self.tracer.begin(f"{s.name}:fwd", "compute", self.step_num) if prof else None
             outs, saved = impl.forward(s.ctx, ins, ws)

@@ -8,7 +8,7 @@ import torch
 
 from flexflow_train_amd import _ffcore as C
 from flexflow_train_amd.core import (ActiMode, AdamOptimizer, AggrMode, DataType, FFConfig, FFModel, LossType,
-                                     MetricsType, SGDOptimizer)
+                                     MetricsType, PoolType, SGDOptimizer)
 
 
 def _mlp(m, B):
@@ -36,6 +36,40 @@ def _embed_concat(m, B):
     t = m.concat([e, d], 1, name="cat")
     m.dense(t, 1, ActiMode.AC_MODE_SIGMOID, name="out")
     return ["ids", "dense"]
+
+
+def _cnn(m, B):
+    x = m.create_tensor([B, 3, 8, 8], DataType.DT_FLOAT, name="img")
+    t = m.conv2d(x, 6, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="c1")
+    t = m.batch_norm(t, relu=True, name="bn")
+    t = m.pool2d(t, 2, 2, 2, 2, 0, 0, PoolType.POOL_MAX, name="mp")
+    t = m.conv2d(t, 4, 3, 3, 2, 2, 1, 1, groups=2, name="c2")
+    t = m.pool2d(t, 2, 2, 1, 1, 1, 1, PoolType.POOL_AVG, name="ap")
+    m.softmax(m.dense(m.flat(t, name="fl"), 5, name="out"))
+    return ["img"]
+
+
+def _math_shapes(m, B):
+    x = m.create_tensor([B, 4, 6], DataType.DT_FLOAT, name="x")
+    s = m.sigmoid(x, name="sg")
+    a = m.add(m.rsqrt(m.scalar_add(s, 0.5, name="sh"), name="rs"), m.pow(s, 3.0, name="p3"), name="a1")
+    b = m.add(m.sin(x, name="si"), m.cos(m.exp(m.scalar_multiply(x, 0.3, name="sc"), name="ex"), name="co"), name="a2")
+    c = m.add(a, m.elu(b, inplace=False, name="el"), name="a3")
+    c = m.reverse(m.transpose(c, [0, 2, 1], name="tr"), 1, name="rv")          # [B, 6, 4]
+    l, r = m.split(c, [2, 4], 1, name="sp")
+    t = m.concat([m.reduce_sum(l, [1], keepdims=True, name="rsum"), m.mean(r, [1], keepdims=True, name="rmean")], 1,
+                 name="cc")                                                     # [B, 2, 4]
+    m.softmax(m.dense(m.flat(t, name="fl"), 3, name="out"))
+    return ["x"]
+
+
+def _attention(m, B):
+    x = m.create_tensor([B, 5, 16], DataType.DT_FLOAT, name="x")
+    kv = m.create_tensor([B, 7, 12], DataType.DT_FLOAT, name="kv")
+    h = m.multihead_attention(x, x, x, 16, 4, name="self")
+    h = m.multihead_attention(h, kv, kv, 16, 2, kdim=6, vdim=5, name="cross")
+    m.softmax(m.dense(m.flat(h, name="fl"), 4, name="out"))
+    return ["x", "kv"]
 
 
 def _run(build, opt, loss, feeds, labels, steps=3, B=8):
@@ -94,6 +128,28 @@ def test_embedding_concat_mse_matches_executor():
     _run(_embed_concat, "adam", "mse", {"ids": ids, "dense": d}, Y)
 
 
+def test_cnn_conv_bn_pool_matches_executor():
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((8, 3, 8, 8)).astype(np.float32)
+    Y = rng.integers(0, 5, (8, 1)).astype(np.int32)
+    _run(_cnn, "sgd", "ce", {"img": X}, Y)
+
+
+def test_math_and_shape_ops_match_executor():
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((8, 4, 6)).astype(np.float32)
+    Y = rng.integers(0, 3, (8, 1)).astype(np.int32)
+    _run(_math_shapes, "adam", "ce", {"x": X}, Y)
+
+
+def test_attention_matches_executor():
+    rng = np.random.default_rng(6)
+    X = rng.standard_normal((8, 5, 16)).astype(np.float32)
+    KV = rng.standard_normal((8, 7, 12)).astype(np.float32)
+    Y = rng.integers(0, 4, (8, 1)).astype(np.int32)
+    _run(_attention, "sgd", "ce", {"x": X, "kv": KV}, Y)
+
+
 def test_fit_local_execution_flag():
     cfg = FFConfig()
     cfg.batch_size = 16
@@ -118,7 +174,8 @@ def test_fit_local_execution_flag():
 
 def test_cost_estimator_and_registry():
     ops = C.LocalTrainingBacking.registered_ops()
-    for t in ("LINEAR", "SOFTMAX", "LAYERNORM", "EMBEDDING", "CONCAT", "BATCHMATMUL", "EW_ADD", "RELU"):
+    for t in ("LINEAR", "SOFTMAX", "LAYERNORM", "EMBEDDING", "CONCAT", "BATCHMATMUL", "EW_ADD", "RELU", "CONV2D",
+              "POOL2D", "BATCHNORM", "MULTIHEAD_ATTENTION", "TRANSPOSE", "SPLIT", "REDUCE_SUM", "GATHER", "EXP"):
         assert t in ops
     lin = C.OpAttrs("LINEAR", out_channels=64)
     ms = C.measure_op_cost_ms(lin, [C.TensorShape([32, 128], C.DataType.FLOAT)])
@@ -130,7 +187,7 @@ def test_unsupported_op_is_rejected():
     cfg = FFConfig()
     cfg.batch_size = 2
     m = FFModel(cfg)
-    x = m.create_tensor([2, 3, 8, 8], DataType.DT_FLOAT, name="img")
-    m.conv2d(x, 8, 3, 3, 1, 1, 1, 1)
+    x = m.create_tensor([2, 16], DataType.DT_FLOAT, name="x")
+    m.top_k(x, 4)
     with pytest.raises(ValueError):
         C.LocalTrainingBacking(m.cg)

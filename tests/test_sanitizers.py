@@ -15,7 +15,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ASAN = os.path.join(ROOT, "bin", "asan")
 REF_SUBST = "/root/reference/substitutions"
-TOOLS = ("ffc-export-model-arch", "ffc-substitution-to-dot", "ffc-protobuf-to-json", "ffc-ffi-test")
+TOOLS = ("ffc-export-model-arch", "ffc-substitution-to-dot", "ffc-protobuf-to-json", "ffc-ffi-test",
+         "ffc-runtime-c-test")
 ENV = dict(os.environ,
            ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1:exitcode=86",
            UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1:exitcode=87")
@@ -59,6 +60,12 @@ def test_c_abi_search_cycle_under_sanitizers(tmp_path):
     """Build a graph through the C ABI, serialise / deserialise it, run the
     strategy search on an 8-GPU machine and query the result."""
     assert "FFI OK" in _run("ffc-ffi-test", str(tmp_path / "cg.json")).stdout
+
+
+def test_c_runtime_api_under_sanitizers():
+    """The legacy FFModel runtime C API: two models trained from C (host
+    local execution of dense / conv / batch norm / pool), handles released."""
+    assert "PASSED (0 failures)" in _run("ffc-runtime-c-test").stdout
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(REF_SUBST, "graph_subst_3_v2.pb")), reason="no corpus")

@@ -132,6 +132,19 @@ def write_ninja(targets: list[str]) -> str:
         exe = os.path.join(ROOT, "bin", "ffc-ffi-test")
         lines.append(f"build {exe}: cc_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_ffi.c')} | {lib}")
         defaults += [lib, exe]
+        # legacy FFModel runtime API (csrc/ffi/flexflow_runtime_c.h): a separate
+        # library, since its symbols overlap the graph API's (as in the reference)
+        lines += ["rule cc_rt_exe",
+                  f"  command = gcc -O2 -std=c11 -I{os.path.join(ROOT, 'csrc', 'ffi')} -o $out $in "
+                  f"-L{os.path.join(PKG, 'lib')} -lflexflow_runtime_c -lm -Wl,-rpath,{os.path.join(PKG, 'lib')}",
+                  "  description = CC $out"]
+        ro = os.path.join("obj", "ffi", "flexflow_runtime_c.cc.o")
+        lines.append(f"build {ro}: cxx {os.path.join(ROOT, 'csrc', 'ffi', 'flexflow_runtime_c.cc')}")
+        rlib = os.path.join(PKG, "lib", "libflexflow_runtime_c.so")
+        lines.append(f"build {rlib}: link_so {ro} {' '.join(core_objs)}")
+        rexe = os.path.join(ROOT, "bin", "ffc-runtime-c-test")
+        lines.append(f"build {rexe}: cc_rt_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_runtime_c.c')} | {rlib}")
+        defaults += [rlib, rexe]
     if "asan" in targets:
         # host-code sanitizer build (ASan/UBSan for host code): the
         # C++ core + C ABI + native CLIs compiled with -fsanitize=address,undefined
@@ -161,6 +174,13 @@ def write_ninja(targets: list[str]) -> str:
         lines.append(f"build {to}: cc_san {os.path.join(ROOT, 'csrc', 'ffi', 'test_ffi.c')}")
         exe = os.path.join(ROOT, "bin", "asan", "ffc-ffi-test")
         lines.append(f"build {exe}: link_san {to} {fo} {' '.join(san_objs)}")
+        defaults.append(exe)
+        ro = os.path.join("obj", "asan", "flexflow_runtime_c.cc.o")
+        lines.append(f"build {ro}: cxx_san {os.path.join(ROOT, 'csrc', 'ffi', 'flexflow_runtime_c.cc')}")
+        rto = os.path.join("obj", "asan", "test_runtime_c.c.o")
+        lines.append(f"build {rto}: cc_san {os.path.join(ROOT, 'csrc', 'ffi', 'test_runtime_c.c')}")
+        exe = os.path.join(ROOT, "bin", "asan", "ffc-runtime-c-test")
+        lines.append(f"build {exe}: link_san {rto} {ro} {' '.join(san_objs)}")
         defaults.append(exe)
         for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "tools", "*.cc"))):
             o = os.path.join("obj", "asan", "tool_" + os.path.basename(s) + ".o")
