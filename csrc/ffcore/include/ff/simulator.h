@@ -48,6 +48,9 @@ struct SimConfig {
   double comm_compute_slowdown = 0.05;   // compute slowdown while a collective overlaps
   bool bf16_weight_grads = true;
   bool parameter_server = false;         // ParamSync::PS instead of all-reduce
+  // row-sparse embedding update (the executor's sparse SGD): an EMBEDDING
+  // table's update touches only the rows its indices name, not the table
+  bool sparse_embedding_update = false;
   const NetworkModel* network = nullptr; // routed transfers / collectives (LogicalTaskgraph mode)
 };
 

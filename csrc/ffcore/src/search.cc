@@ -310,6 +310,7 @@ SimConfig sim_config_from_json(const Json& j) {
   gd("comm_compute_slowdown", c.comm_compute_slowdown);
   gb("bf16_weight_grads", c.bf16_weight_grads);
   gb("parameter_server", c.parameter_server);
+  gb("sparse_embedding_update", c.sparse_embedding_update);
   return c;
 }
 

@@ -287,8 +287,16 @@ SimResult Simulator::simulate(const ParallelComputationGraph& pcg, const std::ma
     for (size_t wi = 0; wi < ws.size(); ++wi) {
       auto const& ps = pcg.shape(ws[wi]);
       const double elems = static_cast<double>(ps.piece_shape().num_elements());
+      double upd = elems;
+      if (cfg_.sparse_embedding_update && node.label.op.type == OpType::EMBEDDING && wi == 0) {
+        // rows named by this piece's indices x row width
+        auto const& ip = pcg.shape(pcg.layer_data_inputs(id).at(0)).piece_shape();
+        auto const& wp = ps.piece_shape();
+        const double width = wp.dims.empty() ? 1.0 : static_cast<double>(wp.dims.back());
+        upd = std::min(elems, static_cast<double>(ip.num_elements()) * width);
+      }
       for (int d : ds)
-        if (d < static_cast<int>(params_on.size())) params_on[d] += elems;
+        if (d < static_cast<int>(params_on.size())) params_on[d] += upd;
       if (ps.discard_copy_degree <= 1) continue;
       const bool gemm_w = wi == 0 && (node.label.op.type == OpType::LINEAR ||
                                       node.label.op.type == OpType::MULTIHEAD_ATTENTION);
