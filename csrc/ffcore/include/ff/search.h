@@ -40,6 +40,9 @@ struct SearchConfig {
   // the share of time_limit MCMC may use before Unity starts
   int unity_budget = -1;
   double mcmc_time_share = 0.5;
+  // graph_optimize: run the machine-mapping DP once on the final PCG and keep
+  // its placements when the simulator prices them below the whole-world ones
+  bool final_machine_mapping = true;
   // rule set added to the built-in parallelization rules (legacy TASO corpus
   // JSON or a substitution-set JSON, load_substitutions); "" = none
   std::string substitution_path;
@@ -54,6 +57,7 @@ struct SearchResult {
   std::map<int, Placement> views;        // PCG node -> devices (empty: whole world)
   double cost = 0;                       // simulated seconds / iteration
   double data_parallel_cost = 0;
+  double unmapped_cost = -1;             // graph_optimize: cost before the final mapping (-1: not run)
   int iterations = 0;
   int evaluated = 0;
   int accepted = 0;

@@ -221,7 +221,6 @@ def _lt(a, b, trans_a, trans_b, bias, act, out, beta, pre, algo=0):
 
 
 _LT_MAX = int(os.environ.get("FF_GEMM_LT_ALGOS", "4"))
-_MARGIN = float(os.environ.get("FF_GEMM_MARGIN", "0.03"))
 
 
 def _lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre):
@@ -401,12 +400,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
             pscratch = None if pre is None else pre.clone()
             times = _time_all({name: (lambda fn=fn: fn(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))
                                for name, fn in cands.items()})
-            choice = min(times, key=times.get)
-            # hysteresis: a one-shot timing on an idle chip ranks candidates
-            # within a few % of each other at random; keep the library GEMM
-            # unless the alternative is clearly faster
-            if "blas" in times and choice != "blas" and times[choice] > (1.0 - _MARGIN) * times["blas"]:
-                choice = "blas"
+            choice = min(times, key=times.get)   # the fastest, no preference for the library
             _TIMES[key] = times
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):

@@ -161,3 +161,18 @@ def test_pcg_strided_views_allowed():
     assert full["feasible"] and cont["feasible"]
     assert full["runtime"] <= cont["runtime"] + 1e-12
     assert full["cache_entries"] > 0
+
+
+def test_graph_optimize_runs_final_mapping():
+    """graph_optimize prices the machine-mapping DP's placements for its
+    final PCG (reported as unmapped_cost vs cost) and keeps them only when
+    the simulator finds them faster than whole-world placements."""
+    from flexflow_train_amd.core import FFConfig
+    from flexflow_train_amd.search import unity
+    m = _towers(batch=64)
+    cfg = FFConfig()
+    cfg.batch_size = 64
+    cfg.search_budget = 20
+    pcg, views, rep = unity.search(m.cg, cfg, 2)
+    assert "unmapped_cost" in rep and rep["cost"] <= rep["unmapped_cost"] + 1e-12
+    assert bool(views) == rep["algorithm"].endswith("+mapping")
