@@ -136,20 +136,31 @@ struct OpCost {
   double forward = 0;   // seconds
   double backward = 0;
   double memory = 0;    // bytes resident per device (weights + grads + optimizer + activations)
+  double workspace = 0; // transient bytes beyond `memory` while the op runs (measured peak)
   double sync = 0;      // weight-gradient all-reduce time
 };
 
-// Optional measured-profile table: op signature -> {fwd_ms, bwd_ms}
+// Optional measured-profile table: op signature -> {fwd_ms, bwd_ms} and, when
+// the profiler tracked the allocator (the reference's TrackedAllocator in
+// local_cost_estimator.cc:29-90), resident_mb (activations alive after the
+// forward: outputs + saved tensors) and peak_mb (allocator peak over forward
+// + backward), both above the op's inputs and weights
+struct ProfileEntry {
+  double fwd_ms = 0, bwd_ms = 0;
+  double resident_mb = -1, peak_mb = -1;  // -1: not measured
+};
 class ProfileTable {
  public:
   void load_json(const Json& j);
   bool lookup(const std::string& key, double& fwd, double& bwd) const;
+  const ProfileEntry* find(const std::string& key) const;
   void put(const std::string& key, double fwd, double bwd);
+  void put(const std::string& key, const ProfileEntry& e) { table_[key] = e; }
   Json to_json() const;
   size_t size() const { return table_.size(); }
 
  private:
-  std::map<std::string, std::pair<double, double>> table_;
+  std::map<std::string, ProfileEntry> table_;
 };
 
 class CostModel {

@@ -288,23 +288,40 @@ double CollectiveCost::p2p(double bytes, const MachineSpecification& s) {
 }
 
 void ProfileTable::load_json(const Json& j) {
-  for (auto const& kv : j.as_object())
-    table_[kv.first] = {kv.second.at("fwd_ms").as_double(), kv.second.at("bwd_ms").as_double()};
+  for (auto const& kv : j.as_object()) {
+    ProfileEntry e;
+    e.fwd_ms = kv.second.at("fwd_ms").as_double();
+    e.bwd_ms = kv.second.at("bwd_ms").as_double();
+    if (kv.second.contains("resident_mb")) e.resident_mb = kv.second.at("resident_mb").as_double();
+    if (kv.second.contains("peak_mb")) e.peak_mb = kv.second.at("peak_mb").as_double();
+    table_[kv.first] = e;
+  }
 }
 bool ProfileTable::lookup(const std::string& key, double& fwd, double& bwd) const {
   auto it = table_.find(key);
   if (it == table_.end()) return false;
-  fwd = it->second.first * 1e-3;
-  bwd = it->second.second * 1e-3;
+  fwd = it->second.fwd_ms * 1e-3;
+  bwd = it->second.bwd_ms * 1e-3;
   return true;
 }
-void ProfileTable::put(const std::string& key, double fwd, double bwd) { table_[key] = {fwd, bwd}; }
+const ProfileEntry* ProfileTable::find(const std::string& key) const {
+  auto it = table_.find(key);
+  return it == table_.end() ? nullptr : &it->second;
+}
+void ProfileTable::put(const std::string& key, double fwd, double bwd) {
+  ProfileEntry e;
+  e.fwd_ms = fwd;
+  e.bwd_ms = bwd;
+  table_[key] = e;
+}
 Json ProfileTable::to_json() const {
   Json j = Json::object();
   for (auto const& kv : table_) {
     Json e = Json::object();
-    e["fwd_ms"] = kv.second.first;
-    e["bwd_ms"] = kv.second.second;
+    e["fwd_ms"] = kv.second.fwd_ms;
+    e["bwd_ms"] = kv.second.bwd_ms;
+    if (kv.second.resident_mb >= 0) e["resident_mb"] = kv.second.resident_mb;
+    if (kv.second.peak_mb >= 0) e["peak_mb"] = kv.second.peak_mb;
     j[kv.first] = e;
   }
   return j;
@@ -370,10 +387,10 @@ OpCost CostModel::op_cost_uncached(const OpAttrs& op, const std::vector<Parallel
   for (auto const& x : outputs) op_.push_back(x.piece_shape());
   std::vector<TensorShape> all = ip;
   all.insert(all.end(), op_.begin(), op_.end());
-  double f = 0, b = 0;
-  if (profiles_.lookup(signature(op, all), f, b)) {
-    c.forward = f;
-    c.backward = b;
+  const ProfileEntry* pe = profiles_.find(signature(op, all));
+  if (pe) {
+    c.forward = pe->fwd_ms * 1e-3;
+    c.backward = pe->bwd_ms * 1e-3;
   } else {
     OpWork w = estimate_op_work(op, ip, wp, op_);
     if (w.matmul_like) {
@@ -441,6 +458,14 @@ OpCost CostModel::op_cost_uncached(const OpAttrs& op, const std::vector<Parallel
   double amem = 0;
   for (auto const& t : ip) amem += static_cast<double>(t.size_bytes());
   for (auto const& t : op_) amem += static_cast<double>(t.size_bytes());
+  if (pe && pe->resident_mb >= 0) {
+    // measured: what the forward leaves alive for the backward, and the
+    // allocator peak over forward + backward beyond it (workspaces, input
+    // gradients, recomputed intermediates)
+    const double resident = pe->resident_mb * 1e6;
+    amem = resident;
+    if (pe->peak_mb >= 0) c.workspace = std::max(0.0, pe->peak_mb * 1e6 - resident);
+  }
   c.memory = wmem + amem;
   c.sync = sync;
   return c;

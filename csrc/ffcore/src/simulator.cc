@@ -384,12 +384,18 @@ SimResult Simulator::simulate(const ParallelComputationGraph& pcg, const std::ma
     if (is_bwd) bwd_end = std::max(bwd_end, r.t.end_time);
   }
   // ---- memory per device
-  std::vector<double> mem(world, 0.0);
+  // resident bytes add up; an op's transient workspace (measured allocator
+  // peak) only while it runs, so each device adds its largest one
+  std::vector<double> mem(world, 0.0), ws(world, 0.0);
   for (int id : order) {
     if (!active(id)) continue;
     for (int d : devset(place(id)))
-      if (d >= 0 && d < world) mem[d] += cost[id].memory;
+      if (d >= 0 && d < world) {
+        mem[d] += cost[id].memory;
+        ws[d] = std::max(ws[d], cost[id].workspace);
+      }
   }
+  for (int d = 0; d < world; ++d) mem[d] += ws[d];
   res.peak_memory = mem.empty() ? 0.0 : *std::max_element(mem.begin(), mem.end());
   if (res.peak_memory > spec.hbm_capacity)
     res.memory_penalty = (res.peak_memory - spec.hbm_capacity) / 1e6 * cfg_.memory_penalty_per_mb;

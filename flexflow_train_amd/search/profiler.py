@@ -68,9 +68,31 @@ def _random_input(shape, dtype, op, device):
     return torch.randn(dims, device=device)
 
 
+def _measure_memory(ex, feeds, g, device) -> Tuple[float, float]:
+    """(resident MB, peak MB) of one eager forward + backward, above the
+    allocation the op's inputs and weights already hold: resident = what the
+    forward leaves alive for the backward (outputs + saved tensors), peak =
+    the caching allocator's high-water mark over forward + backward (the
+    reference's TrackedAllocator, local-execution/src/tracked_allocator.cc)."""
+    ex._saved, ex._env = {}, {}
+    torch.cuda.synchronize(device)
+    base = torch.cuda.memory_allocated(device)
+    torch.cuda.reset_peak_memory_stats(device)
+    ex.forward(feeds, training=True, keep_outputs=True)
+    torch.cuda.synchronize(device)
+    resident = torch.cuda.memory_allocated(device) - base
+    if g is not None:
+        ex.backward(g)
+    torch.cuda.synchronize(device)
+    peak = torch.cuda.max_memory_allocated(device) - base
+    ex._saved, ex._env = {}, {}
+    return max(0.0, resident / 1e6), max(0.0, peak / 1e6)
+
+
 def profile_op(op, in_shapes, device: torch.device, dtype=torch.bfloat16, warmup: int = 3,
-               iters: int = 10) -> Tuple[float, float]:
-    """(forward ms, backward ms) of one operator on its piece shapes."""
+               iters: int = 10, memory: Optional[dict] = None) -> Tuple[float, float]:
+    """(forward ms, backward ms) of one operator on its piece shapes; with a
+    ``memory`` dict on a GPU, also its measured resident / peak MB."""
     pcg, out = _one_op_pcg(op, in_shapes)
     ex = Executor(pcg, DistContext(0, 1, device), ExecConfig(compute_dtype=dtype, device=device),
                   output=(out.node, out.idx))
@@ -120,6 +142,8 @@ def profile_op(op, in_shapes, device: torch.device, dtype=torch.bfloat16, warmup
             fn()
         return timeit(graph.replay)
 
+    if device.type == "cuda" and memory is not None:
+        memory["resident_mb"], memory["peak_mb"] = _measure_memory(ex, feeds, g, device)
     if device.type == "cuda":
         try:
             t_f = graph_time(fwd)
@@ -139,13 +163,15 @@ def build_profile_table(pcgs: Iterable, device: torch.device, out_path: Optional
     for i, (sig, (op, ins)) in enumerate(sigs.items()):
         if sig in table:
             continue
+        mem: dict = {}
         try:
-            f, b = profile_op(op, ins, device)
+            f, b = profile_op(op, ins, device, memory=mem)
         except Exception as e:  # noqa: BLE001 — unsupported op on this device: analytic fallback
             log(f"[profile] skip {op.op_type}: {type(e).__name__}: {str(e)[:120]}")
             continue
-        table[sig] = {"fwd_ms": round(f, 5), "bwd_ms": round(b, 5)}
-        log(f"[profile] {i + 1}/{len(sigs)} {op.op_type:<22} fwd {f:8.4f} ms  bwd {b:8.4f} ms")
+        table[sig] = {"fwd_ms": round(f, 5), "bwd_ms": round(b, 5), **{k: round(v, 3) for k, v in mem.items()}}
+        log(f"[profile] {i + 1}/{len(sigs)} {op.op_type:<22} fwd {f:8.4f} ms  bwd {b:8.4f} ms"
+            + (f"  resident {mem['resident_mb']:.1f} MB  peak {mem['peak_mb']:.1f} MB" if mem else ""))
         if out_path:
             with open(out_path, "w") as fh:
                 json.dump(table, fh, indent=0, sort_keys=True)

@@ -158,3 +158,29 @@ def test_pipeline_stages_overlap_in_simulation():
     assert "XFER 0->1" in r["dot"]
     one = native.simulate(pcg, cm, 1)
     assert r["iteration_time"] > one["iteration_time"]
+
+
+def test_measured_memory_drives_peak():
+    """Profile entries with allocator measurements (resident_mb / peak_mb,
+    search/profiler.py) replace the analytic activation bytes; the largest
+    transient workspace of a device is added once (it is not resident)."""
+    from flexflow_train_amd.search.profiler import collect_signatures
+    m = _chain()
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    cm = native.cost_model(use_profiles=False)
+    base = native.simulate(pcg, cm, 1)["peak_memory"]
+    sigs = collect_signatures([pcg])
+    table = {}
+    for i, sig in enumerate(sigs):
+        table[sig] = {"fwd_ms": 0.01, "bwd_ms": 0.02, "resident_mb": 100.0 * (i + 1), "peak_mb": 100.0 * (i + 1) + 50.0 * i}
+    cm2 = native.cost_model(use_profiles=False)
+    cm2.load_profiles(json.dumps(table))
+    got = native.simulate(pcg, cm2, 1)["peak_memory"]
+    n = len(sigs)
+    resident = sum(100e6 * (i + 1) for i in range(n))
+    workspace = 50e6 * (n - 1)
+    # weights (bf16 copy + fp32 master + Adam m, v + grad = 16 B / param) stay analytic
+    weights = 2 * (256 * 256 + 256) * 16.0
+    assert got == pytest.approx(weights + resident + workspace)
+    assert base > weights      # analytic activations before
+    assert json.loads(cm2.profiles_json())[next(iter(sigs))]["peak_mb"] == pytest.approx(100.0)
