@@ -435,6 +435,20 @@ OpCost CostModel::op_cost_uncached(const OpAttrs& op, const std::vector<Parallel
       c.backward += std::max(2.5 * core_t, s * hop_b);
     }
   }
+  // Attribute (spatial) parallelism: H bands exchange halo rows with their
+  // neighbours before the window op (both directions at once, one xGMI link
+  // each) and return the halo gradients after its backward
+  if ((op.type == OpType::CONV2D || op.type == OpType::POOL2D) && !inputs.empty() && inputs[0].num_dims() == 4 &&
+      inputs[0].dim(2).degree > 1) {
+    const int64_t k = op.i("kernel_h"), st = op.i("stride_h");
+    const double halo_rows = static_cast<double>(std::max<int64_t>(0, k - st));
+    const auto& x = ip[0];
+    const double bytes = halo_rows * static_cast<double>(x.dims[0] * x.dims[1] * x.dims[3]) *
+                         static_cast<double>(size_of(x.dtype));
+    const double t = CollectiveCost::p2p(bytes, spec_);
+    c.forward += t;
+    c.backward += t;
+  }
   // All-to-all expert parallelism: dispatch + combine all-to-alls forward,
   // their transposes backward (token pairs of this piece, bf16 rows).
   if (op.type == OpType::EXPERTS && op.s("expert_parallel_mode") == "alltoall" && op.i("expert_degree") > 1 &&

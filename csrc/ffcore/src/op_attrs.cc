@@ -184,6 +184,25 @@ std::vector<int64_t> broadcast_dims(const OpAttrs& a, std::vector<int64_t> x, st
 
 int64_t conv_out(int64_t in, int64_t k, int64_t s, int64_t p) { return (in + 2 * p - k) / s + 1; }
 
+// Attribute (spatial) parallelism of a window op along H (flexflow_train_amd/
+// parallel/halo.py): shard j of d computes output rows [j OH/d, (j+1) OH/d)
+// from its input rows plus halos taken from its two neighbours; every shard's
+// halo must fit inside one neighbour's rows.
+bool spatial_split_ok(int64_t H, int64_t k, int64_t s, int64_t p, int d) {
+  if (d <= 1) return true;
+  const int64_t OH = conv_out(H, k, s, p);
+  if (H % d || OH % d || OH <= 0) return false;
+  const int64_t Hl = H / d, OHl = OH / d;
+  for (int j = 0; j < d; ++j) {
+    const int64_t lo = j * OHl * s - p, hi = ((j + 1) * OHl - 1) * s - p + k;
+    const int64_t top = std::max<int64_t>(0, j * Hl - std::max<int64_t>(lo, 0));
+    const int64_t bot = std::max<int64_t>(0, std::min<int64_t>(hi, H) - (j + 1) * Hl);
+    if (top > Hl || bot > Hl) return false;
+    if ((j == 0 && top) || (j == d - 1 && bot)) return false;
+  }
+  return true;
+}
+
 std::vector<int> norm_axes(const OpAttrs& a, const std::string& key, int ndims) {
   std::vector<int> r;
   for (auto x : a.ints(key)) r.push_back(normalize_dim(static_cast<int>(x), ndims));
@@ -343,21 +362,26 @@ OpSpec conv2d_spec() {
   };
   s.pout = [](const OpAttrs& a, const PShapes& in) {
     auto const& x = in.at(0);
-    require(x.dim(2).degree == 1 && x.dim(3).degree == 1, a, "H/W (attribute) degree must be 1");
+    // attribute parallelism: H shards with halo exchange (W stays whole)
+    const int dh = x.dim(2).degree;
+    require(x.dim(3).degree == 1, a, "W (attribute) degree must be 1");
+    require(dh == 1 || spatial_split_ok(x.dim(2).size, a.i("kernel_h"), a.i("stride_h"), a.i("padding_h"), dh), a,
+            "H shards need halos wider than one neighbour");
     require(a.i("groups") == 1 || x.dim(1).degree == 1, a, "grouped conv cannot shard channels");
     if (activation_from_string(a.s("activation")) != Activation::NONE)
       require(x.dim(1).degree == 1 && x.sum_degree == 1, a, "fused activation on partial sums");
     auto o = registry()[static_cast<int>(OpType::CONV2D)].out(a, {x.reduced_shape()})[0];
     return PShapes{lift_to_parallel_with_degrees(o, x.sum_degree * x.dim(1).degree, 1,
-                                                 {x.dim(0).degree, x.discard_copy_degree, 1, 1})};
+                                                 {x.dim(0).degree, x.discard_copy_degree, dh, 1})};
   };
   s.pwts = [](const OpAttrs& a, const PShapes& in) {
     auto const& x = in.at(0);
+    const int dh = x.dim(2).degree;
     auto ws = registry()[static_cast<int>(OpType::CONV2D)].wts(a, {x.reduced_shape()});
-    PShapes r{lift_to_parallel_with_degrees(ws[0], 1, x.dim(0).degree * x.sum_degree,
+    PShapes r{lift_to_parallel_with_degrees(ws[0], 1, x.dim(0).degree * dh * x.sum_degree,
                                             {x.discard_copy_degree, x.dim(1).degree, 1, 1})};
     if (ws.size() > 1)
-      r.push_back(lift_to_parallel_with_degrees(ws[1], x.sum_degree * x.dim(1).degree, x.dim(0).degree,
+      r.push_back(lift_to_parallel_with_degrees(ws[1], x.sum_degree * x.dim(1).degree, x.dim(0).degree * dh,
                                                 {x.discard_copy_degree}));
     return r;
   };
@@ -383,11 +407,14 @@ OpSpec pool2d_spec() {
   s.wts = no_weight_shapes;
   s.pout = [](const OpAttrs& a, const PShapes& in) {
     auto const& x = in.at(0);
-    require(x.dim(2).degree == 1 && x.dim(3).degree == 1, a, "H/W degree must be 1");
+    const int dh = x.dim(2).degree;
+    require(x.dim(3).degree == 1, a, "W (attribute) degree must be 1");
+    require(dh == 1 || spatial_split_ok(x.dim(2).size, a.i("kernel_h"), a.i("stride_h"), a.i("padding_h"), dh), a,
+            "H shards need halos wider than one neighbour");
     require(x.sum_degree == 1, a, "pooling a partial-sum tensor");
     auto o = registry()[static_cast<int>(OpType::POOL2D)].out(a, {x.reduced_shape()})[0];
     return PShapes{lift_to_parallel_with_degrees(o, 1, x.discard_copy_degree,
-                                                 {x.dim(0).degree, x.dim(1).degree, 1, 1})};
+                                                 {x.dim(0).degree, x.dim(1).degree, dh, 1})};
   };
   s.pwts = no_pweight_shapes;
   return s;
@@ -412,14 +439,17 @@ OpSpec batchnorm_spec() {
   s.pout = [](const OpAttrs& a, const PShapes& in) {
     auto const& x = in.at(0);
     require(x.sum_degree == 1, a, "normalizing a partial-sum tensor");
-    for (int d = 2; d < x.num_dims(); ++d) require(x.dim(d).degree == 1, a, "spatial degree must be 1");
+    // H shards (attribute parallelism) normalise with their local statistics,
+    // as batch shards do (per-device statistics, the reference's BatchNorm)
+    for (int d = 3; d < x.num_dims(); ++d) require(x.dim(d).degree == 1, a, "W degree must be 1");
     return PShapes{x};
   };
   s.pwts = [](const OpAttrs& a, const PShapes& in) {
     if (!a.b("affine")) return PShapes{};
     auto const& x = in.at(0);
+    const int dh = x.num_dims() > 2 ? x.dim(2).degree : 1;
     auto w = lift_to_parallel_with_degrees(TensorShape{{x.dim(1).size}, x.dtype}, 1,
-                                           x.dim(0).degree * x.discard_copy_degree, {x.dim(1).degree});
+                                           x.dim(0).degree * dh * x.discard_copy_degree, {x.dim(1).degree});
     return PShapes{w, w};
   };
   return s;

@@ -86,6 +86,10 @@ bool is_mp_capable(const OpAttrs& op, MPKind k) {
   }
 }
 
+// The attribute dim the `seq` degree shards: the sequence (dim 1) of a
+// [batch, seq, ...] activation, H (dim 2) of an NCHW image.
+int attribute_dim(const TensorShape& s) { return s.num_dims() == 4 ? 2 : 1; }
+
 // Degrees for a data input of rank r / dims under (batch, seq), with the
 // leading-dim sizes of input 0 used to detect broadcast operands.
 ParallelTensorShape batch_seq_shape(const TensorShape& s, const TensorShape& ref, int b, int q) {
@@ -93,9 +97,10 @@ ParallelTensorShape batch_seq_shape(const TensorShape& s, const TensorShape& ref
   if (s.num_dims() >= 1 && b > 1 && s.num_dims() == ref.num_dims() && s.dims[0] == ref.dims[0] &&
       s.dims[0] % b == 0)
     deg[0] = b;
-  if (s.num_dims() >= 3 && q > 1 && s.num_dims() == ref.num_dims() && s.dims[1] == ref.dims[1] &&
-      s.dims[1] % q == 0)
-    deg[1] = q;
+  const int ad = attribute_dim(s);
+  if (s.num_dims() >= 3 && q > 1 && s.num_dims() == ref.num_dims() && s.dims[ad] == ref.dims[ad] &&
+      s.dims[ad] % q == 0)
+    deg[ad] = q;
   return lift_to_parallel_with_degrees(s, 1, 1, deg);
 }
 
@@ -126,7 +131,7 @@ std::optional<std::vector<ParallelTensorShape>> required_input_shapes(const Comp
   }
   // every requested degree must actually apply to input 0
   if (cfg.batch > 1 && (ref.num_dims() < 1 || ps[0].dim(0).degree != cfg.batch)) return std::nullopt;
-  if (cfg.seq > 1 && (ref.num_dims() < 3 || ps[0].dim(1).degree != cfg.seq)) return std::nullopt;
+  if (cfg.seq > 1 && (ref.num_dims() < 3 || ps[0].dim(attribute_dim(ref)).degree != cfg.seq)) return std::nullopt;
   if (cfg.kind != MPKind::NONE || cfg.model > 1) {
     if (cfg.kind == MPKind::NONE || cfg.model <= 1 || !is_mp_capable(op, cfg.kind)) return std::nullopt;
     switch (cfg.kind) {

@@ -34,8 +34,11 @@ _ACTS = {"none": lambda t: t, "relu": torch.relu, "sigmoid": torch.sigmoid, "tan
 
 
 def _geom(ctx):
+    # an H-sharded input (attribute parallelism) arrives with its halo rows
+    # and border padding attached (parallel/halo.py): no H padding here
+    ph = 0 if ctx.extra.get("halo") is not None else int(ctx.a("padding_h", 0))
     return ((int(ctx.a("stride_h", 1)), int(ctx.a("stride_w", 1))),
-            (int(ctx.a("padding_h", 0)), int(ctx.a("padding_w", 0))),
+            (ph, int(ctx.a("padding_w", 0))),
             int(ctx.a("groups", 1)), ctx.a("activation", "none"))
 
 
@@ -106,6 +109,9 @@ class Conv2DOp(OpImpl):
 
     def forward(self, ctx, inputs, weights):
         x = inputs[0]
+        halo = ctx.extra.get("halo")
+        if halo is not None:
+            x = halo.extend(x)
         W = weights[0]
         b = weights[1] if len(weights) > 1 and ctx.sum_index == 0 else None
         stride, pad, groups, act = _geom(ctx)
@@ -160,6 +166,14 @@ class Conv2DOp(OpImpl):
         return [y.detach()], ("torch", xi, Wr, u, y)
 
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        halo = ctx.extra.get("halo")
+        gx = self._backward(ctx, saved, grad_outputs, weight_grads, need_input_grad)
+        if halo is not None and need_input_grad[0]:
+            # every band takes part in the halo return, with or without a gradient
+            return [halo.fold(gx[0])]
+        return gx
+
+    def _backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
         stride, pad, groups, act = _geom(ctx)
         if saved[0] == "torch":
             _, xi, Wr, u, y = saved
@@ -214,7 +228,7 @@ class Conv2DOp(OpImpl):
             dx = K.conv2d_dgrad(dy, wp, (xshape[0], Cp, xshape[2], xshape[3]), stride, pad)
             return [dx[:, :xshape[1]]]
         acc = ctx.extra.get("grad_acc", [None])[0]
-        use_acc = (acc is not None and acc.is_cuda and acc.dtype == torch.bfloat16 and tuple(acc.shape) == tuple(xshape)
+        use_acc = (acc is not None and ctx.extra.get("halo") is None and acc.is_cuda and acc.dtype == torch.bfloat16 and tuple(acc.shape) == tuple(xshape)
                    and acc.is_contiguous(memory_format=torch.channels_last))
         if _pointwise(R, S, stride, pad, 1):
             def dgrad_gemm(out):
@@ -259,6 +273,9 @@ class Pool2DOp(OpImpl):
     def forward(self, ctx, inputs, weights):
         x = inputs[0]
         k, s, p, avg, act = self._geom(ctx)
+        halo = ctx.extra.get("halo")
+        if halo is not None:
+            return self._halo_forward(ctx, halo, x, k, s, p, avg, act)
         if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and act == "none"
                 and k[0] * k[1] <= 256 and K.use_hip(x)):
             xin = K.nhwc(x)
@@ -273,10 +290,45 @@ class Pool2DOp(OpImpl):
         y = F.avg_pool2d(x, k, s, p, count_include_pad=False) if avg else F.max_pool2d(x, k, s, p)
         return _ACTS[act](y)
 
+    @staticmethod
+    def _banded(xe, me, k, s, p, avg, act):
+        """Pool an H band with its halo / border rows attached (``me`` marks
+        the real rows: the average excludes the border, as count_pad=False)."""
+        ph, pw = 0, p[1]
+        if avg:
+            num = F.avg_pool2d(xe, k, s, (ph, pw), count_include_pad=True)
+            den = F.avg_pool2d(me, k, s, (ph, pw), count_include_pad=True)
+            y = num / den.clamp_min(1e-12)
+        else:
+            y = F.max_pool2d(xe, k, s, (ph, pw))
+        return _ACTS[act](y)
+
+    def _halo_forward(self, ctx, halo, x, k, s, p, avg, act):
+        # the border rows: -inf for max pooling, zeros (and a zero mask) for average
+        halo.pad_value = 0.0 if avg else float("-inf")
+        xe = halo.extend(x)
+        me = None
+        if avg:   # real rows 1, border rows 0 (known locally: no exchange)
+            _, _, _, _, pad_top, pad_bot = halo.plan.rows[halo.index]
+            me = torch.ones((1, 1, xe.shape[2], xe.shape[3]), dtype=xe.dtype, device=xe.device)
+            me[:, :, :pad_top] = 0
+            if pad_bot:
+                me[:, :, xe.shape[2] - pad_bot:] = 0
+        with torch.no_grad():
+            y = self._banded(xe, me, k, s, p, avg, act)
+        return [y.to(x.dtype)], ("halo", xe, me)
+
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
+        k, s, p, avg, act = self._geom(ctx)
+        if saved[0] == "halo":
+            _, xe, me = saved
+            xg = xe.detach().requires_grad_(True)
+            with torch.enable_grad():
+                y = self._banded(xg, me, k, s, p, avg, act)
+            y.backward(grad_outputs[0].to(y.dtype))
+            return [ctx.extra["halo"].fold(xg.grad)] if need_input_grad[0] else [None]
         if not need_input_grad[0]:
             return [None]
-        k, s, p, avg, act = self._geom(ctx)
         if saved[0] == "hip":
             _, xshape, arg = saved
             dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))

@@ -38,6 +38,7 @@ from ..ops import base as opbase
 from ..ops.loss import N_SLOTS, LossFunction, PerfMetrics
 from ..parallel.comm import DistContext, Redistributor
 from ..parallel.layout import Layout, layout_from_pshape, placement
+from ..parallel.halo import HaloGroup, HaloPlan
 from ..parallel.sequence import SeqGroup
 from ..ops.moe import ExpertGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig, ShardedOptimizer
@@ -376,6 +377,25 @@ class Executor:
                 cw = wl.coord(self.rank)
                 if cw is not None:
                     ctx.extra["ep_group"] = ExpertGroup(self.dist, _ep_ranks(cw), cw.shard[0])
+            if t in ("CONV2D", "POOL2D") and in0 is not None and len(in0.shard_dims) == 4 \
+                    and int(in0.shard_dims[2].degree) > 1:
+                # attribute (spatial) parallelism: the ranks holding the other
+                # H bands of the same (batch, channel) slice exchange halos
+                ilay = self.value_layout[real_ins[0]]
+                a_n = attrs[n]
+
+                def _band_ranks(c, lay=ilay):
+                    return [lay.rank_of(dataclasses.replace(c, shard=tuple(c.shard[:2]) + (j,) + tuple(c.shard[3:])))
+                            for j in range(lay.degrees[2])]
+                for r in range(self.world):
+                    cr = ilay.coord(r)
+                    if cr is not None:
+                        self._sp_groups.add(tuple(sorted(_band_ranks(cr))))
+                ci = ilay.coord(self.rank)
+                if ci is not None:
+                    plan = HaloPlan(int(in0.shard_dims[2].size), int(a_n["kernel_h"]), int(a_n.get("stride_h", 1)),
+                                    int(a_n.get("padding_h", 0)), int(in0.shard_dims[2].degree))
+                    ctx.extra["halo"] = HaloGroup(self.dist, _band_ranks(ci), ci.shard[2], plan)
             if t in ("REDUCE_MEAN", "MEAN") and in0 is not None:
                 axes = [int(a) % len(in0.shard_dims) for a in attrs[n].get("axes", [])]
                 deg = math.prod(int(in0.shard_dims[a].degree) for a in axes)

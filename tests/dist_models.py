@@ -156,3 +156,20 @@ def towers(m):
     m.softmax(t, name="sm")
     g = torch.Generator().manual_seed(3)
     return {"x": torch.randn(8, 16, generator=g)}, torch.randint(0, 12, (8,), generator=g)
+
+
+def cnn_spatial(m):
+    """conv / max pool (padded, stride 2) / conv + residual / padded average
+    pool on 16-row images: every window op takes halos from its neighbour
+    band when H is sharded (attribute parallelism)."""
+    from flexflow_train_amd.core import PoolType
+    x = m.create_tensor([4, 3, 16, 10], DataType.DT_FLOAT, name="img")
+    t = m.conv2d(x, 8, 3, 3, 1, 1, 1, 1, ActiMode.AC_MODE_RELU, name="c1")
+    t = m.pool2d(t, 3, 3, 2, 2, 1, 1, PoolType.POOL_MAX, name="p1")
+    u = m.conv2d(t, 8, 5, 3, 1, 1, 2, 1, name="c2")
+    t = m.relu(m.add(t, u, name="res"), name="r2")
+    t = m.pool2d(t, 3, 3, 1, 1, 1, 1, PoolType.POOL_AVG, name="p2")
+    t = m.dense(m.flat(t, name="flat"), 6, name="out")
+    m.softmax(t, name="sm")
+    g = torch.Generator().manual_seed(19)
+    return {"img": torch.randn(4, 3, 16, 10, generator=g)}, torch.randint(0, 6, (4,), generator=g)

@@ -241,3 +241,21 @@ def test_strided_machine_view_placement(tmp_path):
     out = run_distributed(M.towers, 4, path, steps=3)
     assert_params_close(out["params"], ref["params"])
     assert out["stats"]["all_to_all"] + out["stats"]["p2p"] + out["stats"]["all_gather"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_attribute_parallel_conv_halo(tmp_path, world):
+    """Attribute (spatial) parallelism: conv / pool layers on H bands with
+    halo exchange (parallel/halo.py) train exactly like the single process."""
+    ref = run_single(M.cnn_spatial)
+    path = str(tmp_path / "spatial.json")
+    spatial = {"batch": 1, "seq": world}
+    pcg = write_strategy(M.cnn_spatial, world, {k: spatial for k in ("c1", "p1", "c2", "res", "r2", "p2")}, path)
+    from flexflow_train_amd import _ffcore as C
+    degs = {pcg.layer_name(n): list(pcg.shape(C.ValueRef(n, 0)).shard_degrees()) for n in pcg.topo_order()}
+    assert degs["c1"] == [1, 1, world, 1] and degs["p2"] == [1, 1, world, 1]
+    out = run_distributed(M.cnn_spatial, world, path)
+    assert_params_close(out["params"], ref["params"])
+    # 4 window ops x (forward extend + backward fold) x 2 steps, minus c1's
+    # input gradient (the image needs none)
+    assert out["stats"].get("halo", 0) >= 2 * 7, out["stats"]

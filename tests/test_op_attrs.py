@@ -119,8 +119,16 @@ def test_conv2d_parallel_rules():
     assert outs(op, [P([4, 4, 8, 8], [1, 2, 1, 1])]) == [([1, 1, 1, 1], 2, 1)]
     assert outs(op, [P([4, 3, 8, 8], None, 1, 2)]) == [([1, 2, 1, 1], 1, 1)]
     assert weights(op, [P([4, 3, 8, 8], None, 1, 2)]) == [([2, 1, 1, 1], 1, 1), ([2], 1, 1)]
-    with pytest.raises(Exception):   # attribute (H/W) parallelism is not allowed
-        C.infer_parallel_output_shapes(op, [P([4, 3, 8, 8], [1, 1, 2, 1])])
+    # attribute parallelism: H bands (halo exchange, parallel/halo.py); the
+    # weights are replicated over the bands
+    assert outs(op, [P([4, 3, 8, 8], [1, 1, 2, 1])]) == [([1, 1, 2, 1], 1, 1)]
+    assert weights(op, [P([4, 3, 8, 8], [2, 1, 2, 1])]) == [([1, 1, 1, 1], 1, 4), ([1], 1, 4)]
+    with pytest.raises(Exception):   # W stays whole
+        C.infer_parallel_output_shapes(op, [P([4, 3, 8, 8], [1, 1, 1, 2])])
+    wide = C.OpAttrs("CONV2D", out_channels=8, kernel_h=7, kernel_w=3, stride_h=1, stride_w=1, padding_h=3,
+                     padding_w=1, groups=1)
+    with pytest.raises(Exception):   # 1-row bands cannot supply a 3-row halo
+        C.infer_parallel_output_shapes(wide, [P([4, 3, 8, 8], [1, 1, 8, 1])])
 
 
 def test_pool_and_batchnorm():
@@ -129,9 +137,13 @@ def test_pool_and_batchnorm():
     assert outs(pool, [P([4, 3, 8, 8], [2, 1, 1, 1])]) == [([2, 1, 1, 1], 1, 1)]
     (o,) = C.infer_output_shapes(pool, [C.TensorShape([4, 3, 8, 8], C.DataType.FLOAT)])
     assert list(o.dims) == [4, 3, 4, 4]
+    # H bands (2x2 stride 2 windows never cross a band edge: no halo)
+    assert outs(pool, [P([4, 3, 8, 8], [1, 1, 2, 1])]) == [([1, 1, 2, 1], 1, 1)]
     with pytest.raises(Exception):
-        C.infer_parallel_output_shapes(pool, [P([4, 3, 8, 8], [1, 1, 2, 1])])
+        C.infer_parallel_output_shapes(pool, [P([4, 3, 8, 8], [1, 1, 1, 2])])
     bn = C.OpAttrs("BATCHNORM", relu=False)
+    # H bands normalise with local statistics; gamma / beta replicated over them
+    assert weights(bn, [P([4, 4, 8, 8], [1, 1, 2, 1])]) == [([1], 1, 2), ([1], 1, 2)]
     assert weights(bn, [P([4, 4, 8, 8], [1, 2, 1, 1])]) == [([2], 1, 1), ([2], 1, 1)]
     assert weights(bn, [P([4, 4, 8, 8], [2, 1, 1, 1])]) == [([1], 1, 2), ([1], 1, 2)]
 
