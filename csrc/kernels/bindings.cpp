@@ -234,6 +234,11 @@ PYBIND11_MODULE(_ffkernels, m) {
     init_tensor(dt, P(out), shape(piece), shape(full), strides(lo), kind, seed, a, b, c, d, S(st));
   });
   m.def("gemmp_supported", &gemmp_supported);
+  m.def("bmm", [](uintptr_t A, uintptr_t B, uintptr_t C, int batch, int M, int N, int K, int lda, int ldb, int ldc,
+                  int64_t sA, int64_t sB, int64_t sC, bool ta, bool tb, float alpha, float beta, int out_f32,
+                  uintptr_t st) {
+    bmm_bf16(P(A), P(B), P(C), batch, M, N, K, lda, ldb, ldc, sA, sB, sC, ta, tb, alpha, beta, out_f32, S(st));
+  });
   m.def("gemmp", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, uintptr_t aux,
                     uintptr_t dbias, int M, int N, int K, int lda, int ldb, int ldc, bool ta, bool tb, int act,
                     bool act_bwd, float alpha, float beta, int out_f32, int splits, uintptr_t ws, uintptr_t st,

@@ -136,7 +136,8 @@ struct GemmPParams {
   int dbg = 0;                  // ablation bits for timing experiments (gemmp.hip)
   int variant = 0;              // 0: 32x32x16 MFMA (gemmp.hip), 1: 16x16x32 (gemmq.hip), 2: ping-pong (gemmr.hip), 5: persistent gemmt, 6: gemmt with both operands by LDS-DMA,
                                 // 3 / 4: one wave per SIMD, 128x128 wave tile, B staged
-                                // through registers / by LDS-DMA (gemmt.hip)
+                                // through registers / by LDS-DMA (gemmt.hip),
+                                // 8: 64x64 tiles for MLP-sized products (gemms.hip)
 };
 bool gemmp_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b);
 void gemmp_bf16(const GemmPParams& p, hipStream_t st);
@@ -144,6 +145,16 @@ void gemmq_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
 void gemmr_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
 void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t st);
 bool gemmt_supported(const GemmPParams& p);
+// small-tile (64 x 64) MLP GEMM, variant 8 (gemms.hip)
+bool gemms_supported(const GemmPParams& p);
+void gemms_launch(const GemmPParams& p, int splits, hipStream_t st);
+void gemms_launch_batched(const GemmPParams& p, int splits, int batch, int64_t sA, int64_t sB, int64_t sC,
+                          hipStream_t st);
+// batched C[z] = alpha op(A[z]) op(B[z]) + beta C[z] on the 64x64-tile kernel
+// (the reference's batch_matmul_kernels.cu); K % 64 == 0, M / N % 8 == 0
+void bmm_bf16(const void* A, const void* B, void* C, int batch, int M, int N, int K, int lda, int ldb, int ldc,
+              int64_t sA, int64_t sB, int64_t sC, bool trans_a, bool trans_b, float alpha, float beta, int out_f32,
+              hipStream_t st);
 
 // ---- tensorops.hip: general tensor operators (N-d, <= 6 dims)
 struct NdShape {

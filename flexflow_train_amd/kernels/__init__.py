@@ -595,6 +595,44 @@ def gemmp(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, 
     return out
 
 
+def bmm_supported(a, b, trans_a=False, trans_b=False) -> bool:
+    """Batched [..., M, K] x [..., K, N] (same batch dims, bf16, 16-B aligned
+    rows, K % 64, M / N % 8) on the 64x64-tile kernel (gemms.hip)."""
+    if not available() or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda:
+        return False
+    if a.dim() < 3 or a.dim() != b.dim() or a.shape[:-2] != b.shape[:-2] or not hasattr(ext(), "bmm"):
+        return False
+    if not (a.is_contiguous() and b.is_contiguous()) or a.data_ptr() % 16 or b.data_ptr() % 16:
+        return False
+    M, K = (a.shape[-1], a.shape[-2]) if trans_a else (a.shape[-2], a.shape[-1])
+    N = b.shape[-2] if trans_b else b.shape[-1]
+    return K % 64 == 0 and M % 8 == 0 and N % 8 == 0 and a.shape[-1] % 8 == 0 and b.shape[-1] % 8 == 0
+
+
+def bmm(a, b, trans_a=False, trans_b=False, out=None, beta=0.0):
+    """C[z] = op(a[z]) @ op(b[z]) (+ beta C[z]) over the flattened batch dims
+    (the reference's batch_matmul_kernels.cu, here one launch: blockIdx.z =
+    product)."""
+    if not bmm_supported(a, b, trans_a, trans_b):
+        raise ValueError("bmm: unsupported operands")
+    lead = a.shape[:-2]
+    Z = 1
+    for d in lead:
+        Z *= int(d)
+    M, K = (a.shape[-1], a.shape[-2]) if trans_a else (a.shape[-2], a.shape[-1])
+    N = b.shape[-2] if trans_b else b.shape[-1]
+    if out is None:
+        out = torch.empty(*lead, M, N, device=a.device, dtype=torch.bfloat16)
+        beta = 0.0
+    if not out.is_contiguous() or tuple(out.shape[-2:]) != (M, N):
+        raise ValueError("bmm: bad output")
+    ext().bmm(a.data_ptr(), b.data_ptr(), out.data_ptr(), Z, M, N, K, a.shape[-1], b.shape[-1], N,
+              a.shape[-2] * a.shape[-1], b.shape[-2] * b.shape[-1], M * N, bool(trans_a), bool(trans_b), 1.0,
+              float(beta), int(out.dtype == torch.float32), _stream())
+    STATS["bmm"] += 1
+    return out
+
+
 # ---------------------------------------------------------------------------
 # General tensor operators (csrc/kernels/tensorops.hip).  Inputs: contiguous
 # GPU tensors in bf16 or fp32; _check's 16-byte alignment is not required.

@@ -12,6 +12,8 @@ partial-sum replica 0, so the Reduction that follows sums it once.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import kernels as K
@@ -100,7 +102,8 @@ class LinearOp(OpImpl):
                   and K.gemmp_supported(g, W, False, True))
             if ok and _dact_fused_wins(g, W, pre2, act_p, db_p is not None):
                 dx = K.gemmp(g, W, trans_b=True, act=act_p, aux=pre2, act_bwd=True,
-                             dbias=db_p.reshape(-1) if db_p is not None else None, variant=_dact_variant(act_p))
+                             dbias=db_p.reshape(-1) if db_p is not None else None,
+                             variant=_dact_variant(act_p, g.shape[0], W.shape[0]))
                 pctx.extra["grad_is_preact"] = True
                 return [dx.reshape(*dy.shape[:-1], W.shape[0])]
         if need_input_grad[0]:
@@ -117,11 +120,14 @@ _DACT_CHOICE = {}
 _DACT_TIMES = {}
 
 
-def _dact_variant(act: str) -> int:
-    """The fused activation-gradient GEMM runs on gemmt (one wave per SIMD,
-    128x128 wave tiles, operands staged by LDS-DMA) for the activations it
-    instantiates, else on gemmp."""
-    from .gemm import _GT_DMA, _GT_VARIANT
+def _dact_variant(act: str, M: int = 1 << 30, N: int = 1 << 30) -> int:
+    """The fused activation-gradient GEMM runs on the 64x64-tile MLP kernel
+    (gemms.hip) when 256x256 tiles cannot fill the chip, else on gemmt (one
+    wave per SIMD, 128x128 wave tiles, operands staged by LDS-DMA) for the
+    activations it instantiates, else on gemmp."""
+    from .gemm import _GT_DMA, _GT_VARIANT, _small_mn
+    if _small_mn(M, N) and os.environ.get("FF_GEMMS", "1") != "0":
+        return 8
     if not _GT_VARIANT or act not in ("relu", "gelu"):
         return 0
     return 6 if _GT_DMA else _GT_VARIANT   # both operands by LDS-DMA (the dact GEMM is NT)
@@ -142,7 +148,7 @@ def _dact_fused_wins(g, W, pre, act, has_bias) -> bool:
     dx = matmul(g, W, trans_b=True)   # settles the autotuner's pick first
     t = _time_all({
         "fused": lambda: K.gemmp(g, W, trans_b=True, act=act, aux=pre, act_bwd=True,
-                                 dbias=db if has_bias else None, variant=_dact_variant(act)),
+                                 dbias=db if has_bias else None, variant=_dact_variant(act, g.shape[0], W.shape[0])),
         "plain": lambda: (matmul(g, W, trans_b=True),
                           K.colsum_act(dx, pre, act, db if has_bias else None, write_dx=True))})
     fused, plain = t["fused"], t["plain"]
@@ -159,15 +165,32 @@ def dact_report() -> str:
                      for k, (f, p) in _DACT_TIMES.items())
 
 
+def _bmm(a, b, trans_a=False, trans_b=False):
+    """Batched product on the hand-written 64x64-tile kernel (gemms.hip,
+    one launch for the whole batch) when the shapes allow, else torch."""
+    if K.bmm_supported(a, b, trans_a, trans_b):
+        return K.bmm(a, b, trans_a, trans_b)
+    return torch.matmul(a.transpose(-1, -2) if trans_a else a, b.transpose(-1, -2) if trans_b else b)
+
+
 @register("BATCHMATMUL", "MATMUL")
 class BatchMatmulOp(OpImpl):
+    """Parity: batch_matmul_kernels.cu:66-123 (forward, dA = dC B^T, dB = A^T dC)."""
+
     def forward(self, ctx, inputs, weights):
         a, b = inputs
+        if a.dim() == b.dim() and a.dim() >= 3 and a.shape[:-2] == b.shape[:-2]:
+            return [_bmm(a.contiguous(), b.contiguous())], (a, b)
         return [torch.matmul(a, b)], (a, b)
 
     def backward(self, ctx, saved, grad_outputs, weight_grads, need_input_grad):
         a, b = saved
         d = grad_outputs[0]
+        if a.dim() == b.dim() and a.dim() >= 3 and a.shape[:-2] == b.shape[:-2]:
+            d = d.contiguous()
+            da = _bmm(d, b.contiguous(), trans_b=True) if need_input_grad[0] else None
+            db = _bmm(a.contiguous(), d, trans_a=True) if need_input_grad[1] else None
+            return [da, db]
         da = torch.matmul(d, b.transpose(-1, -2)) if need_input_grad[0] else None
         db = torch.matmul(a.transpose(-1, -2), d) if need_input_grad[1] else None
         return [da, db]

@@ -14,8 +14,10 @@ torch.mm / addmm) is the plain library GEMM.  ``FF_GEMM`` selects:
   persistent 256² kernel (``p:s``, csrc/kernels/gemmp.hip, fused bias /
   activation / pre-activation epilogue) and the one-wave-per-SIMD 128x128
   wave-tile kernel (``t:s``, csrc/kernels/gemmt.hip, same epilogues; ``u:s``
-  is the same kernel with B staged by LDS-DMA, ``w:s`` with both) at
-  several split-K degrees (the long-K weight-gradient GEMMs are where split-K
+  is the same kernel with B staged by LDS-DMA, ``w:s`` with both) and, for
+  products whose 256x256 tiles cannot fill the chip, the 64x64-tile MLP
+  kernel (``s:s``, csrc/kernels/gemms.hip, same epilogues) at several
+  split-K degrees (the long-K weight-gradient GEMMs are where split-K
   and gemmt win); the 256² LDS-DMA kernel only with FF_GEMM256=1;
 * ``hip``: always the MFMA kernel; ``blas``: always hipBLASLt.
 
@@ -186,6 +188,24 @@ def _gt(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1, variant=Non
                    splits=splits, variant=_GT_VARIANT if variant is None else variant)
 
 
+def _gs(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
+    """64x64-tile MLP GEMM (csrc/kernels/gemms.hip, gemmp variant 8)."""
+    return K.gemmp(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
+                   splits=splits, variant=8)
+
+
+def _gs_splits(M: int, N: int, Kd: int) -> List[int]:
+    """Split-K degrees that bring a 64x64-tile grid to about one or two
+    workgroups per CU (plain epilogue only; >= 2 K-tiles per split)."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    return sorted({s for s in (2, 4, 8, 16) if tiles * s <= 640 and Kd // 64 >= 2 * s})
+
+
+def _small_mn(M: int, N: int) -> bool:
+    """Products whose 256x256 tiles cannot fill the chip (DLRM's MLPs)."""
+    return ((M + 255) // 256) * ((N + 255) // 256) < 64
+
+
 def _gt_ok(bias, act, out, beta, pre) -> bool:
     """gemmt instantiates the activation epilogues for none / relu / gelu."""
     return _gp_ok(bias, act, out, beta, pre) and act in ("none", "relu", "gelu")
@@ -267,6 +287,11 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
             splits |= {s for s in pow2 if (Kd // 64) % s == 0}
             tiles = ((M + 255) // 256) * ((N + 255) // 256)
             tsplits |= pow2 | {s for s in (round(256 / tiles), round(512 / tiles)) if 2 <= s <= max(1, Kd // 512)}
+        if _small_mn(M, N) and os.environ.get("FF_GEMMS", "1") != "0":
+            c["s:1"] = _gs
+            if bias is None and act == "none" and pre is None:
+                for s in _gs_splits(M, N, Kd):
+                    c[f"s:{s}"] = (lambda s_: (lambda *args: _gs(*args, splits=s_)))(s)
         for s in sorted(splits):
             c[f"p:{s}"] = (lambda s_: (lambda *args: _gp(*args, splits=s_)))(s)
         for s in sorted(tsplits):
@@ -405,7 +430,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
         choice = "hip"
-    if choice[:2] in ("p:", "t:", "u:", "w:") and not K.gemmp_supported(a, b, trans_a, trans_b):
+    if choice[:2] in ("p:", "t:", "u:", "w:", "s:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -433,6 +458,8 @@ def _resolve(name: str):
         return lambda *args: _gt(*args, splits=int(arg), variant=4)
     if kind == "w":
         return lambda *args: _gt(*args, splits=int(arg), variant=6)
+    if kind == "s":
+        return lambda *args: _gs(*args, splits=int(arg))
     return lambda *args: _hip256(*args, splits=int(arg))
 
 

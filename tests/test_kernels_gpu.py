@@ -289,19 +289,22 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6], ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128",
-                                                              "wave128dma", "wave128pers", "wave128dma2"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8], ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128",
+                                                                 "wave128dma", "wave128pers", "wave128dma2", "tile64"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1),
                                             # more work items than CUs: the persistent kernels loop
                                             (4096, 4352, 128, 1), (2048, 2048, 1024, 8),
                                             # 17 K-tiles over 5 splits: gemmt's uneven split (4,4,3,3,3)
-                                            (512, 768, 1088, 5)])
+                                            (512, 768, 1088, 5),
+                                            # DLRM MLP shapes (one K-tile; a 64-wide output)
+                                            (1024, 512, 64, 1), (1024, 64, 512, 1)])
 def test_gemmp(ta, tb, M, N, Kd, splits, variant):
     """Phase-pipelined persistent GEMM (gemmp.hip; variant 1 = gemmq.hip on
     16x16x32 MFMAs, variant 2 = gemmr.hip ping-pong schedule, 3-6 = gemmt.hip
-    one wave per SIMD: register / B by LDS-DMA staging, persistent, both by LDS-DMA): plain / beta / split-K, the fused
+    one wave per SIMD: register / B by LDS-DMA staging, persistent, both by LDS-DMA; 8 = gemms.hip 64x64 tiles):
+    plain / beta / split-K, the fused
     bias+activation+pre-activation epilogue and the activation-gradient +
     bias-gradient epilogue, against fp32 torch."""
     import functools
@@ -334,7 +337,7 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
         torch.nn.functional.gelu(x, approximate="tanh").backward(torch.ones_like(x))
         gr = ref * x.grad
         assert _rel(g, gr) < 1e-2
-        if variant >= 3:   # gemmt sums the fp32 gradient (before its bf16 rounding)
+        if variant >= 3:   # gemmt / gemms sum the fp32 gradient (before its bf16 rounding)
             assert _rel(db, gr.sum(0) + 0.5) < 1e-3
         else:              # the other kernels sum the stored bf16 values
             assert _rel(db, g.float().sum(0) + 0.5) < 1e-4
@@ -352,3 +355,22 @@ def test_dropout_and_cast():
     f = torch.empty(x.numel(), device=DEV)
     K.cast_(x, f)
     assert torch.equal(f, x.float())
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("Z,M,N,Kd", [(12, 128, 64, 64), (3, 264, 136, 192), (2, 512, 512, 512)])
+def test_bmm(ta, tb, Z, M, N, Kd):
+    """Batched product on the 64x64-tile kernel (gemms.hip, blockIdx.z =
+    product), against fp32 torch; plain and beta-accumulate."""
+    torch.manual_seed(5)
+    a = torch.randn(Z, Kd, M, device=DEV, dtype=torch.bfloat16) if ta else torch.randn(Z, M, Kd, device=DEV,
+                                                                                       dtype=torch.bfloat16)
+    b = torch.randn(Z, N, Kd, device=DEV, dtype=torch.bfloat16) if tb else torch.randn(Z, Kd, N, device=DEV,
+                                                                                       dtype=torch.bfloat16)
+    assert K.bmm_supported(a, b, ta, tb)
+    ref = (a.float().transpose(-1, -2) if ta else a.float()) @ (b.float().transpose(-1, -2) if tb else b.float())
+    c = K.bmm(a, b, ta, tb)
+    assert _rel(c, ref) < 1e-2
+    acc = torch.ones(Z, M, N, device=DEV, dtype=torch.float32)
+    K.bmm(a, b, ta, tb, out=acc, beta=1.0)
+    assert _rel(acc, ref + 1) < 1e-2
