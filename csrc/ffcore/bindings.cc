@@ -86,6 +86,7 @@ PYBIND11_MODULE(_ffcore, m) {
       .def("num_elements", &TensorShape::num_elements)
       .def("size_bytes", &TensorShape::size_bytes)
       .def("to_json", [](const TensorShape& s) { return s.to_json().dump(); })
+      .def_static("from_json", [](const std::string& s) { return TensorShape::from_json(Json::parse(s)); })
       .def("__eq__", &TensorShape::operator==)
       .def("__hash__", [](const TensorShape& s) { return std::hash<TensorShape>()(s); })
       .def("__repr__", &TensorShape::str);
@@ -117,6 +118,7 @@ PYBIND11_MODULE(_ffcore, m) {
       .def("piece_shape", &ParallelTensorShape::piece_shape)
       .def("is_valid", &ParallelTensorShape::is_valid)
       .def("to_json", [](const ParallelTensorShape& s) { return s.to_json().dump(); })
+      .def_static("from_json", [](const std::string& s) { return ParallelTensorShape::from_json(Json::parse(s)); })
       .def("__eq__", &ParallelTensorShape::operator==)
       .def("__hash__", [](const ParallelTensorShape& s) { return std::hash<ParallelTensorShape>()(s); })
       .def("__repr__", &ParallelTensorShape::str);
@@ -232,6 +234,7 @@ PYBIND11_MODULE(_ffcore, m) {
       .def("uses", [](const ParallelComputationGraph& p, ValueRef v) { return p.g.uses(v); })
       .def("reinfer_shapes", &ParallelComputationGraph::reinfer_shapes)
       .def("structural_hash", &ParallelComputationGraph::structural_hash)
+      .def("structurally_equal", &ParallelComputationGraph::structurally_equal)
       .def("to_json", [](const ParallelComputationGraph& p) { return p.to_json().dump(); })
       .def_static("from_json",
                   [](const std::string& s) { return ParallelComputationGraph::from_json(Json::parse(s)); })

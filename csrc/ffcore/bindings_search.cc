@@ -462,6 +462,12 @@ void register_ext_bindings(py::module_& m) {
     auto subs = load_substitutions(Json::parse(s), &skipped);
     return py::make_tuple(subs, skipped);
   });
+  // value-semantics round trips (tests/test_ir_properties.py)
+  m.def("machine_view_roundtrip", [](const std::string& s) {
+    const MachineView v = MachineView::from_json(Json::parse(s));
+    return v.to_json().dump();
+  });
+  m.def("layer_config_roundtrip", [](const std::string& s) { return LayerConfig::from_json(Json::parse(s)).to_json().dump(); });
   m.def("substitution_from_json", [](const std::string& s) { return Substitution::from_json(Json::parse(s)); });
   m.def("load_legacy_rules", [](const std::string& s) { return load_legacy_rules(Json::parse(s)); });
 
