@@ -220,7 +220,11 @@ __device__ __forceinline__ bf16x8 tr16(const unsigned char* img, int ks, int o0,
 // output and / or beta != 0 (kept apart: its extra live registers in a shared
 // epilogue made the allocator shuttle accumulators through VGPRs in the loop)
 // kEpiBias: bf16 C = AB + bias (no activation, no pre-activation copy)
-enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3, kEpiGeneral = 4, kEpiBias = 5 };
+// kEpiAccum: bf16 C += AB (alpha 1, beta != 0: the input-gradient GEMMs that
+// accumulate into a residual branch's gradient) on the paired 16-B path, the
+// fp32 values exchanged before packing so the sum is rounded once
+enum Epi : int { kEpiPlain = 0, kEpiBiasAct = 1, kEpiDact = 2, kEpiSplit = 3, kEpiGeneral = 4, kEpiBias = 5,
+                 kEpiAccum = 6 };
 
 // one v_cvt_pk_bf16_f32 per pair (per-element casts pack through perm/alignbit)
 __device__ __forceinline__ unsigned pack2(float a, float b) {
@@ -254,6 +258,40 @@ __device__ __forceinline__ void store_row16(bf16* C, int64_t row_off, int ncol0,
       } else {
         *reinterpret_cast<uint4*>(C + row_off + n) = uint4{sx[0], sy[0], sx[1], sy[1]};
       }
+    }
+  }
+}
+
+// kEpiAccum store of one row block: per block pair (2j, 2j+1) four fp32
+// v_permlane16_swaps give lane row r 8 consecutive columns (the layout of
+// store_row16), then one 16-B read of C, fp32 adds and one 16-B store.
+__device__ __forceinline__ void accum_row16(bf16* C, int64_t row_off, int ncol0, int N, bool mok,
+                                            const f32x4t (&a)[8], float beta, int lane) {
+  const int r = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned s[4][2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto w = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[2 * j][e]), __float_as_uint(a[2 * j + 1][e]),
+                                                      false, false);
+      s[e][0] = w[0];
+      s[e][1] = w[1];
+    }
+    const int n = ncol0 + (2 * j + (r & 1)) * 16 + (r >> 1) * 8;
+    if (mok && n < N) {
+      uint4* p = reinterpret_cast<uint4*>(C + row_off + n);
+      const uint4 old = *p;
+      const unsigned ow[4] = {old.x, old.y, old.z, old.w};
+      unsigned nw[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // dword q holds columns 2q, 2q+1: elements (e = 2 (q & 1), +1) of swap half q >> 1
+        const int h = q >> 1, e0 = 2 * (q & 1);
+        const f32x2t v{__uint_as_float(s[e0][h]), __uint_as_float(s[e0 + 1][h])};
+        nw[q] = pack2v(v + beta * unpack2(ow[q]));
+      }
+      *p = uint4{nw[0], nw[1], nw[2], nw[3]};
     }
   }
 }
@@ -350,6 +388,10 @@ __device__ __forceinline__ void epilogue(const GemmTArgs& g, f32x4t (&acc)[8][8]
     // all 64 at the loop exit) keeps hipcc from permuting the AGPRs first
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[mb][j]));
+    if (EPI == kEpiAccum) {
+      accum_row16(static_cast<bf16*>(g.C), roff, ncol0, g.N, mok, acc[mb], g.beta, lane);
+      continue;
+    }
     uint2 ob[8], pb[8];
 #pragma unroll
     for (int nb = 0; nb < 8; ++nb) {
@@ -885,6 +927,7 @@ void launch_pers(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hi
     case kEpiGeneral * 8:
       hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiGeneral, 0>), grid, block, 0, st, g);
       break;
+    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiAccum, 0>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 0:
       hipLaunchKernelGGL((gemmt_pers_kernel<TA, TB, kEpiBiasAct, 0>), grid, block, 0, st, g);
       break;
@@ -929,6 +972,7 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
     case kEpiGeneral * 8:
       hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiGeneral, 0, S>), grid, block, 0, st, g);
       break;
+    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiAccum, 0, S>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 0:
       hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiBiasAct, 0, S>), grid, block, 0, st, g);
       break;
@@ -969,6 +1013,8 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
                   : p.act_bwd                       ? kEpiDact
                   : (p.bias && !p.pre && !p.act)    ? kEpiBias
                   : (p.bias || p.pre || p.act)      ? kEpiBiasAct
+                  : (!p.out_f32 && p.beta != 0.f && p.alpha == 1.f && !(p.dbg & 64) &&
+                     (reinterpret_cast<uintptr_t>(p.C) & 15) == 0 && p.ldc % 8 == 0) ? kEpiAccum
                   : (p.out_f32 || p.beta != 0.f || p.alpha != 1.f) ? kEpiGeneral
                                                                    : kEpiPlain;
   const int L = p.K / TK / splits;

@@ -322,6 +322,10 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
     c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
     gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
     assert _rel(c3, ref + 1) < 1e-2
+    # bf16 accumulate (gemmt: the paired 16-B read-modify-write epilogue)
+    c4 = torch.full((M, N), 0.5, device=DEV, dtype=torch.bfloat16)
+    gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c4, splits=splits)
+    assert _rel(c4, ref + 0.5) < 1e-2
     if splits == 1:
         bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
