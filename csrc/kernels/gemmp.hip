@@ -531,12 +531,16 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
       n = 256;
     return std::max(8, n);
   }();
+  if (p.variant == 9 && splits == 1 && gemmn_supported(p)) {
+    gemmn_launch(p, st);
+    return;
+  }
   if (p.variant == 8) {
     gemms_launch(p, splits, st);
     if (splits > 1) splitk_reduce(p.workspace, p.C, p.M, p.N, p.ldc, splits, p.beta, p.out_f32, st);
     return;
   }
-  if (p.variant >= 1 && p.variant <= 6) {
+  if ((p.variant >= 1 && p.variant <= 6) || p.variant == 9) {
     if (p.variant == 2 && small) gemmr_launch(p, splits, n_cu, st);
     else if (p.variant >= 3 && small && gemmt_supported(p))
       gemmt_launch(p, splits, p.variant - 3, st);

@@ -137,7 +137,8 @@ struct GemmPParams {
   int variant = 0;              // 0: 32x32x16 MFMA (gemmp.hip), 1: 16x16x32 (gemmq.hip), 2: ping-pong (gemmr.hip), 5: persistent gemmt, 6: gemmt with both operands by LDS-DMA,
                                 // 3 / 4: one wave per SIMD, 128x128 wave tile, B staged
                                 // through registers / by LDS-DMA (gemmt.hip),
-                                // 8: 64x64 tiles for MLP-sized products (gemms.hip)
+                                // 8: 64x64 tiles for MLP-sized products (gemms.hip),
+                                // 9: eight-wave multistage NT kernel (gemmn.hip; other layouts -> gemmq)
 };
 bool gemmp_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b);
 void gemmp_bf16(const GemmPParams& p, hipStream_t st);
@@ -145,6 +146,9 @@ void gemmq_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
 void gemmr_launch(const GemmPParams& p, int splits, int n_cu, hipStream_t st);
 void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t st);
 bool gemmt_supported(const GemmPParams& p);
+// eight-wave multistage NT GEMM, variant 9 (gemmn.hip)
+bool gemmn_supported(const GemmPParams& p);
+void gemmn_launch(const GemmPParams& p, hipStream_t st);
 // small-tile (64 x 64) MLP GEMM, variant 8 (gemms.hip)
 bool gemms_supported(const GemmPParams& p);
 void gemms_launch(const GemmPParams& p, int splits, hipStream_t st);

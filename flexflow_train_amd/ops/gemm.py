@@ -287,6 +287,9 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
             splits |= {s for s in pow2 if (Kd // 64) % s == 0}
             tiles = ((M + 255) // 256) * ((N + 255) // 256)
             tsplits |= pow2 | {s for s in (round(256 / tiles), round(512 / tiles)) if 2 <= s <= max(1, Kd // 512)}
+        if trans_b and not trans_a and bias is None and act == "none" and pre is None \
+                and os.environ.get("FF_GEMMN", "1") != "0":
+            c["n:1"] = lambda *args: _gt(*args, splits=1, variant=9)
         if _small_mn(M, N) and os.environ.get("FF_GEMMS", "1") != "0":
             c["s:1"] = _gs
             if bias is None and act == "none" and pre is None:
@@ -430,7 +433,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
         choice = "hip"
-    if choice[:2] in ("p:", "t:", "u:", "w:", "s:") and not K.gemmp_supported(a, b, trans_a, trans_b):
+    if choice[:2] in ("p:", "t:", "u:", "w:", "s:", "n:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -460,6 +463,8 @@ def _resolve(name: str):
         return lambda *args: _gt(*args, splits=int(arg), variant=6)
     if kind == "s":
         return lambda *args: _gs(*args, splits=int(arg))
+    if kind == "n":
+        return lambda *args: _gt(*args, splits=1, variant=9)
     return lambda *args: _hip256(*args, splits=int(arg))
 
 

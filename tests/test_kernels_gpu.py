@@ -289,8 +289,9 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8], ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128",
-                                                                 "wave128dma", "wave128pers", "wave128dma2", "tile64"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9],
+                         ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128", "wave128dma", "wave128pers",
+                              "wave128dma2", "tile64", "nt8wave"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1),
