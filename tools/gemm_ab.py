@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from flexflow_train_amd import kernels as K  # noqa: E402
 
-T, H, F, V = 16384, 1024, 4096, 30528
+T, H, F, V = 32768, 1024, 4096, 30528   # BERT-large, 64 x 512 tokens per GPU
 
 
 def shapes(only):
@@ -65,8 +65,11 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="fwd,dx,dw")
     ap.add_argument("--shapes", default="")
-    ap.add_argument("--cands", default="", help="comma list of candidate prefixes (blaslt,p,q,r,t)")
+    ap.add_argument("--cands", default="", help="comma list of candidate prefixes (blaslt,p,q,r,t,u,v,w,n)")
+    ap.add_argument("--tokens", type=int, default=T)
+    ap.add_argument("--beta", type=float, default=0.0, help="accumulate into C (bf16 out): C = AB + beta C")
     args = ap.parse_args()
+    globals()["T"] = args.tokens
     dev = "cuda"
     only = set(args.only.split(","))
     for name, kind, kin, nout in shapes(only):
@@ -76,23 +79,26 @@ def main():
         M, N = (a.shape[1] if ta else a.shape[0]), (b.shape[0] if tb else b.shape[1])
         Kd = a.shape[0] if ta else a.shape[1]
         ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
-        cands = {"blaslt": lambda o: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=o)}
+        bt = args.beta
+        cands = {"blaslt": lambda o: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt)}
         splits = [1] if kind != "dw" else [2, 4, 8]
+        variants = {"p": 0, "q": 1, "r": 2, "t": 3, "u": 4, "v": 5, "w": 6}
         for sp in splits:
-            cands[f"p{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp)
-            cands[f"q{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=1)
-            cands[f"r{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=2)
-            cands[f"t{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=3)
-            cands[f"u{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=4)
-            cands[f"v{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=5)
-            cands[f"w{sp}"] = lambda o, sp=sp: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, splits=sp, variant=6)
+            for pre, var in variants.items():
+                cands[f"{pre}{sp}"] = (lambda o, sp=sp, var=var:
+                                       K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt, splits=sp, variant=var))
+        if tb and not ta:   # the eight-wave NT kernel (gemmn.hip)
+            cands["n1"] = lambda o: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt, variant=9)
         if args.cands:
             keep = args.cands.split(",")
             cands = {k: v for k, v in cands.items() if k == "blaslt" and "blaslt" in keep
                      or k != "blaslt" and k.rstrip("0123456789") in keep}
+        if bt:
+            ref = ref + bt * 0.5   # outputs start at 0.5 below
         outs = {k: torch.empty(M, N, device=dev, dtype=torch.bfloat16) for k in cands}
         err = {}
         for k, f in cands.items():
+            outs[k].fill_(0.5)
             f(outs[k])
             torch.cuda.synchronize()
             err[k] = ((outs[k].float() - ref).abs().max() / ref.abs().max()).item()
