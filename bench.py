@@ -159,7 +159,7 @@ def _release(res):
     """Drop a finished run's model, executor and captured graphs before the
     next one (the DP reference) allocates its own."""
     import torch
-    for k in ("model", "ex", "step"):
+    for k in ("model", "ex", "step", "feeds", "labels"):
         res.pop(k, None)
     gc.collect()
     if torch.cuda.is_available():
@@ -275,7 +275,7 @@ def _run_bert(args, world, rank, only_dp: bool):
         prof = {k: round(v, 3) for k, v in list(ex.profile_report().items())[:40]}
     return {"value": t["value"], "ms": t["ms"], "config": conf, "search": dict(model.search_report),
             "data": "synthetic token ids, random-init weights", "model": model, "ex": ex, "step": t["step"],
-            "profile": prof}
+            "profile": prof, "feeds": feeds, "labels": labels}
 
 
 def _parallelism(model, world: int) -> str:
@@ -375,7 +375,7 @@ def _run_zoo(args, world, rank, only_dp: bool):
         prof = {k: round(v, 3) for k, v in list(ex.profile_report().items())[:40]}
     return {"value": t["value"], "ms": t["ms"], "config": conf, "search": dict(model.search_report),
             "data": "synthetic inputs of the model's shape, random-init weights", "model": model, "ex": ex,
-            "step": t["step"], "profile": prof}
+            "step": t["step"], "profile": prof, "feeds": feeds, "labels": labels}
 
 
 if __name__ == "__main__":

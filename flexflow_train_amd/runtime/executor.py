@@ -1483,7 +1483,10 @@ class Executor:
 
     def train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
         self.forward(feeds, training=True)
+        prof = self.cfg.profiling
+        t0 = self.tracer.begin("__loss__:fwd", "compute", self.step_num) if prof else None
         g = self.compute_loss(labels)
+        self.tracer.end(t0)
         self._overlap_lr = (True, lr)
         self._defer_grad_wait = True
         try:
@@ -1491,7 +1494,9 @@ class Executor:
         finally:
             self._overlap_lr = None
             self._defer_grad_wait = False
+        t0 = self.tracer.begin("__update__:fwd", "compute", self.step_num) if prof else None
         self.update(lr)
+        self.tracer.end(t0)
 
     def _overlap_flats(self) -> List[dict]:
         """Flats whose buckets may be updated during the backward pass: one

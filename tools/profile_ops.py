@@ -44,6 +44,65 @@ def uniform_strategies(cg, world):
     return out
 
 
+def in_situ(model_name: str, out_path: str, rounds: int = 3, batch_per_gpu: int = 0):
+    """Per-operator costs measured INSIDE the bench's own data-parallel
+    training step on one GPU: the executor's fused kernels (add + LayerNorm,
+    softmax + cross-entropy, conv -> BN statistics, BN + add + ReLU, GEMM
+    epilogues) are timed as they run, an operator fused into another costs 0,
+    and the fused loss is charged to the trailing softmax.  Each profiled step
+    is queued behind a device busy-wait so the host runs ahead and the event
+    spans measure device time only.  Keys are the cost model's op signatures
+    (the same ones ``build_profile_table`` writes)."""
+    import collections
+    import types
+
+    import bench
+    from flexflow_train_amd.ops.gemm import _gpu_busy
+
+    args = types.SimpleNamespace(gpus=1, steps=2, warmup=3, batch_per_gpu=batch_per_gpu, seq=512, model=model_name,
+                                 layers=None, strategy="dp", no_dp_compare=True, budget=0, gemm="auto", profile=True,
+                                 graph=0)
+    runner = bench._run_bert if model_name.startswith("bert") else bench._run_zoo
+    res = runner(args, 1, 0, only_dp=True)
+    ex, model = res["ex"], res["model"]
+    feeds, labels = res["feeds"], res["labels"]
+    per = collections.defaultdict(float)
+    for _ in range(rounds):
+        ex.tracer.clear()
+        torch.cuda.synchronize()
+        _gpu_busy(400.0)
+        ex.train_step(feeds, labels)
+        for name, _cat, _st, _s, dur in ex.tracer._resolved():
+            per[name] += dur / rounds
+    pcg = model.pcg
+    fused_softmax = getattr(ex, "softmax_fused_step", None)
+    sums = collections.defaultdict(lambda: [0.0, 0.0, 0])
+    for n in pcg.topo_order():
+        op = pcg.layer_op(n)
+        if op.op_type in ("INPUT", "WEIGHT", "NOOP") or pcg.is_weight_path(n) or C.is_parallel_op(op.type):
+            continue
+        nm = pcg.layer_name(n)
+        ins = [pcg.shape(v).piece_shape() for v in pcg.layer_data_inputs(n)]
+        outs = [pcg.shape(C.ValueRef(n, k)).piece_shape() for k in range(pcg.num_outputs(n))]
+        sig = C.CostModel.signature(op, ins + outs)
+        f, b = per.get(f"{nm}:fwd", 0.0), per.get(f"{nm}:bwd", 0.0)
+        if fused_softmax is not None and nm == fused_softmax.name:
+            f += per.get("__loss__:fwd", 0.0)
+        e = sums[sig]
+        e[0] += f
+        e[1] += b
+        e[2] += 1
+    table = {sig: {"fwd_ms": round(f / k, 5), "bwd_ms": round(b / k, 5), "source": "in_situ"}
+             for sig, (f, b, k) in sums.items()}
+    with open(out_path, "w") as fh:
+        json.dump(table, fh, indent=0, sort_keys=True)
+    total = sum(v for k, v in per.items() if not k.startswith("__"))
+    print(json.dumps({"model": model_name, "entries": len(table), "op_ms": round(total, 3),
+                      "loss_ms": round(per.get("__loss__:fwd", 0.0), 3),
+                      "update_ms": round(per.get("__update__:fwd", 0.0), 3),
+                      "bench_ms_per_step": round(res["ms"], 3)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="bert-large",
@@ -52,7 +111,11 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: bench.py's per-GPU batch")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--in-situ", action="store_true",
+                    help="time every operator inside the bench's own 1-GPU training step (fusions included)")
     args = ap.parse_args()
+    if args.in_situ:
+        return in_situ(args.model, args.out, batch_per_gpu=args.batch_per_gpu)
     m = FFModel(FFConfig())
     if args.model in ("bert-large", "bert-base"):
         from flexflow_train_amd.models.bert import bert_base, bert_large, build_bert

@@ -64,16 +64,20 @@ def calibrate(calib_dir, names, out_path=None):
     bench) on top of the committed ones; measured: ``bench_<config>.json``
     (bench.py --strategy dp) in the same directory."""
     from flexflow_train_amd.search import native
-    tables = sorted(os.path.join(calib_dir, f) for f in os.listdir(calib_dir)
-                    if f.startswith("op_costs_") and f.endswith(".json"))
-    os.environ["FF_PROFILE_TABLE"] = os.pathsep.join(tables)
+    # standalone per-op tables first, in-situ tables (op_costs_*_insitu*.json)
+    # last so their entries win
+    tables = sorted((os.path.join(calib_dir, f) for f in os.listdir(calib_dir)
+                     if f.startswith("op_costs_") and f.endswith(".json")), key=lambda p: ("insitu" in p, p))
     rows = []
     for name in names:
         build, bpg, upd, sparse = CALIB[name]
         m = FFModel(FFConfig())
         build(m, bpg)
         pcg = C.data_parallel_pcg(m.cg, 1)
-        cm = native.cost_model(world=1)
+        cm = native.cost_model(world=1, use_profiles=False)
+        for t in tables:
+            with open(t) as fh:
+                cm.load_profiles(fh.read())
         sim = native.simulate(pcg, cm, 1, update_bytes_per_param=upd, sparse_embedding_update=sparse)
         measured = None
         bpath = os.path.join(calib_dir, f"bench_{name}.json")
