@@ -318,6 +318,160 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
 }
 
 // ===========================================================================
+// Forward, software-pipelined across K/V tiles (FFK_ATTN_FWD_PIPE=1): the
+// scores of tile t+1 (S MFMAs) are computed while tile t's softmax runs on
+// the VALU, and tile t's P.V MFMAs follow, so inside ONE wave the matrix cores
+// and the VALU work on different tiles instead of waiting for each other
+// (guide "sm-split"; with one barrier per tile the two waves of a SIMD run in
+// phase, so the overlap has to come from within the wave).  K leads V by one
+// tile in the LDS ring: during iteration t a buffer holds {K(t+1), V(t)}.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(AttnParams P) {
+  constexpr int KS = D / 16, DT = D / 32, KV = 64;
+  constexpr int TILE_BYTES = KV * D * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];  // [K V] x 2
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int bh = CAUSAL ? blockIdx.x : blockIdx.y, b = bh / P.H, hh = bh % P.H;
+  const int q_blk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.x) * 128;
+  const int qw = q_blk + wave * 32;
+  const int q = qw + (lane & 31);
+  const bool q_ok = q < P.Sq;
+
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    qf[ks] = q_ok ? *reinterpret_cast<const bf16x8*>(P.q.p + b * P.q.sb + static_cast<int64_t>(q) * P.q.ss +
+                                                     hh * P.q.sh + ks * 16 + 8 * h)
+                  : bf16x8{};
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+
+  int n_tiles = (P.Sk + KV - 1) / KV;
+  if (CAUSAL) n_tiles = min(n_tiles, (q_blk + 128 + KV - 1) / KV);
+  auto active = [&](int t) { return t < n_tiles && (!CAUSAL || t * KV <= qw + 31); };
+
+  auto scores = [&](const unsigned char* Kt, f32x16 (&s)[2]) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        s[kt] = mfma32(lds_read16(Kt, lds_off<D>(kt * 32 + (lane & 31), 2 * ks + h)), qf[ks], s[kt]);
+    }
+  };
+
+  TileLoader<D, KV> kl, vl;
+  // prologue: K(0) -> buffer 1's K slot (free until iteration 0 ends), K(1) and
+  // V(0) -> buffer 0
+  kl.load(P.k, b, hh, 0, P.Sk);
+  kl.store(smem + 2 * TILE_BYTES);
+  if (n_tiles > 1) kl.load(P.k, b, hh, KV, P.Sk);
+  vl.load(P.v, b, hh, 0, P.Sk);
+  if (n_tiles > 1) kl.store(smem);
+  vl.store(smem + TILE_BYTES);
+  __syncthreads();
+  f32x16 sa[2], sb[2];
+  if (active(0)) scores(smem + 2 * TILE_BYTES, sa);
+  __syncthreads();   // every wave read K(0) before iteration 0 restages buffer 1
+
+  // one tile: softmax(t) on `sc` (+ S(t+1) into `sn` from the current buffer),
+  // then O += V(t)^T P(t)
+  auto step = [&](int t, f32x16 (&sc)[2], f32x16 (&sn)[2]) {
+    const int k0 = t * KV;
+    const unsigned char* buf = smem + (t & 1) * 2 * TILE_BYTES;
+    const unsigned char* Kn = buf;                 // K(t+1)
+    const unsigned char* Vt = buf + TILE_BYTES;    // V(t)
+    const bool more_k = t + 2 < n_tiles, more_v = t + 1 < n_tiles;
+    if (more_k) kl.load(P.k, b, hh, k0 + 2 * KV, P.Sk);
+    if (more_v) vl.load(P.v, b, hh, k0 + KV, P.Sk);
+    const bool act = active(t);
+    // S(t+1): independent of this tile's softmax — the scheduler interleaves
+    // its MFMAs with the VALU work below
+    if (active(t + 1)) scores(Kn, sn);
+    if (act) {
+      const bool need_mask = (k0 + KV > P.Sk) || (CAUSAL && k0 + KV - 1 > qw);
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (key >= P.Sk || (CAUSAL && key > q)) sc[kt][r] = -INFINITY;
+          }
+      }
+      float t0 = fmax3(sc[0][0], sc[0][1], sc[0][2]);
+      float t1 = fmax3(sc[1][0], sc[1][1], sc[1][2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) {
+        t0 = fmax3(t0, sc[0][r], sc[0][r + 1]);
+        t1 = fmax3(t1, sc[1][r], sc[1][r + 1]);
+      }
+      float tmax = fmax3(fmax3(t0, sc[0][15], sc[1][15]), t1, t1);
+      const float tother = __shfl_xor(tmax, 32, 64);
+      tmax = fmax3(tmax, tother, tother);
+      if (__any(tmax > m + 8.f * P.inv_scale_log2)) {
+        const float m_new = fmaxf(m, tmax);
+        const float alpha = (m_new == -INFINITY) ? 1.f : fexp2((m - m_new) * P.scale_log2);
+        m = m_new;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      }
+      const float mc = (m == -INFINITY) ? 0.f : m * P.scale_log2;
+      float psum[2] = {0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fexp2(fmaf(sc[kt][r], P.scale_log2, -mc));
+          sc[kt][r] = pv;
+          psum[kt] += pv;
+        }
+      l += psum[0] + psum[1];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pf = acc_to_frag(sc[kt], st);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(tr_frag<D>(Vt, kt * 32 + 16 * st, dt, lane), pf, o[dt]);
+        }
+    }
+    unsigned char* nb = smem + ((t + 1) & 1) * 2 * TILE_BYTES;
+    if (more_k) kl.store(nb);
+    if (more_v) vl.store(nb + TILE_BYTES);
+    __syncthreads();
+  };
+
+  int t = 0;
+  for (; t + 1 < n_tiles; t += 2) {
+    step(t, sa, sb);
+    step(t + 1, sb, sa);
+  }
+  if (t < n_tiles) step(t, sa, sb);
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (q_ok) {
+    bf16* orow = P.o_out + b * P.o_sb + static_cast<int64_t>(q) * P.o_ss + hh * P.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * g4 + e] * inv);
+        *reinterpret_cast<bf16x4*>(orow + dt * 32 + 8 * g4 + 4 * h) = v;
+      }
+    if (h == 0) P.lse[static_cast<int64_t>(bh) * P.Sq + q] = (lt > 0.f) ? m * P.scale_log2 + log2f(lt) : -INFINITY;
+  }
+}
+
+// ===========================================================================
 // Backward preprocessing: delta[b,h,q] = sum_d dO[q][d] * O[q][d]
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams P) {
@@ -758,6 +912,15 @@ void attention_fwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, fl
   AttnParams P = make_params(t, B, H, Sq, Sk, D, scale);
   const unsigned nq = static_cast<unsigned>((Sq + 127) / 128), nbh = static_cast<unsigned>(B * H);
   dim3 grid = causal ? dim3(nbh, nq) : dim3(nq, nbh), block(256);
+  // read per call (not cached): the A/B tests switch it inside one process
+  const char* pe = getenv("FFK_ATTN_FWD_PIPE");
+  const int pipe = pe ? atoi(pe) : 0;
+  if (pipe && D == 64) {
+    if (causal) hipLaunchKernelGGL((attn_fwd_pipe_kernel<64, true>), grid, block, 0, st, P);
+    else hipLaunchKernelGGL((attn_fwd_pipe_kernel<64, false>), grid, block, 0, st, P);
+    FFK_LAUNCH_CHECK("attention_fwd");
+    return;
+  }
   if (D == 64) {
     if (causal) hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, block, 0, st, P);
     else hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, block, 0, st, P);

@@ -212,6 +212,27 @@ def test_attention_fwd_bwd(causal, D, S, dbias_atomic):
         assert err < 3e-2 * scale, ("dbias", i, float(err), float(scale))
 
 
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("S", [512, 320, 64, 100])
+def test_attention_fwd_pipelined(causal, S, monkeypatch):
+    """The software-pipelined forward (FFK_ATTN_FWD_PIPE=1: S of tile t+1 beside
+    tile t's softmax, K one tile ahead of V) matches the default kernel and
+    fp32 torch, including one- and two-tile sequences and ragged ends."""
+    torch.manual_seed(9)
+    B, H, D = 2, 4, 64
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    monkeypatch.setenv("FFK_ATTN_FWD_PIPE", "0")
+    o0, lse0 = K.attention_fwd(q, k, v, causal=causal)
+    monkeypatch.setenv("FFK_ATTN_FWD_PIPE", "1")
+    o1, lse1 = K.attention_fwd(q, k, v, causal=causal)
+    torch.cuda.synchronize()
+    ref = _ref_attn(q.float(), k.float(), v.float(), causal)
+    assert _rel(o1, ref) < 2e-2, _rel(o1, ref)
+    assert _rel(o1, o0) < 1e-2
+    assert torch.allclose(lse1, lse0, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd", [(512, 1024, 768), (304, 136, 200), (1024, 4096, 1024)])
 def test_gemm(ta, tb, M, N, Kd):

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 from flexflow_train_amd import kernels as K  # noqa: E402
 
-SHAPES = {"bert-large": (32, 512, 16, 64, False), "gpt3-medium": (8, 2048, 16, 64, True)}
+SHAPES = {"bert-large": (64, 512, 16, 64, False), "gpt3-medium": (16, 2048, 16, 64, True)}   # bench batches
 
 
 def _time(fn, iters):
@@ -30,7 +30,30 @@ def _time(fn, iters):
     return a.elapsed_time(b) / iters
 
 
+def pipe_ab(iters, rounds=5):
+    """Interleaved same-process A/B of the forward: FFK_ATTN_FWD_PIPE 0 vs 1."""
+    import statistics
+    for name, (B, S, H, D, causal) in SHAPES.items():
+        g = torch.Generator(device="cuda").manual_seed(0)
+        qkv = torch.randn(B, S, 3, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        o, _ = K.attention_fwd(q, k, v, causal=causal)
+        t = {0: [], 1: []}
+        for _ in range(rounds):
+            for p in (0, 1):
+                os.environ["FFK_ATTN_FWD_PIPE"] = str(p)
+                t[p].append(_time(lambda: K.attention_fwd(q, k, v, causal=causal, out=o), iters))
+        fl = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+        med = {p: statistics.median(v) for p, v in t.items()}
+        print(json.dumps({"shape": name, "fwd_ms_default": round(med[0], 4), "fwd_ms_pipe": round(med[1], 4),
+                          "tflops_default": round(fl / med[0] / 1e9, 1), "tflops_pipe": round(fl / med[1] / 1e9, 1)}),
+              flush=True)
+    os.environ.pop("FFK_ATTN_FWD_PIPE", None)
+
+
 def main():
+    if "--pipe-ab" in sys.argv:
+        return pipe_ab(50)
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     for name, (B, S, H, D, causal) in SHAPES.items():
         g = torch.Generator(device="cuda").manual_seed(0)
