@@ -21,9 +21,10 @@
 //  * LDS images are XOR-swizzled per row so ds_read_b128 row reads are
 //    conflict-free; V^T (and K^T / Q^T / dO^T in the backward) operands come
 //    from ds_read_b64_tr_b16 hardware-transposed reads of the same images.
-//  * backward = dK/dV kernel (key block resident, loops over query tiles,
-//    key on the lane) + dQ kernel (query block resident) -> no float atomics,
-//    deterministic, no [N, N] buffers; delta = rowsum(dO*O) precomputed.
+//  * backward = dQ kernel (query block resident; also computes delta =
+//    rowsum(dO*O) for its queries) then dK/dV kernel (key block resident,
+//    loops over query tiles, key on the lane) -> no float atomics,
+//    deterministic, no [N, N] buffers.
 //
 // Tensor addressing: every tensor is [B, S, H, D] with arbitrary strides for
 // b / s / h and contiguous d, so the fused QKV projection output
@@ -504,7 +505,11 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnParams P) {
 // registers on top and spilled at 168 — a scratch reload inside the loop is a
 // VMEM op, and its vmcnt wait drained the next K / V tile's prefetch every
 // iteration — so the causal form runs 2 waves per SIMD without spills
-template <int D, bool CAUSAL>
+// FUSED_DELTA: delta = rowsum(dO * O) of the block's own queries is computed
+// here from the dO fragments already in registers (plus one 16-B O load per
+// fragment) and written out for the dK / dV kernel, which then runs AFTER
+// this one — the separate delta pass (a full re-read of dO and O) goes away.
+template <int D, bool CAUSAL, bool FUSED_DELTA = false>
 __global__ __launch_bounds__(256, (D == 64 ? (CAUSAL ? 2 : 3) : 1)) void attn_bwd_dq_kernel(AttnParams P) {
   constexpr int KS = D / 16, DT = D / 32, KV = 64;
   constexpr int TILE_BYTES = KV * D * 2;
@@ -528,7 +533,25 @@ __global__ __launch_bounds__(256, (D == 64 ? (CAUSAL ? 2 : 3) : 1)) void attn_bw
                   : bf16x8{};
   }
   const float lse = q_ok ? P.lse[static_cast<int64_t>(bh) * P.Sq + q] : 0.f;
-  const float dlt = q_ok ? P.delta[static_cast<int64_t>(bh) * P.Sq + q] : 0.f;
+  float dlt;
+  if constexpr (FUSED_DELTA) {
+    // lane (q, h) holds d = 16 ks + 8 h .. +8 of dO row q: a partial dot over
+    // those, then the other half from lane ^ 32
+    float part = 0.f;
+    if (q_ok) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 of = *reinterpret_cast<const bf16x8*>(P.o.p + b * P.o.sb + static_cast<int64_t>(q) * P.o.ss +
+                                                           hh * P.o.sh + ks * 16 + 8 * h);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part += bf2f(of[e]) * bf2f(df[ks][e]);
+      }
+    }
+    dlt = part + __shfl_xor(part, 32, 64);
+    if (q_ok && h == 0) P.delta[static_cast<int64_t>(bh) * P.Sq + q] = dlt;
+  } else {
+    dlt = q_ok ? P.delta[static_cast<int64_t>(bh) * P.Sq + q] : 0.f;
+  }
 
   f32x16 dq[DT];
 #pragma unroll
@@ -971,10 +994,18 @@ void attention_bwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, fl
   const unsigned nq = static_cast<unsigned>((Sq + 127) / 128), nbh = static_cast<unsigned>(B * H);
   const unsigned nk = static_cast<unsigned>((Sk + 128 * nkt - 1) / (128 * nkt));
   dim3 gq = causal ? dim3(nbh, nq) : dim3(nq, nbh), gk = causal ? dim3(nbh, nk) : dim3(nk, nbh), block(256);
+  // read per call: the A/B tool switches it inside one process
+  const char* fde = getenv("FFK_ATTN_BWD_FUSED_DELTA");
+  const bool fused_delta = fde ? atoi(fde) != 0 : true;
 #define FFK_ATTN_BWD(DD, CC)                                                          \
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<DD>), gd, block, 0, st, P);               \
-  launch_dkdv<DD, CC>(nkt, gk, block, st, P);                                         \
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, CC>), gq, block, 0, st, P)
+  if (fused_delta) {                                                                  \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, CC, true>), gq, block, 0, st, P);      \
+    launch_dkdv<DD, CC>(nkt, gk, block, st, P);                                       \
+  } else {                                                                            \
+    hipLaunchKernelGGL((attn_bwd_delta_kernel<DD>), gd, block, 0, st, P);             \
+    launch_dkdv<DD, CC>(nkt, gk, block, st, P);                                       \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, CC>), gq, block, 0, st, P);            \
+  }
   if (D == 64) {
     if (causal) { FFK_ATTN_BWD(64, true); }
     else { FFK_ATTN_BWD(64, false); }

@@ -63,16 +63,21 @@ def cost_model(ffconfig=None, world: Optional[int] = None, use_profiles: bool = 
     """Analytic MI355X model + measured op costs.  Tables: ``FF_PROFILE_TABLE``
     (os.pathsep-separated), ``ffconfig.profile_table_file``, and every
     committed ``profiles/op_costs_*.json`` (keys are exact op/piece
-    signatures, so tables for different models/worlds merge safely)."""
+    signatures, so tables for different models/worlds merge safely; where
+    two tables hold the same key the later one in the order below wins)."""
     cm = C.CostModel(machine_spec(ffconfig, world))
     if not use_profiles or os.environ.get("FF_NO_PROFILE_TABLES"):
         return cm
-    paths = [p for p in os.environ.get("FF_PROFILE_TABLE", "").split(os.pathsep) if p]
+    # later tables override earlier entries: committed standalone tables, then
+    # committed in-situ ones (measured inside the fused training step), then
+    # the tables the user named
+    paths = []
+    if os.path.isdir(PROFILE_DIR):
+        paths += sorted((os.path.join(PROFILE_DIR, f) for f in os.listdir(PROFILE_DIR)
+                         if f.startswith("op_costs_") and f.endswith(".json")), key=lambda p: ("insitu" in p, p))
+    paths += [p for p in os.environ.get("FF_PROFILE_TABLE", "").split(os.pathsep) if p]
     if ffconfig is not None and getattr(ffconfig, "profile_table_file", ""):
         paths.append(ffconfig.profile_table_file)
-    if os.path.isdir(PROFILE_DIR):
-        paths += sorted(os.path.join(PROFILE_DIR, f) for f in os.listdir(PROFILE_DIR)
-                        if f.startswith("op_costs_") and f.endswith(".json"))
     for path in paths:
         if os.path.exists(path):
             with open(path) as f:

@@ -233,6 +233,31 @@ def test_attention_fwd_pipelined(causal, S, monkeypatch):
     assert torch.allclose(lse1, lse0, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("D,S", [(64, 512), (64, 200), (128, 320)])
+def test_attention_bwd_fused_delta(causal, D, S, monkeypatch):
+    """delta = rowsum(dO * O) computed inside the dQ kernel (default) gives the
+    same gradients as the separate delta pass (FFK_ATTN_BWD_FUSED_DELTA=0)."""
+    torch.manual_seed(10)
+    B, H = 2, 4
+    qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    o, lse = K.attention_fwd(q, k, v, causal=causal)
+    do = torch.randn_like(o)
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("FFK_ATTN_BWD_FUSED_DELTA", fused)
+        dqkv = torch.empty_like(qkv)
+        K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal)
+        torch.cuda.synchronize()
+        outs.append(dqkv.float())
+    for i, name in enumerate(("dQ", "dK", "dV")):
+        assert _rel(outs[1][:, :, i], outs[0][:, :, i]) < 2e-3, name
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    _ref_attn(qf, kf, vf, causal).backward(do.float())
+    assert _rel(outs[1][:, :, 0], qf.grad) < 3e-2
+
+
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd", [(512, 1024, 768), (304, 136, 200), (1024, 4096, 1024)])
 def test_gemm(ta, tb, M, N, Kd):

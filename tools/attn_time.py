@@ -4,6 +4,7 @@ and GPT-3-medium shapes; FF_PKG_ROOT selects the package tree (same-box A/B of
 two builds: FF_PKG_ROOT=ab_prev python tools/attn_time.py).
 
     python tools/attn_time.py [iters]
+    python tools/attn_time.py --pipe-ab | --delta-ab   (same-process A/B of a kernel switch)
 """
 import json
 import os
@@ -30,30 +31,40 @@ def _time(fn, iters):
     return a.elapsed_time(b) / iters
 
 
-def pipe_ab(iters, rounds=5):
-    """Interleaved same-process A/B of the forward: FFK_ATTN_FWD_PIPE 0 vs 1."""
+def env_ab(var, which, iters, rounds=5):
+    """Interleaved same-process A/B of one kernel switch (env `var` 0 vs 1,
+    read per launch by attention.hip) on the forward or the backward."""
     import statistics
     for name, (B, S, H, D, causal) in SHAPES.items():
         g = torch.Generator(device="cuda").manual_seed(0)
         qkv = torch.randn(B, S, 3, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        o, _ = K.attention_fwd(q, k, v, causal=causal)
+        do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+        dqkv = torch.empty_like(qkv)
+        o, lse = K.attention_fwd(q, k, v, causal=causal)
+        if which == "fwd":
+            fn = lambda: K.attention_fwd(q, k, v, causal=causal, out=o)  # noqa: E731
+        else:
+            fn = lambda: K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1],  # noqa: E731
+                                         dqkv[:, :, 2], causal=causal)
         t = {0: [], 1: []}
         for _ in range(rounds):
             for p in (0, 1):
-                os.environ["FFK_ATTN_FWD_PIPE"] = str(p)
-                t[p].append(_time(lambda: K.attention_fwd(q, k, v, causal=causal, out=o), iters))
-        fl = 4 * B * H * S * S * D * (0.5 if causal else 1.0)
+                os.environ[var] = str(p)
+                t[p].append(_time(fn, iters))
+        fl = 4 * B * H * S * S * D * (0.5 if causal else 1.0) * (1.0 if which == "fwd" else 2.5)
         med = {p: statistics.median(v) for p, v in t.items()}
-        print(json.dumps({"shape": name, "fwd_ms_default": round(med[0], 4), "fwd_ms_pipe": round(med[1], 4),
-                          "tflops_default": round(fl / med[0] / 1e9, 1), "tflops_pipe": round(fl / med[1] / 1e9, 1)}),
-              flush=True)
-    os.environ.pop("FFK_ATTN_FWD_PIPE", None)
+        print(json.dumps({"shape": name, "switch": var, "pass": which, "ms_0": round(med[0], 4),
+                          "ms_1": round(med[1], 4), "tflops_0": round(fl / med[0] / 1e9, 1),
+                          "tflops_1": round(fl / med[1] / 1e9, 1)}), flush=True)
+    os.environ.pop(var, None)
 
 
 def main():
-    if "--pipe-ab" in sys.argv:
-        return pipe_ab(50)
+    if "--pipe-ab" in sys.argv:        # software-pipelined forward
+        return env_ab("FFK_ATTN_FWD_PIPE", "fwd", 50)
+    if "--delta-ab" in sys.argv:       # delta fused into the dQ kernel
+        return env_ab("FFK_ATTN_BWD_FUSED_DELTA", "bwd", 30)
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     for name, (B, S, H, D, causal) in SHAPES.items():
         g = torch.Generator(device="cuda").manual_seed(0)

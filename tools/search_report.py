@@ -20,14 +20,16 @@ from flexflow_train_amd.models.bert import bert_large, build_bert  # noqa: E402
 from flexflow_train_amd.search import unity  # noqa: E402
 
 CONFIGS = {
-    # name: (builder(model, global_batch), per-GPU batch)
-    "bert-large": (lambda m, B: build_bert(m, bert_large(batch_size=B, sequence_length=512)), 32),
+    # name: (builder(model, global_batch), per-GPU batch): bench.py's per-GPU
+    # batches, so a prediction lines up with the driver's weak-scaling runs
+    "bert-large": (lambda m, B: build_bert(m, bert_large(batch_size=B, sequence_length=512)), 64),
     "bert-large-ae": (lambda m, B: build_bert(m, bert_large(batch_size=B, sequence_length=512)), 2),  # AE: batch 8 on 4 GPUs
-    "gpt3-medium": (lambda m, B: Z.build("gpt", m, batch_size=B), 8),
+    "gpt3-medium": (lambda m, B: Z.build("gpt", m, batch_size=B, hidden_size=1024, num_layers=24, num_heads=16,
+                                         sequence_length=2048), 16),
     "dlrm": (lambda m, B: Z.build("dlrm", m, batch_size=B, embedding_size=[1000000] * 8, mlp_bot=[64, 512, 512, 64],
                                   mlp_top=[576, 1024, 1024, 1024, 1]), 1024),
     "mlp_unify": (lambda m, B: Z.build("mlp_unify", m, batch_size=B), 8),
-    "resnet50": (lambda m, B: Z.build("resnet50", m, batch_size=B, image_size=224, num_classes=1000), 32),
+    "resnet50": (lambda m, B: Z.build("resnet50", m, batch_size=B, image_size=224, num_classes=1000), 256),
 }
 
 
