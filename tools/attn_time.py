@@ -60,7 +60,30 @@ def env_ab(var, which, iters, rounds=5):
     os.environ.pop(var, None)
 
 
+def pmc_run(n=5):
+    """A few dispatches of each kernel for a counter pass (rocprofv3 --pmc):
+    forward default, forward pipelined, backward, at both bench shapes."""
+    for name, (B, S, H, D, causal) in SHAPES.items():
+        g = torch.Generator(device="cuda").manual_seed(0)
+        qkv = torch.randn(B, S, 3, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        do = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, generator=g)
+        dqkv = torch.empty_like(qkv)
+        o, lse = K.attention_fwd(q, k, v, causal=causal)
+        for p in ("0", "1"):
+            os.environ["FFK_ATTN_FWD_PIPE"] = p
+            for _ in range(n):
+                K.attention_fwd(q, k, v, causal=causal, out=o)
+        os.environ.pop("FFK_ATTN_FWD_PIPE", None)
+        for _ in range(n):
+            K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal)
+        torch.cuda.synchronize()
+        print(name, "done", flush=True)
+
+
 def main():
+    if "--pmc-run" in sys.argv:
+        return pmc_run()
     if "--pipe-ab" in sys.argv:        # software-pipelined forward
         return env_ab("FFK_ATTN_FWD_PIPE", "fwd", 50)
     if "--delta-ab" in sys.argv:       # delta fused into the dQ kernel

@@ -11,10 +11,19 @@ FETCH_SIZE pass, the achieved HBM read bandwidth.
 import collections
 import csv
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from prof_summary import category  # noqa: E402
+from prof_summary import short  # noqa: E402
+
+
+def category(name: str) -> str:
+    """Kernel name without arguments; hipBLASLt kernels grouped by macro tile."""
+    if "Cijk_" in name:
+        m = re.search(r"MT\d+x\d+x\d+", name)
+        return f"hipBLASLt gemm ({m.group(0) if m else '?'})"
+    return short(name)
 
 
 def main():
