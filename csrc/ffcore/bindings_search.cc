@@ -176,6 +176,36 @@ void register_ext_bindings(py::module_& m) {
     for (auto const& v : get_allowed_machine_views(ts, spec)) r.push_back(v.to_json().dump());
     return r;
   });
+  m.def("get_machine_space_coordinate",
+        [](const std::vector<int>& ts, const std::string& view, const std::vector<int>& coord,
+           const MachineSpecification& spec) -> py::object {
+          auto c = get_machine_space_coordinate(ts, MachineView::from_json(Json::parse(view)), coord, spec);
+          if (!c) return py::none();
+          return py::make_tuple(c->node_idx, c->device_idx);
+        });
+  // start-invariant views as JSON {"dimensions": [...]} (the MachineView
+  // encoding without "start")
+  m.def("start_invariant_from_machine_view", [](const std::string& view) {
+    Json j = MachineView::from_json(Json::parse(view)).to_json();
+    Json o = Json::object();
+    o["dimensions"] = j.at("dimensions");
+    return o.dump();
+  });
+  m.def("machine_view_from_start_invariant", [](const std::string& simv, int node, int device) {
+    Json j = Json::parse(simv);
+    j["start"] = Json(std::vector<int64_t>{node, device});
+    return MachineView::from_json(j).to_json().dump();
+  });
+  m.def("get_machine_space_offset",
+        [](const std::vector<int>& ts, const std::string& simv, const std::vector<int>& coord,
+           const MachineSpecification& spec) -> py::object {
+          Json j = Json::parse(simv);
+          j["start"] = Json(std::vector<int64_t>{0, 0});
+          auto c = get_machine_space_offset(ts, start_invariant_from_machine_view(MachineView::from_json(j)), coord,
+                                            spec);
+          if (!c) return py::none();
+          return py::make_tuple(c->node_idx, c->device_idx);
+        });
   m.def("get_device_ids", [](const std::vector<int>& ts, const std::string& view, const MachineSpecification& spec) {
     return get_device_ids(ts, MachineView::from_json(Json::parse(view)), spec);
   });

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <unordered_map>
 #include <map>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -94,12 +95,28 @@ extern const double kMovementInfeasible;
 // Task space of an operator = the degrees of its output [shard..., sum, copy].
 std::vector<int> operator_task_space(const ParallelTensorShape& out);
 
-// Maps a task coordinate to a machine coordinate (mixed radix per projection).
-MachineSpaceCoordinate get_machine_space_coordinate(const std::vector<int>& task_space, const MachineView& view,
+// Maps a task coordinate to a machine coordinate (mixed radix per projection,
+// first task dimension fastest); nullopt when the coordinate is outside the
+// task space or lands outside the machine.
+std::optional<MachineSpaceCoordinate> get_machine_space_coordinate(const std::vector<int>& task_space, const MachineView& view,
                                                     const std::vector<int>& coord,
                                                     const MachineSpecification& spec);
 std::vector<int> get_device_ids(const std::vector<int>& task_space, const MachineView& view,
                                 const MachineSpecification& spec);
+
+// A view's dimensions without its start (start_invariant_machine_view.h).
+struct StartInvariantMachineView {
+  std::vector<MachineViewDimension> dims;
+  bool operator==(const StartInvariantMachineView& o) const { return dims == o.dims; }
+};
+StartInvariantMachineView start_invariant_from_machine_view(const MachineView& v);
+MachineView machine_view_from_start_invariant(const StartInvariantMachineView& s, const MachineSpaceCoordinate& start);
+// offset of a task from the view's start (the coordinate of the view placed
+// at (0, 0)); nullopt outside the task space or the machine
+std::optional<MachineSpaceCoordinate> get_machine_space_offset(const std::vector<int>& task_space,
+                                                               const StartInvariantMachineView& s,
+                                                               const std::vector<int>& coord,
+                                                               const MachineSpecification& spec);
 // Every strided view (strides up to the machine size, every start, every
 // projection) whose devices fit the machine (allowed_machine_views.cc).
 std::vector<MachineView> get_allowed_machine_views(const std::vector<int>& task_space,
@@ -113,7 +130,7 @@ struct DeviceBlock {
   bool operator<(const DeviceBlock& o) const { return start != o.start ? start < o.start : size < o.size; }
 };
 // Canonical MachineView of an operator with task space `ts` on block `b`
-// (copy axis innermost, implicit replicas innermost of all).
+// (first task dimension strided by the implicit replica count).
 MachineView block_machine_view(const std::vector<int>& ts, const DeviceBlock& b, const MachineSpecification& spec);
 // Power-of-two splits of a block into two disjoint halves-or-quarters.
 std::vector<std::pair<DeviceBlock, DeviceBlock>> get_resource_splits(const DeviceBlock& b);

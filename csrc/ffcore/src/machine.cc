@@ -104,25 +104,50 @@ std::vector<int> operator_task_space(const ParallelTensorShape& out) {
   return ts;
 }
 
-// coefficient of task dim i = stride_i * prod_{j>i, same projection} ts[j]
-// (the last task dim varies fastest, matching the executor's row-major
-// canonical placement).
-MachineSpaceCoordinate get_machine_space_coordinate(const std::vector<int>& ts, const MachineView& view,
-                                                    const std::vector<int>& coord,
-                                                    const MachineSpecification& spec) {
+std::optional<MachineSpaceCoordinate> get_machine_space_coordinate(const std::vector<int>& ts, const MachineView& view,
+                                                                   const std::vector<int>& coord,
+                                                                   const MachineSpecification& spec) {
   if (ts.size() != view.dims.size() || coord.size() != ts.size())
     throw FFError("get_machine_space_coordinate: rank mismatch");
+  // per machine dimension, the task dimensions projected onto it form a mixed
+  // radix with the FIRST one fastest; a dimension's digit weight is the
+  // product of (degree x stride) of the earlier dimensions on the same
+  // projection, times its own stride (machine_view.cc:60-81)
   MachineSpaceCoordinate r = view.start;
+  int64_t coeff_node = 1, coeff_dev = 1;
   for (size_t i = 0; i < ts.size(); ++i) {
-    if (coord[i] < 0 || coord[i] >= ts[i]) throw FFError("task coordinate out of range");
-    int64_t mult = view.dims[i].stride;
-    for (size_t j = i + 1; j < ts.size(); ++j)
-      if (view.dims[j].projection == view.dims[i].projection) mult *= ts[j];
-    if (view.dims[i].projection == ProjectionType::INTRA_NODE) r.device_idx += static_cast<int>(coord[i] * mult);
-    else r.node_idx += static_cast<int>(coord[i] * mult);
+    if (coord[i] < 0 || coord[i] >= ts[i]) return std::nullopt;
+    const int64_t stride = view.dims[i].stride;
+    if (view.dims[i].projection == ProjectionType::INTRA_NODE) {
+      r.device_idx += static_cast<int>(coeff_dev * coord[i] * stride);
+      coeff_dev *= static_cast<int64_t>(ts[i]) * stride;
+    } else {
+      r.node_idx += static_cast<int>(coeff_node * coord[i] * stride);
+      coeff_node *= static_cast<int64_t>(ts[i]) * stride;
+    }
   }
-  (void)spec;
+  if (r.node_idx < 0 || r.node_idx >= spec.num_nodes || r.device_idx < 0 || r.device_idx >= spec.num_gpus_per_node)
+    return std::nullopt;
   return r;
+}
+
+// Start-invariant views (start_invariant_machine_view.cc): the dimensions of a
+// view without its start; offsets are the coordinates of the view placed at
+// (0, 0), checked against the machine.
+StartInvariantMachineView start_invariant_from_machine_view(const MachineView& v) { return {v.dims}; }
+
+MachineView machine_view_from_start_invariant(const StartInvariantMachineView& s, const MachineSpaceCoordinate& start) {
+  MachineView v;
+  v.start = start;
+  v.dims = s.dims;
+  return v;
+}
+
+std::optional<MachineSpaceCoordinate> get_machine_space_offset(const std::vector<int>& ts,
+                                                               const StartInvariantMachineView& s,
+                                                               const std::vector<int>& coord,
+                                                               const MachineSpecification& spec) {
+  return get_machine_space_coordinate(ts, machine_view_from_start_invariant(s, {0, 0}), coord, spec);
 }
 
 static void for_each_coord(const std::vector<int>& ts, const std::function<void(const std::vector<int>&)>& f) {
@@ -143,7 +168,8 @@ std::vector<int> get_device_ids(const std::vector<int>& ts, const MachineView& v
   std::vector<int> ids;
   for_each_coord(ts, [&](const std::vector<int>& c) {
     auto m = get_machine_space_coordinate(ts, view, c, spec);
-    ids.push_back(m.node_idx * spec.num_gpus_per_node + m.device_idx);
+    if (!m) throw FFError("get_device_ids: view " + view.str() + " does not fit the machine");
+    ids.push_back(m->node_idx * spec.num_gpus_per_node + m->device_idx);
   });
   return ids;
 }
@@ -170,8 +196,8 @@ std::vector<MachineView> get_allowed_machine_views(const std::vector<int>& ts, c
         bool ok = true;
         std::vector<int> maxc(ts.size());
         for (int i = 0; i < n; ++i) maxc[i] = ts[i] - 1;
-        auto m = get_machine_space_coordinate(ts, v, maxc, spec);
-        if (m.node_idx >= spec.num_nodes || m.device_idx >= spec.num_gpus_per_node) ok = false;
+        // digit weights are positive, so the largest coordinate lands furthest
+        if (!get_machine_space_coordinate(ts, v, maxc, spec)) ok = false;
         if (ok) {
           auto ids = get_device_ids(ts, v, spec);
           std::sort(ids.begin(), ids.end());
@@ -210,8 +236,10 @@ MachineView block_machine_view(const std::vector<int>& ts, const DeviceBlock& b,
   if (T <= 0 || b.size % T != 0) throw FFError("block_machine_view: task space does not divide the block");
   MachineView v;
   v.start = {b.start / spec.num_gpus_per_node, b.start % spec.num_gpus_per_node};
+  // first dimension strided by the replica count R, the others dense above
+  // it: the view covers the block exactly, R apart within each first-dim run
   const int R = b.size / T;
-  for (size_t i = 0; i < ts.size(); ++i) v.dims.push_back({R, ProjectionType::INTRA_NODE});
+  for (size_t i = 0; i < ts.size(); ++i) v.dims.push_back({i == 0 ? R : 1, ProjectionType::INTRA_NODE});
   return v;
 }
 

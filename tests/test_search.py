@@ -48,7 +48,9 @@ def test_block_machine_view_is_canonical():
     spec = C.MachineSpecification.mi355x(1, 8)
     v = C.block_machine_view([2, 1, 2], 0, 8, spec)  # T=4 on 8 devices -> 2 implicit replicas
     ids = C.get_device_ids([2, 1, 2], v, spec)
-    assert ids == [0, 2, 4, 6]
+    # ids in row-major task order; the first task dimension is the fastest
+    # machine digit (reference machine_view.cc semantics), replicas interleaved
+    assert ids == [0, 4, 2, 6]
 
 
 def test_resource_splits():

@@ -6,7 +6,7 @@ SQ_INSTS_VALU_MFMA_MOPS_BF16 (x512 FLOP) over the dispatch time, and LDS
 bank-conflict rate (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE); with a
 FETCH_SIZE pass, the achieved HBM read bandwidth.
 
-    python tools/pmc_summary.py gpurun_out/pmc/bert1/run_counter_collection.csv [--simds 1024] [--xcds 8]
+    python tools/pmc_summary.py gpurun_out/pmc/bert1/run_counter_collection.csv [--simds 1024] [--xcds 8] [--raw]
 """
 import collections
 import csv
@@ -58,6 +58,11 @@ def main():
         if has_fetch:  # FETCH_SIZE is in KiB
             line += f" {a.get('FETCH_SIZE', 0) * 1024 / (a['ns'] * 1e-9) / 1e9 if a['ns'] else 0.0:11.1f}"
         print(line)
+    if "--raw" in sys.argv:   # every counter, mean per dispatch
+        for name, a in rows[:30]:
+            print(f"{name[:90]}  dispatches={a['n']} mean_us={a['ns'] / a['n'] / 1e3:.1f}")
+            for k in sorted(x for x in a if x not in ("n", "ns")):
+                print(f"    {k:32s} {a[k] / a['n']:18.1f}")
 
 
 if __name__ == "__main__":
