@@ -326,6 +326,17 @@ PYBIND11_MODULE(_ffcore, m) {
     if (i < 0) return py::none();
     return py::cast(t.leaves(i));
   });
+  // strict SP decomposition as binary nested tuples (None if not SP)
+  g.def("sp_decomposition", [=](std::vector<int> n, std::vector<std::pair<int, int>> e) -> py::object {
+    auto t = get_series_parallel_decomposition(mkg(n, e));
+    if (!t || t->root < 0) return py::none();
+    std::function<py::object(int)> conv = [&](int i) -> py::object {
+      const auto& x = t->e[i];
+      if (x.kind == SPTree::LEAF) return py::int_(x.node);
+      return py::make_tuple(x.kind == SPTree::SERIES ? "S" : "P", conv(x.left), conv(x.right));
+    };
+    return conv(t->root);
+  });
   g.def("sp_associative", [=](std::vector<int> n, std::vector<std::pair<int, int>> e, bool left) {
     auto t = sp_of(n, e);
     auto r = left ? left_associative(t) : right_associative(t);

@@ -122,3 +122,46 @@ def test_sp_tree_paths_and_associativity():
 def test_dot_export():
     dot = G.as_dot(N, E)
     assert dot.startswith("digraph") and "->" in dot
+
+
+# ---- get_series_parallel_decomposition, the reference's cases
+# (lib/utils/test/src/utils/graph/series_parallel/get_series_parallel_decomposition.cc)
+def _nary(t):
+    """binary ("S"|"P", l, r) tree -> n-ary normal form: series = tuple of
+    children in order, parallel = frozenset, nested same-kind splits flattened"""
+    if isinstance(t, int):
+        return t
+    kind, l, r = t
+    kids = []
+    for c in (l, r):
+        c = _nary(c)
+        same = (kind == "S" and isinstance(c, tuple) and c[0] == "S") or (kind == "P" and isinstance(c, frozenset))
+        if same:
+            kids.extend(c[1:] if kind == "S" else c)
+        else:
+            kids.append(c)
+    return ("S", *kids) if kind == "S" else frozenset(kids)
+
+
+def S(*k):
+    return ("S", *k)
+
+
+def P(*k):
+    return frozenset(k)
+
+
+@pytest.mark.parametrize("nodes,edges,want", [
+    ([0], [], 0),                                                                  # base case
+    ([0, 1], [], P(0, 1)),                                                         # parallel
+    ([0, 1], [(0, 1)], S(0, 1)),                                                   # serial
+    ([0, 1, 2], [(0, 1), (0, 2)], S(0, P(1, 2))),                                  # composite
+    ([0, 1, 2, 3, 4, 5], [(0, 1), (0, 2), (1, 3), (2, 4), (3, 5), (4, 5)],
+     S(0, P(S(1, 3), S(2, 4)), 5)),                                                # diamond
+    ([0, 1, 2, 3], [(0, 2), (0, 3), (1, 2), (1, 3)], S(P(0, 1), P(2, 3))),        # all-to-all
+    ([0, 1, 2, 3], [(0, 2), (1, 2), (1, 3)], None),                                # N graph: not SP
+    ([0, 1, 2, 3], [(0, 1), (0, 2), (1, 2), (1, 3), (2, 3)], S(0, 1, 2, 3)),      # needs transitive reduction
+], ids=["base", "parallel", "serial", "composite", "diamond", "all_to_all", "non_sp", "transitive"])
+def test_series_parallel_decomposition_reference(nodes, edges, want):
+    t = G.sp_decomposition(nodes, edges)
+    assert (None if t is None else _nary(t)) == want
