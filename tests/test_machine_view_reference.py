@@ -108,3 +108,23 @@ def test_start_invariant_offset_1d(coord, want):
 def test_start_invariant_offset_2d(coord, want):
     simv = json.dumps({"dimensions": [{"stride": 1, "projection": INTER}, {"stride": 2, "projection": INTRA}]})
     assert C.get_machine_space_offset([2, 2], simv, list(coord), C.MachineSpecification.mi355x(2, 4)) == want
+
+
+# ---- get_allowed_machine_views (lib/compiler/test/src/allowed_machine_views.cc)
+def _norm(v):
+    j = json.loads(v)
+    return tuple(j["start"]), tuple((d["stride"], d["projection"]) for d in j["dimensions"])
+
+
+def test_allowed_views_one_degree():
+    got = {_norm(v) for v in C.get_allowed_machine_views([3], C.MachineSpecification.mi355x(1, 5))}
+    assert got == {((0, 0), ((1, INTRA),)), ((0, 1), ((1, INTRA),)), ((0, 2), ((1, INTRA),)),
+                   ((0, 0), ((2, INTRA),))}
+
+
+def test_allowed_views_two_degrees():
+    got = {_norm(v) for v in C.get_allowed_machine_views([2, 3], C.MachineSpecification.mi355x(3, 3))}
+    assert got == {((0, 0), ((1, INTER), (1, INTRA))), ((1, 0), ((1, INTER), (1, INTRA))),
+                   ((0, 0), ((2, INTER), (1, INTRA))),
+                   ((0, 0), ((1, INTRA), (1, INTER))), ((0, 1), ((1, INTRA), (1, INTER))),
+                   ((0, 0), ((2, INTRA), (1, INTER)))}
