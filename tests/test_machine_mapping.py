@@ -176,3 +176,20 @@ def test_graph_optimize_runs_final_mapping():
     pcg, views, rep = unity.search(m.cg, cfg, 2)
     assert "unmapped_cost" in rep and rep["cost"] <= rep["unmapped_cost"] + 1e-12
     assert bool(views) == rep["algorithm"].endswith("+mapping")
+
+
+@pytest.mark.parametrize("nodes,gpus,want", [
+    (1, 1, set()),
+    (2, 2, {((2, 1), (2, 1)), ((1, 2), (1, 2))}),
+    (8, 1, {((1, 1), (7, 1)), ((2, 1), (6, 1)), ((4, 1), (4, 1)), ((6, 1), (2, 1)), ((7, 1), (1, 1))}),
+    (6, 1, {((1, 1), (5, 1)), ((2, 1), (4, 1)), ((4, 1), (2, 1)), ((5, 1), (1, 1))}),
+    (1, 8, {((1, 1), (1, 7)), ((1, 2), (1, 6)), ((1, 4), (1, 4)), ((1, 6), (1, 2)), ((1, 7), (1, 1))}),
+    (1, 6, {((1, 1), (1, 5)), ((1, 2), (1, 4)), ((1, 4), (1, 2)), ((1, 5), (1, 1))}),
+], ids=["none", "2x2", "nodes8", "nodes6", "gpus8", "gpus6"])
+def test_resource_splits_reference_cases(nodes, gpus, want):
+    """lib/compiler/test/src/compiler/machine_mapping/get_machine_resource_splits.cc:
+    power-of-two splits along the node OR the gpu dimension (never both), both
+    orders; as (nodes, gpus_per_node) shape pairs."""
+    splits = json.loads(C.machine_resource_splits(json.dumps({"num_nodes": nodes, "gpus_per_node": gpus})))
+    got = {((a["num_nodes"], a["gpus_per_node"]), (b["num_nodes"], b["gpus_per_node"])) for a, b in splits}
+    assert got == want
