@@ -430,6 +430,39 @@ void register_ext_bindings(py::module_& m) {
     j["cache_entries"] = static_cast<int64_t>(cache.results.size());
     return j.dump();
   });
+  // machine-mapping result combinators on JSON results: null = infeasible,
+  // {"runtime": r, "mapping": {"LR..": view}} (paths as in machine_mapping_dp)
+  auto mm_from = [](const std::string& s) -> MMResult {
+    Json j = Json::parse(s);
+    if (j.is_null()) return std::nullopt;
+    FeasibleMachineMapping f;
+    f.runtime = j.at("runtime").as_double();
+    if (j.contains("mapping"))
+      for (auto const& kv : j.at("mapping").as_object()) {
+        BinaryTreePath p;
+        for (char c : kv.first) p.push_back(c == 'R' ? 1 : 0);
+        f.mapping[p] = MachineView::from_json(kv.second);
+      }
+    return f;
+  };
+  auto mm_to = [](const MMResult& r) -> std::string {
+    if (!r) return "null";
+    Json j = Json::object();
+    j["runtime"] = r->runtime;
+    Json m = Json::object();
+    for (auto const& kv : r->mapping) m[path_to(kv.first)] = kv.second.to_json();
+    j["mapping"] = m;
+    return j.dump();
+  };
+  m.def("mm_series_combine", [=](double comm, const std::string& pre, const std::string& post, bool r_then_l) {
+    return mm_to(series_combine(comm, mm_from(pre), mm_from(post), r_then_l));
+  }, py::arg("comm"), py::arg("pre"), py::arg("post"), py::arg("r_then_l") = false);
+  m.def("mm_parallel_combine", [=](const std::string& l, const std::string& r) {
+    return mm_to(parallel_combine(mm_from(l), mm_from(r)));
+  });
+  m.def("mm_minimize_runtime", [=](const std::string& a, const std::string& b) {
+    return mm_to(minimize_runtime(mm_from(a), mm_from(b)));
+  });
   m.def("machine_resource_splits", [](const std::string& resource) {
     Json out = Json::array();
     for (auto const& sp : get_machine_resource_splits(resource_from(Json::parse(resource)))) {

@@ -193,3 +193,50 @@ def test_resource_splits_reference_cases(nodes, gpus, want):
     splits = json.loads(C.machine_resource_splits(json.dumps({"num_nodes": nodes, "gpus_per_node": gpus})))
     got = {((a["num_nodes"], a["gpus_per_node"]), (b["num_nodes"], b["gpus_per_node"])) for a, b in splits}
     assert got == want
+
+
+# ---- machine-mapping result combinators
+# (lib/compiler/test/src/compiler/machine_mapping/machine_mapping_result.cc)
+_MV0 = {"start": [0, 0], "dimensions": [{"stride": 1, "projection": "INTRA_NODE"}]}
+_MV1 = {"start": [0, 0], "dimensions": [{"stride": 2, "projection": "INTRA_NODE"}]}
+_PRE = {"runtime": 2.0, "mapping": {"L": _MV0, "R": _MV1}}
+_POST = {"runtime": 4.0, "mapping": {"": _MV1}}
+
+
+def _mm(x):
+    return "null" if x is None else json.dumps(x)
+
+
+def _res(s):
+    return json.loads(s)
+
+
+@pytest.mark.parametrize("pre,post", [(None, _POST), (_PRE, None), (None, None)])
+def test_series_combine_infeasible(pre, post):
+    for rtl in (False, True):
+        assert _res(C.mm_series_combine(3.0, _mm(pre), _mm(post), rtl)) is None
+
+
+def test_series_combine_feasible():
+    lr = _res(C.mm_series_combine(3.0, _mm(_PRE), _mm(_POST), False))
+    assert lr == {"runtime": 9.0, "mapping": {"LL": _MV0, "LR": _MV1, "R": _MV1}}
+    rl = _res(C.mm_series_combine(3.0, _mm(_PRE), _mm(_POST), True))
+    assert rl == {"runtime": 9.0, "mapping": {"RL": _MV0, "RR": _MV1, "L": _MV1}}
+
+
+def test_parallel_combine():
+    for a, b in ((None, _POST), (_PRE, None), (None, None)):
+        assert _res(C.mm_parallel_combine(_mm(a), _mm(b))) is None
+    assert _res(C.mm_parallel_combine(_mm(_PRE), _mm(_POST))) == \
+        {"runtime": 4.0, "mapping": {"LL": _MV0, "LR": _MV1, "R": _MV1}}
+
+
+def test_minimize_runtime():
+    faster = {"runtime": 2.0, "mapping": {"L": _MV0, "R": _MV1}}
+    slower = {"runtime": 4.0, "mapping": {"": _MV1}}
+    assert _res(C.mm_minimize_runtime(_mm(None), _mm(slower))) == slower
+    assert _res(C.mm_minimize_runtime(_mm(slower), _mm(None))) == slower
+    assert _res(C.mm_minimize_runtime(_mm(None), _mm(None))) is None
+    assert _res(C.mm_minimize_runtime(_mm(faster), _mm(slower))) == faster
+    assert _res(C.mm_minimize_runtime(_mm(slower), _mm(faster))) == faster
+    assert _res(C.mm_minimize_runtime(_mm(slower), _mm(slower))) == slower
