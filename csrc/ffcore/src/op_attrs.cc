@@ -411,9 +411,12 @@ OpSpec pool2d_spec() {
     require(x.dim(3).degree == 1, a, "W (attribute) degree must be 1");
     require(dh == 1 || spatial_split_ok(x.dim(2).size, a.i("kernel_h"), a.i("stride_h"), a.i("padding_h"), dh), a,
             "H shards need halos wider than one neighbour");
-    require(x.sum_degree == 1, a, "pooling a partial-sum tensor");
+    // average pooling without an activation is linear: partial sums pass
+    // through (pool_2d.cc "PoolOp::AVG does allow sum parallelism")
+    const bool linear = a.s("pool_type") == "avg" && a.s("activation") == "none";
+    require(x.sum_degree == 1 || linear, a, "pooling a partial-sum tensor");
     auto o = registry()[static_cast<int>(OpType::POOL2D)].out(a, {x.reduced_shape()})[0];
-    return PShapes{lift_to_parallel_with_degrees(o, 1, x.discard_copy_degree,
+    return PShapes{lift_to_parallel_with_degrees(o, x.sum_degree, x.discard_copy_degree,
                                                  {x.dim(0).degree, x.dim(1).degree, dh, 1})};
   };
   s.pwts = no_pweight_shapes;
@@ -758,6 +761,7 @@ OpSpec flat_spec() {
     auto const& x = in[0];
     int st = normalize_dim(static_cast<int>(a.i("start_dim")), nd(x));
     int en = normalize_dim(static_cast<int>(a.i("end_dim")), nd(x));
+    if (en < st) return Shapes{x};   // empty range: identity (flat.cc "flatten no dims")
     TensorShape o{{}, x.dtype};
     for (int d = 0; d < st; ++d) o.dims.push_back(x.dims[d]);
     int64_t p = 1;
@@ -771,6 +775,7 @@ OpSpec flat_spec() {
     auto const& x = in[0];
     int st = normalize_dim(static_cast<int>(a.i("start_dim")), x.num_dims());
     int en = normalize_dim(static_cast<int>(a.i("end_dim")), x.num_dims());
+    if (en < st) return PShapes{x};
     for (int d = st + 1; d <= en; ++d) require(x.shard_dims[d].degree == 1, a, "flattened inner dims must be unpartitioned");
     auto o = registry()[static_cast<int>(OpType::FLAT)].out(a, {x.reduced_shape()})[0];
     std::vector<int> deg;
