@@ -189,3 +189,30 @@ def test_ffconfig_substitution_path():
     cfg.substitution_json_path = "/nonexistent/rules.json"
     with pytest.raises(FileNotFoundError):
         unity.substitution_path(cfg)
+
+
+def test_two_linears_sharing_an_input_match_both_ways():
+    """lib/substitutions/test/src/substitutions/pcg_pattern.cc: a pattern of
+    two LINEAR nodes reading the same pattern input, on a graph where a feeds
+    x_matmul and y_matmul (then add), matches exactly twice, with the two
+    pattern nodes swapped, both binding the pattern input to a's value."""
+    import json as _json
+    m = FFModel(FFConfig())
+    a = m.create_tensor([16, 24], DataType.DT_FLOAT, name="a")
+    t0 = m.dense(a, 16, use_bias=False, name="x_matmul")
+    t1 = m.dense(a, 16, use_bias=False, name="y_matmul")
+    m.add(t0, t1, name="add")
+    pcg = C.data_parallel_pcg(m.cg, 2)
+    lin = {"attrs": {}, "constraints": [], "inputs": [[-1, 0]], "num_outputs": -1, "type": "LINEAR"}
+    sub = C.substitution_from_json(_json.dumps({
+        "format": "ffmi355x.substitution.v1", "name": "two_linears", "num_pattern_inputs": 1,
+        "pattern": [lin, lin], "pattern_outputs": [[0, 0], [1, 0]], "output_graph": [], "output_mapping": []}))
+    matches = C.find_pattern_matches(sub, pcg)
+    got = sorted(tuple(pcg.layer_name(n) for n in nm) for nm, _ in matches)
+    assert got == [("x_matmul", "y_matmul"), ("y_matmul", "x_matmul")]
+    feeds = {(v.node, v.idx) for _, im in matches for v in im}
+    assert len(feeds) == 1   # the one value that feeds both matmuls
+    (node, idx), = feeds
+    x = pcg.find_layer("x_matmul") if hasattr(pcg, "find_layer") else None
+    if x is not None:
+        assert any((v.node, v.idx) == (node, idx) for v in pcg.layer_inputs(x))
