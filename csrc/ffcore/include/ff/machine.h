@@ -155,6 +155,7 @@ struct OpCost {
   double memory = 0;    // bytes resident per device (weights + grads + optimizer + activations)
   double workspace = 0; // transient bytes beyond `memory` while the op runs (measured peak)
   double sync = 0;      // weight-gradient all-reduce time
+  bool measured = false; // forward / backward from a measured profile entry
 };
 
 // Optional measured-profile table: op signature -> {fwd_ms, bwd_ms} and, when

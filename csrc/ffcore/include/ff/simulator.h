@@ -51,6 +51,12 @@ struct SimConfig {
   // row-sparse embedding update (the executor's sparse SGD): an EMBEDDING
   // table's update touches only the rows its indices name, not the table
   bool sparse_embedding_update = false;
+  // the executor's kernel fusions (runtime/executor.py): an EW_ADD whose sum
+  // feeds a LAYERNORM on the same devices runs inside the norm
+  // (FUSED_ADD_LAYERNORM), and the graph's final SOFTMAX runs inside the
+  // softmax + cross-entropy loss kernel (one read of the logits, one write of
+  // their gradient, no separate backward)
+  bool executor_fusions = true;
   const NetworkModel* network = nullptr; // routed transfers / collectives (LogicalTaskgraph mode)
 };
 

@@ -419,6 +419,7 @@ OpCost CostModel::op_cost_uncached(const OpAttrs& op, const std::vector<Parallel
   if (pe) {
     c.forward = pe->fwd_ms * 1e-3;
     c.backward = pe->bwd_ms * 1e-3;
+    c.measured = true;
   } else {
     OpWork w = estimate_op_work(op, ip, wp, op_);
     if (w.matmul_like) {

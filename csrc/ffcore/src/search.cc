@@ -332,6 +332,7 @@ SimConfig sim_config_from_json(const Json& j) {
   gb("bf16_weight_grads", c.bf16_weight_grads);
   gb("parameter_server", c.parameter_server);
   gb("sparse_embedding_update", c.sparse_embedding_update);
+  gb("executor_fusions", c.executor_fusions);
   return c;
 }
 

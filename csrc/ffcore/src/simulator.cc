@@ -138,6 +138,37 @@ SimResult Simulator::simulate(const ParallelComputationGraph& pcg, const std::ma
     cost[id] = pcg_node_cost(cm_, pcg, id, static_cast<int>(place(id).size()));
     if (cost[id].sync > 0) any_sync = true;
   }
+  if (cfg_.executor_fusions) {
+    const double bw = spec.hbm_bandwidth;
+    for (int id : order) {
+      if (!active(id) || roles.at(id) != NodeRole::COMPUTE) continue;
+      auto const& nd = pcg.g.node(id);
+      const OpType t = nd.label.op.type;
+      if (t == OpType::LAYERNORM) {
+        auto ins = pcg.layer_data_inputs(id);
+        if (ins.size() != 1) continue;
+        const int p = ins[0].node;
+        if (roles.at(p) != NodeRole::COMPUTE || pcg.g.node(p).label.op.type != OpType::EW_ADD) continue;
+        if (place(p) != place(id)) continue;
+        auto const& pin = pcg.layer_data_inputs(p);
+        if (pin.size() != 2 || !(pcg.shape(pin[0]) == pcg.shape(ins[0])) || !(pcg.shape(pin[1]) == pcg.shape(ins[0])))
+          continue;
+        // the add runs inside the norm: one more input read, plus the sum
+        // written out when something else also reads it (pre-LN residual)
+        if (!cost[id].measured) {
+          const double piece = static_cast<double>(pcg.shape(ins[0]).piece_shape().size_bytes());
+          cost[id].forward += piece / bw * (consumers[p].size() > 1 ? 2.0 : 1.0);
+        }
+        const double sync = cost[p].sync;
+        cost[p] = OpCost{};
+        cost[p].sync = sync;
+      } else if (t == OpType::SOFTMAX && consumers[id].empty() && !cost[id].measured) {
+        const double piece = static_cast<double>(nd.outputs.at(0).shape.piece_shape().size_bytes());
+        cost[id].forward = 2.0 * piece / bw + spec.kernel_launch_overhead;
+        cost[id].backward = 0.0;
+      }
+    }
+  }
   const double bwd_scale = (cfg_.overlap_grad_sync && any_sync) ? 1.0 + cfg_.comm_compute_slowdown : 1.0;
 
   std::vector<Rec> tasks;
