@@ -184,3 +184,31 @@ def test_measured_memory_drives_peak():
     assert got == pytest.approx(weights + resident + workspace)
     assert base > weights      # analytic activations before
     assert json.loads(cm2.profiles_json())[next(iter(sigs))]["peak_mb"] == pytest.approx(100.0)
+
+
+def test_executor_fusions_priced():
+    """The executor runs residual add + LayerNorm as one kernel and the final
+    softmax inside the softmax + cross-entropy loss: with executor_fusions the
+    simulator prices the add at zero (one extra input read in the norm) and
+    the final softmax as one read + one write of the logits, no backward."""
+    m = FFModel(FFConfig())
+    x = m.create_tensor([4096, 1024], DataType.DT_FLOAT, name="x")
+    h = m.dense(x, 1024, name="proj")
+    t = m.layer_norm(m.add(x, h, name="res"), [1], True, 1e-5, name="ln")
+    m.softmax(m.dense(t, 4096, name="head"), name="sm")
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    cm = native.cost_model(world=1, use_profiles=False)
+    fused = native.simulate(pcg, cm, 1, dot=True)
+    plain = native.simulate(pcg, cm, 1, dot=True, executor_fusions=False)
+    assert fused["iteration_time"] < plain["iteration_time"]
+
+    def run(res, name):
+        return sum(t["end"] - t["start"] for t in res["tasks"] if t["name"].split(":")[0] == name and t["type"] in (0, 1))
+    names = {pcg.layer_name(n): n for n in pcg.topo_order()}
+    assert "res" in names and "sm" in names
+    assert run(fused, "res") == 0.0 and run(plain, "res") > 0.0
+    assert run(fused, "ln") > run(plain, "ln")               # the extra input read
+    logits = 4096 * 4096 * 4                                  # fp32 piece of the head output
+    hbm = cm.spec().hbm_bandwidth
+    assert run(fused, "sm") == pytest.approx(2 * logits / hbm + cm.spec().kernel_launch_overhead, rel=1e-6)
+    assert run(plain, "sm") > run(fused, "sm")
