@@ -43,6 +43,10 @@ struct MachineSpecification {
   double hbm_capacity = 288e9;
   double kernel_launch_overhead = 4e-6; // s per kernel (graph-replayed ~1.5 us)
   double collective_latency = 8e-6;     // alpha per collective step
+  // the executor computes in bf16 whatever dtype a tensor is declared with
+  // (fp32 masters aside): analytic memory traffic counts 2 bytes per fp32
+  // element (measured profile entries are used as they are)
+  bool bf16_compute = true;
   int xgmi_links = 7;
   double xgmi_link_bandwidth = 64e9;    // per direction per link
   // Optional effective bus bandwidths (bytes/s) per group size p, from the

@@ -23,6 +23,7 @@ Json MachineSpecification::to_json() const {
   j["collective_latency"] = collective_latency;
   j["xgmi_links"] = xgmi_links;
   j["xgmi_link_bandwidth"] = xgmi_link_bandwidth;
+  j["bf16_compute"] = bf16_compute;
   auto bwmap = [](const std::map<int, double>& m) {
     Json o = Json::object();
     for (auto const& kv : m) o[std::to_string(kv.first)] = kv.second;
@@ -55,6 +56,7 @@ MachineSpecification MachineSpecification::from_json(const Json& j) {
   gd("collective_latency", s.collective_latency);
   gi("xgmi_links", s.xgmi_links);
   gd("xgmi_link_bandwidth", s.xgmi_link_bandwidth);
+  if (j.contains("bf16_compute")) s.bf16_compute = j.at("bf16_compute").as_bool();
   for (const char* key : {"collective_bw", "all_to_all_bw"}) {
     if (!j.contains(key)) continue;
     auto& m = std::string(key) == "collective_bw" ? s.collective_bw : s.all_to_all_bw;
@@ -421,7 +423,14 @@ OpCost CostModel::op_cost_uncached(const OpAttrs& op, const std::vector<Parallel
     c.backward = pe->bwd_ms * 1e-3;
     c.measured = true;
   } else {
-    OpWork w = estimate_op_work(op, ip, wp, op_);
+    // bytes at the dtype the executor computes in
+    auto compute_dtype = [&](std::vector<TensorShape> v) {
+      if (spec_.bf16_compute)
+        for (auto& t : v)
+          if (t.dtype == DataType::FLOAT) t.dtype = DataType::BFLOAT16;
+      return v;
+    };
+    OpWork w = estimate_op_work(op, compute_dtype(ip), compute_dtype(wp), compute_dtype(op_));
     if (w.matmul_like) {
       c.forward = gemm_time(w.flops, w.bytes, w.mfma_efficiency_hint);
       c.backward = 2.0 * c.forward;

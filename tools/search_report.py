@@ -81,6 +81,9 @@ def calibrate(calib_dir, names, out_path=None):
             with open(t) as fh:
                 cm.load_profiles(fh.read())
         sim = native.simulate(pcg, cm, 1, update_bytes_per_param=upd, sparse_embedding_update=sparse)
+        # the analytic MI355X model alone (no measured entries)
+        ana = native.simulate(pcg, native.cost_model(world=1, use_profiles=False), 1, update_bytes_per_param=upd,
+                              sparse_embedding_update=sparse)
         measured = None
         bpath = os.path.join(calib_dir, f"bench_{name}.json")
         if os.path.exists(bpath):
@@ -94,6 +97,9 @@ def calibrate(calib_dir, names, out_path=None):
                "sim_update_ms": round(1000 * sim["update_time"], 3), "measured_ms": measured,
                "error_pct": (round(100.0 * (1000 * sim["iteration_time"] - measured) / measured, 2)
                              if measured else None),
+               "analytic_ms": round(1000 * ana["iteration_time"], 3),
+               "analytic_error_pct": (round(100.0 * (1000 * ana["iteration_time"] - measured) / measured, 2)
+                                      if measured else None),
                "tables": [os.path.basename(t) for t in tables]}
         rows.append(row)
         print(json.dumps(row), flush=True)
