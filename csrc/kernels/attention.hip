@@ -935,7 +935,11 @@ void attention_fwd(const AttnTensors& t, int B, int H, int Sq, int Sk, int D, fl
   AttnParams P = make_params(t, B, H, Sq, Sk, D, scale);
   const unsigned nq = static_cast<unsigned>((Sq + 127) / 128), nbh = static_cast<unsigned>(B * H);
   dim3 grid = causal ? dim3(nbh, nq) : dim3(nq, nbh), block(256);
-  // read per call (not cached): the A/B tests switch it inside one process
+  // read per call (not cached): the A/B tests switch it inside one process.
+  // Opt-in: 2 waves / SIMD (226 VGPRs) against the default's 3, and slower at
+  // both bench shapes (BERT 0.145 vs 0.118 ms, GPT causal 0.253 vs 0.212 ms,
+  // profiles/r4/attn_pipe_ab_r4.jsonl): the third wave hides more than the
+  // in-wave overlap gains
   const char* pe = getenv("FFK_ATTN_FWD_PIPE");
   const int pipe = pe ? atoi(pe) : 0;
   if (pipe && D == 64) {
