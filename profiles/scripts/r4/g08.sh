@@ -35,3 +35,5 @@ for SH in "1024 4096 32768 1 0 6:4 3:4" "32768 1024 4096 0 1 6:1 4:1"; do
   done
 done
 echo gemm pmc done
+cd $R && timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r4g08/bench_bert.json 2> gpurun_out/r4g08/bench_bert.err || exit 1
+tail -1 gpurun_out/r4g08/bench_bert.json | cut -c1-200
