@@ -360,7 +360,9 @@ def embedding_bwd(idx, dout, dweight, aggr: str = "none"):
     # contributions per (copy, row) and a workspace of at most 64 MiB
     rows = B * L
     copies = 1
-    if rows > 8 * n:
+    # tables of <= 8 rows without bags take the register-accumulating kernel
+    # (embedding.hip embed_bwd_small_kernel): no replicas
+    if rows > 8 * n and not (n <= 8 and aggr == "none"):
         copies = int(min(256, rows // (8 * n), max(1, (64 << 20) // max(1, n * D * 4))))
     ws = torch.zeros(copies * n * D, device=dweight.device, dtype=torch.float32) if copies > 1 else None
     ext().embedding_bwd(_dt(dout), 64 if idx.dtype == torch.int64 else 32, _p(idx), _p(dout), _p(dweight), B, L, D,

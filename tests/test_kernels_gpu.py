@@ -169,6 +169,19 @@ def test_embedding(aggr):
     assert _rel(dW, Wf.grad) < 1e-2
 
 
+@pytest.mark.parametrize("n,rows,D", [(2, 32768, 1024), (5, 3000, 768), (8, 100, 64), (1, 513, 136)])
+def test_embedding_small_table_backward(n, rows, D):
+    """Token-type sized tables (<= 8 rows): register-accumulated backward."""
+    torch.manual_seed(12)
+    idx = torch.randint(0, n, (rows,), device=DEV)
+    dout = torch.randn(rows, D, device=DEV, dtype=torch.bfloat16)
+    dW = torch.full((n, D), 0.5, device=DEV)
+    K.embedding_bwd(idx, dout, dW, "none")
+    ref = torch.full((n, D), 0.5, device=DEV).index_add_(0, idx, dout.float())
+    torch.cuda.synchronize()
+    assert _rel(dW, ref) < 1e-4
+
+
 def _ref_attn(q, k, v, causal):
     qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))  # [B,H,S,D]
     s = qf @ kf.transpose(-1, -2) / math.sqrt(q.shape[-1])
