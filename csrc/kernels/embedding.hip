@@ -134,41 +134,62 @@ __global__ __launch_bounds__(256) void embed_bwd_wave_kernel(const I* __restrict
 
 // Tiny tables (token-type / segment embeddings: num_entries <= E <= 8, no
 // bag): every lookup row lands in one of E table rows, so a scatter of fp32
-// atomics is all same-address contention.  Instead each thread owns one 8-
-// column chunk of a strided set of rows and keeps E x 8 partial sums in
-// registers (the entry selected by predication, no dynamic register index),
-// then adds them with E x 8 atomics: ~1M atomics for 32k rows x 1024 columns
-// instead of 33M.
+// atomics is all same-address contention.  Instead: E masked column sums,
+// laid out like colsum_act (elementwise.hip) — a block's 4 waves cover 512
+// columns (8 per lane) of a slab of rows, 8 rows in flight per wave, the
+// entry picked by predication (no dynamic register index); the waves' sums
+// meet in LDS and each block adds E x 512 values with one atomic each.
 template <typename T, typename I, int E>
 __global__ __launch_bounds__(256) void embed_bwd_small_kernel(const I* __restrict__ idx, const T* __restrict__ dout,
                                                               float* __restrict__ dW, int64_t rows, int D,
                                                               int64_t num_entries) {
-  const int cpr = D / 8;
-  const int64_t g = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  const int64_t lanes = (static_cast<int64_t>(gridDim.x) * 256) / cpr;   // row lanes
-  if (g >= lanes * cpr) return;
-  const int col = static_cast<int>(g % cpr) * 8;
+  __shared__ float red[4][E][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + lane * 8;
+  const bool active = col < D;
   float acc[E][8];
 #pragma unroll
   for (int q = 0; q < E; ++q)
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[q][k] = 0.f;
-  for (int64_t r = g / cpr; r < rows; r += lanes) {
-    const int64_t e = static_cast<int64_t>(idx[r]);
-    float v[8];
-    load8<T>(dout + r * D + col, v);
+  const int64_t per = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  constexpr int U = 8;
+  if (active) {
+    for (int64_t r = r0 + wave; r < r1; r += 4 * U) {
+      float v[U][8];
+      int64_t e[U];
 #pragma unroll
-    for (int q = 0; q < E; ++q) {
-      const float m = (e == q) ? 1.f : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = r + 4 * u;
+        if (rr < r1) {
+          e[u] = static_cast<int64_t>(idx[rr]);
+          load8<T>(dout + rr * D + col, v[u]);
+        } else {
+          e[u] = -1;
+        }
+      }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[q][k] += m * v[k];
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+          const float m = (e[u] == q) ? 1.f : 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[q][k] += m * v[u][k];
+        }
     }
   }
 #pragma unroll
-  for (int q = 0; q < E; ++q) {
-    if (q >= num_entries) break;
+  for (int q = 0; q < E; ++q)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(dW + static_cast<int64_t>(q) * D + col + k, acc[q][k]);
+    for (int k = 0; k < 8; ++k) red[wave][q][lane * 8 + k] = acc[q][k];
+  __syncthreads();
+  for (int j = threadIdx.x; j < E * 512; j += 256) {
+    const int q = j / 512, c = j % 512;
+    const int cc = blockIdx.x * 512 + c;
+    if (q < num_entries && cc < D)
+      atomicAdd(dW + static_cast<int64_t>(q) * D + cc, red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c]);
   }
 }
 
@@ -206,11 +227,14 @@ void embedding_bwd(int dtype, int index_bits, const void* idx, const void* dout,
                    int mode, int64_t num_entries, float* workspace, int copies, hipStream_t st) {
   if (D % 8 != 0) throw std::invalid_argument("embedding: dim must be a multiple of 8");
   if (copies < 1) copies = 1;
-  if (num_entries <= 8 && L == 1 && mode == 0 && D / 8 <= 256 * 256) {
+  if (num_entries <= 8 && L == 1 && mode == 0) {
     const int64_t rows = B;
-    const int grid = 256;   // 65536 threads: ~rows / (65536 / (D / 8)) rows each
+    // ~1024 blocks in total, >= 64 rows per block (colsum_act's split)
+    const int gx = (D + 511) / 512;
+    const int gy = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((1024 + gx - 1) / gx, (rows + 63) / 64)));
+    const dim3 grid(gx, gy);
 #define FFK_ES(T, I, EE)                                                                                      \
-  hipLaunchKernelGGL((embed_bwd_small_kernel<T, I, EE>), dim3(grid), dim3(256), 0, st,                        \
+  hipLaunchKernelGGL((embed_bwd_small_kernel<T, I, EE>), grid, dim3(256), 0, st,                              \
                      static_cast<const I*>(idx), static_cast<const T*>(dout), dW, rows, D, num_entries)
 #define FFK_ES_E(T, I)                                                                                        \
   if (num_entries <= 2) FFK_ES(T, I, 2);                                                                      \
