@@ -8,6 +8,8 @@
 // gathered whole; the backward scatter-adds fp32 rows with per-column atomics
 // shaped as contiguous 256-byte wave segments (guide G12), into the flat fp32
 // gradient buffer.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -227,7 +229,8 @@ void embedding_bwd(int dtype, int index_bits, const void* idx, const void* dout,
                    int mode, int64_t num_entries, float* workspace, int copies, hipStream_t st) {
   if (D % 8 != 0) throw std::invalid_argument("embedding: dim must be a multiple of 8");
   if (copies < 1) copies = 1;
-  if (num_entries <= 8 && L == 1 && mode == 0) {
+  const char* se = getenv("FFK_EMB_SMALL");   // read per call: A/B and bisection switch
+  if (num_entries <= 8 && L == 1 && mode == 0 && !(se && atoi(se) == 0)) {
     const int64_t rows = B;
     // ~1024 blocks in total, >= 64 rows per block (colsum_act's split)
     const int gx = (D + 511) / 512;

@@ -362,7 +362,8 @@ def embedding_bwd(idx, dout, dweight, aggr: str = "none"):
     copies = 1
     # tables of <= 8 rows without bags take the register-accumulating kernel
     # (embedding.hip embed_bwd_small_kernel): no replicas
-    if rows > 8 * n and not (n <= 8 and aggr == "none"):
+    small = n <= 8 and aggr == "none" and os.environ.get("FFK_EMB_SMALL", "1") != "0"
+    if rows > 8 * n and not small:
         copies = int(min(256, rows // (8 * n), max(1, (64 << 20) // max(1, n * D * 4))))
     ws = torch.zeros(copies * n * D, device=dweight.device, dtype=torch.float32) if copies > 1 else None
     ext().embedding_bwd(_dt(dout), 64 if idx.dtype == torch.int64 else 32, _p(idx), _p(dout), _p(dweight), B, L, D,
