@@ -170,16 +170,18 @@ __global__ __launch_bounds__(256) void embed_bwd_small_kernel(const I* __restric
           load8<T>(dout + rr * D + col, v[u]);
         } else {
           e[u] = -1;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[u][k] = 0.f;
         }
       }
+      // select, not multiply-by-mask: 0 * (inf or nan) of a row that belongs
+      // to another entry would poison the sum
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int q = 0; q < E; ++q) {
-          const float m = (e[u] == q) ? 1.f : 0.f;
+        for (int q = 0; q < E; ++q)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) acc[q][k] += m * v[u][k];
-        }
+          for (int k = 0; k < 8; ++k) acc[q][k] += (e[u] == q) ? v[u][k] : 0.f;
     }
   }
 #pragma unroll

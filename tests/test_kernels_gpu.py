@@ -180,6 +180,14 @@ def test_embedding_small_table_backward(n, rows, D):
     ref = torch.full((n, D), 0.5, device=DEV).index_add_(0, idx, dout.float())
     torch.cuda.synchronize()
     assert _rel(dW, ref) < 1e-4
+    # a non-finite gradient row stays in its own table row
+    if n > 1 and rows >= 2:
+        dout[0] = float("inf")
+        dW2 = torch.zeros(n, D, device=DEV)
+        K.embedding_bwd(idx, dout, dW2, "none")
+        torch.cuda.synchronize()
+        other = [e for e in range(n) if e != int(idx[0])]
+        assert torch.isfinite(dW2[other]).all()
 
 
 def _ref_attn(q, k, v, causal):
