@@ -708,8 +708,9 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (STG == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // B of tile kt+1 landed
-    if (STG == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (nothing newer in flight)
+    // (DBG 128: no wait — a timing ablation of the exposed load latency)
+    if (STG == 1 && !(DBG & 128)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // B of tile kt+1 landed
+    if (STG == 2 && !(DBG & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // k-step 1 reads + LDS writes done
     if (!(DBG & 4)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -946,8 +947,17 @@ void launch_pers(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hi
   }
 }
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, int S>
 void launch_dbg(const GemmTArgs& g, dim3 grid, dim3 block, hipStream_t st) {
+  if constexpr (S != 0) {   // LDS-DMA forms: the load-wait ablation only
+    switch (g.dbg) {
+      case 128: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 128>), grid, block, 0, st, g); break;
+      case 136: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 136>), grid, block, 0, st, g); break;
+      case 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 8>), grid, block, 0, st, g); break;
+      default: throw std::invalid_argument("gemmt: unsupported ablation bits");
+    }
+    return;
+  }
   switch (g.dbg) {
     case 1: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 1>), grid, block, 0, st, g); break;
     case 2: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, 0, 2>), grid, block, 0, st, g); break;
@@ -963,8 +973,8 @@ void launch_dbg(const GemmTArgs& g, dim3 grid, dim3 block, hipStream_t st) {
 
 template <bool TA, bool TB, int S>
 void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
-  if constexpr (!TA && S == 0) {
-    if (g.dbg && epi == kEpiPlain) return launch_dbg<TA, TB>(g, grid, block, st);
+  if constexpr (!TA) {
+    if (g.dbg && epi == kEpiPlain) return launch_dbg<TA, TB, S>(g, grid, block, st);
   }
   switch (epi * 8 + act) {
     case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S>), grid, block, 0, st, g); break;

@@ -5,8 +5,10 @@ waits or barriers removed the results are garbage).  gemmp / gemmq (variants
 NN / NT only, ``--gemmt``): 1 = no global loads in the loop, 2 = no LDS
 writes (the loads then die too), 4 = no mid-tile barrier, 8 = no epilogue,
 15 = all of them (MFMAs + fragment reads only), 16 = non-temporal epilogue stores, 32 = C staged through
-LDS and stored as whole rows (a correct result: its error is reported).  Interleaved rounds in one
-process:  python tools/gemm_ablate.py [--gemmt]"""
+LDS and stored as whole rows (a correct result: its error is reported).  LDS-DMA forms
+(GEMMT_ABL_VARIANT=4 or 6): 128 = no wait for the next K-tile's loads (exposed load latency),
+8 = no epilogue, 136 = both.  Interleaved rounds in one
+process:  [GEMMT_ABL_VARIANT=6 GEMMT_DBG=0,128,8,136] python tools/gemm_ablate.py [--gemmt]"""
 import json
 import os
 import statistics
@@ -34,9 +36,10 @@ def main():
             if ta:
                 continue
             cands["blaslt"] = lambda: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=out)
+            var = int(os.environ.get("GEMMT_ABL_VARIANT", "3"))
             for dbg in [int(x) for x in os.environ.get("GEMMT_DBG", "0,8,32").split(",")]:
                 cands[f"t_d{dbg}"] = lambda dbg=dbg: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=out, splits=sp,
-                                                             variant=3, _dbg=dbg)
+                                                             variant=var, _dbg=dbg)
         else:
             for v in (0, 1):
                 for dbg in (0, 1, 2, 3):
