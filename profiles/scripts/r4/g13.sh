@@ -5,6 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r4g13
 export TMPDIR=/tmp
+export FF_BENCH_REHEARSAL=1   # gloo on one GPU is allowed, the JSON line names the backend
 FF_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29517 bench.py --model bert-large --gpus 2 --steps 3 --warmup 1 \
   --batch-per-gpu 16 > gpurun_out/r4g13/bert_2rank.json 2> gpurun_out/r4g13/bert_2rank.err \
