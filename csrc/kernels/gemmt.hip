@@ -740,6 +740,228 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     epilogue<EPI, ACT, (DBG & 16) != 0, STAGE_C>(g, acc, m0, n0, split, wm, wn, lane, smem + wave * 32768);
 }
 
+// ---- Both operands K-outer (C = A^T B, the weight-gradient GEMMs), LDS-DMA
+// staged into PADDED images so every fragment read is one base VGPR plus an
+// immediate offset.
+//
+// The swizzled 256-B-row image above spreads the 8 rows a 32-lane group reads
+// over the banks by XOR-ing the 16-B chunk with row bits, i.e. with the bits
+// that also select the 16-column block mb: each (mb, half) fragment address
+// is a different per-lane value, and the loop spent 104 v_add_u32 per K-tile
+// (next to 128 MFMAs and 64 transposed reads) re-forming them from the buffer
+// pointer.  Here a half image is 64 k-rows of 128 columns at a 288-B pitch
+// (256 B + 32 B pad, so consecutive physical rows start 32 B = 8 banks
+// apart) with k-row bits 2 and 3 swapped: the rows a 32-lane group reads,
+// 8g + {0..3} for g = 0, 1 (and + 4 for the second read, + 16 for g = 2, 3),
+// land on 8 consecutive physical rows = 8 distinct 32-B bank groups.  A
+// fragment address is then
+//   lane base + buffer * KK_PT + ks * 32 rows + mb * 32 B (+ 4 rows for the
+//   second half-read)
+// with everything after the lane base a compile-time immediate of
+// ds_read_b64_tr_b16 (< 64 KiB with the LDS order [A0][A1][B0][B1]).
+// The DMA writes each 1-KiB piece lane-linearly; a lane's global source is
+// the element its physical slot holds (pad slots re-load a neighbour's 16 B
+// of the same row).  A half is 18 pieces: 9 per wave per operand.
+constexpr int KK_PITCH = 288;
+constexpr int KK_PH = 64 * KK_PITCH;   // one 128-column half image (18 KiB)
+constexpr int KK_PT = 2 * KK_PH;       // one operand tile
+constexpr int KK_NP = 9;               // DMA pieces per wave per operand tile
+
+__device__ __forceinline__ int kk_swap23(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+// per-lane voffset (bytes, K-tile 0) of DMA piece i of `wave` (half wave >> 1)
+__device__ __forceinline__ unsigned kk_dma_voff(int ld, int outer0, int i, int wave, int lane) {
+  const int b = (9 * (wave & 1) + i) * 1024 + lane * 16;
+  const int prow = b / KK_PITCH;
+  int w = b - prow * KK_PITCH;
+  if (w >= 256) w -= 32;   // pad slot: same row, a neighbour's bytes
+  const int r = kk_swap23(prow);
+  const int col = (wave >> 1) * 128 + w / 2;
+  return (static_cast<unsigned>(r) * static_cast<unsigned>(ld) + static_cast<unsigned>(outer0 + col)) * 2u;
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x4 kk_tr(unsigned a) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+// fragment (k-step KS, 16-column block MB) of buffer BUF; base = lane base
+// fragment (k-step KS, 16-column block MB) of the buffer whose lane base is `base`
+template <int KS, int MB>
+__device__ __forceinline__ bf16x8 kk_frag(unsigned base) {
+  constexpr int O = KS * 32 * KK_PITCH + MB * 32;
+  return cat44(kk_tr<O>(base), kk_tr<O + 8 * KK_PITCH>(base));   // k-row + 4 = physical row + 8
+}
+
+// K-contiguous A operand (gemmt_kernel's 128-B-row image): 16-row block MB
+// of the k-step whose lane base is `base`
+template <int MB>
+__device__ __forceinline__ bf16x8 kk_row(unsigned base) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(MB * 16 * 128));
+  return r;
+}
+
+template <typename F, int... I>
+__device__ __forceinline__ void kk_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// TA: A K-outer (padded image, as B); !TA: A K-contiguous (gemmt_kernel's
+// swizzled 128-B-row image, ds_read_b128 at lane base + immediate)
+template <bool TA, int EPI, int ACT>
+__global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kk_kernel(
+    GemmTArgs g) {
+  constexpr int SA = TA ? KK_PT : 2 * HALF;   // A tile bytes per buffer
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SA + 2 * KK_PT];  // [A0][A1][B0][B1]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int gm = (g.M + TM - 1) / TM, gn = (g.N + TN - 1) / TN;
+  const int nwg = gm * gn;
+  const int bid = xcd_remap(blockIdx.x, nwg * g.splits);
+  const int split = bid / nwg, t = bid % nwg;
+  const int per_group = GROUP * gn;
+  const int first_m = (t / per_group) * GROUP;
+  const int gsize = min(gm - first_m, GROUP);
+  const int m0 = (first_m + (t % per_group) % gsize) * TM;
+  const int n0 = ((t % per_group) / gsize) * TN;
+  const int KT = g.K / TK, Lb = KT / g.splits, rem = KT % g.splits;
+  const int L = Lb + (split < rem ? 1 : 0);
+  const int kt0 = split * Lb + min(split, rem);
+
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.A), static_cast<short>(0), g.bytesA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.B), static_cast<short>(0), g.bytesB, 0x00020000);
+  const unsigned kstepA = TA ? static_cast<unsigned>(TK * g.lda * 2) : TK * 2u;
+  const unsigned kstepB = static_cast<unsigned>(TK * g.ldb * 2);
+  unsigned dvA[KK_NP], dvB[KK_NP];
+#pragma unroll
+  for (int i = 0; i < KK_NP; ++i) {
+    dvA[i] = TA ? kk_dma_voff(g.lda, m0, i, wave, lane) : i < 2 ? dma_voff<false>(g.lda, m0, i, wave, lane) : 0u;
+    dvB[i] = kk_dma_voff(g.ldb, n0, i, wave, lane);
+  }
+  // this wave's first DMA piece of an operand tile (buffer 0)
+  const int dpiece = (wave >> 1) * KK_PH + 9 * (wave & 1) * 1024;
+  unsigned char* const sA = smem;
+  unsigned char* const sB = smem + 2 * SA;
+  auto dmaB = [&](int buf, unsigned kbyte, int i) __attribute__((always_inline)) {
+    dma16(rB, sB + buf * KK_PT + dpiece + i * 1024, dvB[i], __builtin_amdgcn_readfirstlane(kbyte));
+  };
+  // K-contiguous A: 8 pieces per wave, KiB j = 8 wave + i = rows 8j..8j+7,
+  // per-lane voffset by i & 1 and the rows beyond in the scalar offset
+  auto dmaA = [&](int buf, unsigned kbyte, int i) __attribute__((always_inline)) {
+    if (TA) {
+      dma16(rA, sA + buf * SA + dpiece + i * 1024, dvA[i], __builtin_amdgcn_readfirstlane(kbyte));
+    } else {
+      const unsigned so = kbyte + static_cast<unsigned>(8 * (i - (i & 1))) * static_cast<unsigned>(g.lda) * 2u;
+      dma16(rA, sA + buf * SA + (wave * 8 + i) * 1024, dvA[i & 1], __builtin_amdgcn_readfirstlane(so));
+    }
+  };
+
+  // lane base of the fragment reads (LDS byte address)
+  const int gq = lane >> 4, iq = lane & 15;
+  const int lrow = kk_swap23(8 * gq + (iq >> 2));
+  const unsigned lds0 = static_cast<unsigned>(
+      reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) unsigned char*)smem));
+  const unsigned lbase = lds0 + static_cast<unsigned>(lrow * KK_PITCH + 8 * (iq & 3));
+  const unsigned baseB = lbase + static_cast<unsigned>(2 * SA + wn * KK_PH);
+  // A lane bases of k-step 0 / 1 (the K-outer image takes the k-step as an immediate)
+  auto rowbase = [&](int ks) -> unsigned {
+    const int r = lane & 15;
+    return lds0 + static_cast<unsigned>((wm * 128 + r) * 128 + (t_slot128(r, ks * 4 + (lane >> 4)) << 4));
+  };
+  const unsigned baseA0 = TA ? lbase + static_cast<unsigned>(wm * KK_PH) : rowbase(0);
+  const unsigned baseA1 = TA ? baseA0 : rowbase(1);
+
+  f32x4t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4t{};
+  bf16x8 fa[8], fbx[8], fby[8];
+  constexpr auto S8 = std::make_integer_sequence<int, 8>{};
+
+  auto readA = [&](auto KSC, auto MBC, unsigned base) __attribute__((always_inline)) -> bf16x8 {
+    constexpr int ks = decltype(KSC)::value, mb = decltype(MBC)::value;
+    if constexpr (TA) return kk_frag<ks, mb>(base);
+    else return kk_row<mb>(base);
+  };
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+
+  // ---- prologue: tile 0 -> buffer 0, tile 1 -> buffer 1, k-step 0 fragments
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+#pragma unroll
+    for (int i = 0; i < (TA ? KK_NP : 8); ++i) dmaA(b, static_cast<unsigned>(kt0 + b) * kstepA, i);
+#pragma unroll
+    for (int i = 0; i < KK_NP; ++i) dmaB(b, static_cast<unsigned>(kt0 + b) * kstepB, i);
+  }
+  // tile 0 landed (tile 1's 18 / 17 pieces in flight)
+  if constexpr (TA) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  kk_for([&](auto MB) __attribute__((always_inline)) {
+    constexpr int mb = decltype(MB)::value;
+    fa[mb] = readA(K0{}, MB, baseA0);
+    fbx[mb] = kk_frag<0, mb>(baseB);
+  }, S8);
+
+  // same two-phase schedule as gemmt_kernel STG 2; the buffer's lane bases
+  // are the only per-tile VALU work (4 adds)
+  for (int kt = 0; kt < L; ++kt) {
+    const int cur = kt & 1;
+    const unsigned pa = static_cast<unsigned>(cur * SA), pna = static_cast<unsigned>((cur ^ 1) * SA);
+    const unsigned pb = static_cast<unsigned>(cur * KK_PT), pnb = static_cast<unsigned>((cur ^ 1) * KK_PT);
+    const unsigned aC = baseA1 + pa, bC = baseB + pb, aN = baseA0 + pna, bN = baseB + pnb;
+    const unsigned ka = static_cast<unsigned>(kt0 + kt + 2) * kstepA;
+    const unsigned kb = static_cast<unsigned>(kt0 + kt + 2) * kstepB;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // phase A: k-step 0 (fa, fbx) | read k-step 1 of the current buffer into (fa, fby)
+    kk_for([&](auto MB) __attribute__((always_inline)) {
+      constexpr int mb = decltype(MB)::value;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
+      fa[mb] = readA(K1{}, MB, aC);
+      fby[mb] = kk_frag<1, mb>(bC);
+    }, S8);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile kt+1 (next buffer) landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // k-step 1 reads done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // phase B: k-step 1 (fa, fby) | read k-step 0 of the next buffer into (fa, fbx),
+    // DMA tile kt+2 into the current one (its reads retired at the barrier)
+    kk_for([&](auto MB) __attribute__((always_inline)) {
+      constexpr int mb = decltype(MB)::value;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
+      fa[mb] = readA(K0{}, MB, aN);
+      fbx[mb] = kk_frag<0, mb>(bN);
+      dmaA(cur, ka, mb);
+      dmaB(cur, kb, mb);
+      if (mb == 7) {
+        if (TA) dmaA(cur, ka, 8);
+        dmaB(cur, kb, 8);
+      }
+    }, S8);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) if (0) asm volatile("" : "+a"(acc[i][j]));
+  epilogue<EPI, ACT, false, false>(g, acc, m0, n0, split, wm, wn, lane, nullptr);
+}
+
 // Persistent form (variant 5): one workgroup per CU walks its work items
 // (tiles x K-splits) b, b + grid, ...; the K-tile stream runs on across item
 // boundaries, so the last two iterations of an item already stage the next
@@ -999,6 +1221,39 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
   }
 }
 
+template <bool TA>
+void launch_kk(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
+  switch (epi * 8 + act) {
+    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0>), grid, block, 0, st, g); break;
+    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0>), grid, block, 0, st, g); break;
+    case kEpiGeneral * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0>), grid, block, 0, st, g); break;
+    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0>), grid, block, 0, st, g); break;
+    case kEpiBiasAct * 8 + 0:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0>), grid, block, 0, st, g);
+      break;
+    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0>), grid, block, 0, st, g); break;
+    case kEpiBiasAct * 8 + 1:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 4:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4>), grid, block, 0, st, g);
+      break;
+    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4>), grid, block, 0, st, g); break;
+    default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
+  }
+}
+
+// padded-image kernel for A^T B and A B: opt-in (FFK_GEMMT_KK=1) until its
+// GPU A/B against the swizzled-image gemmt_kernel is in
+bool kk_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("FFK_GEMMT_KK");
+    return e != nullptr && e[0] != '0';
+  }();
+  return on;
+}
+
 }  // namespace
 
 // the bias / activation / activation-gradient and plain bf16 epilogues take
@@ -1044,10 +1299,18 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
     else if (p.trans_a && !p.trans_b) launch_pers<true, false>(g, pgrid, block, epi, p.act, st);
     else launch_pers<true, true>(g, pgrid, block, epi, p.act, st);
   } else if (stage_mode == 3) {   // both operands by LDS-DMA
-    if (!p.trans_a && !p.trans_b) launch_t<false, false, 2>(g, grid, block, epi, p.act, st);
-    else if (!p.trans_a && p.trans_b) launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
-    else if (p.trans_a && !p.trans_b) launch_t<true, false, 2>(g, grid, block, epi, p.act, st);
-    else launch_t<true, true, 2>(g, grid, block, epi, p.act, st);
+    const bool kk = kk_enabled() && !p.dbg;
+    if (!p.trans_a && !p.trans_b) {
+      if (kk) launch_kk<false>(g, grid, block, epi, p.act, st);
+      else launch_t<false, false, 2>(g, grid, block, epi, p.act, st);
+    } else if (!p.trans_a && p.trans_b) {
+      launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
+    } else if (p.trans_a && !p.trans_b) {
+      if (kk) launch_kk<true>(g, grid, block, epi, p.act, st);
+      else launch_t<true, false, 2>(g, grid, block, epi, p.act, st);
+    } else {
+      launch_t<true, true, 2>(g, grid, block, epi, p.act, st);
+    }
   } else if (stage_mode == 1) {
     if (!p.trans_a && !p.trans_b) launch_t<false, false, 1>(g, grid, block, epi, p.act, st);
     else if (!p.trans_a && p.trans_b) launch_t<false, true, 1>(g, grid, block, epi, p.act, st);
