@@ -810,7 +810,7 @@ __device__ __forceinline__ void kk_for(F&& f, std::integer_sequence<int, I...>) 
 
 // TA: A K-outer (padded image, as B); !TA: A K-contiguous (gemmt_kernel's
 // swizzled 128-B-row image, ds_read_b128 at lane base + immediate)
-template <bool TA, int EPI, int ACT>
+template <bool TA, int EPI, int ACT, int SCH = 0>
 __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kk_kernel(
     GemmTArgs g) {
   constexpr int SA = TA ? KK_PT : 2 * HALF;   // A tile bytes per buffer
@@ -913,6 +913,47 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     fbx[mb] = kk_frag<0, mb>(baseB);
   }, S8);
 
+  // SCH 1: one side instruction after each MFMA of an 8-MFMA group (the B
+  // fragment's two reads, the A fragment's read(s), then the group's DMA
+  // pieces), each pinned by sched_barrier, instead of the group's reads
+  // clustered after its 8 MFMAs
+  auto group = [&](auto MBC, auto KSC, const bf16x8 (&fin)[8], bf16x8 (&fout)[8], unsigned aB, unsigned bB,
+                   int dbuf, unsigned ka_, unsigned kb_) __attribute__((always_inline)) {
+    constexpr int mb = decltype(MBC)::value, ks = decltype(KSC)::value;
+    constexpr int OB = ks * 32 * KK_PITCH + mb * 32;
+    bf16x4 b0, b1, a0, a1;
+    bf16x8 ar;
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][0] = mfma16(fin[0], fa[mb], acc[mb][0]);
+    b0 = kk_tr<OB>(bB);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][1] = mfma16(fin[1], fa[mb], acc[mb][1]);
+    b1 = kk_tr<OB + 8 * KK_PITCH>(bB);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][2] = mfma16(fin[2], fa[mb], acc[mb][2]);
+    if constexpr (TA) a0 = kk_tr<OB>(aB);
+    else ar = kk_row<mb>(aB);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][3] = mfma16(fin[3], fa[mb], acc[mb][3]);
+    if constexpr (TA) a1 = kk_tr<OB + 8 * KK_PITCH>(aB);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][4] = mfma16(fin[4], fa[mb], acc[mb][4]);
+    if (dbuf >= 0) dmaA(dbuf, ka_, mb);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][5] = mfma16(fin[5], fa[mb], acc[mb][5]);
+    if (dbuf >= 0) dmaB(dbuf, kb_, mb);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][6] = mfma16(fin[6], fa[mb], acc[mb][6]);
+    if (dbuf >= 0 && mb == 7 && TA) dmaA(dbuf, ka_, 8);
+    __builtin_amdgcn_sched_barrier(0);
+    acc[mb][7] = mfma16(fin[7], fa[mb], acc[mb][7]);
+    if (dbuf >= 0 && mb == 7) dmaB(dbuf, kb_, 8);
+    __builtin_amdgcn_sched_barrier(0);
+    fout[mb] = cat44(b0, b1);
+    if constexpr (TA) fa[mb] = cat44(a0, a1);
+    else fa[mb] = ar;
+  };
+
   // same two-phase schedule as gemmt_kernel STG 2; the buffer's lane bases
   // are the only per-tile VALU work (4 adds)
   for (int kt = 0; kt < L; ++kt) {
@@ -926,11 +967,15 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     // phase A: k-step 0 (fa, fbx) | read k-step 1 of the current buffer into (fa, fby)
     kk_for([&](auto MB) __attribute__((always_inline)) {
       constexpr int mb = decltype(MB)::value;
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SCH == 0) {
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
-      fa[mb] = readA(K1{}, MB, aC);
-      fby[mb] = kk_frag<1, mb>(bC);
+        for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
+        fa[mb] = readA(K1{}, MB, aC);
+        fby[mb] = kk_frag<1, mb>(bC);
+      } else {
+        group(MB, K1{}, fbx, fby, aC, bC, -1, 0u, 0u);
+      }
     }, S8);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile kt+1 (next buffer) landed
@@ -941,16 +986,20 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     // DMA tile kt+2 into the current one (its reads retired at the barrier)
     kk_for([&](auto MB) __attribute__((always_inline)) {
       constexpr int mb = decltype(MB)::value;
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SCH == 0) {
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
-      fa[mb] = readA(K0{}, MB, aN);
-      fbx[mb] = kk_frag<0, mb>(bN);
-      dmaA(cur, ka, mb);
-      dmaB(cur, kb, mb);
-      if (mb == 7) {
-        if (TA) dmaA(cur, ka, 8);
-        dmaB(cur, kb, 8);
+        for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
+        fa[mb] = readA(K0{}, MB, aN);
+        fbx[mb] = kk_frag<0, mb>(bN);
+        dmaA(cur, ka, mb);
+        dmaB(cur, kb, mb);
+        if (mb == 7) {
+          if (TA) dmaA(cur, ka, 8);
+          dmaB(cur, kb, 8);
+        }
+      } else {
+        group(MB, K0{}, fby, fbx, aN, bN, cur, ka, kb);
       }
     }, S8);
     __builtin_amdgcn_sched_barrier(0);
@@ -1221,27 +1270,40 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
   }
 }
 
-template <bool TA>
-void launch_kk(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
+template <bool TA, int SCH>
+void launch_kk_s(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
   switch (epi * 8 + act) {
-    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0>), grid, block, 0, st, g); break;
-    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0>), grid, block, 0, st, g); break;
-    case kEpiGeneral * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0>), grid, block, 0, st, g); break;
-    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0>), grid, block, 0, st, g); break;
+    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0, SCH>), grid, block, 0, st, g); break;
+    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0, SCH>), grid, block, 0, st, g); break;
+    case kEpiGeneral * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0, SCH>), grid, block, 0, st, g); break;
+    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0, SCH>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 0:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0, SCH>), grid, block, 0, st, g);
       break;
-    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0>), grid, block, 0, st, g); break;
+    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0, SCH>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 1:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1, SCH>), grid, block, 0, st, g);
       break;
     case kEpiBiasAct * 8 + 4:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4, SCH>), grid, block, 0, st, g);
       break;
-    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1>), grid, block, 0, st, g); break;
-    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1, SCH>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4, SCH>), grid, block, 0, st, g); break;
     default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
   }
+}
+
+// interleaved group schedule by default: 1.5-11 % faster per GEMM and +0.7 %
+// on the BERT-large step (profiles/r4/ab_gemmt_kk_sched_r4.txt);
+// FFK_GEMMT_KK_SCHED=0 keeps the clustered one
+template <bool TA>
+void launch_kk(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
+  static const int sch = [] {
+    const char* e = std::getenv("FFK_GEMMT_KK_SCHED");
+    return e != nullptr && e[0] == '0' ? 0 : 1;
+  }();
+  if (sch == 1) launch_kk_s<TA, 1>(g, grid, block, epi, act, st);
+  else launch_kk_s<TA, 0>(g, grid, block, epi, act, st);
 }
 
 // padded-image kernel for A^T B and A B (FFK_GEMMT_KK=0 keeps the
