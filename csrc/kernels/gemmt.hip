@@ -502,7 +502,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* l
 // both by LDS-DMA (no staging registers, no ds_write in the loop)
 // DBG (timing ablations only, results are garbage): 1 = no global loads in
 // the loop, 2 = no LDS writes in the loop, 4 = no mid-tile barrier, 8 = no
-// epilogue
+// epilogue; 256 (STG 2, a schedule variant with valid results): each
+// group's fragment reads (and phase B's DMA issues) interleaved 1:1 with its
+// MFMAs
 template <bool TA, bool TB, int EPI, int ACT, int STG, int DBG = 0>
 __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kernel(
     GemmTArgs g) {
@@ -687,7 +689,14 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       // one memory instruction between MFMAs (an MFMA leaves the SIMD's issue
       // free for 8 of its 16 cycles); the fragment re-reads go last, after
       // the group's final use of fa[mb]
-      if (STG == 2) {
+      if (STG == 2 && (DBG & 256)) {   // reads interleaved 1:1 with the group's MFMAs
+#pragma unroll
+        for (int r = 0; r < NRD; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 - NRD, 0);
+      } else if (STG == 2) {
         __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
       } else {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -705,7 +714,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       } else {
         __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
+      if (!(STG == 2 && (DBG & 256))) __builtin_amdgcn_sched_group_barrier(0x100, NRD, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
     // (DBG 128: no wait — a timing ablation of the exposed load latency)
@@ -724,6 +733,19 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
       fbx[mb] = rdB(nxt, mb, 0);
       if (STG == 2) dmaA(cur, kt0 + kt + 2, mb);
       if (STG >= 1) dmaB(cur, kt0 + kt + 2, mb);  // tile kt's buffer: its reads retired at the barrier
+      if (STG == 2 && (DBG & 256)) {   // reads, then the two DMA issues, one per MFMA
+#pragma unroll
+        for (int r = 0; r < NRD; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 - NRD - 2, 0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -1223,6 +1245,7 @@ void launch_dbg(const GemmTArgs& g, dim3 grid, dim3 block, hipStream_t st) {
   if constexpr (S != 0) {   // LDS-DMA forms: the load-wait ablation only
     switch (g.dbg) {
       case 128: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 128>), grid, block, 0, st, g); break;
+      case 256: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 256>), grid, block, 0, st, g); break;
       case 136: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 136>), grid, block, 0, st, g); break;
       case 8: hipLaunchKernelGGL((gemmt_kernel<TA, TB, kEpiPlain, 0, S, 8>), grid, block, 0, st, g); break;
       default: throw std::invalid_argument("gemmt: unsupported ablation bits");

@@ -48,7 +48,7 @@ def main():
         errs = {}
         if "--gemmt" in sys.argv:
             ref = ((a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float()))
-            for k in ("t_d0", "t_d32"):
+            for k in ("t_d0", "t_d32", "t_d256"):
                 if k in cands:
                     cands[k]()
                     errs[k + "_err"] = round(((out.float() - ref).norm() / ref.norm()).item(), 5)
