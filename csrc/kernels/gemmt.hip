@@ -832,11 +832,12 @@ __device__ __forceinline__ void kk_for(F&& f, std::integer_sequence<int, I...>) 
 
 // TA: A K-outer (padded image, as B); !TA: A K-contiguous (gemmt_kernel's
 // swizzled 128-B-row image, ds_read_b128 at lane base + immediate)
-template <bool TA, int EPI, int ACT, int SCH = 0>
+template <bool TA, int EPI, int ACT, int SCH = 0, bool TB = false>
 __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kk_kernel(
     GemmTArgs g) {
   constexpr int SA = TA ? KK_PT : 2 * HALF;   // A tile bytes per buffer
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SA + 2 * KK_PT];  // [A0][A1][B0][B1]
+  constexpr int SB = TB ? 2 * HALF : KK_PT;   // B tile bytes per buffer (TB: K-contiguous image)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SA + 2 * SB];  // [A0][A1][B0][B1]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -860,19 +861,24 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   const __amdgpu_buffer_rsrc_t rB =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.B), static_cast<short>(0), g.bytesB, 0x00020000);
   const unsigned kstepA = TA ? static_cast<unsigned>(TK * g.lda * 2) : TK * 2u;
-  const unsigned kstepB = static_cast<unsigned>(TK * g.ldb * 2);
+  const unsigned kstepB = TB ? TK * 2u : static_cast<unsigned>(TK * g.ldb * 2);
   unsigned dvA[KK_NP], dvB[KK_NP];
 #pragma unroll
   for (int i = 0; i < KK_NP; ++i) {
     dvA[i] = TA ? kk_dma_voff(g.lda, m0, i, wave, lane) : i < 2 ? dma_voff<false>(g.lda, m0, i, wave, lane) : 0u;
-    dvB[i] = kk_dma_voff(g.ldb, n0, i, wave, lane);
+    dvB[i] = !TB ? kk_dma_voff(g.ldb, n0, i, wave, lane) : i < 2 ? dma_voff<false>(g.ldb, n0, i, wave, lane) : 0u;
   }
   // this wave's first DMA piece of an operand tile (buffer 0)
   const int dpiece = (wave >> 1) * KK_PH + 9 * (wave & 1) * 1024;
   unsigned char* const sA = smem;
   unsigned char* const sB = smem + 2 * SA;
   auto dmaB = [&](int buf, unsigned kbyte, int i) __attribute__((always_inline)) {
-    dma16(rB, sB + buf * KK_PT + dpiece + i * 1024, dvB[i], __builtin_amdgcn_readfirstlane(kbyte));
+    if (!TB) {
+      dma16(rB, sB + buf * SB + dpiece + i * 1024, dvB[i], __builtin_amdgcn_readfirstlane(kbyte));
+    } else {
+      const unsigned so = kbyte + static_cast<unsigned>(8 * (i - (i & 1))) * static_cast<unsigned>(g.ldb) * 2u;
+      dma16(rB, sB + buf * SB + (wave * 8 + i) * 1024, dvB[i & 1], __builtin_amdgcn_readfirstlane(so));
+    }
   };
   // K-contiguous A: 8 pieces per wave, KiB j = 8 wave + i = rows 8j..8j+7,
   // per-lane voffset by i & 1 and the rows beyond in the scalar offset
@@ -891,7 +897,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   const unsigned lds0 = static_cast<unsigned>(
       reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) unsigned char*)smem));
   const unsigned lbase = lds0 + static_cast<unsigned>(lrow * KK_PITCH + 8 * (iq & 3));
-  const unsigned baseB = lbase + static_cast<unsigned>(2 * SA + wn * KK_PH);
+
   // A lane bases of k-step 0 / 1 (the K-outer image takes the k-step as an immediate)
   auto rowbase = [&](int ks) -> unsigned {
     const int r = lane & 15;
@@ -899,6 +905,12 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   };
   const unsigned baseA0 = TA ? lbase + static_cast<unsigned>(wm * KK_PH) : rowbase(0);
   const unsigned baseA1 = TA ? baseA0 : rowbase(1);
+  auto rowbaseB = [&](int ks) -> unsigned {
+    const int r = lane & 15;
+    return lds0 + static_cast<unsigned>(2 * SA + (wn * 128 + r) * 128 + (t_slot128(r, ks * 4 + (lane >> 4)) << 4));
+  };
+  const unsigned baseB0 = TB ? rowbaseB(0) : lbase + static_cast<unsigned>(2 * SA + wn * KK_PH);
+  const unsigned baseB1 = TB ? rowbaseB(1) : baseB0;
 
   f32x4t acc[8][8];
 #pragma unroll
@@ -913,6 +925,11 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     if constexpr (TA) return kk_frag<ks, mb>(base);
     else return kk_row<mb>(base);
   };
+  auto readB = [&](auto KSC, auto MBC, unsigned base) __attribute__((always_inline)) -> bf16x8 {
+    constexpr int ks = decltype(KSC)::value, mb = decltype(MBC)::value;
+    if constexpr (TB) return kk_row<mb>(base);
+    else return kk_frag<ks, mb>(base);
+  };
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
 
@@ -922,17 +939,19 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
     for (int i = 0; i < (TA ? KK_NP : 8); ++i) dmaA(b, static_cast<unsigned>(kt0 + b) * kstepA, i);
 #pragma unroll
-    for (int i = 0; i < KK_NP; ++i) dmaB(b, static_cast<unsigned>(kt0 + b) * kstepB, i);
+    for (int i = 0; i < (TB ? 8 : KK_NP); ++i) dmaB(b, static_cast<unsigned>(kt0 + b) * kstepB, i);
   }
   // tile 0 landed (tile 1's 18 / 17 pieces in flight)
-  if constexpr (TA) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+  constexpr int NPT = (TA ? KK_NP : 8) + (TB ? 8 : KK_NP);   // DMA issues per K-tile per wave
+  if constexpr (NPT == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else if constexpr (NPT == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   kk_for([&](auto MB) __attribute__((always_inline)) {
     constexpr int mb = decltype(MB)::value;
     fa[mb] = readA(K0{}, MB, baseA0);
-    fbx[mb] = kk_frag<0, mb>(baseB);
+    fbx[mb] = readB(K0{}, MB, baseB0);
   }, S8);
 
   // SCH 1: one side instruction after each MFMA of an 8-MFMA group (the B
@@ -944,13 +963,14 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     constexpr int mb = decltype(MBC)::value, ks = decltype(KSC)::value;
     constexpr int OB = ks * 32 * KK_PITCH + mb * 32;
     bf16x4 b0, b1, a0, a1;
-    bf16x8 ar;
+    bf16x8 ar, br;
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][0] = mfma16(fin[0], fa[mb], acc[mb][0]);
-    b0 = kk_tr<OB>(bB);
+    if constexpr (TB) br = kk_row<mb>(bB);
+    else b0 = kk_tr<OB>(bB);
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][1] = mfma16(fin[1], fa[mb], acc[mb][1]);
-    b1 = kk_tr<OB + 8 * KK_PITCH>(bB);
+    if constexpr (!TB) b1 = kk_tr<OB + 8 * KK_PITCH>(bB);
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][2] = mfma16(fin[2], fa[mb], acc[mb][2]);
     if constexpr (TA) a0 = kk_tr<OB>(aB);
@@ -969,9 +989,10 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     if (dbuf >= 0 && mb == 7 && TA) dmaA(dbuf, ka_, 8);
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][7] = mfma16(fin[7], fa[mb], acc[mb][7]);
-    if (dbuf >= 0 && mb == 7) dmaB(dbuf, kb_, 8);
+    if (dbuf >= 0 && mb == 7 && !TB) dmaB(dbuf, kb_, 8);
     __builtin_amdgcn_sched_barrier(0);
-    fout[mb] = cat44(b0, b1);
+    if constexpr (TB) fout[mb] = br;
+    else fout[mb] = cat44(b0, b1);
     if constexpr (TA) fa[mb] = cat44(a0, a1);
     else fa[mb] = ar;
   };
@@ -981,8 +1002,8 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   for (int kt = 0; kt < L; ++kt) {
     const int cur = kt & 1;
     const unsigned pa = static_cast<unsigned>(cur * SA), pna = static_cast<unsigned>((cur ^ 1) * SA);
-    const unsigned pb = static_cast<unsigned>(cur * KK_PT), pnb = static_cast<unsigned>((cur ^ 1) * KK_PT);
-    const unsigned aC = baseA1 + pa, bC = baseB + pb, aN = baseA0 + pna, bN = baseB + pnb;
+    const unsigned pb = static_cast<unsigned>(cur * SB), pnb = static_cast<unsigned>((cur ^ 1) * SB);
+    const unsigned aC = baseA1 + pa, bC = baseB1 + pb, aN = baseA0 + pna, bN = baseB0 + pnb;
     const unsigned ka = static_cast<unsigned>(kt0 + kt + 2) * kstepA;
     const unsigned kb = static_cast<unsigned>(kt0 + kt + 2) * kstepB;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -994,7 +1015,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
         for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
         fa[mb] = readA(K1{}, MB, aC);
-        fby[mb] = kk_frag<1, mb>(bC);
+        fby[mb] = readB(K1{}, MB, bC);
       } else {
         group(MB, K1{}, fbx, fby, aC, bC, -1, 0u, 0u);
       }
@@ -1013,12 +1034,12 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
         for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fby[nb], fa[mb], acc[mb][nb]);
         fa[mb] = readA(K0{}, MB, aN);
-        fbx[mb] = kk_frag<0, mb>(bN);
+        fbx[mb] = readB(K0{}, MB, bN);
         dmaA(cur, ka, mb);
         dmaB(cur, kb, mb);
         if (mb == 7) {
           if (TA) dmaA(cur, ka, 8);
-          dmaB(cur, kb, 8);
+          if (!TB) dmaB(cur, kb, 8);
         }
       } else {
         group(MB, K0{}, fby, fbx, aN, bN, cur, ka, kb);
@@ -1293,25 +1314,25 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
   }
 }
 
-template <bool TA, int SCH>
+template <bool TA, int SCH, bool TB>
 void launch_kk_s(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
   switch (epi * 8 + act) {
-    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0, SCH>), grid, block, 0, st, g); break;
-    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0, SCH>), grid, block, 0, st, g); break;
-    case kEpiGeneral * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0, SCH>), grid, block, 0, st, g); break;
-    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0, SCH>), grid, block, 0, st, g); break;
+    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0, SCH, TB>), grid, block, 0, st, g); break;
+    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0, SCH, TB>), grid, block, 0, st, g); break;
+    case kEpiGeneral * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0, SCH, TB>), grid, block, 0, st, g); break;
+    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0, SCH, TB>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 0:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0, SCH>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0, SCH, TB>), grid, block, 0, st, g);
       break;
-    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0, SCH>), grid, block, 0, st, g); break;
+    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0, SCH, TB>), grid, block, 0, st, g); break;
     case kEpiBiasAct * 8 + 1:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1, SCH>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1, SCH, TB>), grid, block, 0, st, g);
       break;
     case kEpiBiasAct * 8 + 4:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4, SCH>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4, SCH, TB>), grid, block, 0, st, g);
       break;
-    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1, SCH>), grid, block, 0, st, g); break;
-    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4, SCH>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1, SCH, TB>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4, SCH, TB>), grid, block, 0, st, g); break;
     default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
   }
 }
@@ -1319,14 +1340,14 @@ void launch_kk_s(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hi
 // interleaved group schedule by default: 1.5-11 % faster per GEMM and +0.7 %
 // on the BERT-large step (profiles/r4/ab_gemmt_kk_sched_r4.txt);
 // FFK_GEMMT_KK_SCHED=0 keeps the clustered one
-template <bool TA>
+template <bool TA, bool TB = false>
 void launch_kk(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
   static const int sch = [] {
     const char* e = std::getenv("FFK_GEMMT_KK_SCHED");
     return e != nullptr && e[0] == '0' ? 0 : 1;
   }();
-  if (sch == 1) launch_kk_s<TA, 1>(g, grid, block, epi, act, st);
-  else launch_kk_s<TA, 0>(g, grid, block, epi, act, st);
+  if (sch == 1) launch_kk_s<TA, 1, TB>(g, grid, block, epi, act, st);
+  else launch_kk_s<TA, 0, TB>(g, grid, block, epi, act, st);
 }
 
 // padded-image kernel for A^T B and A B (FFK_GEMMT_KK=0 keeps the
@@ -1337,6 +1358,17 @@ bool kk_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("FFK_GEMMT_KK");
     return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+// A B^T through the same kernel (both operands K-contiguous, reads at lane
+// base + immediate issued from asm, so hipcc's waitcnt pass does not make
+// each LDS-DMA issue wait for the older fragment reads): FFK_GEMMT_KK_NT=1
+bool kk_nt_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("FFK_GEMMT_KK_NT");
+    return e != nullptr && e[0] == '1';
   }();
   return on;
 }
@@ -1391,7 +1423,8 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
       if (kk) launch_kk<false>(g, grid, block, epi, p.act, st);
       else launch_t<false, false, 2>(g, grid, block, epi, p.act, st);
     } else if (!p.trans_a && p.trans_b) {
-      launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
+      if (kk && kk_nt_enabled()) launch_kk<false, true>(g, grid, block, epi, p.act, st);
+      else launch_t<false, true, 2>(g, grid, block, epi, p.act, st);
     } else if (p.trans_a && !p.trans_b) {
       if (kk) launch_kk<true>(g, grid, block, epi, p.act, st);
       else launch_t<true, false, 2>(g, grid, block, epi, p.act, st);
