@@ -1364,11 +1364,14 @@ bool kk_enabled() {
 
 // A B^T through the same kernel (both operands K-contiguous, reads at lane
 // base + immediate issued from asm, so hipcc's waitcnt pass does not make
-// each LDS-DMA issue wait for the older fragment reads): FFK_GEMMT_KK_NT=1
+// each LDS-DMA issue wait for the older fragment reads: 12 waits per K-tile
+// in gemmt_kernel's loop, 3 here).  0.7-5.6 % faster per GEMM than
+// gemmt_kernel on the BERT input-gradient shapes (hipBLASLt still ahead on
+// most, profiles/r4/ab_gemmt_kk_nt_r4.txt); FFK_GEMMT_KK_NT=0 for A/B runs
 bool kk_nt_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("FFK_GEMMT_KK_NT");
-    return e != nullptr && e[0] == '1';
+    return e == nullptr || e[0] != '0';
   }();
   return on;
 }
