@@ -66,3 +66,21 @@ def test_lds_budget_and_max_immediate():
     assert 4 * pt <= 160 * 1024            # [A0][A1][B0][B1]
     # B reads: base holds 2 * A tile + half; immediates add buffer + k-step + block + 4 rows
     assert pt + 32 * PITCH + 7 * 32 + 8 * PITCH < 65536
+
+
+def _slot128(r, c):
+    return c ^ ((r >> 1) & 7)
+
+
+def test_k_contiguous_reads_are_immediates():
+    """K-contiguous operand (gemmt's 128-B-row image): row16's offset for
+    16-row block mb equals the k-step's lane base (block 0) + mb * 2048, the
+    immediate of gemmt_kk_kernel's asm ds_read_b128."""
+    for w in range(2):
+        for ks in range(2):
+            for lane in range(64):
+                r0 = lane & 15
+                base = (w * 128 + r0) * 128 + (_slot128(r0, ks * 4 + (lane >> 4)) << 4)
+                for mb in range(8):
+                    r = w * 128 + mb * 16 + (lane & 15)
+                    assert r * 128 + (_slot128(r, ks * 4 + (lane >> 4)) << 4) == base + mb * 2048
