@@ -997,65 +997,6 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     else fa[mb] = ar;
   };
 
-  // SCH 3: as SCH 1 with each group's reads one group ahead (fragment 0 read
-  // at the phase start, group g reads fragment g + 1), so the last group's
-  // 8 MFMAs cover the read latency before the phase-end wait; the A
-  // fragments alternate between fa and fa1 by phase
-  bf16x8 fa1[8];
-  auto pre0 = [&](auto KSC, bf16x8 (&fout)[8], bf16x8 (&faout)[8], unsigned aB, unsigned bB)
-      __attribute__((always_inline)) {
-    constexpr int ks = decltype(KSC)::value;
-    faout[0] = readA(KSC, K0{}, aB);
-    fout[0] = readB(KSC, K0{}, bB);
-    (void)ks;
-  };
-  auto group3 = [&](auto MBC, auto KSC, const bf16x8 (&fin)[8], const bf16x8 (&fain)[8], bf16x8 (&fout)[8],
-                    bf16x8 (&faout)[8], unsigned aB, unsigned bB, int dbuf, unsigned ka_, unsigned kb_)
-      __attribute__((always_inline)) {
-    constexpr int mb = decltype(MBC)::value, ks = decltype(KSC)::value;
-    constexpr int rb = mb < 7 ? mb + 1 : 7;   // fragment read by this group (none in group 7)
-    constexpr int OB = ks * 32 * KK_PITCH + rb * 32;
-    bf16x4 b0, b1, a0, a1;
-    bf16x8 ar, br;
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][0] = mfma16(fin[0], fain[mb], acc[mb][0]);
-    if constexpr (mb < 7) {
-      if constexpr (TB) br = kk_row<rb>(bB);
-      else b0 = kk_tr<OB>(bB);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][1] = mfma16(fin[1], fain[mb], acc[mb][1]);
-    if constexpr (mb < 7 && !TB) b1 = kk_tr<OB + 8 * KK_PITCH>(bB);
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][2] = mfma16(fin[2], fain[mb], acc[mb][2]);
-    if constexpr (mb < 7) {
-      if constexpr (TA) a0 = kk_tr<OB>(aB);
-      else ar = kk_row<rb>(aB);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][3] = mfma16(fin[3], fain[mb], acc[mb][3]);
-    if constexpr (mb < 7 && TA) a1 = kk_tr<OB + 8 * KK_PITCH>(aB);
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][4] = mfma16(fin[4], fain[mb], acc[mb][4]);
-    if (dbuf >= 0) dmaA(dbuf, ka_, mb);
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][5] = mfma16(fin[5], fain[mb], acc[mb][5]);
-    if (dbuf >= 0) dmaB(dbuf, kb_, mb);
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][6] = mfma16(fin[6], fain[mb], acc[mb][6]);
-    if (dbuf >= 0 && mb == 7 && TA) dmaA(dbuf, ka_, 8);
-    __builtin_amdgcn_sched_barrier(0);
-    acc[mb][7] = mfma16(fin[7], fain[mb], acc[mb][7]);
-    if (dbuf >= 0 && mb == 7 && !TB) dmaB(dbuf, kb_, 8);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (mb < 7) {
-      if constexpr (TB) fout[rb] = br;
-      else fout[rb] = cat44(b0, b1);
-      if constexpr (TA) faout[rb] = cat44(a0, a1);
-      else faout[rb] = ar;
-    }
-  };
-
   // same two-phase schedule as gemmt_kernel STG 2; the buffer's lane bases
   // are the only per-tile VALU work (4 adds)
   for (int kt = 0; kt < L; ++kt) {
@@ -1066,23 +1007,6 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     const unsigned ka = static_cast<unsigned>(kt0 + kt + 2) * kstepA;
     const unsigned kb = static_cast<unsigned>(kt0 + kt + 2) * kstepB;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (SCH == 3) {
-      pre0(K1{}, fby, fa1, aC, bC);
-      kk_for([&](auto MB) __attribute__((always_inline)) {
-        group3(MB, K1{}, fbx, fa, fby, fa1, aC, bC, -1, 0u, 0u);
-      }, S8);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      pre0(K0{}, fbx, fa, aN, bN);
-      kk_for([&](auto MB) __attribute__((always_inline)) {
-        group3(MB, K0{}, fby, fa1, fbx, fa, aN, bN, cur, ka, kb);
-      }, S8);
-      __builtin_amdgcn_sched_barrier(0);
-      continue;
-    }
     // phase A: k-step 0 (fa, fbx) | read k-step 1 of the current buffer into (fa, fby)
     kk_for([&](auto MB) __attribute__((always_inline)) {
       constexpr int mb = decltype(MB)::value;
@@ -1420,10 +1344,9 @@ template <bool TA, bool TB = false>
 void launch_kk(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
   static const int sch = [] {
     const char* e = std::getenv("FFK_GEMMT_KK_SCHED");
-    return e != nullptr && e[0] == '0' ? 0 : e != nullptr && e[0] == '3' ? 3 : 1;
+    return e != nullptr && e[0] == '0' ? 0 : 1;
   }();
-  if (sch == 3) launch_kk_s<TA, 3, TB>(g, grid, block, epi, act, st);
-  else if (sch == 1) launch_kk_s<TA, 1, TB>(g, grid, block, epi, act, st);
+  if (sch == 1) launch_kk_s<TA, 1, TB>(g, grid, block, epi, act, st);
   else launch_kk_s<TA, 0, TB>(g, grid, block, epi, act, st);
 }
 
