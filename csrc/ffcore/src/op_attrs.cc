@@ -442,17 +442,19 @@ OpSpec batchnorm_spec() {
   s.pout = [](const OpAttrs& a, const PShapes& in) {
     auto const& x = in.at(0);
     require(x.sum_degree == 1, a, "normalizing a partial-sum tensor");
-    // H shards (attribute parallelism) normalise with their local statistics,
-    // as batch shards do (per-device statistics, the reference's BatchNorm)
-    for (int d = 3; d < x.num_dims(); ++d) require(x.dim(d).degree == 1, a, "W degree must be 1");
+    // spatial (H / W) degrees must be 1, as in the reference
+    // (lib/op-attrs/src/op-attrs/ops/batch_norm.cc): a band would normalise
+    // with its own statistics and change what the model computes, so the
+    // search has to Combine the bands before a BatchNorm.  Batch shards keep
+    // per-device statistics (the reference's data-parallel BatchNorm).
+    for (int d = 2; d < x.num_dims(); ++d) require(x.dim(d).degree == 1, a, "spatial degrees must be 1");
     return PShapes{x};
   };
   s.pwts = [](const OpAttrs& a, const PShapes& in) {
     if (!a.b("affine")) return PShapes{};
     auto const& x = in.at(0);
-    const int dh = x.num_dims() > 2 ? x.dim(2).degree : 1;
     auto w = lift_to_parallel_with_degrees(TensorShape{{x.dim(1).size}, x.dtype}, 1,
-                                           x.dim(0).degree * dh * x.discard_copy_degree, {x.dim(1).degree});
+                                           x.dim(0).degree * x.discard_copy_degree, {x.dim(1).degree});
     return PShapes{w, w};
   };
   return s;

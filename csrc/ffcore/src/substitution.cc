@@ -502,8 +502,13 @@ std::optional<ParallelComputationGraph> apply_substitution(const ParallelComputa
             ins.push_back(out.add_weight(rn.outputs[0].shape.reduced_shape(), wshapes[i],
                                          rn.outputs[0].initializer, rn.outputs[0].create_grad, rn.label.name));
           } else {
-            ins.push_back(out.add_weight(wshapes[i].reduced_shape(), wshapes[i],
-                                         default_initializer(op.type, wn.at(i)), true, name + "." + wn.at(i)));
+            // a weight with no matched source would be created fresh: a new
+            // name and a default initializer, which drops the user's
+            // initializer and breaks get/set of weights by name and checkpoint
+            // keys.  Such rewrites are rejected (the TASO corpus is on by
+            // default, so this path is reachable in ordinary searches).
+            (void)wn;
+            return std::nullopt;
           }
         }
       }

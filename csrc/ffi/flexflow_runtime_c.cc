@@ -301,14 +301,23 @@ struct RtLoader {
   RtTensor* batch = nullptr;
   std::vector<float> full;  // num_samples x sample
   int64_t num_samples = 0, sample = 0, next = 0;
+  // integer samples (embedding ids) are staged in the runtime's fp32 tensor
+  // storage: exact only up to 2^24, so larger ids are refused instead of
+  // silently rounded onto a neighbouring row
+  static float exact_id(int64_t v) {
+    if (v > (int64_t{1} << 24) || v < -(int64_t{1} << 24))
+      throw std::invalid_argument("dataloader: integer sample " + std::to_string(v) +
+                                  " exceeds 2^24 and cannot be stored exactly");
+    return static_cast<float>(v);
+  }
   void load(const void* src, int dt, int64_t n) {
     full.resize(static_cast<size_t>(n));
     if (dt == DT_INT32) {
       auto p = static_cast<const int32_t*>(src);
-      for (int64_t i = 0; i < n; ++i) full[i] = static_cast<float>(p[i]);
+      for (int64_t i = 0; i < n; ++i) full[i] = exact_id(p[i]);
     } else if (dt == DT_INT64) {
       auto p = static_cast<const int64_t*>(src);
-      for (int64_t i = 0; i < n; ++i) full[i] = static_cast<float>(p[i]);
+      for (int64_t i = 0; i < n; ++i) full[i] = exact_id(p[i]);
     } else {
       std::memcpy(full.data(), src, sizeof(float) * static_cast<size_t>(n));
     }

@@ -438,6 +438,34 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
 
+def sync_choices() -> int:
+    """Make every rank use the same kernel for the same GEMM signature.
+
+    Each rank times its candidates on its own, and near-ties can then fall
+    differently on different ranks.  Replicas that must stay bitwise equal
+    without a gradient sync (the bias gradients of partial-sum replicas,
+    ops/dense.py) would then drift.  Every rank's decisions are all-gathered,
+    and for each signature the lowest rank that tuned it decides.  This is a
+    collective: all ranks call it, outside graph capture.  Returns the number
+    of decisions this rank changed."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 0
+    from .dense import _DACT_CHOICE   # fused-vs-plain activation-gradient decisions
+    tables = (_CHOICE, _DACT_CHOICE)
+    objs: List[Any] = [None] * dist.get_world_size()
+    dist.all_gather_object(objs, [dict(t) for t in tables])
+    changed = 0
+    for i, table in enumerate(tables):
+        merged: Dict[Tuple, Any] = {}
+        for d in objs:          # rank order: the lowest rank that tuned a signature wins
+            for k, v in ((d or [{}] * len(tables))[i]).items():
+                merged.setdefault(k, v)
+        changed += sum(1 for k, v in merged.items() if table.get(k, v) != v)
+        table.update(merged)
+    return changed
+
+
 def _align(t: torch.Tensor) -> int:
     p = t.data_ptr()
     return 16 if p % 16 == 0 else (8 if p % 8 == 0 else 2)

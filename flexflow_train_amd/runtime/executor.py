@@ -1497,6 +1497,13 @@ class Executor:
         t0 = self.tracer.begin("__update__:fwd", "compute", self.step_num) if prof else None
         self.update(lr)
         self.tracer.end(t0)
+        if (self.dist.distributed and not getattr(self, "_choices_synced", False)
+                and self.cfg.device.type == "cuda" and not torch.cuda.is_current_stream_capturing()):
+            # the first step tuned every GEMM signature on each rank on its own:
+            # agree on one kernel per signature before later steps / the capture
+            from ..ops.gemm import sync_choices
+            sync_choices()
+            self._choices_synced = True
 
     def _overlap_flats(self) -> List[dict]:
         """Flats whose buckets may be updated during the backward pass: one

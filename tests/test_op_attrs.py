@@ -142,8 +142,9 @@ def test_pool_and_batchnorm():
     with pytest.raises(Exception):
         C.infer_parallel_output_shapes(pool, [P([4, 3, 8, 8], [1, 1, 1, 2])])
     bn = C.OpAttrs("BATCHNORM", relu=False)
-    # H bands normalise with local statistics; gamma / beta replicated over them
-    assert weights(bn, [P([4, 4, 8, 8], [1, 1, 2, 1])]) == [([1], 1, 2), ([1], 1, 2)]
+    # H bands would normalise with local statistics: rejected (a Combine first)
+    with pytest.raises(Exception):
+        C.infer_parallel_output_shapes(bn, [P([4, 4, 8, 8], [1, 1, 2, 1])])
     assert weights(bn, [P([4, 4, 8, 8], [1, 2, 1, 1])]) == [([2], 1, 1), ([2], 1, 1)]
     assert weights(bn, [P([4, 4, 8, 8], [2, 1, 1, 1])]) == [([1], 1, 2), ([1], 1, 2)]
 
