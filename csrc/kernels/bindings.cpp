@@ -282,6 +282,23 @@ PYBIND11_MODULE(_ffkernels, m) {
                             uintptr_t st) { conv2d_dgrad(cshape(shp), P(dy), P(w), P(dx), beta, S(st)); });
   m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws, int splits,
                             uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), F(ws), splits, S(st)); });
+  m.def("gemm_f32", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int64_t M, int64_t N,
+                       int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool ta, bool tb, int act, float alpha,
+                       float beta, int in_f32, int out_f32, uintptr_t st, int batch, int64_t sa, int64_t sb,
+                       int64_t sc) {
+    gemm_f32(P(A), P(B), P(C), P(bias), P(pre), M, N, K, lda, ldb, ldc, ta, tb, act, alpha, beta, in_f32, out_f32,
+             S(st), batch, sa, sb, sc);
+  });
+  m.def("conv32_fwd", [=](std::vector<int> shp, int groups, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y,
+                          int act, int in_f32, uintptr_t st) {
+    conv32_fwd(cshape(shp), groups, P(x), P(w), P(bias), P(y), act, in_f32, S(st));
+  });
+  m.def("conv32_dgrad", [=](std::vector<int> shp, int groups, uintptr_t dy, uintptr_t w, uintptr_t dx, float beta,
+                            int in_f32, uintptr_t st) {
+    conv32_dgrad(cshape(shp), groups, P(dy), P(w), P(dx), beta, in_f32, S(st));
+  });
+  m.def("conv32_wgrad", [=](std::vector<int> shp, int groups, uintptr_t x, uintptr_t dy, uintptr_t dw, int in_f32,
+                            uintptr_t st) { conv32_wgrad(cshape(shp), groups, P(x), P(dy), F(dw), in_f32, S(st)); });
   m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st, uintptr_t ws) {
     bn_stats(P(x), F(stats), M, C, S(st), F(ws));
   });

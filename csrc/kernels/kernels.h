@@ -228,6 +228,23 @@ int64_t conv2d_wgrad_ws_floats(const ConvShape& s, int splits);
 void conv2d_wgrad(const ConvShape& s, const void* x, const void* dy, float* dw, float* ws, int splits,
                   hipStream_t st);
 
+// ---- igemm32.hip: exact-fp32 MFMA (v_mfma_f32_32x32x2_f32) GEMM and
+// convolutions; fp32 or bf16 inputs (in_f32), fp32 accumulation.
+// GEMM: C = act(alpha op(A) op(B) + bias) [pre := pre-activation] (+ beta C),
+// bias / pre / C in the output dtype (out_f32).
+void gemm_f32(const void* A, const void* B, void* C, const void* bias, void* pre, int64_t M, int64_t N, int64_t K,
+              int64_t lda, int64_t ldb, int64_t ldc, bool trans_a, bool trans_b, int act, float alpha, float beta,
+              int in_f32, int out_f32, hipStream_t st, int batch = 1, int64_t sa = 0, int64_t sb = 0,
+              int64_t sc = 0);
+// Grouped NHWC convolutions (any groups dividing C and K; weight
+// [K][R][S][C/groups]); outputs in the input dtype, dw fp32 (+=).
+void conv32_fwd(const ConvShape& cs, int groups, const void* x, const void* w, const void* bias, void* y, int act,
+                int in_f32, hipStream_t st);
+void conv32_dgrad(const ConvShape& cs, int groups, const void* dy, const void* w, void* dx, float beta, int in_f32,
+                  hipStream_t st);
+void conv32_wgrad(const ConvShape& cs, int groups, const void* x, const void* dy, float* dw, int in_f32,
+                  hipStream_t st);
+
 // ---- bnpool.hip: BatchNorm (training) + pooling over NHWC bf16 [M][C]
 // ws (optional, 32*C floats): 16 atomic buckets -> full-grid reduction (else the grid is capped)
 void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws = nullptr);

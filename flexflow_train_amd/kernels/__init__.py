@@ -933,6 +933,153 @@ def conv2d_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), splits:
     STATS["conv2d_wgrad"] += 1
 
 
+def _rm2d(t: torch.Tensor) -> torch.Tensor:
+    """A 2-D operand the kernels can address as rows of unit-stride elements
+    (size-1 dims may carry any stride)."""
+    if t.shape[1] == 1 or t.stride(1) == 1:
+        return t
+    return t.contiguous()
+
+
+def _ld2d(t: torch.Tensor) -> int:
+    """Leading dimension of a row-major 2-D tensor (its row stride; a
+    single row or a size-1 row dim reports the row length)."""
+    if t.shape[0] == 1:
+        return max(1, t.shape[1])
+    return t.stride(0)
+
+
+def gemm_f32(a, b, trans_a=False, trans_b=False, bias=None, act="none", alpha=1.0, beta=0.0, out=None, pre=None,
+             out_dtype=None):
+    """C = act(alpha op(a) op(b) + bias) (+ beta C) on the exact-fp32 MFMA
+    (igemm32.hip).  a / b: 2-D fp32 (or bf16) with unit inner stride;
+    bias / pre / out in the output dtype (default: the inputs')."""
+    if a.dtype != b.dtype or a.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("gemm_f32: operands must share dtype fp32 / bf16")
+    if a.dim() != 2 or b.dim() != 2:
+        raise ValueError("gemm_f32: operands must be 2-D")
+    a, b = _rm2d(a), _rm2d(b)
+    if not (a.is_cuda and b.is_cuda):
+        raise ValueError("gemm_f32: GPU tensors expected")
+    M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if Kd != Kb:
+        raise ValueError(f"gemm_f32: inner dims differ ({Kd} vs {Kb})")
+    dt = out_dtype or (out.dtype if out is not None else a.dtype)
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=dt)
+        beta = 0.0
+    if tuple(out.shape) != (M, N) or (out.stride(1) != 1 and N > 1) or out.dtype not in (torch.float32,
+                                                                                        torch.bfloat16):
+        raise ValueError("gemm_f32: bad output")
+    # bias is read in the inputs' dtype, pre written in the output's
+    for name, t, want in (("bias", bias, a.dtype), ("pre", pre, out.dtype)):
+        if t is not None and (t.dtype != want or not t.is_contiguous() or not t.is_cuda):
+            raise ValueError(f"gemm_f32: {name} must be a contiguous GPU {want} tensor")
+    if bias is not None and bias.numel() != N:
+        raise ValueError("gemm_f32: bias must have N elements")
+    if pre is not None and (pre.numel() != M * N or _ld2d(out) != N):
+        raise ValueError("gemm_f32: pre needs a dense output")
+    ext().gemm_f32(_p(a), _p(b), _p(out), _p(bias), _p(pre), M, N, Kd, _ld2d(a), _ld2d(b), _ld2d(out),
+                   bool(trans_a), bool(trans_b), ACT_CODES[act], float(alpha), float(beta),
+                   int(a.dtype == torch.float32), int(out.dtype == torch.float32), _stream(), 1, 0, 0, 0)
+    STATS["gemm_f32"] += 1
+    return out
+
+
+def bmm_f32(a, b, trans_a=False, trans_b=False, alpha=1.0):
+    """Batched fp32 product over the leading dims (one launch, blockIdx.z =
+    batch): a [..., M, K] (or [..., K, M]), b [..., K, N] (or [..., N, K])."""
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or a.dim() < 3 or a.shape[:-2] != b.shape[:-2]:
+        raise ValueError("bmm_f32: fp32 operands with equal batch dims")
+    lead = a.shape[:-2]
+    a3 = a.reshape(-1, a.shape[-2], a.shape[-1]).contiguous()
+    b3 = b.reshape(-1, b.shape[-2], b.shape[-1]).contiguous()
+    M, Kd = (a3.shape[2], a3.shape[1]) if trans_a else (a3.shape[1], a3.shape[2])
+    Kb, N = (b3.shape[2], b3.shape[1]) if trans_b else (b3.shape[1], b3.shape[2])
+    if Kd != Kb:
+        raise ValueError("bmm_f32: inner dims differ")
+    nb = a3.shape[0]
+    out = torch.empty(nb, M, N, device=a.device, dtype=torch.float32)
+    if nb > 65535:
+        raise ValueError("bmm_f32: batch > 65535")
+    ext().gemm_f32(_p(a3), _p(b3), _p(out), 0, 0, M, N, Kd, a3.stride(1), b3.stride(1), N, bool(trans_a),
+                   bool(trans_b), 0, float(alpha), 0.0, 1, 1, _stream(), nb, a3.stride(0), b3.stride(0), M * N)
+    STATS["gemm_f32"] += 1
+    return out.reshape(*lead, M, N)
+
+
+def _check_nhwc_any(t: torch.Tensor, name: str, dtype):
+    if not t.is_cuda or t.dtype != dtype:
+        raise ValueError(f"{name}: expected a GPU {dtype} tensor")
+    if t.dim() != 4 or not t.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError(f"{name}: expected a 4-d channels_last tensor")
+
+
+def _conv32_geom(x_shape, K, R, S, stride, pad, dil, groups):
+    N, C, H, W = x_shape
+    if groups <= 0 or C % groups or K % groups:
+        raise ValueError(f"conv32: C={C} and K={K} must be multiples of groups={groups}")
+    return [int(N), int(H), int(W), int(C), int(K), int(R), int(S), int(stride[0]), int(stride[1]),
+            int(pad[0]), int(pad[1]), int(dil[0]), int(dil[1])]
+
+
+def conv32_fwd(x, w, bias=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1, act: str = "none"):
+    """Grouped / fp32 convolution (igemm32.hip): x [N,C,H,W] channels_last
+    fp32 or bf16, w [K,R,S,C/groups] contiguous in x's dtype -> y channels_last."""
+    _check_nhwc_any(x, "x", x.dtype)
+    K_, R, S, Cg = w.shape
+    _check(w, "w", x.dtype)
+    if Cg * groups != x.shape[1]:
+        raise ValueError(f"conv32: weight has {Cg} x {groups} input channels, input has {x.shape[1]}")
+    g = _conv32_geom(x.shape, K_, R, S, stride, pad, dil, groups)
+    P, Q = conv_out_hw(x.shape[2], x.shape[3], R, S, *stride, *pad, *dil)
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != K_ or not bias.is_contiguous()):
+        raise ValueError("conv32: bias must be a contiguous [K] tensor in x's dtype")
+    y = torch.empty((x.shape[0], K_, P, Q), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    ext().conv32_fwd(g, int(groups), _p(x), _p(w), _p(bias), _p(y), ACT_CODES[act], int(x.dtype == torch.float32),
+                     _stream())
+    STATS["conv32_fwd"] += 1
+    return y
+
+
+def conv32_dgrad(dy, w, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1, out=None,
+                 beta: float = 0.0):
+    _check_nhwc_any(dy, "dy", dy.dtype)
+    K_, R, S, Cg = w.shape
+    _check(w, "w", dy.dtype)
+    g = _conv32_geom(x_shape, K_, R, S, stride, pad, dil, groups)
+    P, Q = conv_out_hw(x_shape[2], x_shape[3], R, S, *stride, *pad, *dil)
+    if tuple(dy.shape) != (x_shape[0], K_, P, Q) or Cg * groups != x_shape[1]:
+        raise ValueError(f"conv32_dgrad: dy {tuple(dy.shape)} / weight {tuple(w.shape)} do not match {tuple(x_shape)}")
+    if out is None:
+        out = torch.empty(tuple(x_shape), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        beta = 0.0
+    else:
+        _check_nhwc_any(out, "dx", dy.dtype)
+        if tuple(out.shape) != tuple(x_shape):
+            raise ValueError("conv32_dgrad: out has the wrong shape")
+    ext().conv32_dgrad(g, int(groups), _p(dy), _p(w), _p(out), float(beta), int(dy.dtype == torch.float32), _stream())
+    STATS["conv32_dgrad"] += 1
+    return out
+
+
+def conv32_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1):
+    """dw (fp32, contiguous, layout [K][R][S][C/groups]) += weight gradient."""
+    _check_nhwc_any(x, "x", x.dtype)
+    _check_nhwc_any(dy, "dy", x.dtype)
+    K_ = dy.shape[1]
+    g = _conv32_geom(x.shape, K_, R, S, stride, pad, dil, groups)
+    P, Q = conv_out_hw(x.shape[2], x.shape[3], R, S, *stride, *pad, *dil)
+    if tuple(dy.shape) != (x.shape[0], K_, P, Q):
+        raise ValueError("conv32_wgrad: dy shape mismatch")
+    if (not dw.is_cuda or dw.dtype != torch.float32 or not dw.is_contiguous()
+            or dw.numel() != K_ * R * S * (x.shape[1] // groups)):
+        raise ValueError("conv32_wgrad: dw must be a contiguous fp32 [K,R,S,C/groups] buffer")
+    ext().conv32_wgrad(g, int(groups), _p(x), _p(dy), _p(dw), int(x.dtype == torch.float32), _stream())
+    STATS["conv32_wgrad"] += 1
+
+
 def bn_stats(x, stats):
     _check_nhwc(x, "x")
     C = x.shape[1]

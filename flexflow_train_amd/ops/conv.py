@@ -107,6 +107,13 @@ class Conv2DOp(OpImpl):
                 and (x.shape[1] % 8 == 0 or x.shape[1] < 8) and act in ("none", "relu", "sigmoid", "tanh")
                 and K.use_hip(x))
 
+    @staticmethod
+    def _native32(x, act):
+        """fp32 models and grouped convolutions (ResNeXt): the exact-fp32 MFMA
+        implicit GEMM (igemm32.hip), any channel count per group."""
+        return (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)
+                and act in ("none", "relu", "sigmoid", "tanh") and K.use_hip(x))
+
     def forward(self, ctx, inputs, weights):
         x = inputs[0]
         halo = ctx.extra.get("halo")
@@ -153,8 +160,17 @@ class Conv2DOp(OpImpl):
             if stats is not None:
                 y._ff_bn_stats = stats
             return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape))
-        # library path (grouped convs, CPU): the autograd graph recorded here is
-        # replayed in backward — no forward recomputation
+        if self._native32(x, act):
+            wp = W.reshape(Kc, R, S, C)   # physical [K][R][S][C/groups]
+            if wp.dtype != x.dtype:
+                wp = wp.to(x.dtype)
+            wp = wp.contiguous()
+            xin = x.contiguous(memory_format=torch.channels_last)
+            bias = None if b is None else b.to(x.dtype).contiguous()
+            y = K.conv32_fwd(xin, wp, bias, stride, pad, groups=groups, act=act)
+            return [y], ("hip32", xin, wp, y if act != "none" else None, tuple(x.shape), groups)
+        # library path (CPU): the autograd graph recorded here is replayed in
+        # backward — no forward recomputation
         xi = x.detach().requires_grad_(ctx.training and x.is_floating_point())
         Wr = W.detach().requires_grad_(ctx.training)
         with torch.enable_grad():
@@ -185,6 +201,8 @@ class Conv2DOp(OpImpl):
                 acc_grad(weight_grads[1], u.grad.float().sum((0, 2, 3)))
             return [xi.grad if (xi.requires_grad and need_input_grad[0]) else None]
 
+        if saved[0] == "hip32":
+            return self._backward32(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act)
         _, xin, wp, y, xshape = saved
         Kc, R, S, Cp = wp.shape
         dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))
@@ -259,6 +277,41 @@ class Conv2DOp(OpImpl):
             K.conv2d_dgrad(dy, wp, xshape, stride, pad, out=acc, beta=1.0)
             return [acc]
         return [K.conv2d_dgrad(dy, wp, xshape, stride, pad)]
+
+
+    @staticmethod
+    def _backward32(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act):
+        _, xin, wp, y, xshape, groups = saved
+        Kc, R, S, Cg = wp.shape
+        dy = grad_outputs[0].to(xin.dtype).contiguous(memory_format=torch.channels_last)
+        if act == "relu":
+            dy = torch.where(y > 0, dy, torch.zeros((), device=dy.device, dtype=dy.dtype))
+        elif act in ("sigmoid", "tanh"):
+            yf = y.float()
+            d = yf * (1 - yf) if act == "sigmoid" else 1 - yf * yf
+            dy = (dy.float() * d).to(xin.dtype).contiguous(memory_format=torch.channels_last)
+        if len(weight_grads) > 1 and weight_grads[1] is not None:
+            d2 = dy.permute(0, 2, 3, 1).reshape(-1, Kc)
+            if Kc % 8 == 0:
+                K.colsum_act(d2, None, "none", weight_grads[1], write_dx=False)
+            else:
+                acc_grad(weight_grads[1], d2.float().sum(0))
+        dW = weight_grads[0]
+        if dW is not None:
+            if dW.dtype == torch.float32 and dW.is_contiguous():
+                K.conv32_wgrad(xin, dy, dW.view(-1), R, S, stride, pad, groups=groups)
+            else:
+                tmp = torch.zeros(dW.numel(), device=dy.device, dtype=torch.float32)
+                K.conv32_wgrad(xin, dy, tmp, R, S, stride, pad, groups=groups)
+                acc_grad(dW, tmp.view(dW.shape))
+        if not need_input_grad[0]:
+            return [None]
+        acc = ctx.extra.get("grad_acc", [None])[0]
+        if (acc is not None and ctx.extra.get("halo") is None and acc.is_cuda and acc.dtype == xin.dtype
+                and tuple(acc.shape) == tuple(xshape) and acc.is_contiguous(memory_format=torch.channels_last)):
+            K.conv32_dgrad(dy, wp, xshape, stride, pad, groups=groups, out=acc, beta=1.0)
+            return [acc]
+        return [K.conv32_dgrad(dy, wp, xshape, stride, pad, groups=groups)]
 
 
 @register("POOL2D")

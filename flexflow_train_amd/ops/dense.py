@@ -40,9 +40,12 @@ class LinearOp(OpImpl):
         x2 = x.reshape(-1, x.shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
-        if x2.is_cuda and x2.dtype == torch.bfloat16:
+        if x2.is_cuda and x2.dtype in (torch.bfloat16, torch.float32):
+            # bf16: the autotuned MFMA GEMMs; fp32: the exact-fp32 MFMA kernel
+            # (igemm32.hip) -- no library GEMM either way
+            Wc = W if W.dtype == x2.dtype else W.to(x2.dtype)
             pre = torch.empty(x2.shape[0], W.shape[1], device=x2.device, dtype=x2.dtype) if act != "none" else None
-            y = matmul(x2, W, bias=b, act=act, pre=pre)
+            y = matmul(x2, Wc, bias=b, act=act, pre=pre)
         else:
             u = x2 @ W.to(x2.dtype)
             if b is not None:
@@ -69,7 +72,8 @@ class LinearOp(OpImpl):
             # the consumer's dX GEMM already applied act' and accumulated db (gemmp epilogue)
             act = "none"
             db = None
-        if dy2.is_cuda and dy2.dtype == torch.bfloat16 and K.available() and dy2.shape[1] % 8 == 0:
+        if (dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float32) and K.available() and dy2.shape[1] % 8 == 0
+                and (pre is None or pre.dtype == dy2.dtype)):
             if act != "none":
                 g = K.colsum_act(dy2, pre, act, db, write_dx=True)
             else:
@@ -89,6 +93,8 @@ class LinearOp(OpImpl):
         if dW is not None:
             if dW.is_cuda and g.dtype == torch.bfloat16:
                 wgrad_matmul(ctx, x2, g, dW, ctx.extra.get("wgrad_beta", [1.0])[0])
+            elif dW.is_cuda and g.dtype == torch.float32 and x2.dtype == torch.float32 and dW.dtype == torch.float32:
+                matmul(x2, g, trans_a=True, out=dW, beta=ctx.extra.get("wgrad_beta", [1.0])[0])
             else:
                 acc_grad(dW, x2.float().t() @ g.float())
         dx = None
@@ -111,7 +117,7 @@ class LinearOp(OpImpl):
             if acc is not None and acc.is_cuda and acc.dtype == g.dtype and acc.is_contiguous():
                 matmul(g, W, trans_b=True, out=acc.view(-1, W.shape[0]), beta=1.0)
                 return [acc]
-            dx = matmul(g, W, trans_b=True) if g.is_cuda else (g @ W.to(g.dtype).t())
+            dx = matmul(g, W if W.dtype == g.dtype else W.to(g.dtype), trans_b=True) if g.is_cuda else (g @ W.to(g.dtype).t())
             dx = dx.reshape(*dy.shape[:-1], W.shape[0])
         return [dx]
 
@@ -170,6 +176,8 @@ def _bmm(a, b, trans_a=False, trans_b=False):
     one launch for the whole batch) when the shapes allow, else torch."""
     if K.bmm_supported(a, b, trans_a, trans_b):
         return K.bmm(a, b, trans_a, trans_b)
+    if a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32 and K.use_hip(a, b):
+        return K.bmm_f32(a, b, trans_a, trans_b)   # exact-fp32 MFMA (igemm32.hip)
     return torch.matmul(a.transpose(-1, -2) if trans_a else a, b.transpose(-1, -2) if trans_b else b)
 
 

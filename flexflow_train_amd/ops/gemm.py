@@ -146,6 +146,31 @@ def _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre):
     return A @ B
 
 
+def _f32(a, b, trans_a, trans_b, bias, act, out, beta, pre):
+    """fp32 operands: the exact-fp32 MFMA kernel (csrc/kernels/igemm32.hip),
+    the counterpart of the reference's fp32 cublasGemmEx
+    (linear_kernels.cu:124-131).  No library GEMM on this path."""
+    a = a if a.stride(1) == 1 else a.contiguous()
+    b = b if b.stride(1) == 1 else b.contiguous()
+    if bias is not None and bias.dtype != torch.float32:
+        bias = bias.float()
+    if bias is not None:
+        bias = bias.contiguous()
+    if out is not None and out.stride(1) != 1:
+        r = K.gemm_f32(a, b, trans_a, trans_b, bias=bias, act=act)
+        if beta:
+            out.mul_(beta).add_(r.to(out.dtype))
+        else:
+            out.copy_(r)
+        return out
+    if pre is not None and pre.dtype != (out.dtype if out is not None else torch.float32):
+        p32 = torch.empty(pre.shape, device=pre.device, dtype=torch.float32)
+        r = K.gemm_f32(a, b, trans_a, trans_b, bias=bias, act=act, alpha=1.0, beta=beta, out=out, pre=p32)
+        pre.copy_(p32)
+        return r
+    return K.gemm_f32(a, b, trans_a, trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre)
+
+
 def _hip(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
     return K.gemm(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, beta=beta, out=out, pre=pre,
                   splits=splits)
@@ -404,6 +429,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
     """C = act(op(a) @ op(b) + bias) (+ beta * out).  2-D operands."""
     if not a.is_cuda:
         return _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre)
+    if a.dtype == torch.float32 and b.dtype == torch.float32 and K.use_hip(a, b):
+        return _f32(a, b, trans_a, trans_b, bias, act, out, beta, pre)
     hip_ok = _hip_ok(a, b, trans_a, trans_b) and (
         out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0))
     if not hip_ok or _MODE == "blas":

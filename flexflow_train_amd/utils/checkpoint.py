@@ -1,18 +1,32 @@
 """Checkpoint / resume.
 
 Reference: the legacy runtime has no real checkpointing (SURVEY §5.4 —
-only Tensor.get_tensor/set_tensor round-trips and the strategy file); this
-module provides sharded checkpoints for the per-rank executor:
+only Tensor.get_tensor/set_tensor round-trips and the strategy file, and the
+new FFI's CG (de)serialisation, lib/pcg/ffi/include/flexflow/pcg.h:45-54);
+this module provides sharded checkpoints for the per-rank executor.  A
+checkpoint directory holds:
 
-* ``save_checkpoint(model, dir)``: every rank writes ``rank<r>.pt`` holding
-  its LOGICAL weight pieces (with their boxes in the full tensor) and its
-  flat optimizer state; rank 0 writes ``meta.json`` (world, step, strategy
-  fingerprint, parameter shapes).  Files are written with ``torch.save`` of
-  plain tensors/dicts and read back with ``weights_only=True``.
-* ``load_checkpoint(model, dir)``: same world + same strategy -> exact resume
-  (weights + optimizer state + step).  Different world or strategy -> the
-  full logical weights are reassembled from every rank's boxes and
-  re-sliced for the new layout (optimizer state restarts).
+* ``rank<r>.pt`` (every rank): its LOGICAL weight pieces with their boxes in
+  the full tensor, the same pieces of its optimizer state (Adam m / v,
+  momentum), the flat optimizer state as stored (for an exact same-layout
+  resume), the per-flat step counters and the torch CPU / GPU RNG states.
+  Written with ``torch.save`` of plain tensors / dicts, read back with
+  ``weights_only=True``.
+* ``meta.json`` (rank 0, written last: a directory with it is complete):
+  world, step, strategy fingerprint, parameter shapes, progress.
+* ``model.json`` — the computation graph in the CG JSON v1 format
+  (``ComputationGraph.to_json``), when the FFModel is known.
+* ``strategy.json`` — the parallel strategy (PCG + placements) in the
+  ``--import-strategy`` format, so ``FFConfig.import_strategy_file`` can
+  rebuild the exact layout the checkpoint was written under.
+
+``load_checkpoint(model, dir)``: same world + same strategy -> exact resume
+(weights + optimizer state + step + RNG).  Different world or strategy ->
+the full logical weights AND optimizer state are reassembled from every
+rank's boxes and re-sliced for the new layout, the step counters carried
+over.  Only the ZeRO-sharded optimizer (``shard_optimizer``) keeps its state
+rank-local and restarts it on a layout change (meta records
+``optimizer_resharded: false``).
 """
 from __future__ import annotations
 
@@ -46,6 +60,10 @@ def save_checkpoint(model, path: str, progress: Optional[dict] = None):
             pass
     ex.dist.barrier()
     st = ex.state_dict()
+    st["opt_pieces"] = _optimizer_pieces(ex)
+    st["rng"] = {"cpu": torch.get_rng_state()}
+    if torch.cuda.is_available() and ex.cfg.device.type == "cuda":
+        st["rng"]["cuda"] = torch.cuda.get_rng_state(ex.cfg.device)
     tmp = os.path.join(path, f"rank{ex.rank}.pt.tmp")
     torch.save(st, tmp)
     os.replace(tmp, os.path.join(path, f"rank{ex.rank}.pt"))
@@ -56,6 +74,17 @@ def save_checkpoint(model, path: str, progress: Optional[dict] = None):
                 "params": {p.name: list(p.logical_shape) for p in ex.params}}
         if progress is not None:
             meta["progress"] = progress
+        meta["optimizer"] = {"keys": ex._opt_state_keys(), "sharded": bool(ex.cfg.shard_optimizer)}
+        cg = getattr(model, "cg", None)
+        if cg is not None:
+            with open(os.path.join(path, "model.json.tmp"), "w") as f:
+                f.write(cg.to_json())
+            os.replace(os.path.join(path, "model.json.tmp"), os.path.join(path, "model.json"))
+            meta["model"] = "model.json"
+        from ..search.strategy import export_strategy
+        export_strategy(os.path.join(path, "strategy.json"), ex.pcg, ex.views,
+                        {"world": ex.world, "source": "checkpoint"})
+        meta["strategy"] = "strategy.json"
         with open(os.path.join(path, "meta.json.tmp"), "w") as f:
             json.dump(meta, f, indent=1)
         os.replace(os.path.join(path, "meta.json.tmp"), os.path.join(path, "meta.json"))
@@ -118,6 +147,58 @@ def _assemble_full(path: str, world: int) -> Dict[str, torch.Tensor]:
     return full
 
 
+def _optimizer_pieces(ex) -> Dict[str, dict]:
+    """This rank's LOGICAL pieces of every weight's optimizer state (the
+    canonical owner of each shard only), boxed like the weights."""
+    keys = ex._opt_state_keys()
+    out: Dict[str, dict] = {}
+    if not keys or ex.cfg.shard_optimizer:
+        return out
+    for p in ex.params:
+        if not p.group:
+            continue
+        c = p.layout.coord(ex.rank)
+        if c is None or c.b != 0 or c.rep != 0 or c.a != 0:
+            continue
+        opt = ex.flats[p.flat_id]["opt"]
+        rec = {"box": p.layout.box(c.shard), "logical_shape": p.logical_shape}
+        for k in keys:
+            flat = getattr(opt, k, None)
+            if flat is None:
+                continue
+            piece = flat[p.offset:p.offset + p.numel].view(p.layout.piece_shape)
+            rec[k] = ex._to_logical(p, piece).detach().float().cpu().clone()
+        out[p.name] = rec
+    return out
+
+
+def _assemble_optimizer(path: str, world: int) -> Dict[str, Dict[str, torch.Tensor]]:
+    full: Dict[str, Dict[str, torch.Tensor]] = {}
+    for r in range(world):
+        f = os.path.join(path, f"rank{r}.pt")
+        if not os.path.exists(f):
+            continue
+        st = torch.load(f, map_location="cpu", weights_only=True)
+        for name, rec in st.get("opt_pieces", {}).items():
+            box = tuple(slice(lo, hi) for lo, hi in rec["box"])
+            for k, t in rec.items():
+                if k in ("box", "logical_shape"):
+                    continue
+                dst = full.setdefault(name, {}).get(k)
+                if dst is None:
+                    dst = full[name][k] = torch.zeros(tuple(rec["logical_shape"]), dtype=torch.float32)
+                dst[box] = t.reshape(dst[box].shape)
+    return full
+
+
+def _restore_rng(st: dict, ex):
+    rng = st.get("rng") or {}
+    if "cpu" in rng:
+        torch.set_rng_state(rng["cpu"])
+    if "cuda" in rng and torch.cuda.is_available() and ex.cfg.device.type == "cuda":
+        torch.cuda.set_rng_state(rng["cuda"], ex.cfg.device)
+
+
 def read_checkpoint_meta(path: str) -> dict:
     with open(os.path.join(path, "meta.json")) as f:
         return json.load(f)
@@ -129,9 +210,12 @@ def load_checkpoint(model, path: str, strict: bool = True):
     if meta.get("format") != "ffmi355x.checkpoint.v1":
         raise ValueError(f"{path}: not a checkpoint")
     same = meta["world"] == ex.world and meta["fingerprint"] == _fingerprint(ex)
-    if same and os.path.exists(os.path.join(path, f"rank{ex.rank}.pt")):
-        st = torch.load(os.path.join(path, f"rank{ex.rank}.pt"), map_location="cpu", weights_only=True)
+    mine = os.path.join(path, f"rank{ex.rank}.pt")
+    if same and os.path.exists(mine):
+        st = torch.load(mine, map_location="cpu", weights_only=True)
         ex.load_state_dict(st)
+        _restore_rng(st, ex)
+        meta["resharded"] = False
     else:
         full = _assemble_full(path, meta["world"])
         names = set(ex.parameter_names())
@@ -144,5 +228,32 @@ def load_checkpoint(model, path: str, strict: bool = True):
             if p.group and p.compute is not p.master:
                 p.compute.copy_(p.master)
         ex.step_num = int(meta.get("step", 0))
+        # optimizer state: reassembled per weight and re-sliced like the weights
+        opt_ok = not ex.cfg.shard_optimizer and not meta.get("optimizer", {}).get("sharded", False)
+        if opt_ok:
+            ofull = _assemble_optimizer(path, meta["world"])
+            for n in names & set(ofull):
+                ex.set_optimizer_state(n, ofull[n])
+            steps = _flat_steps(path, meta["world"])
+            for f in ex.flats:
+                f["opt"].step_num = steps if steps is not None else ex.step_num
+        r0 = os.path.join(path, f"rank{ex.rank if ex.rank < meta['world'] else 0}.pt")
+        if os.path.exists(r0):
+            _restore_rng(torch.load(r0, map_location="cpu", weights_only=True), ex)
+        meta["resharded"] = True
+        meta["optimizer_resharded"] = opt_ok
     ex.dist.barrier()
     return meta
+
+
+def _flat_steps(path: str, world: int) -> Optional[int]:
+    """The optimizer step counter (Adam's bias correction) of the saved run:
+    every flat of a run steps together, so rank 0's first flat says it."""
+    for r in range(world):
+        f = os.path.join(path, f"rank{r}.pt")
+        if os.path.exists(f):
+            st = torch.load(f, map_location="cpu", weights_only=True)
+            opts = st.get("optimizer") or []
+            if opts:
+                return int(opts[0]["step"])
+    return None

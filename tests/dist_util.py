@@ -148,3 +148,60 @@ def run_recompile(model_fn, world, strategy_file, steps_before=2, steps_after=2)
         mp.start_processes(_recompile_worker, args=(world, free_port(), model_fn, strategy_file, steps_before,
                                                     steps_after, out), nprocs=world, join=True, start_method="spawn")
         return torch.load(out, weights_only=True)
+
+
+def _ckpt_worker(rank, world, port, model_fn, strategy_file, steps, seed, ckpt_dir, mode, out_path, optimizer):
+    """Train ``steps`` steps and save a checkpoint (mode "save", weights drawn
+    like _train), or load one (possibly written under another world /
+    strategy) and train ``steps`` more (mode "load")."""
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
+    from flexflow_train_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    cfg = FFConfig()
+    cfg.seed = seed
+    if strategy_file:
+        cfg.import_strategy_file = strategy_file
+    else:
+        cfg.only_data_parallel = True
+    model = FFModel(cfg)
+    feeds, labels = model_fn(model)
+    opt = SGDOptimizer(model, lr=0.05, momentum=0.9) if optimizer == "sgd" else AdamOptimizer(model, alpha=1e-3)
+    model.compile(optimizer=opt, loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY])
+    ex = model.executor
+    meta = {}
+    if mode == "save":
+        g = torch.Generator().manual_seed(seed)
+        for name in sorted(ex.parameter_names()):
+            ex.set_parameter(name, torch.randn(ex.get_parameter(name).shape, generator=g) * 0.2)
+    else:
+        meta = load_checkpoint(model, ckpt_dir)
+    for _ in range(steps):
+        ex.train_step(feeds, labels)
+    if mode == "save":
+        save_checkpoint(model, ckpt_dir)
+    params = {n: ex.get_parameter(n).detach().cpu().clone() for n in sorted(ex.parameter_names())}
+    if rank == 0:
+        torch.save({"params": params, "meta": {k: v for k, v in meta.items() if isinstance(v, (bool, int, str))}},
+                   out_path)
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_checkpointed(model_fn, ckpt_dir: str, save_world: int, load_world: int, save_strategy: Optional[str] = None,
+                     load_strategy: Optional[str] = None, steps_before: int = 2, steps_after: int = 2, seed: int = 0,
+                     optimizer: str = "adam") -> Dict:
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "out.pt")
+        mp.start_processes(_ckpt_worker, args=(save_world, free_port(), model_fn, save_strategy, steps_before, seed,
+                                               ckpt_dir, "save", out, optimizer),
+                           nprocs=save_world, join=True, start_method="spawn")
+        mp.start_processes(_ckpt_worker, args=(load_world, free_port(), model_fn, load_strategy, steps_after, seed,
+                                               ckpt_dir, "load", out, optimizer),
+                           nprocs=load_world, join=True, start_method="spawn")
+        return torch.load(out, weights_only=True)
