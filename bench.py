@@ -61,7 +61,10 @@ def main():
                                                                    "288 GB of HBM per GPU (profiles/batch_sweep_r3.txt)")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--model", default="bert-large",
-                    choices=["bert-large", "bert-base", "resnet50", "dlrm", "gpt3-medium"])
+                    choices=["bert-large", "bert-base", "resnet50", "resnext50", "inception-v3", "dlrm",
+                             "gpt3-medium"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32"],
+                    help="compute dtype (float32: the exact-fp32 MFMA kernels; the headline metric is bf16)")
     ap.add_argument("--layers", type=int, default=None, help="override (debug only; invalidates the metric)")
     ap.add_argument("--strategy", default="search", choices=["search", "dp"])
     ap.add_argument("--no-dp-compare", action="store_true",
@@ -109,7 +112,7 @@ def main():
         print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(res["value"], 2),
                           "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
-                          "vs_baseline": None, "dtype": "bf16", "data": res["data"], "config": conf,
+                          "vs_baseline": None, "dtype": args.dtype, "data": res["data"], "config": conf,
                           "world_size": dist_world, "backend": backend}), flush=True)
         if os.environ.get("FF_GEMM_REPORT"):
             from flexflow_train_amd.ops.dense import dact_report
@@ -227,6 +230,7 @@ def _run_bert(args, world, rank, only_dp: bool):
     cfg.print_freq = 0
     cfg.profiling = args.profile
     cfg.only_data_parallel = only_dp
+    cfg.compute_dtype = "float32" if args.dtype == "float32" else "bfloat16"
     cfg.search_budget = args.budget or _AE_BUDGET["bert"]
     model = FFModel(cfg)
     build_bert(model, bcfg)
@@ -305,11 +309,14 @@ def _parallelism(model, world: int) -> str:
 # data parallelism at any budget, and 400 iterations cost ~50 s per run at 8
 # GPUs); DLRM keeps 400 — with 20 iterations the search shards only one of
 # the eight tables (predicted 1.13x vs 14.8x over DP at 8 GPUs)
-_AE_BUDGET = {"bert": 30, "gpt": 30, "dlrm": 400, "resnet50": 400}
+_AE_BUDGET = {"bert": 30, "gpt": 30, "dlrm": 400, "resnet50": 400, "resnext50": 20, "inception_v3": 10}
 
 _ZOO = {
     # bench name -> (zoo name, per-GPU batch, config overrides, optimizer, extra config for the JSON line)
     "resnet50": ("resnet50", 256, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
+    # the reference's OSDI'22 AE CNNs (scripts/osdi22ae/resnext-50.sh, inception.sh)
+    "resnext50": ("resnext50", 64, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
+    "inception-v3": ("inception_v3", 64, dict(image_size=299, num_classes=1000), "sgd", {"image_size": 299}),
     "dlrm": ("dlrm", 1024, dict(embedding_size=[1000000] * 8, sparse_feature_size=64, mlp_bot=[64, 512, 512, 64],
                                 mlp_top=[576, 1024, 1024, 1024, 1]), "sgd", {"tables": "8x1M", "sparse": 64}),
     "gpt3-medium": ("gpt", 16, dict(hidden_size=1024, num_layers=24, num_heads=16, sequence_length=2048),
@@ -335,11 +342,13 @@ def _run_zoo(args, world, rank, only_dp: bool):
     cfg.print_freq = 0
     cfg.profiling = args.profile
     cfg.only_data_parallel = only_dp
+    cfg.compute_dtype = "float32" if args.dtype == "float32" else "bfloat16"
     cfg.search_budget = args.budget or _AE_BUDGET.get(zname, 400)
     model = FFModel(cfg)
     inputs, out, mcfg = Z.build(zname, model, batch_size=global_batch, **over)
     ce = Z.loss_of(zname) == Z.LOSS_CE
-    optimizer = (SGDOptimizer(model, lr=0.01, momentum=0.9 if zname == "resnet50" else 0.0) if opt == "sgd"
+    optimizer = (SGDOptimizer(model, lr=0.01, momentum=0.9 if zname in ("resnet50", "resnext50", "inception_v3")
+                              else 0.0) if opt == "sgd"
                  else AdamOptimizer(model, alpha=1e-4, weight_decay=0.01, decoupled=True))
     t0 = time.time()
     model.compile(optimizer=optimizer,
