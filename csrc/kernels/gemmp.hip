@@ -510,7 +510,8 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
   // the non-persistent gemmt spreads the remainder K-tiles over the first
   // splits (QKV dW: 48 tiles x 5 splits = 240 workgroups); every other
   // kernel streams the same number of K-tiles per work item
-  const bool uneven = ((p.variant == 3 || p.variant == 4 || p.variant == 6) && small && gemmt_supported(p)) ||
+  const bool uneven = ((p.variant == 3 || p.variant == 4 || p.variant == 6 || p.variant == 10) && small &&
+                       gemmt_supported(p)) ||
                       p.variant == 8;
   if (!uneven)
     while (nk % splits) --splits;
@@ -540,7 +541,7 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
     if (splits > 1) splitk_reduce(p.workspace, p.C, p.M, p.N, p.ldc, splits, p.beta, p.out_f32, st);
     return;
   }
-  if ((p.variant >= 1 && p.variant <= 6) || p.variant == 9) {
+  if ((p.variant >= 1 && p.variant <= 6) || p.variant == 9 || p.variant == 10) {
     if (p.variant == 2 && small) gemmr_launch(p, splits, n_cu, st);
     else if (p.variant >= 3 && small && gemmt_supported(p))
       gemmt_launch(p, splits, p.variant - 3, st);

@@ -832,7 +832,14 @@ __device__ __forceinline__ void kk_for(F&& f, std::integer_sequence<int, I...>) 
 
 // TA: A K-outer (padded image, as B); !TA: A K-contiguous (gemmt_kernel's
 // swizzled 128-B-row image, ds_read_b128 at lane base + immediate)
-template <bool TA, int EPI, int ACT, int SCH = 0, bool TB = false>
+// RS: the K-tile after next is loaded into registers (buffer_load_dwordx4,
+// one 16-B piece per lane per DMA piece) in phase A and written lane-linearly
+// with ds_write_b128 into the SAME image the LDS-DMA builds, one K-tile later.
+// An LDS-DMA piece costs the issuing wave 60-185 cycles of issue among MFMAs
+// (MI355X_MICROARCH.md cycle constants, 'LDS-DMA piece issue cost'); a
+// buffer_load + ds_write_b128 pair ~20, inside the MFMA gaps, and the loads
+// get a whole K-tile (not one phase) to land.
+template <bool TA, int EPI, int ACT, int SCH = 0, bool TB = false, bool RS = false>
 __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemmt_kk_kernel(
     GemmTArgs g) {
   constexpr int SA = TA ? KK_PT : 2 * HALF;   // A tile bytes per buffer
@@ -891,6 +898,43 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     }
   };
 
+  // register staging (RS): piece i of A in R[i], of B in R[NPA + i]
+  constexpr int NPA = TA ? KK_NP : 8, NPB = TB ? 8 : KK_NP;
+  i32x4t R[RS ? NPA + NPB : 1];
+  auto ldA = [&](unsigned kbyte, int i) __attribute__((always_inline)) {
+    if constexpr (RS) {
+      if (TA) {
+        R[i] = __builtin_amdgcn_raw_buffer_load_b128(rA, dvA[i], __builtin_amdgcn_readfirstlane(kbyte), 0);
+      } else {
+        const unsigned so = kbyte + static_cast<unsigned>(8 * (i - (i & 1))) * static_cast<unsigned>(g.lda) * 2u;
+        R[i] = __builtin_amdgcn_raw_buffer_load_b128(rA, dvA[i & 1], __builtin_amdgcn_readfirstlane(so), 0);
+      }
+    }
+  };
+  auto ldB = [&](unsigned kbyte, int i) __attribute__((always_inline)) {
+    if constexpr (RS) {
+      if (!TB) {
+        R[NPA + i] = __builtin_amdgcn_raw_buffer_load_b128(rB, dvB[i], __builtin_amdgcn_readfirstlane(kbyte), 0);
+      } else {
+        const unsigned so = kbyte + static_cast<unsigned>(8 * (i - (i & 1))) * static_cast<unsigned>(g.ldb) * 2u;
+        R[NPA + i] = __builtin_amdgcn_raw_buffer_load_b128(rB, dvB[i & 1], __builtin_amdgcn_readfirstlane(so), 0);
+      }
+    }
+  };
+  // the lane-linear LDS position the DMA would have written piece i to
+  auto wrA = [&](int buf, int i) __attribute__((always_inline)) {
+    if constexpr (RS) {
+      unsigned char* d = sA + buf * SA + (TA ? dpiece + i * 1024 : (wave * 8 + i) * 1024) + lane * 16;
+      *reinterpret_cast<i32x4t*>(d) = R[i];
+    }
+  };
+  auto wrB = [&](int buf, int i) __attribute__((always_inline)) {
+    if constexpr (RS) {
+      unsigned char* d = sB + buf * SB + (!TB ? dpiece + i * 1024 : (wave * 8 + i) * 1024) + lane * 16;
+      *reinterpret_cast<i32x4t*>(d) = R[NPA + i];
+    }
+  };
+
   // lane base of the fragment reads (LDS byte address)
   const int gq = lane >> 4, iq = lane & 15;
   const int lrow = kk_swap23(8 * gq + (iq >> 2));
@@ -933,16 +977,28 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
 
-  // ---- prologue: tile 0 -> buffer 0, tile 1 -> buffer 1, k-step 0 fragments
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-#pragma unroll
-    for (int i = 0; i < (TA ? KK_NP : 8); ++i) dmaA(b, static_cast<unsigned>(kt0 + b) * kstepA, i);
-#pragma unroll
-    for (int i = 0; i < (TB ? 8 : KK_NP); ++i) dmaB(b, static_cast<unsigned>(kt0 + b) * kstepB, i);
-  }
-  // tile 0 landed (tile 1's 18 / 17 pieces in flight)
+  // ---- prologue: tile 0 -> buffer 0, tile 1 -> buffer 1 (RS: tile 0 ->
+  // buffer 0 by DMA, tile 1 -> registers), k-step 0 fragments
   constexpr int NPT = (TA ? KK_NP : 8) + (TB ? 8 : KK_NP);   // DMA issues per K-tile per wave
+  if constexpr (RS) {
+#pragma unroll
+    for (int i = 0; i < NPA; ++i) dmaA(0, static_cast<unsigned>(kt0) * kstepA, i);
+#pragma unroll
+    for (int i = 0; i < NPB; ++i) dmaB(0, static_cast<unsigned>(kt0) * kstepB, i);
+#pragma unroll
+    for (int i = 0; i < NPA; ++i) ldA(static_cast<unsigned>(kt0 + 1) * kstepA, i);
+#pragma unroll
+    for (int i = 0; i < NPB; ++i) ldB(static_cast<unsigned>(kt0 + 1) * kstepB, i);
+  } else {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int i = 0; i < NPA; ++i) dmaA(b, static_cast<unsigned>(kt0 + b) * kstepA, i);
+#pragma unroll
+      for (int i = 0; i < NPB; ++i) dmaB(b, static_cast<unsigned>(kt0 + b) * kstepB, i);
+    }
+  }
+  // tile 0 landed (tile 1's 18 / 17 / 16 pieces in flight, by DMA or into registers)
   if constexpr (NPT == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
   else if constexpr (NPT == 17) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -959,7 +1015,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
   // pieces), each pinned by sched_barrier, instead of the group's reads
   // clustered after its 8 MFMAs
   auto group = [&](auto MBC, auto KSC, const bf16x8 (&fin)[8], bf16x8 (&fout)[8], unsigned aB, unsigned bB,
-                   int dbuf, unsigned ka_, unsigned kb_) __attribute__((always_inline)) {
+                   int dbuf, unsigned ka_, unsigned kb_, int wbuf = -1) __attribute__((always_inline)) {
     constexpr int mb = decltype(MBC)::value, ks = decltype(KSC)::value;
     constexpr int OB = ks * 32 * KK_PITCH + mb * 32;
     bf16x4 b0, b1, a0, a1;
@@ -981,15 +1037,31 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][4] = mfma16(fin[4], fa[mb], acc[mb][4]);
     if (dbuf >= 0) dmaA(dbuf, ka_, mb);
+    if (RS && wbuf >= 0) {
+      wrA(wbuf, mb);
+      ldA(ka_, mb);
+    }
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][5] = mfma16(fin[5], fa[mb], acc[mb][5]);
     if (dbuf >= 0) dmaB(dbuf, kb_, mb);
+    if (RS && wbuf >= 0) {
+      wrB(wbuf, mb);
+      ldB(kb_, mb);
+    }
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][6] = mfma16(fin[6], fa[mb], acc[mb][6]);
     if (dbuf >= 0 && mb == 7 && TA) dmaA(dbuf, ka_, 8);
+    if (RS && wbuf >= 0 && mb == 7 && TA) {
+      wrA(wbuf, 8);
+      ldA(ka_, 8);
+    }
     __builtin_amdgcn_sched_barrier(0);
     acc[mb][7] = mfma16(fin[7], fa[mb], acc[mb][7]);
     if (dbuf >= 0 && mb == 7 && !TB) dmaB(dbuf, kb_, 8);
+    if (RS && wbuf >= 0 && mb == 7 && !TB) {
+      wrB(wbuf, 8);
+      ldB(kb_, 8);
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (TB) fout[mb] = br;
     else fout[mb] = cat44(b0, b1);
@@ -1016,13 +1088,16 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
         for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = mfma16(fbx[nb], fa[mb], acc[mb][nb]);
         fa[mb] = readA(K1{}, MB, aC);
         fby[mb] = readB(K1{}, MB, bC);
+      } else if constexpr (RS) {
+        // stage tile kt+1 (registers) into the next buffer, load tile kt+2
+        group(MB, K1{}, fbx, fby, aC, bC, -1, ka, kb, cur ^ 1);
       } else {
         group(MB, K1{}, fbx, fby, aC, bC, -1, 0u, 0u);
       }
     }, S8);
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile kt+1 (next buffer) landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // k-step 1 reads done
+    if constexpr (!RS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile kt+1 (next buffer) landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // k-step 1 reads (RS: and the staging writes) done
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // phase B: k-step 1 (fa, fby) | read k-step 0 of the next buffer into (fa, fbx),
@@ -1042,7 +1117,7 @@ __global__ __launch_bounds__(NTHREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 
           if (!TB) dmaB(cur, kb, 8);
         }
       } else {
-        group(MB, K0{}, fby, fbx, aN, bN, cur, ka, kb);
+        group(MB, K0{}, fby, fbx, aN, bN, RS ? -1 : cur, ka, kb);
       }
     }, S8);
     __builtin_amdgcn_sched_barrier(0);
@@ -1314,25 +1389,39 @@ void launch_t(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipSt
   }
 }
 
-template <bool TA, int SCH, bool TB>
+template <bool TA, int SCH, bool TB, bool RS = false>
 void launch_kk_s(const GemmTArgs& g, dim3 grid, dim3 block, int epi, int act, hipStream_t st) {
   switch (epi * 8 + act) {
-    case kEpiPlain * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0, SCH, TB>), grid, block, 0, st, g); break;
-    case kEpiSplit * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0, SCH, TB>), grid, block, 0, st, g); break;
-    case kEpiGeneral * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0, SCH, TB>), grid, block, 0, st, g); break;
-    case kEpiAccum * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0, SCH, TB>), grid, block, 0, st, g); break;
-    case kEpiBiasAct * 8 + 0:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0, SCH, TB>), grid, block, 0, st, g);
+    case kEpiPlain * 8:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiPlain, 0, SCH, TB, RS>), grid, block, 0, st, g);
       break;
-    case kEpiBias * 8: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0, SCH, TB>), grid, block, 0, st, g); break;
+    case kEpiSplit * 8:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiSplit, 0, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
+    case kEpiGeneral * 8:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiGeneral, 0, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
+    case kEpiAccum * 8:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiAccum, 0, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
+    case kEpiBiasAct * 8 + 0:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 0, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
+    case kEpiBias * 8:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBias, 0, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
     case kEpiBiasAct * 8 + 1:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1, SCH, TB>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 1, SCH, TB, RS>), grid, block, 0, st, g);
       break;
     case kEpiBiasAct * 8 + 4:
-      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4, SCH, TB>), grid, block, 0, st, g);
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiBiasAct, 4, SCH, TB, RS>), grid, block, 0, st, g);
       break;
-    case kEpiDact * 8 + 1: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1, SCH, TB>), grid, block, 0, st, g); break;
-    case kEpiDact * 8 + 4: hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4, SCH, TB>), grid, block, 0, st, g); break;
+    case kEpiDact * 8 + 1:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 1, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
+    case kEpiDact * 8 + 4:
+      hipLaunchKernelGGL((gemmt_kk_kernel<TA, kEpiDact, 4, SCH, TB, RS>), grid, block, 0, st, g);
+      break;
     default: throw std::invalid_argument("gemmt: activation without an instantiated epilogue");
   }
 }
@@ -1420,7 +1509,11 @@ void gemmt_launch(const GemmPParams& p, int splits, int stage_mode, hipStream_t 
     else if (!p.trans_a && p.trans_b) launch_pers<false, true>(g, pgrid, block, epi, p.act, st);
     else if (p.trans_a && !p.trans_b) launch_pers<true, false>(g, pgrid, block, epi, p.act, st);
     else launch_pers<true, true>(g, pgrid, block, epi, p.act, st);
-  } else if (stage_mode == 3) {   // both operands by LDS-DMA
+  } else if (stage_mode == 7 && !(p.trans_a && p.trans_b)) {   // kk images, register-staged (variant 10)
+    if (!p.trans_a && !p.trans_b) launch_kk_s<false, 1, false, true>(g, grid, block, epi, p.act, st);
+    else if (!p.trans_a && p.trans_b) launch_kk_s<false, 1, true, true>(g, grid, block, epi, p.act, st);
+    else launch_kk_s<true, 1, false, true>(g, grid, block, epi, p.act, st);
+  } else if (stage_mode == 3 || stage_mode == 7) {   // both operands by LDS-DMA
     const bool kk = kk_enabled() && !p.dbg;
     if (!p.trans_a && !p.trans_b) {
       if (kk) launch_kk<false>(g, grid, block, epi, p.act, st);

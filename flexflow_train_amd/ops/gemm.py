@@ -206,6 +206,7 @@ def _gp(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
 # three
 _GT_VARIANT = int(os.environ.get("FF_GEMMT_VARIANT", "3"))
 _GT_DMA = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_DMA", "1") != "0"
+_GT_RS = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_RS", "1") != "0"
 
 
 def _gt(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1, variant=None):
@@ -328,6 +329,12 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
                 if _GT_DMA:
                     c[f"u:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=4)))(s)
                     c[f"w:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=6)))(s)
+                if _GT_RS and not (trans_a and trans_b):
+                    # the padded-image kernel with register staging (variant 10):
+                    # 1-11 % ahead of "w" on the weight-gradient and long-K
+                    # input-gradient shapes, behind it on the K = 1024 forwards
+                    # (profiles/r5/ab_gemmt_kk_rs_r5.txt) -- timed, not assumed
+                    c[f"x:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=10)))(s)
     return c
 
 
@@ -460,7 +467,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
         choice = "hip"
-    if choice[:2] in ("p:", "t:", "u:", "w:", "s:", "n:") and not K.gemmp_supported(a, b, trans_a, trans_b):
+    if choice[:2] in ("p:", "t:", "u:", "w:", "x:", "s:", "n:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -516,6 +523,8 @@ def _resolve(name: str):
         return lambda *args: _gt(*args, splits=int(arg), variant=4)
     if kind == "w":
         return lambda *args: _gt(*args, splits=int(arg), variant=6)
+    if kind == "x":
+        return lambda *args: _gt(*args, splits=int(arg), variant=10)
     if kind == "s":
         return lambda *args: _gs(*args, splits=int(arg))
     if kind == "n":

@@ -356,9 +356,9 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9],
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10],
                          ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128", "wave128dma", "wave128pers",
-                              "wave128dma2", "tile64", "nt8wave"])
+                              "wave128dma2", "tile64", "nt8wave", "wave128regstage"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1),
@@ -385,30 +385,35 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
     af = a.float().t() if ta else a.float()
     bf = b.float().t() if tb else b.float()
     ref = af @ bf
+    # bf16 inputs, fp32 accumulation: against the fp32 product of the same
+    # bf16 values only the output rounding remains (bf16: 2^-9 per element,
+    # ~1.2e-3 relative Frobenius); a systematic 0.5 % error in one K-tile
+    # phase would exceed these bounds
+    BF, F32 = 3e-3, 2e-5
     c = gemmp(a, b, trans_a=ta, trans_b=tb, splits=splits)
-    assert _rel(c, ref) < 1e-2
+    assert _rel(c, ref) < BF
     c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
     gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
-    assert _rel(c3, ref + 1) < 1e-2
+    assert _rel(c3, ref + 1) < F32
     # bf16 accumulate (gemmt: the paired 16-B read-modify-write epilogue)
     c4 = torch.full((M, N), 0.5, device=DEV, dtype=torch.bfloat16)
     gemmp(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c4, splits=splits)
-    assert _rel(c4, ref + 0.5) < 1e-2
+    assert _rel(c4, ref + 0.5) < BF
     if splits == 1:
         bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         c2 = gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
         u = ref + bias.float()
-        assert _rel(gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias), u) < 1e-2   # bias only
-        assert _rel(pre, u) < 1e-2
-        assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
+        assert _rel(gemmp(a, b, trans_a=ta, trans_b=tb, bias=bias), u) < BF   # bias only
+        assert _rel(pre, u) < BF
+        assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < BF
         aux = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
         db = torch.full((N,), 0.5, device=DEV)
         g = gemmp(a, b, trans_a=ta, trans_b=tb, act="gelu", aux=aux, act_bwd=True, dbias=db)
         x = aux.float().requires_grad_(True)
         torch.nn.functional.gelu(x, approximate="tanh").backward(torch.ones_like(x))
         gr = ref * x.grad
-        assert _rel(g, gr) < 1e-2
+        assert _rel(g, gr) < BF
         if variant >= 3:   # gemmt / gemms sum the fp32 gradient (before its bf16 rounding)
             assert _rel(db, gr.sum(0) + 0.5) < 1e-3
         else:              # the other kernels sum the stored bf16 values

@@ -82,7 +82,7 @@ def main():
         bt = args.beta
         cands = {"blaslt": lambda o: K.blaslt_gemm(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt)}
         splits = [1] if kind != "dw" else [2, 4, 8]
-        variants = {"p": 0, "q": 1, "r": 2, "t": 3, "u": 4, "v": 5, "w": 6}
+        variants = {"p": 0, "q": 1, "r": 2, "t": 3, "u": 4, "v": 5, "w": 6, "x": 10}
         for sp in splits:
             for pre, var in variants.items():
                 cands[f"{pre}{sp}"] = (lambda o, sp=sp, var=var:
