@@ -55,6 +55,7 @@ class DistContext:
         self.force_collectives = force_collectives
         self._groups: Dict[Tuple[int, ...], object] = {}
         self.stats = {"all_reduce": 0, "all_gather": 0, "all_to_all": 0, "p2p": 0, "local": 0, "bytes": 0}
+        self.msg_sizes: Dict[str, set] = {}
         # runtime/graphs.SegmentRecorder while a distributed step is being
         # captured: in-place collectives become segment boundaries
         self.recorder = None
@@ -123,6 +124,7 @@ class DistContext:
     def all_reduce_(self, t: torch.Tensor, ranks: Sequence[int], async_op: bool = False):
         if not self.syncs(ranks):
             return None
+        self.note_size("all_reduce", t.numel() * t.element_size())
         self.stats["all_reduce"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
         grp = self.group(ranks)
@@ -180,6 +182,13 @@ class DistContext:
             self._issue(lambda: dist.all_gather_into_tensor(t, piece, group=grp), False)
         else:
             dist.all_gather(list(t.split(chunk)), t[i * chunk:(i + 1) * chunk].clone(), group=self.group(ranks))
+
+    def note_size(self, kind: str, nbytes: int):
+        """Message sizes the step issues, per collective kind (the collective
+        cost model is calibrated at these sizes: parallel/calibrate.py)."""
+        s = self.msg_sizes.setdefault(kind, set())
+        if len(s) < 64:
+            s.add(int(nbytes))
 
     def max_scalar(self, v: float) -> float:
         if not self.distributed:
@@ -285,6 +294,14 @@ def make_plan(src: Layout, dst: Layout, world: int) -> Plan:
             groups.append(g)
     if ok and src.sum_degree > dst.sum_degree:
         return Plan("all_reduce", contributions, dst_boxes, src_boxes, groups)
+    # reduce_scatter: the partial-sum replicas of one box, each member keeping
+    # an equal slice of the sum along one dim (a row-parallel output going to a
+    # sharded consumer): one reduce_scatter_tensor over the group instead of an
+    # all_to_all of the partial slices plus a local sum
+    if src.sum_degree > dst.sum_degree:
+        rs = _reduce_scatter_groups(contributions, dst_boxes)
+        if rs is not None:
+            return Plan("reduce_scatter", contributions, dst_boxes, src_boxes, rs[0], gather_dim=rs[1])
     # all_gather: each rank assembles its dst box from its group's own pieces
     groups = []
     ok = src.sum_degree == dst.sum_degree
@@ -322,9 +339,55 @@ def make_plan(src: Layout, dst: Layout, world: int) -> Plan:
     # whole exchange is ONE all_to_all with per-rank split sizes (RCCL spreads
     # it over all xGMI links at once) instead of a batch of point-to-point ops
     pairs = [(r, c.src_rank) for r, cl in contributions.items() for c in cl]
+    # only the ranks that send or receive take part (a pipeline-stage boundary
+    # involves the two stages' ranks, not the world)
+    involved = tuple(sorted({r for r, _ in pairs if any(c.src_rank != r for c in contributions[r])} |
+                            {m for r, m in pairs if m != r}))
+    sub = [involved] if 1 < len(involved) < world else []
     if len(pairs) == len(set(pairs)) and os.environ.get("FF_REDIST_P2P", "0") != "1":
-        return Plan("all_to_all", contributions, dst_boxes, src_boxes, [])
+        return Plan("all_to_all", contributions, dst_boxes, src_boxes, sub)
     return Plan("p2p", contributions, dst_boxes, src_boxes, [])
+
+
+def _reduce_scatter_groups(contributions, dst_boxes):
+    """(groups, dim) when every rank's destination box is its equal slice,
+    along one dim, of one source box whose partial sums its group's members
+    hold (the members being exactly the ranks that receive the slices), with
+    the slices in the members' rank order; else None."""
+    groups: List[Tuple[int, ...]] = []
+    rdim = -1
+    for r, cl in contributions.items():
+        if not cl:
+            return None
+        g = tuple(sorted(c.src_rank for c in cl))
+        b0 = cl[0].src_box
+        if r not in g or len(set(g)) != len(g) or len(g) < 2:
+            return None
+        if any(c.src_box != b0 or c.part != dst_boxes[r] for c in cl):
+            return None
+        boxes = []
+        for m in g:
+            cm = contributions.get(m)
+            if (cm is None or dst_boxes.get(m) is None or tuple(sorted(c.src_rank for c in cm)) != g
+                    or any(c.src_box != b0 for c in cm)):
+                return None
+            boxes.append(dst_boxes[m])
+        diffs = {i for b in boxes for i, (x, y) in enumerate(zip(b, b0)) if x != y}
+        if len(diffs) != 1:
+            return None
+        d = diffs.pop()
+        if rdim not in (-1, d):
+            return None
+        rdim = d
+        starts = [b[d][0] for b in boxes]
+        sizes = [b[d][1] - b[d][0] for b in boxes]
+        # equal slices, tiling the source box in the members' (sorted) order
+        if len(set(sizes)) != 1 or starts != sorted(starts) or starts[0] != b0[d][0] \
+                or starts[-1] + sizes[-1] != b0[d][1] or len(set(starts)) != len(starts):
+            return None
+        if g not in groups:
+            groups.append(g)
+    return (groups, rdim) if rdim >= 0 else None
 
 
 def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_shape: Sequence[int],
@@ -343,28 +406,58 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
         if c.part == my_src:
             return x
         return x[rel_slices(c.part, my_src)].contiguous()
+    if plan.kind in ("all_reduce", "reduce_scatter", "all_gather") and not any(me in g for g in plan.groups):
+        return None   # these plans' groups are exactly the receivers: nothing to send or receive here
     if plan.kind == "all_reduce":
         y = x.clone()
         g = next(g for g in plan.groups if me in g)
         ctx.all_reduce_(y, g)
         return y
+    if plan.kind == "reduce_scatter":
+        g = next(g for g in plan.groups if me in g)
+        ctx.stats["reduce_scatter"] = ctx.stats.get("reduce_scatter", 0) + 1
+        d = plan.gather_dim
+        n = len(g)
+        # chunk i of the flat input = member g[i]'s slice (g is sorted and the
+        # slices follow it along d): contiguous as it stands when d is the
+        # outermost dim with a non-trivial extent, one packing copy otherwise
+        xs = x.contiguous()
+        if all(xs.shape[i] == 1 for i in range(d)):
+            inp = xs.reshape(-1)
+        else:
+            inp = torch.stack(xs.chunk(n, dim=d)).reshape(-1)
+        out = torch.empty(dst_shape, dtype=xs.dtype, device=xs.device)
+        grp = ctx.group(g)
+        ctx.note_size("reduce_scatter", inp.numel() * inp.element_size())
+        ctx._issue(lambda: dist.reduce_scatter_tensor(out.view(-1), inp, group=grp), False)
+        return out.to(dtype)
     if plan.kind == "all_gather":
         g = next(g for g in plan.groups if me in g)
         ctx.stats["all_gather"] += 1
         xs = x.contiguous()
-        outs = [torch.empty_like(xs) for _ in g]
+        n = len(g)
         grp = ctx.group(g)
-        ctx._issue(lambda: dist.all_gather(outs, xs, group=grp), False)
-        order = sorted(range(len(g)), key=lambda i: plan.src_boxes[g[i]][plan.gather_dim][0])
+        # one all_gather_into_tensor into [n, *piece] (member order = sorted
+        # ranks), then the members' pieces in box order along the gather dim:
+        # a view when the pieces already follow that order on the outermost
+        # dim, one copy (movedim + reshape) otherwise -- no list + cat
+        flat = torch.empty((n,) + tuple(xs.shape), dtype=xs.dtype, device=xs.device)
+        ctx.note_size("all_gather", flat.numel() * flat.element_size())
+        ctx._issue(lambda: dist.all_gather_into_tensor(flat.view(-1), xs.view(-1), group=grp), False)
+        order = sorted(range(n), key=lambda i: plan.src_boxes[g[i]][plan.gather_dim][0])
         # members holding identical boxes (implicit replicas) appear once
-        seen, parts = set(), []
+        seen, keep = set(), []
         for i in order:
             b = plan.src_boxes[g[i]]
             if b in seen:
                 continue
             seen.add(b)
-            parts.append(outs[i])
-        return torch.cat(parts, dim=plan.gather_dim)
+            keep.append(i)
+        d = plan.gather_dim
+        sel = flat if keep == list(range(n)) else flat[torch.tensor(keep, device=flat.device)]
+        if all(xs.shape[i] == 1 for i in range(d)):
+            return sel.reshape(tuple(xs.shape[:d]) + (len(keep) * xs.shape[d],) + tuple(xs.shape[d + 1:]))
+        return sel.movedim(0, d).reshape(tuple(xs.shape[:d]) + (len(keep) * xs.shape[d],) + tuple(xs.shape[d + 1:]))
     if plan.kind == "all_to_all":
         return _exchange_all_to_all(plan, x, ctx, dst_shape, dtype, device)
     # ---- generic point-to-point
@@ -416,8 +509,23 @@ def _exchange_all_to_all(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext
     sendbuf = torch.cat(parts) if parts else torch.empty(0, dtype=dtype, device=device)
     recvbuf = torch.empty(sum(out_sizes), dtype=sendbuf.dtype, device=device)
     sendbuf = sendbuf.to(device)
-    ctx._issue(lambda: dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=out_sizes,
-                                              input_split_sizes=in_sizes), False)
+    if plan.groups:
+        # a sub-group exchange (pipeline-stage boundary): ranks outside it take
+        # no part; members address each other by group rank (sorted order)
+        g = plan.groups[0]
+        if me not in g:
+            return None if my_dst is None else torch.zeros(dst_shape, dtype=dtype, device=device)
+        grp = ctx.group(g)
+        gi = [in_sizes[m] for m in g]
+        go = [out_sizes[m] for m in g]
+        ctx.stats["all_to_all_subgroup"] = ctx.stats.get("all_to_all_subgroup", 0) + 1
+        ctx.note_size("all_to_all", sendbuf.numel() * sendbuf.element_size())
+        ctx._issue(lambda: dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=go, input_split_sizes=gi,
+                                                  group=grp), False)
+    else:
+        ctx.note_size("all_to_all", sendbuf.numel() * sendbuf.element_size())
+        ctx._issue(lambda: dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=out_sizes,
+                                                  input_split_sizes=in_sizes), False)
     if my_dst is None:
         return None
     result = torch.zeros(dst_shape, dtype=dtype, device=device)

@@ -59,13 +59,13 @@ PROFILE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.pa
                            "profiles")
 
 
-def cost_model(ffconfig=None, world: Optional[int] = None, use_profiles: bool = True):
+def cost_model(ffconfig=None, world: Optional[int] = None, use_profiles: bool = True, spec=None):
     """Analytic MI355X model + measured op costs.  Tables: ``FF_PROFILE_TABLE``
     (os.pathsep-separated), ``ffconfig.profile_table_file``, and every
     committed ``profiles/op_costs_*.json`` (keys are exact op/piece
     signatures, so tables for different models/worlds merge safely; where
     two tables hold the same key the later one in the order below wins)."""
-    cm = C.CostModel(machine_spec(ffconfig, world))
+    cm = C.CostModel(spec if spec is not None else machine_spec(ffconfig, world))
     if not use_profiles or os.environ.get("FF_NO_PROFILE_TABLES"):
         return cm
     # later tables override earlier entries: committed standalone tables, then

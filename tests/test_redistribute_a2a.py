@@ -15,12 +15,24 @@ from flexflow_train_amd.parallel.layout import Layout, rel_slices
 
 
 def _cases(world):
+    """(src, dst, the plan kind the engine must pick; None = not checked)."""
     S = (8, 12, 4)
-    return [
-        (Layout(S, (world, 1, 1), block=world), Layout(S, (1, world if 12 % world == 0 else 1, 1), block=world)),
-        (Layout(S, (1, 1, 1), a_deg=world, block=world), Layout(S, (world, 1, 1), block=world)),
-        (Layout(S, (1, 2, 1), block=world), Layout(S, (2, 1, 1), block=2, start=world - 2)),
+    cases = [
+        (Layout(S, (world, 1, 1), block=world), Layout(S, (1, world if 12 % world == 0 else 1, 1), block=world),
+         None),
+        # partial sums -> batch shards: one reduce_scatter_tensor
+        (Layout(S, (1, 1, 1), a_deg=world, block=world), Layout(S, (world, 1, 1), block=world), "reduce_scatter"),
+        # partial sums -> shards of an inner dim (packed once, then reduce-scattered)
+        (Layout(S, (1, 1, 1), a_deg=2, block=2), Layout(S, (1, 2, 1), block=2), "reduce_scatter"),
+        (Layout(S, (1, 2, 1), block=world), Layout(S, (2, 1, 1), block=2, start=world - 2), None),
+        # shards -> replicated: all_gather_into_tensor, outermost and inner dims
+        (Layout(S, (world, 1, 1), block=world), Layout(S, (1, 1, 1), block=world), "all_gather"),
+        (Layout(S, (1, 2, 1), block=2), Layout(S, (1, 1, 1), block=2), "all_gather"),
     ]
+    if world >= 4:
+        # a stage boundary that involves 3 of 4 ranks: a sub-group all_to_all
+        cases.append((Layout(S, (2, 1, 1), block=2, start=0), Layout(S, (1, 1, 1), block=1, start=2), "all_to_all"))
+    return cases
 
 
 def _worker(rank, world, port, p2p, errs):
@@ -32,7 +44,9 @@ def _worker(rank, world, port, p2p, errs):
         ctx = DistContext(rank, world, torch.device("cpu"))
         red = Redistributor(ctx)
         g = torch.Generator().manual_seed(0)
-        for src, dst in _cases(world):
+        for src, dst, kind in _cases(world):
+            if kind is not None and not p2p:
+                assert make_plan(src, dst, world).kind == kind, (src, dst, make_plan(src, dst, world).kind)
             full = torch.randn(src.sizes, generator=g)
             cs = src.coord(rank)
             x = None
@@ -49,6 +63,10 @@ def _worker(rank, world, port, p2p, errs):
             torch.testing.assert_close(y, want)
         key = "p2p" if p2p else "all_to_all"
         assert ctx.stats[key] > 0, ctx.stats
+        if not p2p:
+            assert ctx.stats.get("reduce_scatter", 0) >= 1 and ctx.stats["all_gather"] >= 1, ctx.stats
+            if world >= 4:
+                assert ctx.stats.get("all_to_all_subgroup", 0) >= 1 or rank == 3, ctx.stats
     except BaseException as e:  # noqa: BLE001
         errs.put(repr(e))
         raise
