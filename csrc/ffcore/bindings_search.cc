@@ -368,6 +368,21 @@ void register_ext_bindings(py::module_& m) {
     }
     return py::make_tuple(r.runtime, r.feasible, views_to_py(r.views), r.to_json().dump());
   }, py::arg("pcg"), py::arg("cost_model"), py::arg("world"), py::arg("contiguous_only") = false);
+  m.def("mm_subtree_signatures", [](const ParallelComputationGraph& p) {
+    return get_machine_mapping_problem_tree(p).tree.signatures();
+  });
+  // map several PCGs in turn through ONE mapping cache (the joint search's
+  // shared MachineMappingCache): per PCG (runtime, cache entries, hits so far)
+  m.def("machine_mapping_sequence", [](const std::vector<ParallelComputationGraph>& ps, const CostModel& cm,
+                                       int world) {
+    MMCache cache;
+    std::vector<std::tuple<double, int64_t, int64_t>> out;
+    for (auto const& p : ps) {
+      auto r = get_optimal_machine_mapping(p, cm, world, MachineMappingOptions{}, &cache);
+      out.emplace_back(r.runtime, static_cast<int64_t>(cache.results.size()), static_cast<int64_t>(cache.hits));
+    }
+    return out;
+  });
   m.def("machine_mapping_problem_tree", [](const ParallelComputationGraph& p) {
     auto prob = get_machine_mapping_problem_tree(p);
     Json j = Json::object();

@@ -81,6 +81,10 @@ struct MMProblemTree {
   int add_parallel(int l, int r);
   std::vector<BinaryTreePath> leaf_paths(int idx) const;
   int subtree_at(int idx, const BinaryTreePath& path) const;  // -1 if invalid
+  // content signature of every subtree (index -> 128-bit hex string): equal
+  // signatures = identical leaves (op attrs, input / weight / output parallel
+  // shapes, synthetic ids), split kinds and movements
+  std::vector<std::string> signatures() const;
 };
 
 // A sub-machine: nodes [node_offset, +num_nodes) x GPUs [gpu_offset, +gpus_per_node).
@@ -141,6 +145,13 @@ struct MMContext {
   size_t max_boundary_assignments = 4096;  // cap on one side's boundary view assignments
 };
 
+// Memo of solved subproblems.  Keys name a subtree by its CONTENT (a
+// signature of its leaves' op attrs + parallel shapes, its splits and their
+// movements: MMProblemTree::signatures), not by its index in one tree, so
+// one cache can serve every PCG a search visits: a rewrite that changes a few
+// operators leaves the other subtrees' entries valid (the reference's
+// MachineMappingCache keyed by MachineMappingState, machine_mapping_cache.cc,
+// shared across the states of unity_algorithm.cc:37-90).
 struct MMCache {
   std::map<std::string, MMResult> results;
   size_t hits = 0, misses = 0;
@@ -191,7 +202,8 @@ struct MachineMappingOptions {
   bool contiguous_only = false;
 };
 
+// `shared`: a cache reused across calls (a search's states); null = private
 MachineMappingResult get_optimal_machine_mapping(const ParallelComputationGraph& pcg, const CostModel& cm, int world,
-                                                 const MachineMappingOptions& opt = {});
+                                                 const MachineMappingOptions& opt = {}, MMCache* shared = nullptr);
 
 }  // namespace ff

@@ -34,7 +34,14 @@ struct SearchConfig {
   double group_move_prob = 0.6; // propose the same config for every layer of the same signature
   uint64_t seed = 0x5eed;
   double time_limit = 60.0;     // seconds
-  bool use_machine_mapping = false;  // Unity cost: DP machine mapping (else simulator)
+  // Unity cost of every state: its DP machine mapping (shared subtree cache)
+  // simulated, against whole-world placements (false: whole-world only, the
+  // mapping DP runs once on the winner -- final_machine_mapping)
+  bool use_machine_mapping = true;
+  double mapping_alpha = 1.2;   // map states whose whole-world cost <= best so far * this
+  int max_mapped_states = 64;   // at most this many mappings per search (-1: no cap); the
+                                // first states popped are the cheapest, so the cap keeps the
+                                // mapping on the search's front
   // graph_optimize: Unity best-first pops (-1: `budget`, the reference's
   // single --budget drives the whole search, unity_algorithm.cc:37-90) and
   // the share of time_limit MCMC may use before Unity starts
@@ -66,6 +73,9 @@ struct SearchResult {
   int rules = 0;                         // Unity: rules tried (built-in + rule set)
   int rule_set_rules = 0;                // Unity: of which from the rule set
   std::vector<std::string> best_rules;   // Unity: rewrites from the initial PCG to the best one
+  int64_t mapping_cache_entries = 0;     // Unity joint search: shared mapping-cache size / hits
+  int64_t mapping_cache_hits = 0;
+  int mapped_states = 0;                 // states priced with their own machine mapping
   Json to_json(const ComputationGraph* cg = nullptr) const;
 };
 

@@ -197,6 +197,53 @@ MMResult minimize_runtime(const MMResult& a, const MMResult& b) {
 }
 
 // ---------------------------------------------------------------------------
+// subtree signatures (content keys of the shared cache)
+namespace {
+uint64_t fnv(const std::string& s, uint64_t h) {
+  for (unsigned char ch : s) {
+    h ^= ch;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+std::string pshape_str(const ParallelTensorShape& p) { return p.to_json().dump(); }
+std::string paths_str(const std::set<BinaryTreePath>& ps) {
+  std::string s;
+  for (auto const& p : ps) {
+    s += "[";
+    for (int x : p) s += std::to_string(x) + ",";
+    s += "]";
+  }
+  return s;
+}
+}  // namespace
+
+std::vector<std::string> MMProblemTree::signatures() const {
+  std::vector<std::string> out(e.size());
+  std::vector<std::string> text(e.size());
+  // children are added before their parents (add_series / add_parallel take
+  // existing indices), so one forward pass sees every child first
+  for (size_t i = 0; i < e.size(); ++i) {
+    auto const& x = e[i];
+    std::string d;
+    if (x.kind == LEAF) {
+      d = "L" + x.leaf.op.to_json().dump() + "#" + x.leaf.id;
+      for (auto const& v : x.leaf.inputs) d += "i" + pshape_str(v);
+      for (auto const& v : x.leaf.weights) d += "w" + pshape_str(v);
+      for (auto const& v : x.leaf.outputs) d += "o" + pshape_str(v);
+    } else {
+      d = (x.kind == SERIES ? "S(" : "P(") + out[x.left] + "," + out[x.right] + ")";
+      for (auto const& m : x.movement) d += "m" + pshape_str(m.shape) + paths_str(m.src) + ">" + paths_str(m.dst);
+    }
+    char buf[40];
+    snprintf(buf, sizeof(buf), "%016llx%016llx", static_cast<unsigned long long>(fnv(d, 1469598103934665603ull)),
+             static_cast<unsigned long long>(fnv(d, 0x9e3779b97f4a7c15ull)));
+    out[i] = buf;
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
 // the DP
 namespace {
 
@@ -204,9 +251,10 @@ struct Solver {
   MMCache& cache;
   const MMContext& ctx;
   const MMProblemTree& t;
+  std::vector<std::string> sig = t.signatures();
 
   MMResult solve(int idx, const MachineResource& res, const MachineMappingConstraints& c) {
-    std::string key = std::to_string(idx) + "@" + res.str() + "|" + c.key();
+    std::string key = sig[idx] + "@" + res.str() + "|" + c.key();
     auto it = cache.results.find(key);
     if (it != cache.results.end()) {
       ++cache.hits;
@@ -483,7 +531,7 @@ Json MachineMappingResult::to_json() const {
 }
 
 MachineMappingResult get_optimal_machine_mapping(const ParallelComputationGraph& pcg, const CostModel& cm, int world,
-                                                 const MachineMappingOptions& opt) {
+                                                 const MachineMappingOptions& opt, MMCache* shared) {
   MachineMappingResult out;
   auto const& spec = cm.spec();
   const int gpn = std::max(1, spec.num_gpus_per_node);
@@ -520,7 +568,8 @@ MachineMappingResult get_optimal_machine_mapping(const ParallelComputationGraph&
     view_cache.emplace(key, vs);
     return vs;
   };
-  MMCache cache;
+  MMCache local;
+  MMCache& cache = shared ? *shared : local;
   MMResult r = get_optimal_machine_mapping(cache, ctx, prob.tree, res);
   out.cache_entries = cache.results.size();
   if (!r) {

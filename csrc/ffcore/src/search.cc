@@ -36,6 +36,9 @@ Json SearchResult::to_json(const ComputationGraph* cg) const {
     Json br = Json::array();
     for (auto const& n : best_rules) br.push_back(n);
     j["best_rules"] = br;
+    j["mapping_cache_entries"] = mapping_cache_entries;
+    j["mapping_cache_hits"] = mapping_cache_hits;
+    j["mapped_states"] = mapped_states;
   }
   if (cg && !strategy.empty()) j["strategy"] = strategy_to_json(*cg, strategy);
   Json v = Json::object();
@@ -159,15 +162,37 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   SimConfig sim = cfg.sim;
   sim.world = cfg.world;
   Simulator S(cm, sim);
+  // joint search (unity_algorithm.cc:37-90): every state is priced with its
+  // own DP machine mapping, through ONE mapping cache keyed by subtree
+  // content, so a rewrite re-solves only the subtrees it changed
+  MMCache mm_cache;
+  double best_so_far = kInf;
+  int mapped_states = 0;
   auto cost_of = [&](const ParallelComputationGraph& g, std::map<int, Placement>* views) -> double {
     try {
-      if (cfg.use_machine_mapping) {
-        auto m = get_optimal_machine_mapping(g, cm, cfg.world);
-        if (!m.feasible) return kInf;
-        if (views) *views = m.views;
-        return S.simulate(g, m.views).iteration_time;
+      const double whole = S.simulate(g).iteration_time;
+      if (views) views->clear();
+      // the DP mapping (~0.1-0.5 s on a BERT-large PCG) runs for every state
+      // whose whole-world cost is within mapping_alpha of the best so far:
+      // the states the queue can still pop ahead of the best
+      if (cfg.use_machine_mapping && cfg.world > 1 && whole <= best_so_far * cfg.mapping_alpha &&
+          (cfg.max_mapped_states < 0 || mapped_states < cfg.max_mapped_states)) {
+        auto m = get_optimal_machine_mapping(g, cm, cfg.world, MachineMappingOptions{}, &mm_cache);
+        ++mapped_states;
+        if (m.feasible) {
+          // the simulator prices the mapped placements against the
+          // whole-world ones (the DP's per-op sum has no overlap); the better
+          // one is the state's cost and placement
+          const double mapped = S.simulate(g, m.views).iteration_time;
+          if (mapped < whole) {
+            if (views) *views = m.views;
+            best_so_far = std::min(best_so_far, mapped);
+            return mapped;
+          }
+        }
       }
-      return S.simulate(g).iteration_time;
+      best_so_far = std::min(best_so_far, whole);
+      return whole;
     } catch (const FFError&) {
       return kInf;
     }
@@ -218,6 +243,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
       auto matches = find_pattern_matches(rule.pattern, cur, ix, 4096);
       prof[4] += now_s() - tm;
       for (auto const& m : matches) {
+        if (now_s() - t0 > cfg.time_limit) break;
         double ta = now_s();
         auto next = apply_substitution(cur, rule, m);
         prof[0] += now_s() - ta;
@@ -252,6 +278,9 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
     fprintf(stderr, "unity: apply %.2fs checks %.2fs hash %.2fs cost %.2fs match %.2fs total %.2fs\n", prof[0], prof[1],
             prof[2], prof[3], prof[4], now_s() - t0);
   R.iterations = it;
+  R.mapping_cache_entries = static_cast<int64_t>(mm_cache.results.size());
+  R.mapping_cache_hits = static_cast<int64_t>(mm_cache.hits);
+  R.mapped_states = mapped_states;
   R.pcg = states[best];
   R.views = state_views[best];
   R.cost = best_cost;
@@ -283,6 +312,9 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
     auto u = unity_search(m.pcg, cm, uc);
     best.rules = u.rules;
     best.rule_set_rules = u.rule_set_rules;
+    best.mapping_cache_entries = u.mapping_cache_entries;
+    best.mapping_cache_hits = u.mapping_cache_hits;
+    best.mapped_states = u.mapped_states;
     if (u.cost < best.cost * 0.999) {
       u.data_parallel_cost = m.data_parallel_cost;
       u.strategy.clear();
@@ -294,7 +326,7 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
   // final machine mapping (the reference's Unity cost is the mapping DP's;
   // here per-state costs use whole-world placements and the DP, ~0.1 s on a
   // BERT-large PCG, runs once on the winner)
-  if (cfg.final_machine_mapping && !cfg.use_machine_mapping && cfg.world > 1 && best.views.empty()) {
+  if (cfg.final_machine_mapping && cfg.world > 1 && best.views.empty()) {
     try {
       auto mm = get_optimal_machine_mapping(best.pcg, cm, cfg.world);
       if (mm.feasible) {
@@ -351,6 +383,8 @@ SearchConfig search_config_from_json(const Json& j) {
   if (j.contains("seed")) c.seed = static_cast<uint64_t>(j.at("seed").as_int());
   gd("time_limit", c.time_limit);
   gb("use_machine_mapping", c.use_machine_mapping);
+  gd("mapping_alpha", c.mapping_alpha);
+  gi("max_mapped_states", c.max_mapped_states);
   gb("final_machine_mapping", c.final_machine_mapping);
   gi("unity_budget", c.unity_budget);
   gd("mcmc_time_share", c.mcmc_time_share);
