@@ -19,6 +19,7 @@
 #include "ff/machine.h"
 #include "ff/mapping.h"
 #include "ff/parallelize.h"
+#include "ff/pipeline.h"
 #include "ff/simulator.h"
 #include "ff/substitution.h"
 
@@ -50,6 +51,12 @@ struct SearchConfig {
   // graph_optimize: run the machine-mapping DP once on the final PCG and keep
   // its placements when the simulator prices them below the whole-world ones
   bool final_machine_mapping = true;
+  // graph_optimize: pipeline-parallel candidates (ff/pipeline.h) priced at
+  // `micro_batches` micro-batches per optimizer step against the searched
+  // strategy run on the same micro-batches; with 1 micro-batch a pipeline
+  // can only idle (all costs are then per batch, as without it)
+  bool pipeline = true;
+  int micro_batches = 1;
   // rule set added to the built-in parallelization rules (legacy TASO corpus
   // JSON or a substitution-set JSON, load_substitutions); "" = none
   std::string substitution_path;
@@ -76,6 +83,9 @@ struct SearchResult {
   int64_t mapping_cache_entries = 0;     // Unity joint search: shared mapping-cache size / hits
   int64_t mapping_cache_hits = 0;
   int mapped_states = 0;                 // states priced with their own machine mapping
+  int pipeline_stages = 0;               // > 0: the pipeline plan won (views = stage blocks)
+  int micro_batches = 1;                 // costs are per micro-batch of a step of this many
+  Json pipeline = Json::array();         // every pipeline candidate priced
   Json to_json(const ComputationGraph* cg = nullptr) const;
 };
 

@@ -40,6 +40,9 @@ Json SearchResult::to_json(const ComputationGraph* cg) const {
     j["mapping_cache_hits"] = mapping_cache_hits;
     j["mapped_states"] = mapped_states;
   }
+  j["micro_batches"] = static_cast<int64_t>(micro_batches);
+  if (pipeline_stages > 0) j["pipeline_stages"] = static_cast<int64_t>(pipeline_stages);
+  if (!pipeline.as_array().empty()) j["pipeline_candidates"] = pipeline;
   if (cg && !strategy.empty()) j["strategy"] = strategy_to_json(*cg, strategy);
   Json v = Json::object();
   for (auto const& kv : views) v[std::to_string(kv.first)] = Json(std::vector<int64_t>(kv.second.begin(), kv.second.end()));
@@ -343,6 +346,40 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
     } catch (const FFError&) {
     }
   }
+  // pipeline parallelism: stage cuts x micro-batches, at equal work
+  if (cfg.pipeline && cfg.world > 1) {
+    const int M = std::max(1, cfg.micro_batches);
+    SimConfig sim = cfg.sim;
+    sim.world = cfg.world;
+    Simulator S(cm, sim);
+    try {
+      const double t_best = micro_batched_step_time(S.simulate(best.pcg, best.views), M);
+      const double t_dp = micro_batched_step_time(S.simulate(data_parallel_pcg(cg, cfg.world)), M);
+      const PipelinePlan* win = nullptr;
+      auto cands = pipeline_candidates(cg, cm, cfg.world, M, sim);
+      Json list = Json::array();
+      for (auto const& p : cands) {
+        list.push_back(p.to_json());
+        if (p.step_time < t_best * 0.99 && (!win || p.step_time < win->step_time)) win = &p;
+      }
+      best.pipeline = list;
+      best.micro_batches = M;
+      double chosen = t_best;
+      if (win) {
+        best.pcg = win->pcg;
+        best.views = win->views;
+        best.pipeline_stages = win->stages;
+        best.strategy.clear();
+        best.algorithm += "+pipeline";
+        chosen = win->step_time;
+      }
+      if (M > 1 || win) {   // per micro-batch of an M-micro-batch step
+        best.cost = chosen / M;
+        best.data_parallel_cost = t_dp / M;
+      }
+    } catch (const FFError&) {
+    }
+  }
   best.elapsed = now_s() - t0;
   return best;
 }
@@ -384,6 +421,8 @@ SearchConfig search_config_from_json(const Json& j) {
   gd("time_limit", c.time_limit);
   gb("use_machine_mapping", c.use_machine_mapping);
   gd("mapping_alpha", c.mapping_alpha);
+  gb("pipeline", c.pipeline);
+  gi("micro_batches", c.micro_batches);
   gi("max_mapped_states", c.max_mapped_states);
   gb("final_machine_mapping", c.final_machine_mapping);
   gi("unity_budget", c.unity_budget);

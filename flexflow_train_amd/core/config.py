@@ -64,6 +64,10 @@ class FFConfig:
     seed: int = 0
     shard_optimizer: bool = False      # ZeRO-style sharded optimizer state (reduce-scatter + all-gather)
     bucket_mb: int = 64                # gradient all-reduce bucket size
+    # micro-batches per optimizer step: fit() accumulates this many batches
+    # (GPipe order, Executor.train_step_pipelined) before one update, and the
+    # strategy search prices pipeline-parallel stage splits at that count
+    micro_batches: int = 1
     enable_hipgraph: bool = True       # fit(): capture the training iteration as a hipGraph (1 GPU)
     parameter_sync: str = "nccl"       # "nccl" (all-reduce) | "ps" (reference ParamSync::PS)
     cpu_only: bool = False             # run on the host even when a GPU is visible
@@ -169,6 +173,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--compute-dtype", dest="compute_dtype", type=str)
     a("--shard-optimizer", "--zero", dest="shard_optimizer", action="store_const", const=True)
     a("--bucket-mb", dest="bucket_mb", type=int)
+    a("--micro-batches", dest="micro_batches", type=int)
     a("--disable-hipgraph", dest="enable_hipgraph", action="store_const", const=False)
     a("--python-data-loader", dest="native_data_loader", action="store_const", const=False)
     a("--local-execution", dest="local_execution", action="store_const", const=True)

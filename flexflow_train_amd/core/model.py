@@ -767,7 +767,8 @@ class FFModel:
         bs = batch_size or self.ffconfig.batch_size
         if getattr(self, "local_backing", None) is not None:
             return self._fit_local(xs, y, bs, epochs, batch_hooks)
-        native = self._native_loader(xs, y, bs)
+        mb = max(1, int(getattr(self.ffconfig, "micro_batches", 1) or 1))
+        native = self._native_loader(xs, y, bs) if mb == 1 else None
         if native is not None:
             return self._fit_native(native, epochs, batch_hooks)
         loaders = [d if isinstance(d, SingleDataLoader) else SingleDataLoader(self, self._inputs[i], d)
@@ -777,8 +778,9 @@ class FFModel:
             l.batch_size = bs
         num_samples = ylo.num_samples
         iters = num_samples // bs
-        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
+        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable() and mb == 1
         graphed = None
+        pending = []    # micro-batches of the current optimizer step (mb > 1)
         start_epoch, start_it = self._resume_fit(iters)
         ex.zero_metrics()
         if ex.cfg.device.type == "cuda":
@@ -798,7 +800,15 @@ class FFModel:
                     batch_hooks[0](it)
                 feeds = {self._inputs[i].name: torch.as_tensor(l.next_batch()) for i, l in enumerate(loaders)}
                 labels = torch.as_tensor(ylo.next_batch())
-                if use_graph and not first:
+                if mb > 1:
+                    # FFConfig.micro_batches: mb batches per optimizer step, in
+                    # GPipe order over the searched pipeline stages
+                    pending.append((feeds, labels))
+                    if len(pending) == mb or it == iters - 1:
+                        ex.train_step_pipelined([f for f, _ in pending], [l for _, l in pending],
+                                                lr=self._optimizer.cfg.lr)
+                        pending = []
+                elif use_graph and not first:
                     # the first iteration ran eagerly (autotune / allocator
                     # warm-up); capture the next one and replay it from then on
                     if graphed is None:
@@ -807,7 +817,8 @@ class FFModel:
                 else:
                     ex.train_step(feeds, labels, lr=self._optimizer.cfg.lr)
                 first = False
-                self._after_fit_step(epoch, it, iters)
+                if not pending:   # checkpoints only between optimizer steps
+                    self._after_fit_step(epoch, it, iters)
                 if batch_hooks:
                     batch_hooks[1](it)
                 # perf_metrics() all-reduces across ranks: every rank calls it, rank 0 prints
@@ -948,8 +959,9 @@ class FFModel:
         ex = self.executor
         iters = loader.iters_per_epoch
         num_samples = iters * loader.batch
-        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
+        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable() and mb == 1
         graphed = None
+        pending = []    # micro-batches of the current optimizer step (mb > 1)
         start_epoch, start_it = self._resume_fit(iters)
         if start_epoch or start_it:
             loader.start(start_epoch * iters + start_it)

@@ -57,6 +57,10 @@ def _search_local(cg, ffconfig, world: int):
         # (unity_algorithm.cc:37-90), over the built-in rules + the rule set
         "unity_budget": budget,
         "substitution_path": substitution_path(ffconfig),
+        # pipeline-parallel stage splits priced against the other strategies
+        # at equal work: micro_batches batches per optimizer step
+        "micro_batches": max(1, int(getattr(ffconfig, "micro_batches", 1) or 1)),
+        "pipeline": True,
     }
     algo = ffconfig.search_algorithm
     if algo == "mcmc":
