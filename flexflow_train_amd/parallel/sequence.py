@@ -21,8 +21,11 @@ runtime lowers it here:
   log-sum-exp (the flash kernel emits log2-domain LSE).  Backward circulates
   (K, V, dK, dV) the same way using the *global* LSE and output, which makes
   every block's contribution exact; one extra hop returns dK/dV home.
-  Causal masking skips blocks above the diagonal.  Works for any head
-  count; transfer of the next block overlaps the current block's compute.
+  Causal masking skips blocks above the diagonal; with a causal mask the
+  zig-zag layout (rank i holds chunks i and 2s-1-i of 2s) balances the work
+  over the ranks.  Works for any head count; the next block's transfer
+  (forward and backward) and the dK/dV accumulator hop overlap the current
+  block's compute, and every transfer is capturable in a segmented hipGraph.
 """
 from __future__ import annotations
 
@@ -31,8 +34,6 @@ from typing import List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
-
-from ..runtime.graphs import check_capturable
 
 from .. import kernels as K
 
@@ -153,18 +154,37 @@ def ulysses_bwd(do, saved, causal, scale, grp: SeqGroup):
 
 
 # --------------------------------------------------------------------- ring
-def _exchange(tensors: List[torch.Tensor], grp: SeqGroup) -> List[torch.Tensor]:
-    """Send ``tensors`` to the next rank, receive the previous rank's."""
-    check_capturable("ring attention exchange")
-    recv = [torch.empty_like(t) for t in tensors]
-    ops = []
-    for t in tensors:
-        ops.append(dist.P2POp(dist.isend, t.contiguous(), grp.next_rank(), group=grp.pg))
-    for r in recv:
-        ops.append(dist.P2POp(dist.irecv, r, grp.prev_rank(), group=grp.pg))
-    reqs = dist.batch_isend_irecv(ops)
-    grp.dist_ctx.stats["ring_p2p"] = grp.dist_ctx.stats.get("ring_p2p", 0) + len(tensors)
-    return reqs, recv
+class _Reqs:
+    """The requests of one batched isend/irecv as a single waitable work."""
+
+    def __init__(self, reqs):
+        self.reqs = list(reqs or [])
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        return True
+
+
+def _exchange(tensors: List[torch.Tensor], grp: SeqGroup):
+    """Send ``tensors`` to the next rank and receive the previous rank's,
+    asynchronously: returns (work, received buffers).  The receive buffers
+    are allocated before the transfer is issued and the transfer goes through
+    DistContext._issue, so inside a segmented hipGraph capture it becomes a
+    segment boundary re-issued at replay (runtime/graphs.py) and the compute
+    between issue and ``work.wait()`` runs while the blocks move."""
+    send = [t.contiguous() for t in tensors]
+    recv = [torch.empty_like(t) for t in send]
+    nxt, prv, pg = grp.next_rank(), grp.prev_rank(), grp.pg
+
+    def fn():
+        ops = [dist.P2POp(dist.isend, t, nxt, group=pg) for t in send]
+        ops += [dist.P2POp(dist.irecv, r, prv, group=pg) for r in recv]
+        return _Reqs(dist.batch_isend_irecv(ops))
+
+    work = grp.dist_ctx._issue(fn, True)
+    grp.dist_ctx.stats["ring_p2p"] = grp.dist_ctx.stats.get("ring_p2p", 0) + len(send)
+    return work, recv
 
 
 def ring_fwd(q, k, v, causal, scale, grp: SeqGroup):
@@ -181,46 +201,191 @@ def ring_fwd(q, k, v, causal, scale, grp: SeqGroup):
             o_j, lse_j = block_attention(q, cur[0], cur[1], causal and j == i, scale)
             o, lse = merge(o, lse, o_j, lse_j)
         if pending is not None:
-            for r in pending[0]:
-                r.wait()
+            pending[0].wait()
             cur = pending[1]
     o = o.to(q.dtype)
     return o, (q, k, v, o, lse.contiguous())
 
 
-def ring_bwd(do, saved, causal, scale, grp: SeqGroup):
-    q, k, v, o, lse = saved
+def _ring_bwd_loop(q, k, v, grp: SeqGroup, block_grads):
+    """The backward ring shared by the contiguous and zig-zag layouts.
+
+    K/V blocks circulate forward with the next hop issued BEFORE the block's
+    compute; the dK/dV accumulator of the block a rank holds travels one step
+    behind: the accumulator received from the previous rank is waited for
+    only after this rank's own contribution to that block is computed, so
+    both transfers overlap compute.  ``block_grads(j, k_j, v_j)`` returns
+    (dq contribution, dk_j, dv_j) for the block owned by rank j (None where
+    the causal mask skips it).  After s steps the last accumulator hop lands
+    on the block's owner."""
     s, i = grp.size, grp.index
-    do = do.contiguous()
     dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
-    cur = [k, v, torch.zeros(k.shape, dtype=torch.float32, device=k.device),
-           torch.zeros(v.shape, dtype=torch.float32, device=v.device)]
+    kv = [k, v]
+    acc_pending = None
     for t in range(s):
         j = (i - t) % s
-        if not (causal and j > i):
-            dq_j, dk_j, dv_j = block_attention_bwd(q, cur[0], cur[1], o, lse, do, causal and j == i, scale)
-            dq += dq_j.float()
-            cur[2] = cur[2] + dk_j.float()
-            cur[3] = cur[3] + dv_j.float()
-        if t < s - 1:
-            reqs, cur = _exchange(cur, grp)
-            for r in reqs:
-                r.wait()
-    # the block we hold belongs to rank i+1: one more hop returns dK/dV home
-    if s > 1:
-        reqs, back = _exchange(cur[2:], grp)
-        for r in reqs:
-            r.wait()
-        dk, dv = back
-    else:
-        dk, dv = cur[2], cur[3]
+        kv_pending = _exchange(kv, grp) if t < s - 1 else None
+        g = block_grads(j, kv[0], kv[1])
+        if g is not None:
+            dq_j, dk_j, dv_j = g
+            dq += dq_j
+        else:
+            dk_j = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
+            dv_j = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
+        if acc_pending is not None:
+            acc_pending[0].wait()
+            dk_j = dk_j + acc_pending[1][0]
+            dv_j = dv_j + acc_pending[1][1]
+        acc_pending = _exchange([dk_j, dv_j], grp) if s > 1 else (None, [dk_j, dv_j])
+        if kv_pending is not None:
+            kv_pending[0].wait()
+            kv = kv_pending[1]
+    if acc_pending[0] is not None:
+        acc_pending[0].wait()
+    dk, dv = acc_pending[1]
     return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
 
 
+def ring_bwd(do, saved, causal, scale, grp: SeqGroup):
+    q, k, v, o, lse = saved
+    i = grp.index
+    do = do.contiguous()
+
+    def block_grads(j, k_j, v_j):
+        if causal and j > i:
+            return None
+        dq_j, dk_j, dv_j = block_attention_bwd(q, k_j, v_j, o, lse, do, causal and j == i, scale)
+        return dq_j.float(), dk_j.float(), dv_j.float()
+
+    return _ring_bwd_loop(q, k, v, grp, block_grads)
+
+
+# ---------------------------------------------------------- zig-zag ring
+# Causal ring attention over contiguous sequence shards is unbalanced: rank i
+# attends to i + 1 blocks, so the last rank does s blocks of work while the
+# first does one.  The zig-zag layout cuts the sequence into 2s chunks and
+# gives rank i chunks i and 2s-1-i (one early, one late): every ring step then
+# costs every rank half a block (the diagonal step a causal block), whatever
+# i and j.  The rest of the model keeps contiguous shards; q/k/v are moved
+# into the zig-zag layout by one all-to-all (stacked) and the output back by
+# another (two each way in the backward).
+
+def _contig(c: int, s: int):
+    return c // 2, c % 2                      # chunk -> (owner, slot)
+
+
+def _zigzag(c: int, s: int):
+    return (c, 0) if c < s else (2 * s - 1 - c, 1)
+
+
+def _relayout(x: torch.Tensor, grp: SeqGroup, before, after) -> torch.Tensor:
+    """Move the two sequence chunks of ``x`` [B, S_local, ...] (dim 1 split
+    in halves = chunk slots) from layout ``before`` to layout ``after``
+    (chunk c -> (owner, slot)) with one variable-split all-to-all."""
+    s, i = grp.size, grp.index
+    B, Sl = x.shape[0], x.shape[1]
+    if Sl % 2:
+        raise ValueError(f"zig-zag ring attention needs an even local sequence length, got {Sl}")
+    parts = x.reshape(B, 2, Sl // 2, *x.shape[2:])
+    chunks = range(2 * s)
+    out_c = sorted((c for c in chunks if before(c, s)[0] == i), key=lambda c: after(c, s))
+    in_c = sorted((c for c in chunks if after(c, s)[0] == i), key=lambda c: (before(c, s)[0], after(c, s)[1]))
+    send = torch.stack([parts[:, before(c, s)[1]] for c in out_c], 0).reshape(len(out_c), -1).contiguous()
+    recv = torch.empty_like(send)
+    in_splits = [sum(1 for c in out_c if after(c, s)[0] == r) for r in range(s)]
+    out_splits = [sum(1 for c in in_c if before(c, s)[0] == r) for r in range(s)]
+    pg = grp.pg
+    grp.dist_ctx._issue(lambda: dist.all_to_all_single(recv, send, out_splits, in_splits, group=pg), False)
+    grp.dist_ctx.stats["sp_all_to_all"] = grp.dist_ctx.stats.get("sp_all_to_all", 0) + 1
+    out = torch.empty_like(parts)
+    shp = parts.shape[:1] + parts.shape[2:]
+    for n, c in enumerate(in_c):
+        out[:, after(c, s)[1]] = recv[n].view(shp)
+    return out.reshape(x.shape)
+
+
+def _to_zigzag(ts: Sequence[torch.Tensor], grp: SeqGroup) -> List[torch.Tensor]:
+    st = torch.stack([t.contiguous() for t in ts], 2)          # [B, Sl, n, ...]: one all-to-all for all
+    z = _relayout(st, grp, _contig, _zigzag)
+    return [z[:, :, n].contiguous() for n in range(len(ts))]
+
+
+def _from_zigzag(ts: Sequence[torch.Tensor], grp: SeqGroup) -> List[torch.Tensor]:
+    st = torch.stack([t.contiguous() for t in ts], 2)
+    c = _relayout(st, grp, _zigzag, _contig)
+    return [c[:, :, n].contiguous() for n in range(len(ts))]
+
+
+def ring_zigzag_fwd(q, k, v, causal, scale, grp: SeqGroup):
+    """Causal ring attention over zig-zag chunks (see above)."""
+    s, i = grp.size, grp.index
+    grp.dist_ctx.stats["ring_zigzag"] = grp.dist_ctx.stats.get("ring_zigzag", 0) + 1
+    qz, kz, vz = _to_zigzag([q, k, v], grp)
+    h = qz.shape[1] // 2
+    o = lse = None
+    cur = [kz, vz]
+    for t in range(s):
+        j = (i - t) % s
+        pending = _exchange(cur, grp) if t < s - 1 else None
+        if j == i:                      # own chunks: causal over [chunk i, chunk 2s-1-i]
+            o, lse = merge(None, None, *block_attention(qz, cur[0], cur[1], True, scale))
+        elif j < i:                     # both query chunks see the early key chunk j only
+            o_j, lse_j = block_attention(qz, cur[0][:, :h], cur[1][:, :h], False, scale)
+            o, lse = merge(o, lse, o_j, lse_j)
+        else:                           # the late query chunk sees both of rank j's chunks
+            o_j, lse_j = block_attention(qz[:, h:], cur[0], cur[1], False, scale)
+            o_hi, lse_hi = merge(o[:, h:], lse[:, :, h:], o_j, lse_j)
+            o = torch.cat([o[:, :h], o_hi], 1)
+            lse = torch.cat([lse[:, :, :h], lse_hi], 2)
+        if pending is not None:
+            pending[0].wait()
+            cur = pending[1]
+    oz = o.to(q.dtype)
+    (out,) = _from_zigzag([oz], grp)
+    return out, (qz, kz, vz, oz, lse.contiguous())
+
+
+def ring_zigzag_bwd(do, saved, causal, scale, grp: SeqGroup):
+    qz, kz, vz, oz, lse = saved
+    i = grp.index
+    (doz,) = _to_zigzag([do], grp)
+    h = qz.shape[1] // 2
+    q_hi, o_hi, do_hi = qz[:, h:].contiguous(), oz[:, h:].contiguous(), doz[:, h:].contiguous()
+    lse_hi = lse[:, :, h:].contiguous()
+
+    def block_grads(j, k_j, v_j):
+        if j == i:
+            dq, dk, dv = block_attention_bwd(qz, k_j, v_j, oz, lse, doz, True, scale)
+            return dq.float(), dk.float(), dv.float()
+        dk = torch.zeros(k_j.shape, dtype=torch.float32, device=k_j.device)
+        dv = torch.zeros(v_j.shape, dtype=torch.float32, device=v_j.device)
+        if j < i:
+            dq, dk_lo, dv_lo = block_attention_bwd(qz, k_j[:, :h].contiguous(), v_j[:, :h].contiguous(), oz, lse,
+                                                   doz, False, scale)
+            dk[:, :h] = dk_lo.float()
+            dv[:, :h] = dv_lo.float()
+            return dq.float(), dk, dv
+        dq_hi, dk_f, dv_f = block_attention_bwd(q_hi, k_j, v_j, o_hi, lse_hi, do_hi, False, scale)
+        dq = torch.zeros(qz.shape, dtype=torch.float32, device=qz.device)
+        dq[:, h:] = dq_hi.float()
+        return dq, dk_f.float(), dv_f.float()
+
+    dqz, dkz, dvz = _ring_bwd_loop(qz, kz, vz, grp, block_grads)
+    return tuple(_from_zigzag([dqz, dkz, dvz], grp))
+
+
 def choose_mode(attrs: dict, heads_local: int, grp: SeqGroup) -> str:
+    """auto: Ulysses when the local heads split over the group, else ring
+    (zig-zag when causal); "ring" with a causal mask also runs zig-zag unless
+    "ring_contiguous" is asked for."""
     mode = str(attrs.get("seq_parallel_mode", "auto"))
+    causal = bool(attrs.get("causal", False))
     if mode == "auto":
         mode = "ulysses" if heads_local % grp.size == 0 else "ring"
+    if mode == "ring" and causal:
+        mode = "ring_zigzag"
+    if mode == "ring_contiguous":
+        mode = "ring"
     if mode == "ulysses" and heads_local % grp.size:
         raise ValueError(f"ulysses sequence parallelism needs heads ({heads_local}) divisible by {grp.size}")
     return mode
@@ -229,7 +394,10 @@ def choose_mode(attrs: dict, heads_local: int, grp: SeqGroup) -> str:
 def sp_attention_fwd(q, k, v, causal, scale, grp: SeqGroup, mode: str):
     if mode == "ulysses":
         o, saved = ulysses_fwd(q, k, v, causal, scale, grp)
+    elif mode == "ring_zigzag" and causal:
+        o, saved = ring_zigzag_fwd(q, k, v, causal, scale, grp)
     else:
+        mode = "ring"
         o, saved = ring_fwd(q, k, v, causal, scale, grp)
     return o, (mode, saved)
 
@@ -238,4 +406,6 @@ def sp_attention_bwd(do, saved, causal, scale, grp: SeqGroup):
     mode, inner = saved
     if mode == "ulysses":
         return ulysses_bwd(do, inner, causal, scale, grp)
+    if mode == "ring_zigzag":
+        return ring_zigzag_bwd(do, inner, causal, scale, grp)
     return ring_bwd(do, inner, causal, scale, grp)

@@ -1532,34 +1532,62 @@ class Executor:
             f["opt"].step_range(b["lo"], b["hi"], lr=self._overlap_lr[1])
         b["updated"] = True
 
+    def pipeline_stages(self) -> int:
+        """Distinct device blocks the strategy places operators on (1 when
+        every operator spans the whole world)."""
+        blocks = {tuple(v) for v in self.views.values()} if self.views else set()
+        return max(1, len(blocks))
+
     def train_step_pipelined(self, feeds_list: Sequence[Dict[str, torch.Tensor]], labels_list: Sequence[torch.Tensor],
-                             lr: Optional[float] = None):
+                             lr: Optional[float] = None, schedule: str = "1f1b"):
         """One optimizer step over ``len(feeds_list)`` micro-batches (each of
-        the compiled batch shape), GPipe order: every forward, then every
-        backward in reverse, gradients accumulated, one synchronisation + update.
+        the compiled batch shape): gradients accumulated over the
+        micro-batches, one synchronisation + update.
 
         With a strategy that places consecutive layers on disjoint device
         blocks (machine views = pipeline stages), every rank walks the same
         step list, so stage s runs micro-batch i+1's forward while stage s+1
-        runs micro-batch i's (the stage-boundary transfers are the only
-        rendezvous) — pipeline parallelism with the fill / drain bubble of
-        GPipe; with one stage it is plain gradient accumulation.  The loss
-        gradient of each micro-batch is scaled by 1/m, so the update equals
-        the one of a single batch m times larger."""
+        runs micro-batch i's (the stage-boundary transfers, all-to-alls on
+        the two stages' ranks only, are the only rendezvous).  ``schedule``:
+
+          * ``"gpipe"`` -- every forward, then every backward in reverse: m
+            micro-batches of activations live at the peak;
+          * ``"1f1b"`` -- S (= pipeline stages) warm-up forwards, then one
+            backward per forward (B0 F_S B1 F_S+1 ...), then the drain: at
+            most S micro-batches live, the same bubble.
+
+        With one stage it is plain gradient accumulation.  The loss gradient
+        of each micro-batch is scaled by 1/m, so the update equals the one of
+        a single batch m times larger."""
         m = len(feeds_list)
         if m == 0 or m != len(labels_list):
             raise ValueError("train_step_pipelined: need one label tensor per micro-batch")
-        stash = []
-        for f, lab in zip(feeds_list, labels_list):
-            self.forward(f, training=True)
-            g = self.compute_loss(lab)
-            if g is not None and m > 1:
-                g = g / m
-            stash.append((self._saved, self._env, g))
-        for i in range(m - 1, -1, -1):
-            self._saved, self._env, g = stash[i]
-            stash[i] = None
-            self.backward(g, zero_grads=(i == m - 1), accumulate=(i != m - 1), sync=(i == 0))
+        if schedule not in ("gpipe", "1f1b"):
+            raise ValueError(f"train_step_pipelined: unknown schedule {schedule!r}")
+        if schedule == "gpipe":
+            order = [("F", i) for i in range(m)] + [("B", i) for i in range(m - 1, -1, -1)]
+        else:
+            w = min(m, self.pipeline_stages())
+            order = [("F", i) for i in range(w)]
+            for i in range(m):
+                order.append(("B", i))
+                if i + w < m:
+                    order.append(("F", i + w))
+        stash: Dict[int, tuple] = {}
+        n_back = 0
+        self.peak_live_micro_batches = 0
+        for kind, i in order:
+            if kind == "F":
+                self.forward(feeds_list[i], training=True)
+                g = self.compute_loss(labels_list[i])
+                if g is not None and m > 1:
+                    g = g / m
+                stash[i] = (self._saved, self._env, g)
+                self.peak_live_micro_batches = max(self.peak_live_micro_batches, len(stash))
+            else:
+                self._saved, self._env, g = stash.pop(i)
+                self.backward(g, zero_grads=(n_back == 0), accumulate=(n_back > 0), sync=(n_back == m - 1))
+                n_back += 1
         self.update(lr)
 
     def make_graphed_train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, warmup: int = 2):

@@ -88,6 +88,10 @@ def attention_ring_causal(m):
     return _seq_attention(m, "ring", True)
 
 
+def attention_ring_contiguous_causal(m):
+    return _seq_attention(m, "ring_contiguous", True)
+
+
 def attention_ulysses_causal(m):
     return _seq_attention(m, "ulysses", True)
 

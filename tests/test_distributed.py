@@ -59,10 +59,11 @@ def test_bert_tiny_data_parallel_adam():
 
 
 @pytest.mark.parametrize("fn", ["attention_ulysses", "attention_ring", "attention_ring_causal",
-                                "attention_ulysses_causal"])
+                                "attention_ring_contiguous_causal", "attention_ulysses_causal"])
 def test_attention_sequence_parallel(tmp_path, fn):
-    """Sequence-sharded attention (Ulysses all-to-all / ring attention)
-    matches the single-process run."""
+    """Sequence-sharded attention (Ulysses all-to-all / ring attention;
+    causal ring = zig-zag chunks unless ring_contiguous) matches the
+    single-process run."""
     model_fn = getattr(M, fn)
     ref = run_single(model_fn)
     path = str(tmp_path / "seq.json")
@@ -71,9 +72,10 @@ def test_attention_sequence_parallel(tmp_path, fn):
     assert_params_close(out["params"], ref["params"])
     kind = "sp_all_to_all" if "ulysses" in fn else "ring_p2p"
     assert out["stats"].get(kind, 0) > 0, out["stats"]
+    assert (out["stats"].get("ring_zigzag", 0) > 0) == (fn == "attention_ring_causal"), out["stats"]
 
 
-@pytest.mark.parametrize("fn", ["attention_ring_causal", "attention_ulysses"])
+@pytest.mark.parametrize("fn", ["attention_ring_causal", "attention_ring_contiguous_causal", "attention_ulysses"])
 def test_attention_sequence_parallel_4way(tmp_path, fn):
     model_fn = getattr(M, fn)
     ref = run_single(model_fn)

@@ -7,6 +7,7 @@ import json
 import os
 import tempfile
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -54,10 +55,10 @@ def _build(strategy_file=None, seed=0):
     return ex
 
 
-def _train(ex, steps=2):
+def _train(ex, steps=2, schedule="1f1b"):
     feeds, labels = _micro()
     for _ in range(steps):
-        ex.train_step_pipelined(feeds, labels)
+        ex.train_step_pipelined(feeds, labels, schedule=schedule)
     return {n: ex.get_parameter(n).detach().cpu().clone() for n in sorted(ex.parameter_names())}
 
 
@@ -80,35 +81,43 @@ def _stage_strategy(path):
     export_strategy(path, pcg, views, {"world": 2, "source": "test"})
 
 
-def _worker(rank, world, port, strategy, out):
+def _worker(rank, world, port, strategy, out, schedule="1f1b"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(1)
     ex = _build(strategy)
-    params = _train(ex)
+    params = _train(ex, schedule=schedule)
     if rank == 0:
-        torch.save({"params": params, "stats": dict(ex.dist.stats)}, out)
+        torch.save({"params": params, "stats": dict(ex.dist.stats), "stages": ex.pipeline_stages(),
+                    "peak": ex.peak_live_micro_batches}, out)
     import torch.distributed as dist
 
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gradient_accumulation_matches_full_batch():
+@pytest.mark.parametrize("schedule", ["gpipe", "1f1b"])
+def test_gradient_accumulation_matches_full_batch(schedule):
     ref = run_single(M.mlp)
-    got = _train(_build())
+    ex = _build()
+    got = _train(ex, schedule=schedule)
     assert_params_close(got, ref["params"], rtol=1e-4, atol=1e-5)
+    # one stage: 1F1B keeps one micro-batch live, GPipe all of them
+    assert ex.peak_live_micro_batches == (1 if schedule == "1f1b" else 2)
 
 
-def test_two_stage_pipeline_matches_full_batch():
+@pytest.mark.parametrize("schedule", ["gpipe", "1f1b"])
+def test_two_stage_pipeline_matches_full_batch(schedule):
     ref = run_single(M.mlp)
     with tempfile.TemporaryDirectory() as d:
         strat = os.path.join(d, "pp.json")
         _stage_strategy(strat)
         out = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(2, free_port(), strat, out), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(2, free_port(), strat, out, schedule), nprocs=2, join=True,
+                           start_method="spawn")
         res = torch.load(out, weights_only=True)
     assert_params_close(res["params"], ref["params"], rtol=1e-4, atol=1e-5)
+    assert res["stages"] == 2 and res["peak"] == 2
     # the stage boundary moved activations / gradients between the ranks
     assert res["stats"].get("all_to_all", 0) + res["stats"].get("p2p", 0) > 0, res["stats"]
 
