@@ -959,9 +959,8 @@ class FFModel:
         ex = self.executor
         iters = loader.iters_per_epoch
         num_samples = iters * loader.batch
-        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable() and mb == 1
+        use_graph = bool(self.ffconfig.enable_hipgraph) and self._graph_capable()
         graphed = None
-        pending = []    # micro-batches of the current optimizer step (mb > 1)
         start_epoch, start_it = self._resume_fit(iters)
         if start_epoch or start_it:
             loader.start(start_epoch * iters + start_it)
