@@ -24,29 +24,11 @@
 #include <vector>
 
 #include "ff/computation_graph.h"
+#include "ff/training_backing.h"
 
 namespace ff {
 
-struct HostTensor {
-  std::vector<int64_t> dims;
-  std::vector<float> v;
-  int64_t numel() const { return static_cast<int64_t>(v.size()); }
-  void resize(const std::vector<int64_t>& d);
-};
-
-struct LocalOptimizer {
-  std::string kind = "sgd";  // sgd | adam
-  double lr = 0.01, momentum = 0.0, weight_decay = 0.0;
-  bool nesterov = false;
-  double beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8;
-};
-
-struct LocalMetrics {
-  double loss_sum = 0.0;
-  int64_t correct = 0, samples = 0;
-};
-
-class LocalTrainingBacking {
+class LocalTrainingBacking : public TrainingBacking {
  public:
   // loss: "sparse_categorical_crossentropy" | "categorical_crossentropy" |
   // "mean_squared_error" | "identity"
@@ -60,24 +42,33 @@ class LocalTrainingBacking {
   void set_weight(const std::string& name, const std::vector<float>& data);
   std::vector<float> get_weight(const std::string& name) const;
   std::vector<float> get_output() const;  // the graph's (last layer's) output
-  ValueRef output() const { return output_; }
+  ValueRef output() const override { return output_; }
   // the slot of any graph tensor (or its gradient); nullptr if none is kept
-  HostTensor* slot(const ValueRef& v, bool grad = false);
-  LocalOptimizer& optimizer() { return opt_; }
+  HostTensor* slot(const ValueRef& v, bool grad = false) override;
+  LocalOptimizer& optimizer() override { return opt_; }
   // runs one operator layer's forward on the current slot contents
-  void forward_layer(int node);
+  void forward_layer(int node) override;
 
-  void forward();
+  void forward() override;
   // loss + metrics on the output, then the full backward pass
-  void backward(const std::vector<float>& labels);
-  void update();
+  void backward(const std::vector<float>& labels) override;
+  void update() override;
   void train_step(const std::vector<float>& labels) {
     forward();
     backward(labels);
     update();
   }
-  const LocalMetrics& metrics() const { return metrics_; }
-  void reset_metrics() { metrics_ = LocalMetrics{}; }
+  const LocalMetrics& metrics() const override { return metrics_; }
+  void reset_metrics() override { metrics_ = LocalMetrics{}; }
+  std::string device() const override { return "cpu"; }
+  // operator layers in topo order / whether a tensor carries a gradient
+  const std::vector<int>& order() const { return order_; }
+  bool needs_grad(const ValueRef& v) const {
+    auto it = needs_grad_.find(v);
+    return it != needs_grad_.end() && it->second;
+  }
+  const std::string& loss() const { return loss_; }
+  bool fused_softmax_ce() const { return fused_softmax_ce_; }
   // per layer name: accumulated forward / backward milliseconds
   std::map<std::string, std::pair<double, double>> layer_times_ms() const;
 

@@ -353,8 +353,17 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
     sim.world = cfg.world;
     Simulator S(cm, sim);
     try {
-      const double t_best = micro_batched_step_time(S.simulate(best.pcg, best.views), M);
+      double t_best = micro_batched_step_time(S.simulate(best.pcg, best.views), M);
       const double t_dp = micro_batched_step_time(S.simulate(data_parallel_pcg(cg, cfg.world)), M);
+      if (M > 1 && t_dp < t_best * 0.999) {
+        // the winner of the one-batch search loses to DP once its forward /
+        // backward repeats M times per synchronisation: keep DP
+        best.pcg = data_parallel_pcg(cg, cfg.world);
+        best.views.clear();
+        best.strategy.clear();
+        best.algorithm += "+dp_at_micro_batches";
+        t_best = t_dp;
+      }
       const PipelinePlan* win = nullptr;
       auto cands = pipeline_candidates(cg, cm, cfg.world, M, sim);
       Json list = Json::array();

@@ -1,0 +1,659 @@
+// GPU training backing of the legacy C API (ff/training_backing.h).
+//
+// Parity: the reference's C API (python/flexflow_c.cc:183-194, model
+// compile / forward / backward / update) drives its GPU runtime; here the
+// same entry points (csrc/ffi/flexflow_runtime_c.cc) drive this backing when a
+// GPU is visible.  Design, single process / single GPU:
+//  * every graph tensor and gradient lives in one device arena (256-B
+//    aligned pieces); weights are initialised by the CPU backing's
+//    initialisers (same values as a CPU run with the same seed) and uploaded;
+//  * operators: LINEAR on the exact-fp32 MFMA GEMM (igemm32.hip: bias and the
+//    activation in its epilogue, the pre-activation kept for backward), the
+//    last SOFTMAX fused with sparse cross-entropy (softmax.hip), MSE
+//    (tensorops.hip), element-wise activations / binaries / scalar ops /
+//    reshapes / softmax by the small kernels below; a graph with any other
+//    operator stays on the CPU backing (make_device_backing returns null);
+//  * the host slots are mirrors: slot() copies a tensor out when the device
+//    copy is newer and marks it written, and the next device step copies
+//    written mirrors back -- the inline-mapping protocol of the reference's
+//    regions, without Legion;
+//  * SGD (momentum, Nesterov, L2) and Adam (L2 folded into the gradient, as
+//    the CPU backing and the reference's adam_update) on the device.
+// Everything runs on one HIP stream; metrics accumulate on the device and are
+// read back when asked for.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ff/local_exec.h"
+#include "ff/training_backing.h"
+#include "kernels.h"
+
+namespace ff {
+namespace {
+
+#define FFD_CHECK(x)                                                                                  \
+  do {                                                                                                \
+    hipError_t e_ = (x);                                                                              \
+    if (e_ != hipSuccess) throw FFError(std::string("device backing: ") + #x + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ----------------------------------------------------------------- kernels
+constexpr int kDtF32 = 0;   // the kernel library's fp32 dtype code (csrc/kernels/common.h DType)
+
+enum DAct : int { A_NONE = 0, A_RELU = 1, A_SIGMOID = 2, A_TANH = 3, A_GELU = 4, A_ELU = 5 };
+
+__device__ __forceinline__ float d_act(int a, float x) {
+  switch (a) {
+    case A_RELU: return x > 0.f ? x : 0.f;
+    case A_SIGMOID: return 1.f / (1.f + expf(-x));
+    case A_TANH: return tanhf(x);
+    case A_GELU: {
+      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+      return 0.5f * x * (1.f + tanhf(u));
+    }
+    case A_ELU: return x > 0.f ? x : expf(x) - 1.f;
+    default: return x;
+  }
+}
+__device__ __forceinline__ float d_act_grad(int a, float x) {
+  switch (a) {
+    case A_RELU: return x > 0.f ? 1.f : 0.f;
+    case A_SIGMOID: {
+      const float s = 1.f / (1.f + expf(-x));
+      return s * (1.f - s);
+    }
+    case A_TANH: {
+      const float t = tanhf(x);
+      return 1.f - t * t;
+    }
+    case A_GELU: {
+      const float k = 0.7978845608028654f;
+      const float u = k * (x + 0.044715f * x * x * x);
+      const float t = tanhf(u);
+      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+    }
+    case A_ELU: return x > 0.f ? 1.f : expf(x);
+    default: return 1.f;
+  }
+}
+
+#define GRID_LOOP(i, n) for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < (n); i += 256ll * gridDim.x)
+
+__global__ __launch_bounds__(256) void k_act(const float* x, float* y, int64_t n, int a) {
+  GRID_LOOP(i, n) y[i] = d_act(a, x[i]);
+}
+// dx += dy * act'(x)   (x = the activation's input)
+__global__ __launch_bounds__(256) void k_act_bwd(const float* dy, const float* x, float* dx, int64_t n, int a) {
+  GRID_LOOP(i, n) dx[i] += dy[i] * d_act_grad(a, x[i]);
+}
+// g = dy * act'(pre)
+__global__ __launch_bounds__(256) void k_act_grad(const float* dy, const float* pre, float* g, int64_t n, int a) {
+  GRID_LOOP(i, n) g[i] = dy[i] * d_act_grad(a, pre[i]);
+}
+__global__ __launch_bounds__(256) void k_axpy(const float* x, float* y, int64_t n, float a) {
+  GRID_LOOP(i, n) y[i] += a * x[i];
+}
+// db[j] += sum_r g[r, j]: one thread per column, rows strided
+__global__ __launch_bounds__(256) void k_colsum(const float* g, float* db, int64_t rows, int64_t cols) {
+  const int64_t j = blockIdx.x * 256ll + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.f;
+  for (int64_t r = 0; r < rows; ++r) s += g[r * cols + j];
+  db[j] += s;
+}
+// op: 0 add 1 sub 2 mul 3 div 4 max 5 min
+__global__ __launch_bounds__(256) void k_binary(const float* a, const float* b, float* y, int64_t n, int op) {
+  GRID_LOOP(i, n) {
+    const float u = a[i], v = b[i];
+    float r;
+    switch (op) {
+      case 0: r = u + v; break;
+      case 1: r = u - v; break;
+      case 2: r = u * v; break;
+      case 3: r = u / v; break;
+      case 4: r = fmaxf(u, v); break;
+      default: r = fminf(u, v); break;
+    }
+    y[i] = r;
+  }
+}
+__global__ __launch_bounds__(256) void k_binary_bwd(const float* g, const float* a, const float* b, float* da,
+                                                    float* db, int64_t n, int op) {
+  GRID_LOOP(i, n) {
+    const float u = a[i], v = b[i], d = g[i];
+    float ga = 0.f, gb = 0.f;
+    switch (op) {
+      case 0: ga = d; gb = d; break;
+      case 1: ga = d; gb = -d; break;
+      case 2: ga = d * v; gb = d * u; break;
+      case 3: ga = d / v; gb = -d * u / (v * v); break;
+      case 4: (u >= v ? ga : gb) = d; break;
+      default: (u <= v ? ga : gb) = d; break;
+    }
+    if (da) da[i] += ga;
+    if (db) db[i] += gb;
+  }
+}
+// op: 0 *s 1 +s 2 -s 3 /s
+__global__ __launch_bounds__(256) void k_scalar(const float* x, float* y, int64_t n, int op, float s) {
+  GRID_LOOP(i, n) {
+    const float u = x[i];
+    y[i] = op == 0 ? u * s : op == 1 ? u + s : op == 2 ? u - s : u / s;
+  }
+}
+// softmax over the last dim, one block per row
+__global__ __launch_bounds__(256) void k_softmax(const float* x, float* y, int64_t cols) {
+  __shared__ float red[256];
+  const float* xr = x + blockIdx.x * cols;
+  float* yr = y + blockIdx.x * cols;
+  float m = -INFINITY;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) m = fmaxf(m, xr[j]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  m = red[0];
+  __syncthreads();
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) s += expf(xr[j] - m);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float inv = 1.f / red[0];
+  for (int64_t j = threadIdx.x; j < cols; j += 256) yr[j] = expf(xr[j] - m) * inv;
+}
+// dx += y * (dy - sum(dy * y)), one block per row
+__global__ __launch_bounds__(256) void k_softmax_bwd(const float* dy, const float* y, float* dx, int64_t cols) {
+  __shared__ float red[256];
+  const int64_t base = blockIdx.x * cols;
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) s += dy[base + j] * y[base + j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float dot = red[0];
+  for (int64_t j = threadIdx.x; j < cols; j += 256) dx[base + j] += y[base + j] * (dy[base + j] - dot);
+}
+// fused softmax + cross-entropy on probabilities p (the softmax output):
+// g[logits] += (p - onehot(y)) * scale; metrics {loss, correct, rows}
+__global__ __launch_bounds__(256) void k_sparse_ce(const float* p, const int* labels, float* g, float* metrics,
+                                                   int64_t rows, int64_t cols, float scale) {
+  const int64_t r = blockIdx.x * 256ll + threadIdx.x;
+  if (r >= rows) return;
+  const float* pr = p + r * cols;
+  const int y = labels[r];
+  int am = 0;
+  for (int64_t j = 1; j < cols; ++j)
+    if (pr[j] > pr[am]) am = static_cast<int>(j);
+  for (int64_t j = 0; j < cols; ++j) g[r * cols + j] += (pr[j] - (j == y ? 1.f : 0.f)) * scale;
+  const float py = (y >= 0 && y < cols) ? pr[y] : 1.f;
+  atomicAdd(metrics + 0, -logf(fmaxf(py, 1e-30f)));
+  atomicAdd(metrics + 1, am == y ? 1.f : 0.f);
+}
+__global__ __launch_bounds__(256) void k_sgd(float* w, const float* g, float* buf, int64_t n, float lr, float mom,
+                                             float wd, int nesterov) {
+  GRID_LOOP(i, n) {
+    float gg = g[i] + wd * w[i];
+    if (buf) {
+      buf[i] = mom * buf[i] + gg;
+      gg = nesterov ? gg + mom * buf[i] : buf[i];
+    }
+    w[i] -= lr * gg;
+  }
+}
+__global__ __launch_bounds__(256) void k_adam(float* w, const float* g, float* m, float* v, int64_t n, float lr,
+                                              float b1, float b2, float eps, float wd, float bc1, float bc2) {
+  GRID_LOOP(i, n) {
+    const float gg = g[i] + wd * w[i];
+    m[i] = b1 * m[i] + (1.f - b1) * gg;
+    v[i] = b2 * v[i] + (1.f - b2) * gg * gg;
+    w[i] -= lr * (m[i] / bc1) / (sqrtf(v[i] / bc2) + eps);
+  }
+}
+
+int grid_of(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))); }
+
+int dact_of(const std::string& s) {
+  if (s == "relu") return A_RELU;
+  if (s == "sigmoid") return A_SIGMOID;
+  if (s == "tanh") return A_TANH;
+  if (s == "gelu") return A_GELU;
+  if (s == "elu") return A_ELU;
+  return A_NONE;
+}
+int dact_of(OpType t) {
+  switch (t) {
+    case OpType::RELU: return A_RELU;
+    case OpType::SIGMOID: return A_SIGMOID;
+    case OpType::TANH: return A_TANH;
+    case OpType::GELU: return A_GELU;
+    case OpType::ELU: return A_ELU;
+    default: return -1;
+  }
+}
+// the igemm32 epilogue's activation codes (elementwise.hip Act)
+int gemm_act(int a) { return a == A_RELU ? 1 : a == A_SIGMOID ? 2 : a == A_TANH ? 3 : a == A_GELU ? 4 : 0; }
+int binary_of(OpType t) {
+  switch (t) {
+    case OpType::EW_ADD: return 0;
+    case OpType::EW_SUB: return 1;
+    case OpType::EW_MUL: return 2;
+    case OpType::EW_DIV: return 3;
+    case OpType::EW_MAX: return 4;
+    case OpType::EW_MIN: return 5;
+    default: return -1;
+  }
+}
+int scalar_of(OpType t) {
+  switch (t) {
+    case OpType::SCALAR_MULTIPLY: return 0;
+    case OpType::SCALAR_ADD: return 1;
+    case OpType::SCALAR_SUB: return 2;
+    case OpType::SCALAR_TRUE_DIV: return 3;
+    default: return -1;
+  }
+}
+bool is_view(OpType t) { return t == OpType::FLAT || t == OpType::RESHAPE; }
+
+// why the device cannot run operator `t` (empty: it can)
+std::string unsupported(const ComputationGraph& cg, int n) {
+  const auto& node = cg.g.node(n);
+  const OpType t = node.label.op.type;
+  if (t == OpType::LINEAR) {
+    const std::string a = node.label.op.s("activation");
+    if (!a.empty() && a != "none" && dact_of(a) == A_NONE) return "LINEAR activation " + a;
+    return "";
+  }
+  if (dact_of(t) >= 0 || binary_of(t) >= 0 || scalar_of(t) >= 0 || is_view(t) || t == OpType::SOFTMAX) {
+    if (binary_of(t) >= 0) {
+      auto ins = cg.layer_data_inputs(n);
+      if (cg.shape(ins[0]).num_elements() != cg.shape(ins[1]).num_elements())
+        return "broadcasting " + to_string(t);
+    }
+    return "";
+  }
+  return "operator " + to_string(t);
+}
+
+class DeviceTrainingBacking final : public TrainingBacking {
+ public:
+  DeviceTrainingBacking(const ComputationGraph& cg, LocalOptimizer opt, const std::string& loss, uint64_t seed,
+                        int dev)
+      : cg_(cg), host_(cg, std::move(opt), loss, seed), dev_(dev) {
+    FFD_CHECK(hipSetDevice(dev_));
+    FFD_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    // one arena: every value, gradient, pre-activation and optimizer buffer
+    std::vector<std::pair<Key, int64_t>> want;
+    for (int n : cg_.layers_in_topo_order()) {
+      const auto& node = cg_.g.node(n);
+      for (size_t i = 0; i < node.outputs.size(); ++i) {
+        ValueRef v{n, static_cast<int>(i)};
+        if (!host_.slot(v, false)) continue;
+        want.push_back({Key{v, 0}, host_.slot(v, false)->numel()});
+        if (host_.slot(v, true)) want.push_back({Key{v, 1}, host_.slot(v, true)->numel()});
+      }
+    }
+    for (int n : host_.order()) {
+      const auto& node = cg_.g.node(n);
+      if (node.label.op.type == OpType::LINEAR && dact_of(node.label.op.s("activation")) != A_NONE)
+        want.push_back({Key{{n, 0}, 2}, host_.slot({n, 0}, false)->numel()});   // pre-activation
+      tmp_elems_ = std::max(tmp_elems_, host_.slot({n, 0}, false)->numel());
+    }
+    const ValueRef out = host_.output();
+    rows_ = 1;
+    cols_ = 1;
+    {
+      const auto& d = host_.slot(out, false)->dims;
+      cols_ = d.empty() ? 1 : d.back();
+      rows_ = host_.slot(out, false)->numel() / std::max<int64_t>(cols_, 1);
+    }
+    int64_t total = 0;
+    auto align = [](int64_t n) { return (n + 63) / 64 * 64; };   // 256 B
+    for (auto const& w : want) total += align(w.second);
+    total += align(tmp_elems_) * 2 + align(rows_) + 64;
+    FFD_CHECK(hipMalloc(&arena_, static_cast<size_t>(std::max<int64_t>(total, 64)) * sizeof(float)));
+    FFD_CHECK(hipMemsetAsync(arena_, 0, static_cast<size_t>(std::max<int64_t>(total, 64)) * sizeof(float), st_));
+    int64_t off = 0;
+    for (auto const& w : want) {
+      buf_[w.first] = {arena_ + off, w.second};
+      off += align(w.second);
+    }
+    tmp_ = arena_ + off;
+    off += align(tmp_elems_);
+    tmp2_ = arena_ + off;
+    off += align(tmp_elems_);
+    labels_ = reinterpret_cast<int*>(arena_ + off);
+    off += align(rows_);
+    metrics_d_ = arena_ + off;   // 8 floats
+    // every value / gradient slot starts host-written: the first step uploads
+    for (auto const& kv : buf_)
+      if (kv.first.kind < 2) state_[kv.first] = HOST;
+  }
+  ~DeviceTrainingBacking() override {
+    if (st_) (void)hipStreamSynchronize(st_);
+    if (arena_) (void)hipFree(arena_);
+    for (auto& kv : opt_state_) (void)hipFree(kv.second);
+    if (st_) (void)hipStreamDestroy(st_);
+  }
+
+  HostTensor* slot(const ValueRef& v, bool grad) override {
+    HostTensor* h = host_.slot(v, grad);
+    if (!h) return nullptr;
+    Key k{v, grad ? 1 : 0};
+    auto it = state_.find(k);
+    if (it != state_.end() && it->second == DEVICE) {
+      const Buf& b = buf_.at(k);
+      FFD_CHECK(hipMemcpyAsync(h->v.data(), b.p, b.n * sizeof(float), hipMemcpyDeviceToHost, st_));
+      FFD_CHECK(hipStreamSynchronize(st_));
+    }
+    if (it != state_.end()) it->second = HOST;   // the caller may write through the pointer
+    return h;
+  }
+  ValueRef output() const override { return host_.output(); }
+  LocalOptimizer& optimizer() override { return host_.optimizer(); }
+
+  void forward_layer(int n) override {
+    push();
+    fwd(n);
+  }
+  void forward() override {
+    push();
+    for (int n : host_.order()) fwd(n);
+  }
+  void backward(const std::vector<float>& labels) override;
+  void update() override;
+  const LocalMetrics& metrics() const override {
+    float m[8];
+    FFD_CHECK(hipMemcpyAsync(m, metrics_d_, sizeof(m), hipMemcpyDeviceToHost, st_));
+    FFD_CHECK(hipStreamSynchronize(st_));
+    metrics_.loss_sum = m[0];
+    metrics_.correct = static_cast<int64_t>(std::llround(m[1]));
+    metrics_.samples = samples_;
+    return metrics_;
+  }
+  void reset_metrics() override {
+    FFD_CHECK(hipMemsetAsync(metrics_d_, 0, 8 * sizeof(float), st_));
+    samples_ = 0;
+  }
+  std::string device() const override { return "gpu:" + std::to_string(dev_); }
+
+ private:
+  struct Key {
+    ValueRef v;
+    int kind;  // 0 value, 1 gradient, 2 pre-activation
+    bool operator<(const Key& o) const { return v < o.v || (v == o.v && kind < o.kind); }
+  };
+  struct Buf {
+    float* p = nullptr;
+    int64_t n = 0;
+  };
+  enum Where { HOST, DEVICE, SYNCED };
+
+  float* val(const ValueRef& v) { return buf_.at(Key{v, 0}).p; }
+  float* grad(const ValueRef& v) {
+    auto it = buf_.find(Key{v, 1});
+    return it == buf_.end() ? nullptr : it->second.p;
+  }
+  int64_t numel(const ValueRef& v) const { return buf_.at(Key{v, 0}).n; }
+  void mark(const ValueRef& v, int kind) { state_[Key{v, kind}] = DEVICE; }
+
+  // host-written mirrors -> device
+  void push() {
+    for (auto& kv : state_) {
+      if (kv.second != HOST) continue;
+      const HostTensor* h = host_.slot(kv.first.v, kv.first.kind == 1);
+      const Buf& b = buf_.at(kv.first);
+      FFD_CHECK(hipMemcpyAsync(b.p, h->v.data(), b.n * sizeof(float), hipMemcpyHostToDevice, st_));
+      kv.second = SYNCED;
+    }
+    FFD_CHECK(hipStreamSynchronize(st_));   // the host buffers may be rewritten after return
+  }
+
+  void fwd(int n);
+  void bwd(int n);
+
+  const ComputationGraph& cg_;
+  LocalTrainingBacking host_;
+  int dev_;
+  hipStream_t st_ = nullptr;
+  float* arena_ = nullptr;
+  float *tmp_ = nullptr, *tmp2_ = nullptr, *metrics_d_ = nullptr;
+  int* labels_ = nullptr;
+  int64_t tmp_elems_ = 1, rows_ = 1, cols_ = 1, step_ = 0, samples_ = 0;
+  std::map<Key, Buf> buf_;
+  std::map<Key, Where> state_;
+  std::map<std::pair<int, int>, float*> opt_state_;   // (weight node, 0: momentum / m, 1: v)
+  mutable LocalMetrics metrics_;
+};
+
+void DeviceTrainingBacking::fwd(int n) {
+  const auto& node = cg_.g.node(n);
+  const OpAttrs& op = node.label.op;
+  const OpType t = op.type;
+  const auto ins = cg_.layer_data_inputs(n);
+  const ValueRef o{n, 0};
+  float* y = val(o);
+  const int64_t ne = numel(o);
+  if (t == OpType::LINEAR) {
+    const auto ws = cg_.layer_weights(n);
+    const auto& wd = host_.slot(ws[0], false)->dims;
+    const int64_t in = wd[0], outc = wd[1], rows = numel(ins[0]) / in;
+    const int a = dact_of(op.s("activation"));
+    float* pre = a != A_NONE ? buf_.at(Key{o, 2}).p : nullptr;
+    ffk::gemm_f32(val(ins[0]), val(ws[0]), y, ws.size() > 1 ? val(ws[1]) : nullptr, pre, rows, outc, in, in, outc,
+                  outc, false, false, gemm_act(a), 1.f, 0.f, 1, 1, st_);
+  } else if (dact_of(t) >= 0) {
+    hipLaunchKernelGGL(k_act, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), y, ne, dact_of(t));
+  } else if (binary_of(t) >= 0) {
+    hipLaunchKernelGGL(k_binary, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), val(ins[1]), y, ne,
+                       binary_of(t));
+  } else if (scalar_of(t) >= 0) {
+    hipLaunchKernelGGL(k_scalar, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), y, ne, scalar_of(t),
+                       static_cast<float>(op.f("scalar")));
+  } else if (is_view(t)) {
+    FFD_CHECK(hipMemcpyAsync(y, val(ins[0]), ne * sizeof(float), hipMemcpyDeviceToDevice, st_));
+  } else if (t == OpType::SOFTMAX) {
+    const auto& d = host_.slot(o, false)->dims;
+    const int64_t cols = d.empty() ? 1 : d.back();
+    hipLaunchKernelGGL(k_softmax, dim3(static_cast<unsigned>(ne / cols)), dim3(256), 0, st_, val(ins[0]), y, cols);
+  } else {
+    throw FFError("device backing: no device implementation for " + to_string(t));
+  }
+  FFD_CHECK(hipGetLastError());
+  mark(o, 0);
+}
+
+void DeviceTrainingBacking::bwd(int n) {
+  const auto& node = cg_.g.node(n);
+  const OpAttrs& op = node.label.op;
+  const OpType t = op.type;
+  const auto ins = cg_.layer_data_inputs(n);
+  const ValueRef o{n, 0};
+  float* dy = grad(o);
+  if (!dy) return;
+  const int64_t ne = numel(o);
+  if (t == OpType::LINEAR) {
+    const auto ws = cg_.layer_weights(n);
+    const auto& wd = host_.slot(ws[0], false)->dims;
+    const int64_t in = wd[0], outc = wd[1], rows = numel(ins[0]) / in;
+    const int a = dact_of(op.s("activation"));
+    const float* g = dy;
+    if (a != A_NONE) {
+      hipLaunchKernelGGL(k_act_grad, dim3(grid_of(ne)), dim3(256), 0, st_, dy, buf_.at(Key{o, 2}).p, tmp_, ne, a);
+      g = tmp_;
+    }
+    if (float* dw = grad(ws[0]))   // dW += x^T g
+      ffk::gemm_f32(val(ins[0]), g, dw, nullptr, nullptr, in, outc, rows, in, outc, outc, true, false, 0, 1.f, 1.f, 1,
+                    1, st_);
+    if (ws.size() > 1)
+      if (float* db = grad(ws[1]))
+        hipLaunchKernelGGL(k_colsum, dim3(static_cast<unsigned>((outc + 255) / 256)), dim3(256), 0, st_, g, db, rows,
+                           outc);
+    if (float* dx = grad(ins[0]))   // dX += g W^T
+      ffk::gemm_f32(g, val(ws[0]), dx, nullptr, nullptr, rows, in, outc, outc, outc, in, false, true, 0, 1.f, 1.f, 1,
+                    1, st_);
+  } else if (dact_of(t) >= 0) {
+    if (float* dx = grad(ins[0]))
+      hipLaunchKernelGGL(k_act_bwd, dim3(grid_of(ne)), dim3(256), 0, st_, dy, val(ins[0]), dx, ne, dact_of(t));
+  } else if (binary_of(t) >= 0) {
+    hipLaunchKernelGGL(k_binary_bwd, dim3(grid_of(ne)), dim3(256), 0, st_, dy, val(ins[0]), val(ins[1]),
+                       grad(ins[0]), grad(ins[1]), ne, binary_of(t));
+  } else if (scalar_of(t) >= 0) {
+    const int s = scalar_of(t);
+    const float k = static_cast<float>(op.f("scalar"));
+    if (float* dx = grad(ins[0]))
+      hipLaunchKernelGGL(k_axpy, dim3(grid_of(ne)), dim3(256), 0, st_, dy, dx, ne,
+                         s == 0 ? k : s == 3 ? 1.f / k : 1.f);
+  } else if (is_view(t)) {
+    if (float* dx = grad(ins[0])) hipLaunchKernelGGL(k_axpy, dim3(grid_of(ne)), dim3(256), 0, st_, dy, dx, ne, 1.f);
+  } else if (t == OpType::SOFTMAX) {
+    const auto& d = host_.slot(o, false)->dims;
+    const int64_t cols = d.empty() ? 1 : d.back();
+    if (float* dx = grad(ins[0]))
+      hipLaunchKernelGGL(k_softmax_bwd, dim3(static_cast<unsigned>(ne / cols)), dim3(256), 0, st_, dy, val(o), dx,
+                         cols);
+  }
+  FFD_CHECK(hipGetLastError());
+  for (auto const& v : ins)
+    if (grad(v)) mark(v, 1);
+  for (auto const& v : cg_.layer_weights(n))
+    if (grad(v)) mark(v, 1);
+}
+
+void DeviceTrainingBacking::backward(const std::vector<float>& labels) {
+  push();
+  for (auto const& kv : buf_)
+    if (kv.first.kind == 1) FFD_CHECK(hipMemsetAsync(kv.second.p, 0, kv.second.n * sizeof(float), st_));
+  const ValueRef out = host_.output();
+  const std::string& loss = host_.loss();
+  const float* p = val(out);
+  samples_ += rows_;
+  if (loss == "sparse_categorical_crossentropy") {
+    if (static_cast<int64_t>(labels.size()) != rows_) throw FFError("device backing: label size mismatch");
+    std::vector<int> li(labels.size());
+    for (size_t i = 0; i < labels.size(); ++i) li[i] = static_cast<int>(labels[i]);
+    FFD_CHECK(hipMemcpyAsync(labels_, li.data(), li.size() * sizeof(int), hipMemcpyHostToDevice, st_));
+    // gradient w.r.t. the logits (the fused softmax's input)
+    const ValueRef tgt = cg_.layer_data_inputs(out.node)[0];
+    float* g = grad(tgt);
+    hipLaunchKernelGGL(k_sparse_ce, dim3(static_cast<unsigned>((rows_ + 255) / 256)), dim3(256), 0, st_, p, labels_,
+                       g ? g : tmp2_, metrics_d_, rows_, cols_, 1.f / static_cast<float>(rows_));
+    FFD_CHECK(hipStreamSynchronize(st_));   // `li` leaves scope
+    if (g) mark(tgt, 1);
+  } else if (loss == "mean_squared_error" || loss == "mean_squared_error_avg_reduce") {
+    if (static_cast<int64_t>(labels.size()) != numel(out)) throw FFError("device backing: label size mismatch");
+    FFD_CHECK(hipMemcpyAsync(tmp2_, labels.data(), labels.size() * sizeof(float), hipMemcpyHostToDevice, st_));
+    float* g = grad(out);
+    // metrics block {loss, -, count, sq err, abs err}: slot 2 is not used here
+    ffk::mse_loss_full(kDtF32, kDtF32, p, tmp2_, g ? tmp_ : nullptr, metrics_d_, numel(out),
+                       2.f / static_cast<float>(rows_ * cols_), 1, cols_, 0, st_);
+    if (g) {
+      hipLaunchKernelGGL(k_axpy, dim3(grid_of(numel(out))), dim3(256), 0, st_, tmp_, g, numel(out), 1.f);
+      mark(out, 1);
+    }
+    FFD_CHECK(hipStreamSynchronize(st_));   // `labels` may be freed by the caller
+  } else {
+    throw FFError("device backing: loss " + loss);
+  }
+  FFD_CHECK(hipGetLastError());
+  const auto& ord = host_.order();
+  for (auto it = ord.rbegin(); it != ord.rend(); ++it) {
+    if (host_.fused_softmax_ce() && *it == out.node) continue;
+    if (!host_.needs_grad({*it, 0})) continue;
+    bwd(*it);
+  }
+}
+
+void DeviceTrainingBacking::update() {
+  push();
+  ++step_;
+  const LocalOptimizer& o = host_.optimizer();
+  for (auto const& kv : buf_) {
+    if (kv.first.kind != 1 || cg_.g.node(kv.first.v.node).label.op.type != OpType::WEIGHT) continue;
+    const ValueRef v = kv.first.v;
+    const int* l = &v.node;
+    float* g = kv.second.p;
+    float* w = val(v);
+    const int64_t n = numel(v);
+    auto state = [&](int which) {
+      auto key = std::make_pair(*l, which);
+      auto it = opt_state_.find(key);
+      if (it != opt_state_.end()) return it->second;
+      float* p = nullptr;
+      FFD_CHECK(hipMalloc(&p, std::max<int64_t>(n, 1) * sizeof(float)));
+      FFD_CHECK(hipMemsetAsync(p, 0, std::max<int64_t>(n, 1) * sizeof(float), st_));
+      return opt_state_[key] = p;
+    };
+    if (o.kind == "adam") {
+      const float bc1 = 1.f - static_cast<float>(std::pow(o.beta1, static_cast<double>(step_)));
+      const float bc2 = 1.f - static_cast<float>(std::pow(o.beta2, static_cast<double>(step_)));
+      hipLaunchKernelGGL(k_adam, dim3(grid_of(n)), dim3(256), 0, st_, w, g, state(0), state(1), n,
+                         static_cast<float>(o.lr), static_cast<float>(o.beta1), static_cast<float>(o.beta2),
+                         static_cast<float>(o.epsilon), static_cast<float>(o.weight_decay), bc1, bc2);
+    } else {
+      hipLaunchKernelGGL(k_sgd, dim3(grid_of(n)), dim3(256), 0, st_, w, g, o.momentum != 0.0 ? state(0) : nullptr, n,
+                         static_cast<float>(o.lr), static_cast<float>(o.momentum),
+                         static_cast<float>(o.weight_decay), o.nesterov ? 1 : 0);
+    }
+    FFD_CHECK(hipGetLastError());
+    mark(v, 0);
+  }
+}
+
+}  // namespace
+
+std::unique_ptr<TrainingBacking> make_device_backing(const ComputationGraph& cg, LocalOptimizer opt,
+                                                     const std::string& loss, uint64_t seed, std::string* why) {
+  auto no = [&](const std::string& m) -> std::unique_ptr<TrainingBacking> {
+    if (why) *why = m;
+    return nullptr;
+  };
+  const char* want = std::getenv("FF_C_API_DEVICE");
+  if (want && std::strcmp(want, "cpu") == 0) return no("FF_C_API_DEVICE=cpu");
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    (void)hipGetLastError();
+    return no("no GPU visible");
+  }
+  for (int n : cg.layers_in_topo_order()) {
+    const OpType t = cg.g.node(n).label.op.type;
+    if (t == OpType::INPUT || t == OpType::WEIGHT) continue;
+    const std::string u = unsupported(cg, n);
+    if (!u.empty()) return no("no device implementation: " + u);
+  }
+  if (loss != "sparse_categorical_crossentropy" && loss != "mean_squared_error" &&
+      loss != "mean_squared_error_avg_reduce")
+    return no("loss " + loss + " runs on the CPU backing");
+  // the fused softmax + CE needs the graph to end in SOFTMAX
+  if (loss == "sparse_categorical_crossentropy") {
+    int last = -1;
+    for (int n : cg.layers_in_topo_order()) {
+      const OpType t = cg.g.node(n).label.op.type;
+      if (t != OpType::INPUT && t != OpType::WEIGHT) last = n;
+    }
+    if (last < 0 || cg.g.node(last).label.op.type != OpType::SOFTMAX)
+      return no("cross-entropy without a final softmax");
+  }
+  int dev = 0;
+  if (const char* d = std::getenv("FF_C_API_GPU")) dev = std::atoi(d);
+  if (dev < 0 || dev >= count) dev = 0;
+  return std::unique_ptr<TrainingBacking>(new DeviceTrainingBacking(cg, std::move(opt), loss, seed, dev));
+}
+
+}  // namespace ff

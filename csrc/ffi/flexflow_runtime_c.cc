@@ -97,7 +97,8 @@ struct RtMetrics {
 struct RtModel {
   RtConfig cfg;
   ff::ComputationGraph cg;
-  std::unique_ptr<ff::LocalTrainingBacking> be;
+  std::unique_ptr<ff::TrainingBacking> be;
+  std::string device = "cpu", device_note;
   ff::LocalOptimizer opt;
   std::string loss = "sparse_categorical_crossentropy";
   bool sparse_labels = true;
@@ -343,6 +344,17 @@ extern "C" {
 
 const char* flexflow_runtime_last_error(void) { return g_err.c_str(); }
 
+const char* flexflow_model_get_device(flexflow_model_t h) {
+  static thread_local std::string out;
+  out.clear();
+  guard_void([&] {
+    auto* m = M(h);
+    out = m->be ? m->device : "uncompiled";
+    if (m->be && m->device == "cpu" && !m->device_note.empty()) out += " (" + m->device_note + ")";
+  });
+  return out.c_str();
+}
+
 // ---- FFConfig ------------------------------------------------------------
 flexflow_config_t flexflow_config_create(void) {
   auto* c = new RtConfig();
@@ -433,7 +445,11 @@ void flexflow_model_compile(flexflow_model_t h, enum LossType loss_type, int*, i
       default: m->loss = "identity";
     }
     m->sparse_labels = loss_type == LOSS_SPARSE_CATEGORICAL_CROSSENTROPY;
-    m->be = std::make_unique<ff::LocalTrainingBacking>(m->cg, m->opt, m->loss, 0);
+    // the GPU backing when a GPU is visible and every operator has a device
+    // implementation (FF_C_API_DEVICE=cpu keeps the host), else the CPU one
+    m->be = ff::make_device_backing(m->cg, m->opt, m->loss, 0, &m->device_note);
+    if (!m->be) m->be = std::make_unique<ff::LocalTrainingBacking>(m->cg, m->opt, m->loss, 0);
+    m->device = m->be->device();
     // data written before compile moves into the backing's slots
     for (auto& kv : m->tensors) {
       RtTensor* t = kv.second.get();

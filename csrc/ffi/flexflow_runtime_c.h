@@ -84,6 +84,9 @@ enum MetricsType {
 };
 
 FF_RT_API const char* flexflow_runtime_last_error(void);
+/* where a compiled model trains: "gpu:<n>" (the HIP backing) or "cpu" (with
+ * the reason the GPU backing was not taken, e.g. "cpu (no GPU visible)") */
+FF_RT_API const char* flexflow_model_get_device(flexflow_model_t model);
 
 /* ---- FFConfig ---------------------------------------------------------- */
 FF_RT_API flexflow_config_t flexflow_config_create(void);

@@ -70,6 +70,7 @@ static int test_mlp(flexflow_config_t cfg) {
   int metrics[1] = {METRICS_ACCURACY};
   flexflow_model_compile(model, LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics, 1, COMP_MODE_TRAINING);
   flexflow_model_init_layers(model);
+  printf("device %s\n", flexflow_model_get_device(model));
   flexflow_tensor_t label = flexflow_model_get_label_tensor(model);
   CHECK(flexflow_tensor_get_dim(label, 0) == 1 && flexflow_tensor_get_dim(label, 1) == B,
         "label tensor is [batch, 1]");
@@ -204,6 +205,49 @@ static int test_cnn(flexflow_config_t cfg) {
   return 0;
 }
 
+/* three SGD steps of a two-layer MLP (tanh, sigmoid heads; MSE), the
+ * trained weights printed with full precision: the GPU and the CPU backings
+ * must agree (tests/test_runtime_c_gpu.py runs this twice) */
+static void test_parity(flexflow_config_t cfg) {
+  enum { PB = 16, PF = 24, PH = 40, PO = 3 };
+  flexflow_model_t model = flexflow_model_create(cfg);
+  int dims[2] = {PB, PF};
+  flexflow_tensor_t x = flexflow_tensor_create(model, 2, dims, DT_FLOAT, true);
+  flexflow_initializer_t null_init = flexflow_initializer_create_null();
+  flexflow_op_t no_op = {NULL};
+  flexflow_tensor_t t = flexflow_model_add_dense(model, x, PH, AC_MODE_TANH, true, DT_FLOAT, no_op, null_init,
+                                                 null_init, REG_MODE_NONE, 0.f, "p1");
+  t = flexflow_model_add_dense(model, t, PO, AC_MODE_SIGMOID, true, DT_FLOAT, no_op, null_init, null_init,
+                               REG_MODE_NONE, 0.f, "p2");
+  flexflow_adam_optimizer_t adam = flexflow_adam_optimizer_create(model, 0.01, 0.9, 0.999, 0.0, 1e-8);
+  flexflow_model_set_adam_optimizer(model, adam);
+  int metrics[1] = {METRICS_MEAN_SQUARED_ERROR};
+  flexflow_model_compile(model, LOSS_MEAN_SQUARED_ERROR_AVG_REDUCE, metrics, 1, COMP_MODE_TRAINING);
+  float xs[PB * PF], ys[PB * PO];
+  for (int i = 0; i < PB * PF; ++i) xs[i] = cosf(0.11f * (float)i);
+  for (int i = 0; i < PB * PO; ++i) ys[i] = 0.5f + 0.4f * sinf(0.3f * (float)i);
+  int ldims[2] = {PB, PO};
+  flexflow_tensor_set_tensor_float(x, model, 2, dims, xs);
+  flexflow_tensor_set_tensor_float(flexflow_model_get_label_tensor(model), model, 2, ldims, ys);
+  for (int step = 0; step < 3; ++step) {
+    flexflow_model_forward(model, -1);
+    flexflow_model_zero_gradients(model);
+    flexflow_model_backward(model, -1);
+    flexflow_model_update(model);
+  }
+  flexflow_op_t l2 = flexflow_model_get_layer_by_id(model, 1);
+  float w[PH * PO];
+  flexflow_parameter_get_weights_float(flexflow_op_get_parameter_by_id(l2, 0), model, w);
+  double sum = 0.0, asum = 0.0;
+  for (int i = 0; i < PH * PO; ++i) {
+    sum += w[i];
+    asum += fabs(w[i]);
+  }
+  printf("parity device %s w2_sum %.9g w2_abs %.9g w2_0 %.9g\n", flexflow_model_get_device(model), sum, asum, w[0]);
+  flexflow_adam_optimizer_destroy(adam);
+  flexflow_model_destroy(model);
+}
+
 static void test_configs(void) {
   char* argv[] = {"prog", "-b", "32", "--epochs", "3", "--arch-mlp-bot", "13-512-256-64", "--arch-embedding-size",
                   "1000-1000", "--arch-sparse-feature-size", "64", "--dataset", "/tmp/x.h5", "-ll:gpu", "8"};
@@ -239,6 +283,7 @@ int main(int argc, char** argv) {
   flexflow_config_parse_args_default(cfg);
   test_mlp(cfg);
   test_cnn(cfg);
+  test_parity(cfg);
   flexflow_config_destroy(cfg);
   finish_flexflow_task();
   printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);

@@ -226,6 +226,24 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("unary_op", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, int64_t n, int op, float s, int bwd,
                        uintptr_t st) { unary_op(dt, P(x), P(dy), P(y), n, op, s, bwd, S(st)); });
+  m.def("mse_loss_full", [](int dt, int ldt, uintptr_t p, uintptr_t y, uintptr_t g, uintptr_t metrics, int64_t n,
+                            float scale, int full, int64_t cols, int64_t rows, uintptr_t st) {
+    mse_loss_full(dt, ldt, P(p), P(y), P(g), F(metrics), n, scale, full, cols, rows, S(st));
+  });
+  m.def("narrow_linear_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t pre, int64_t M,
+                                int64_t K, int64_t N, int act, uintptr_t st) {
+    narrow_linear_fwd(P(x), P(w), F(bias), P(y), P(pre), M, K, N, act, S(st));
+  });
+  m.def("narrow_linear_dgrad", [](uintptr_t dy, uintptr_t pre, uintptr_t w, uintptr_t dx, int64_t M, int64_t K,
+                                  int64_t N, int act, float beta, uintptr_t st) {
+    narrow_linear_dgrad(P(dy), P(pre), P(w), P(dx), M, K, N, act, beta, S(st));
+  });
+  m.def("narrow_wgrad_blocks", [](int64_t M) { return narrow_wgrad_blocks(M); });
+  m.def("narrow_linear_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t pre, uintptr_t part, int blocks, uintptr_t dw,
+                                  int dw_dtype, float beta, uintptr_t db, int64_t M, int64_t K, int64_t N, int act,
+                                  uintptr_t st) {
+    narrow_linear_wgrad(P(x), P(dy), P(pre), F(part), blocks, P(dw), dw_dtype, beta, F(db), M, K, N, act, S(st));
+  });
   m.def("mse_loss", [](int dt, uintptr_t p, uintptr_t y, uintptr_t g, uintptr_t metrics, int64_t n, float scale,
                        uintptr_t st) { mse_loss(dt, P(p), P(y), P(g), F(metrics), n, scale, S(st)); });
   m.def("init_tensor", [=](int dt, uintptr_t out, std::vector<int64_t> piece, std::vector<int64_t> full,
@@ -299,8 +317,8 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("conv32_wgrad", [=](std::vector<int> shp, int groups, uintptr_t x, uintptr_t dy, uintptr_t dw, int in_f32,
                             uintptr_t st) { conv32_wgrad(cshape(shp), groups, P(x), P(dy), F(dw), in_f32, S(st)); });
-  m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st, uintptr_t ws) {
-    bn_stats(P(x), F(stats), M, C, S(st), F(ws));
+  m.def("bn_stats", [](uintptr_t x, uintptr_t stats, int64_t M, int C, uintptr_t st, uintptr_t ws, int ws_clean) {
+    bn_stats(P(x), F(stats), M, C, S(st), F(ws), ws_clean);
   });
   m.def("bn_finalize", [](uintptr_t stats, uintptr_t g, uintptr_t b, int pdt, uintptr_t rm, uintptr_t rv,
                           uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t rstd, int C, double count,
@@ -312,9 +330,9 @@ PYBIND11_MODULE(_ffkernels, m) {
                        int relu, uintptr_t st) { bn_apply(P(x), P(res), F(scale), F(shift), P(y), M, C, relu, S(st)); });
   m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t g, int pdt,
                      uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, uintptr_t ws, int64_t M, int C,
-                     int relu, uintptr_t st, uintptr_t ss) {
+                     int relu, uintptr_t st, uintptr_t ss, int ws_clean) {
     bn_bwd(P(dy), P(x), P(y), F(mean), F(rstd), P(g), pdt, P(dx), P(dres), F(dg), F(db), F(ws), M, C, relu, S(st),
-           F(ss));
+           F(ss), ws_clean);
   });
   // pool geometry: [N,H,W,C,R,S,sh,sw,ph,pw,avg,count_pad]
   auto pshape = [](const std::vector<int>& v) {

@@ -23,6 +23,9 @@
 // Pooling: forward one thread per (output pixel, 8 channels), max pooling
 // records the winning tap as a byte; backward is a gather over the windows
 // that cover an input pixel (no atomics, deterministic).
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -68,7 +71,10 @@ dim3 red_grid(const RedGeom& r, int64_t M) {
 
 // MODE 0: stats of x  -> out[0:C] += sum x, out[C:2C] += sum x^2
 // MODE 1: bwd reduce  -> out[0:C] += sum g,  out[C:2C] += sum g*xhat
-template <int MODE>
+// U rows per thread and iteration, their loads issued before any math (raw
+// 16-B vectors, 4 VGPRs each): a wave keeps U (MODE 0) or 2U / 3U (MODE 1)
+// KiB in flight instead of 1 / 2 / 3, which is what the HBM latency needs.
+template <int MODE, int U>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                         const bf16* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, float* __restrict__ out,
@@ -93,32 +99,49 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16* __restrict__
     }
   }
   if (gok) {
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RL + rl; r < M; r += static_cast<int64_t>(gridDim.x) * RL) {
-      const int64_t off = r * C + c0;
-      float xv[8];
-      load8(x + off, xv);
-      if (MODE == 0) {
+    const int64_t step = static_cast<int64_t>(gridDim.x) * RL;
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RL + rl; r < M; r += U * step) {
+      bf16x8 xr[U], gr[U], yr[U];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          a[i] += xv[i];
-          b[i] += xv[i] * xv[i];
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = r + u * step;
+        if (rr < M) {
+          const int64_t off = rr * C + c0;
+          xr[u] = *reinterpret_cast<const bf16x8*>(x + off);
+          if (MODE == 1) {
+            gr[u] = *reinterpret_cast<const bf16x8*>(dy + off);
+            if (relu == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + off);
+          }
         }
-      } else {
-        float g[8];
-        load8(dy + off, g);
-        if (relu == 1) {
-          float yv[8];
-          load8(y + off, yv);
+      }
 #pragma unroll
-          for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
-        } else if (relu == 2) {  // ReLU mask recomputed from x (the forward's y is not re-read)
+      for (int u = 0; u < U; ++u) {
+        if (r + u * step >= M) break;
+        float xv[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) g[i] = xv[i] * sc[i] + sh[i] > 0.f ? g[i] : 0.f;
-        }
+        for (int i = 0; i < 8; ++i) xv[i] = bf2f(xr[u][i]);
+        if (MODE == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          a[i] += g[i];
-          b[i] += g[i] * (xv[i] - mu[i]) * rs[i];
+          for (int i = 0; i < 8; ++i) {
+            a[i] += xv[i];
+            b[i] += xv[i] * xv[i];
+          }
+        } else {
+          float g[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[i] = bf2f(gr[u][i]);
+          if (relu == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) g[i] = bf2f(yr[u][i]) > 0.f ? g[i] : 0.f;
+          } else if (relu == 2) {  // ReLU mask recomputed from x (the forward's y is not re-read)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) g[i] = xv[i] * sc[i] + sh[i] > 0.f ? g[i] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            a[i] += g[i];
+            b[i] += g[i] * (xv[i] - mu[i]) * rs[i];
+          }
         }
       }
     }
@@ -166,49 +189,67 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, const void* 
   }
 }
 
+template <int U>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16* __restrict__ y,
                                                        int64_t nvec, int C, int relu) {
-  for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t off = v * 8;
-    const int c0 = static_cast<int>(off % C);
-    float xv[8];
-    load8(x + off, xv);
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c0), s1 = *reinterpret_cast<const f32x4*>(scale + c0 + 4);
-    const f32x4 h0 = *reinterpret_cast<const f32x4*>(shift + c0), h1 = *reinterpret_cast<const f32x4*>(shift + c0 + 4);
+  const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v0 = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v0 < nvec; v0 += U * step) {
+    bf16x8 xr[U], rr[U];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      xv[i] = xv[i] * s0[i] + h0[i];
-      xv[i + 4] = xv[i + 4] * s1[i] + h1[i];
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * step;
+      if (v < nvec) {
+        xr[u] = *reinterpret_cast<const bf16x8*>(x + v * 8);
+        if (res) rr[u] = *reinterpret_cast<const bf16x8*>(res + v * 8);
+      }
     }
-    if (res) {
-      float rv[8];
-      load8(res + off, rv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) xv[i] += rv[i];
-    }
-    if (relu) {
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * step;
+      if (v >= nvec) break;
+      const int64_t off = v * 8;
+      const int c0 = static_cast<int>(off % C);
+      float xv[8];
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c0), s1 = *reinterpret_cast<const f32x4*>(scale + c0 + 4);
+      const f32x4 h0 = *reinterpret_cast<const f32x4*>(shift + c0), h1 = *reinterpret_cast<const f32x4*>(shift + c0 + 4);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) xv[i] = xv[i] > 0.f ? xv[i] : 0.f;
+      for (int i = 0; i < 4; ++i) {
+        xv[i] = bf2f(xr[u][i]) * s0[i] + h0[i];
+        xv[i + 4] = bf2f(xr[u][i + 4]) * s1[i] + h1[i];
+      }
+      if (res) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[i] += bf2f(rr[u][i]);
+      }
+      if (relu) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[i] = xv[i] > 0.f ? xv[i] : 0.f;
+      }
+      store8(y + off, xv);
     }
-    store8(y + off, xv);
   }
 }
 
 // per-channel backward coefficients: dx = A*g + B*x + D with
 // A = gamma*rstd, B = -A*rstd*mean(g*xhat), D = -A*mean(g) - B*mean;
 // also dgamma += sum(g*xhat), dbeta += sum(g).
-__global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* __restrict__ mean,
+__global__ void bn_bwd_coef_kernel(float* __restrict__ sums, const float* __restrict__ mean,
                                    const float* __restrict__ rstd, const void* gamma, int pdt, float* __restrict__ coef,
-                                   float* dgamma, float* dbeta, int C, float inv_count) {
+                                   float* dgamma, float* dbeta, int C, float inv_count, int reset) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s1 = 0.f, s2 = 0.f;
   for (int k = 0; k < kBnBuckets; ++k) {
     s1 += sums[static_cast<int64_t>(k) * 2 * C + c];
     s2 += sums[static_cast<int64_t>(k) * 2 * C + C + c];
+  }
+  if (reset) {  // a persistent workspace leaves this kernel zeroed for the next reduction
+    for (int k = 0; k < kBnBuckets; ++k) {
+      sums[static_cast<int64_t>(k) * 2 * C + c] = 0.f;
+      sums[static_cast<int64_t>(k) * 2 * C + C + c] = 0.f;
+    }
   }
   const float A = (gamma ? ldp(gamma, pdt, c) : 1.f) * rstd[c];
   const float B = -A * rstd[c] * s2 * inv_count;
@@ -219,42 +260,59 @@ __global__ void bn_bwd_coef_kernel(const float* __restrict__ sums, const float* 
   if (dgamma) dgamma[c] += s2;
 }
 
+template <int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ y, const float* __restrict__ coef,
                                                            bf16* __restrict__ dx, bf16* __restrict__ dres,
                                                            int64_t nvec, int C, int relu,
                                                            const float* __restrict__ ss) {
-  for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t off = v * 8;
-    const int c0 = static_cast<int>(off % C);
-    float g[8], xv[8];
-    load8(dy + off, g);
-    load8(x + off, xv);
-    if (relu == 1) {
-      float yv[8];
-      load8(y + off, yv);
+  const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t v0 = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v0 < nvec; v0 += U * step) {
+    bf16x8 gr[U], xr[U], yr[U];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
-    } else if (relu == 2) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4 s4 = *reinterpret_cast<const f32x4*>(ss + c0 + 4 * h);
-        const f32x4 h4 = *reinterpret_cast<const f32x4*>(ss + C + c0 + 4 * h);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) g[4 * h + i] = xv[4 * h + i] * s4[i] + h4[i] > 0.f ? g[4 * h + i] : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * step;
+      if (v < nvec) {
+        gr[u] = *reinterpret_cast<const bf16x8*>(dy + v * 8);
+        xr[u] = *reinterpret_cast<const bf16x8*>(x + v * 8);
+        if (relu == 1) yr[u] = *reinterpret_cast<const bf16x8*>(y + v * 8);
       }
     }
-    if (dres) store8(dres + off, g);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 A = *reinterpret_cast<const f32x4*>(coef + c0 + 4 * h);
-      const f32x4 B = *reinterpret_cast<const f32x4*>(coef + C + c0 + 4 * h);
-      const f32x4 D = *reinterpret_cast<const f32x4*>(coef + 2 * C + c0 + 4 * h);
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = v0 + u * step;
+      if (v >= nvec) break;
+      const int64_t off = v * 8;
+      const int c0 = static_cast<int>(off % C);
+      float g[8], xv[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) g[4 * h + i] = A[i] * g[4 * h + i] + B[i] * xv[4 * h + i] + D[i];
+      for (int i = 0; i < 8; ++i) {
+        g[i] = bf2f(gr[u][i]);
+        xv[i] = bf2f(xr[u][i]);
+      }
+      if (relu == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[i] = bf2f(yr[u][i]) > 0.f ? g[i] : 0.f;
+      } else if (relu == 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 s4 = *reinterpret_cast<const f32x4*>(ss + c0 + 4 * h);
+          const f32x4 h4 = *reinterpret_cast<const f32x4*>(ss + C + c0 + 4 * h);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g[4 * h + i] = xv[4 * h + i] * s4[i] + h4[i] > 0.f ? g[4 * h + i] : 0.f;
+        }
+      }
+      if (dres) store8(dres + off, g);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 A = *reinterpret_cast<const f32x4*>(coef + c0 + 4 * h);
+        const f32x4 B = *reinterpret_cast<const f32x4*>(coef + C + c0 + 4 * h);
+        const f32x4 D = *reinterpret_cast<const f32x4*>(coef + 2 * C + c0 + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[4 * h + i] = A[i] * g[4 * h + i] + B[i] * xv[4 * h + i] + D[i];
+      }
+      store8(dx + off, g);
     }
-    store8(dx + off, g);
   }
 }
 
@@ -382,25 +440,50 @@ int ew_blocks(int64_t n) { return static_cast<int>(std::min<int64_t>((n + 255) /
 
 }  // namespace
 
-__global__ void bn_fold_buckets_kernel(const float* __restrict__ ws, float* __restrict__ stats, int C2) {
+__global__ void bn_fold_buckets_kernel(float* __restrict__ ws, float* __restrict__ stats, int C2, int reset) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C2) return;
   float s = 0.f;
   for (int k = 0; k < kBnBuckets; ++k) s += ws[static_cast<int64_t>(k) * C2 + c];
   stats[c] += s;
+  if (reset)
+    for (int k = 0; k < kBnBuckets; ++k) ws[static_cast<int64_t>(k) * C2 + c] = 0.f;
 }
 
-void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws) {
+// rows / vectors per thread and iteration of the reduction and apply passes
+// (FFK_BN_UNROLL: 1, 2 or 4; read once)
+static int bn_unroll() {
+  static const int u = [] {
+    const char* e = getenv("FFK_BN_UNROLL");
+    const int v = e ? atoi(e) : 4;
+    return v == 1 || v == 2 ? v : 4;
+  }();
+  return u;
+}
+template <typename F>
+static void with_unroll(F&& f) {
+  switch (bn_unroll()) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    default: f(std::integral_constant<int, 4>{}); break;
+  }
+}
+
+void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws, int ws_clean) {
   if (C % 8) throw std::invalid_argument("bn_stats: C must be a multiple of 8");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
   dim3 grid = red_grid(r, M);
   if (!ws) grid.x = std::min(grid.x, 256u);  // single [2][C] target: bound the same-address atomics
-  else (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
-  hipLaunchKernelGGL((bn_reduce_kernel<0>), grid, dim3(256), 0, st, static_cast<const bf16*>(x), nullptr,
-                     nullptr, nullptr, nullptr, ws ? ws : stats, M, C, r.GL, 0, nullptr, ws ? kBnBuckets : 1);
+  else if (!ws_clean) (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
+  with_unroll([&](auto uu) {
+    hipLaunchKernelGGL((bn_reduce_kernel<0, decltype(uu)::value>), grid, dim3(256), 0, st,
+                       static_cast<const bf16*>(x), nullptr, nullptr, nullptr, nullptr, ws ? ws : stats, M, C, r.GL,
+                       0, nullptr, ws ? kBnBuckets : 1);
+  });
   if (ws)
-    hipLaunchKernelGGL(bn_fold_buckets_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, ws, stats, 2 * C);
+    hipLaunchKernelGGL(bn_fold_buckets_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, ws, stats, 2 * C,
+                       ws_clean);
   FFK_LAUNCH_CHECK("bn_stats");
 }
 
@@ -417,30 +500,39 @@ void bn_apply(const void* x, const void* residual, const float* scale, const flo
   if (C % 8) throw std::invalid_argument("bn_apply: C must be a multiple of 8");
   const int64_t nvec = M * C / 8;
   if (nvec <= 0) return;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, st, static_cast<const bf16*>(x),
-                     static_cast<const bf16*>(residual), scale, shift, static_cast<bf16*>(y), nvec, C, relu);
+  with_unroll([&](auto uu) {
+    constexpr int U = decltype(uu)::value;
+    hipLaunchKernelGGL(bn_apply_kernel<U>, dim3(ew_blocks((nvec + U - 1) / U)), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), static_cast<const bf16*>(residual), scale, shift,
+                       static_cast<bf16*>(y), nvec, C, relu);
+  });
   FFK_LAUNCH_CHECK("bn_apply");
 }
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
-            int relu, hipStream_t st, const float* scale_shift) {
+            int relu, hipStream_t st, const float* scale_shift, int ws_clean) {
   if (C % 8) throw std::invalid_argument("bn_bwd: C must be a multiple of 8");
   if (relu == 1 && !y) throw std::invalid_argument("bn_bwd: ReLU mask from y needs y");
   if (relu == 2 && !scale_shift) throw std::invalid_argument("bn_bwd: ReLU mask from x needs the scale / shift");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
-  hipLaunchKernelGGL((bn_reduce_kernel<1>), red_grid(r, M), dim3(256), 0, st, static_cast<const bf16*>(x),
-                     static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean, rstd, ws, M, C, r.GL, relu,
-                     scale_shift, kBnBuckets);
+  if (!ws_clean) (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
+  with_unroll([&](auto uu) {
+    hipLaunchKernelGGL((bn_reduce_kernel<1, decltype(uu)::value>), red_grid(r, M), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean,
+                       rstd, ws, M, C, r.GL, relu, scale_shift, kBnBuckets);
+  });
   float* coef = ws + 2 * C * kBnBuckets;
   hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, mean, rstd, gamma,
-                     param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M));
+                     param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M), ws_clean);
   const int64_t nvec = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, st, static_cast<const bf16*>(dy),
-                     static_cast<const bf16*>(x), static_cast<const bf16*>(y), coef, static_cast<bf16*>(dx),
-                     static_cast<bf16*>(dres), nvec, C, relu, scale_shift);
+  with_unroll([&](auto uu) {
+    constexpr int U = decltype(uu)::value;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<U>, dim3(ew_blocks((nvec + U - 1) / U)), dim3(256), 0, st,
+                       static_cast<const bf16*>(dy), static_cast<const bf16*>(x), static_cast<const bf16*>(y), coef,
+                       static_cast<bf16*>(dx), static_cast<bf16*>(dres), nvec, C, relu, scale_shift);
+  });
   FFK_LAUNCH_CHECK("bn_bwd");
 }
 

@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -348,6 +350,230 @@ void axpby(int dtype, const void* x, void* y, int64_t n, float a, float b, hipSt
                        static_cast<float*>(y), n / 8, a, b);
   else throw std::invalid_argument("axpby: dtype");
   FFK_LAUNCH_CHECK("axpby");
+}
+
+// ------------------------------------------------------------ narrow Linear
+// Linear layers with a narrow output, N <= 8 (DLRM's 1-wide sigmoid head, any
+// width the 16-B-row GEMM epilogues cannot write): GEMV-shaped and bound by
+// reading X once, so no MFMA tile fits them.  W (K x N, row-major) is held in
+// LDS transposed as fp32 [N][K]; one wave per row, each lane 8 consecutive k
+// per 512-column step (16-B loads).  The activation (forward) and its
+// derivative (backward, from the saved pre-activation) are applied in the
+// same passes, so no separate element-wise kernel runs for the head.
+constexpr int kNarrowLds = 16384;   // floats: K * N <= 16384
+
+template <int N>
+__device__ __forceinline__ void narrow_stage_w(const bf16* __restrict__ w, float* wt, int K) {
+  for (int i = threadIdx.x; i < K * N; i += blockDim.x) wt[(i % N) * K + i / N] = bf2f(w[i]);
+  __syncthreads();
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void narrow_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                         const float* __restrict__ bias, bf16* __restrict__ y,
+                                                         bf16* __restrict__ pre, int M, int K, int act) {
+  __shared__ float wt[kNarrowLds];
+  narrow_stage_w<N>(w, wt, K);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int m = blockIdx.x * 4 + wv; m < M; m += gridDim.x * 4) {
+    float acc[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) acc[n] = 0.f;
+    const bf16* xr = x + static_cast<int64_t>(m) * K;
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {
+      float xv[8];
+      ld8<bf16>(xr + k0, xv);
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[n] = __builtin_fmaf(xv[j], wt[n * K + k0 + j], acc[n]);
+    }
+    float v = 0.f;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const float t = wave_sum(acc[n]);
+      if (lane == n) v = t;
+    }
+    if (lane < N) {
+      if (bias) v += bias[lane];
+      const int64_t o = static_cast<int64_t>(m) * N + lane;
+      if (pre) pre[o] = f2bf(v);
+      y[o] = f2bf(act_apply(act, v, 1.f));
+    }
+  }
+}
+
+// g[n] = dy[m, n] * act'(pre[m, n]) of one row (every lane of the wave)
+template <int N>
+__device__ __forceinline__ void narrow_row_grad(const bf16* __restrict__ dy, const bf16* __restrict__ pre, int64_t m,
+                                                int act, float* g) {
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float d = bf2f(dy[m * N + n]);
+    if (act != kIdentity) d *= act_grad(act, bf2f(pre[m * N + n]), 1.f);
+    g[n] = d;
+  }
+}
+
+// dX[m, :] = g[m, :] W^T (+ beta dX)
+template <int N>
+__global__ __launch_bounds__(256) void narrow_dgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ pre,
+                                                           const bf16* __restrict__ w, bf16* __restrict__ dx, int M,
+                                                           int K, int act, float beta) {
+  __shared__ float wt[kNarrowLds];
+  narrow_stage_w<N>(w, wt, K);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int m = blockIdx.x * 4 + wv; m < M; m += gridDim.x * 4) {
+    float g[N];
+    narrow_row_grad<N>(dy, pre, m, act, g);
+    bf16* dr = dx + static_cast<int64_t>(m) * K;
+    for (int k0 = lane * 8; k0 < K; k0 += 512) {
+      float o[8], prev[8];
+      if (beta != 0.f) ld8<bf16>(dr + k0, prev);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = beta != 0.f ? beta * prev[j] : 0.f;
+#pragma unroll
+        for (int n = 0; n < N; ++n) v = __builtin_fmaf(g[n], wt[n * K + k0 + j], v);
+        o[j] = v;
+      }
+      u16x8 pk;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pk[j] = f2u(o[j]);
+      *reinterpret_cast<u16x8*>(dr + k0) = pk;
+    }
+  }
+}
+
+// per row block b: part[b][k][n] = sum_{m in b} x[m, k] g[m, n] (k < K),
+// part[b][K][n] = sum_{m in b} g[m, n] (the bias gradient)
+template <int N>
+__global__ __launch_bounds__(256) void narrow_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                           const bf16* __restrict__ pre, float* __restrict__ part,
+                                                           int M, int K, int act, int rows) {
+  const int m0 = blockIdx.x * rows, m1 = min(M, m0 + rows);
+  float* out = part + static_cast<int64_t>(blockIdx.x) * (K + 1) * N;
+  for (int k0 = threadIdx.x * 8; k0 < K; k0 += 256 * 8) {
+    float acc[8][N];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int n = 0; n < N; ++n) acc[j][n] = 0.f;
+    for (int m = m0; m < m1; ++m) {
+      float g[N], xv[8];
+      narrow_row_grad<N>(dy, pre, m, act, g);
+      ld8<bf16>(x + static_cast<int64_t>(m) * K + k0, xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int n = 0; n < N; ++n) acc[j][n] = __builtin_fmaf(xv[j], g[n], acc[j][n]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int n = 0; n < N; ++n) out[(k0 + j) * N + n] = acc[j][n];
+  }
+  if (threadIdx.x < N) {
+    float sb = 0.f;
+    for (int m = m0; m < m1; ++m) {
+      float g[N];
+      narrow_row_grad<N>(dy, pre, m, act, g);
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+        if (n == static_cast<int>(threadIdx.x)) sb += g[n];
+    }
+    out[K * N + threadIdx.x] = sb;
+  }
+}
+
+// dW = beta dW + sum_b part[b][:K]; db += sum_b part[b][K]
+template <typename TW>
+__global__ __launch_bounds__(256) void narrow_wgrad_finish_kernel(const float* __restrict__ part, int blocks, int KN,
+                                                                  int N, TW* __restrict__ dw, float beta,
+                                                                  float* __restrict__ db) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= KN + N) return;
+  float s = 0.f;
+  for (int b = 0; b < blocks; ++b) s += part[static_cast<int64_t>(b) * (KN + N) + i];
+  if (i < KN) {
+    if (dw) {
+      const float prev = beta != 0.f ? static_cast<float>(dw[i]) * beta : 0.f;
+      dw[i] = static_cast<TW>(prev + s);
+    }
+  } else if (db) {
+    db[i - KN] += s;
+  }
+}
+
+template <typename F>
+static void narrow_dispatch(int N, const char* what, F&& f) {
+  switch (N) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    default: throw std::invalid_argument(std::string(what) + ": N must be 1..8");
+  }
+}
+
+static void narrow_check(int64_t M, int64_t K, int64_t N, const char* what) {
+  if (M <= 0 || K <= 0 || K % 8 || N < 1 || N > 8 || K * N > kNarrowLds || M > (1LL << 31) - 1)
+    throw std::invalid_argument(std::string(what) + ": shape outside the narrow-Linear kernel (K % 8, K*N <= 16384)");
+}
+
+static int narrow_grid(int64_t M) { return static_cast<int>(std::min<int64_t>((M + 3) / 4, 1024)); }
+
+void narrow_linear_fwd(const void* x, const void* w, const float* bias, void* y, void* pre, int64_t M, int64_t K,
+                       int64_t N, int act, hipStream_t st) {
+  narrow_check(M, K, N, "narrow_linear_fwd");
+  narrow_dispatch(static_cast<int>(N), "narrow_linear_fwd", [&](auto nn) {
+    hipLaunchKernelGGL(narrow_fwd_kernel<decltype(nn)::value>, dim3(narrow_grid(M)), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), static_cast<const bf16*>(w), bias, static_cast<bf16*>(y),
+                       static_cast<bf16*>(pre), static_cast<int>(M), static_cast<int>(K), act);
+  });
+  FFK_LAUNCH_CHECK("narrow_linear_fwd");
+}
+
+void narrow_linear_dgrad(const void* dy, const void* pre, const void* w, void* dx, int64_t M, int64_t K, int64_t N,
+                         int act, float beta, hipStream_t st) {
+  narrow_check(M, K, N, "narrow_linear_dgrad");
+  narrow_dispatch(static_cast<int>(N), "narrow_linear_dgrad", [&](auto nn) {
+    hipLaunchKernelGGL(narrow_dgrad_kernel<decltype(nn)::value>, dim3(narrow_grid(M)), dim3(256), 0, st,
+                       static_cast<const bf16*>(dy), static_cast<const bf16*>(pre), static_cast<const bf16*>(w),
+                       static_cast<bf16*>(dx), static_cast<int>(M), static_cast<int>(K), act, beta);
+  });
+  FFK_LAUNCH_CHECK("narrow_linear_dgrad");
+}
+
+int narrow_wgrad_blocks(int64_t M) { return static_cast<int>(std::min<int64_t>(256, (M + 31) / 32)); }
+
+void narrow_linear_wgrad(const void* x, const void* dy, const void* pre, float* part, int blocks, void* dw,
+                         int dw_dtype, float beta, float* db, int64_t M, int64_t K, int64_t N, int act,
+                         hipStream_t st) {
+  narrow_check(M, K, N, "narrow_linear_wgrad");
+  if (blocks < 1) throw std::invalid_argument("narrow_linear_wgrad: blocks");
+  const int rows = static_cast<int>((M + blocks - 1) / blocks);
+  narrow_dispatch(static_cast<int>(N), "narrow_linear_wgrad", [&](auto nn) {
+    hipLaunchKernelGGL(narrow_wgrad_kernel<decltype(nn)::value>, dim3(blocks), dim3(256), 0, st,
+                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), static_cast<const bf16*>(pre), part,
+                       static_cast<int>(M), static_cast<int>(K), act, rows);
+  });
+  FFK_LAUNCH_CHECK("narrow_linear_wgrad");
+  const int KN = static_cast<int>(K * N);
+  const int g = (KN + static_cast<int>(N) + 255) / 256;
+  if (dw_dtype == kF32 || dw == nullptr)
+    hipLaunchKernelGGL(narrow_wgrad_finish_kernel<float>, dim3(g), dim3(256), 0, st, part, blocks, KN,
+                       static_cast<int>(N), static_cast<float*>(dw), beta, db);
+  else if (dw_dtype == kBF16)
+    hipLaunchKernelGGL(narrow_wgrad_finish_kernel<bf16>, dim3(g), dim3(256), 0, st, part, blocks, KN,
+                       static_cast<int>(N), static_cast<bf16*>(dw), beta, db);
+  else
+    throw std::invalid_argument("narrow_linear_wgrad: dW dtype");
+  FFK_LAUNCH_CHECK("narrow_linear_wgrad_finish");
 }
 
 }  // namespace ffk

@@ -202,8 +202,20 @@ void topk_rows(int dtype, const void* x, void* vals, int64_t* idx, int64_t rows,
 // op: 0 +s 1 -s 2 *s 3 /s 4 pow 5 log 6 sqrt 7 rsqrt 8 sin 9 cos 10 leaky_relu 11 ceil 12 round 13 identity
 void unary_op(int dtype, const void* x, const void* dy, void* y, int64_t n, int op, float scalar, int backward,
               hipStream_t st);
+// narrow Linear (N <= 8 outputs): forward with bias + activation, input
+// gradient and weight / bias gradient with the activation derivative fused
+void narrow_linear_fwd(const void* x, const void* w, const float* bias, void* y, void* pre, int64_t M, int64_t K,
+                       int64_t N, int act, hipStream_t st);
+void narrow_linear_dgrad(const void* dy, const void* pre, const void* w, void* dx, int64_t M, int64_t K, int64_t N,
+                         int act, float beta, hipStream_t st);
+int narrow_wgrad_blocks(int64_t M);
+void narrow_linear_wgrad(const void* x, const void* dy, const void* pre, float* part, int blocks, void* dw,
+                         int dw_dtype, float beta, float* db, int64_t M, int64_t K, int64_t N, int act,
+                         hipStream_t st);
 void mse_loss(int dtype, const void* pred, const void* label, void* grad, float* metrics, int64_t n, float scale,
               hipStream_t st);
+void mse_loss_full(int dtype, int label_dtype, const void* pred, const void* label, void* grad, float* metrics,
+                   int64_t n, float scale, int full, int64_t cols, int64_t rows, hipStream_t st);
 // kind: 0 uniform[a,b) 1 normal(a,b) 2 truncated normal(a,b) in [c,d] 3 constant a
 void init_tensor(int dtype, void* out, const NdShape& piece, const NdShape& full, const NdStrides& box_lo, int kind,
                  uint64_t seed, float a, float b, float c, float d, hipStream_t st);
@@ -246,8 +258,9 @@ void conv32_wgrad(const ConvShape& cs, int groups, const void* x, const void* dy
                   hipStream_t st);
 
 // ---- bnpool.hip: BatchNorm (training) + pooling over NHWC bf16 [M][C]
-// ws (optional, 32*C floats): 16 atomic buckets -> full-grid reduction (else the grid is capped)
-void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws = nullptr);
+// ws (optional, 32*C floats): 16 atomic buckets -> full-grid reduction (else the grid is capped);
+// ws_clean: ws is zero on entry and is left zero (a persistent workspace: no memset per call)
+void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws = nullptr, int ws_clean = 0);
 void bn_finalize(const float* stats, const void* gamma, const void* beta, int param_dtype, float* running_mean,
                  float* running_var, float* scale, float* shift, float* mean, float* rstd, int C, double count,
                  float momentum, float eps, hipStream_t st);
@@ -259,7 +272,7 @@ void bn_apply(const void* x, const void* residual, const float* scale, const flo
 // scale_shift ([2][C]: scale, shift) — y is not read
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
-            int relu, hipStream_t st, const float* scale_shift = nullptr);
+            int relu, hipStream_t st, const float* scale_shift = nullptr, int ws_clean = 0);
 struct PoolShape {
   int N = 0, H = 0, W = 0, C = 0, R = 1, S = 1, sh = 1, sw = 1, ph = 0, pw = 0;
   int avg = 0, count_pad = 0;

@@ -341,15 +341,18 @@ __global__ __launch_bounds__(256) void unary_kernel(const T* __restrict__ x, con
 }
 
 // ------------------------------------------------------------------- MSE
-// grad = scale * (p - y); metrics[0] += sum (p-y)^2, metrics[1] += sum |p-y|,
-// metrics[2] += count (rows)
-template <typename T>
-__global__ __launch_bounds__(256) void mse_kernel(const T* __restrict__ p, const T* __restrict__ y,
+// grad = scale * (p - y); metrics[0] += sum (p-y)^2, metrics[1] += sum |p-y|
+// (``full``: the loss-metrics block of ops/loss.py, slots loss 0, count 2,
+// squared error 3, absolute error 4: loss += sum (p-y)^2 / C, count += rows,
+// so no element-wise torch kernels run around the loss).  Labels may be fp32
+// or the prediction's dtype.
+template <typename T, typename L>
+__global__ __launch_bounds__(256) void mse_kernel(const T* __restrict__ p, const L* __restrict__ y,
                                                   T* __restrict__ grad, float* __restrict__ metrics, int64_t n,
-                                                  float scale) {
+                                                  float scale, int full, float inv_c, float rows) {
   float se = 0.f, ae = 0.f;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
-    const float d = ld<T>(p + i) - ld<T>(y + i);
+    const float d = ld<T>(p + i) - static_cast<float>(y[i]);
     se += d * d;
     ae += fabsf(d);
     if (grad) st<T>(grad + i, scale * d);
@@ -358,8 +361,15 @@ __global__ __launch_bounds__(256) void mse_kernel(const T* __restrict__ p, const
   se = block_sum<256>(se, red);
   ae = block_sum<256>(ae, red + 4);
   if (threadIdx.x == 0 && metrics) {
-    atomicAdd(metrics + 0, se);
-    atomicAdd(metrics + 1, ae);
+    if (full) {
+      atomicAdd(metrics + 0, se * inv_c);
+      if (blockIdx.x == 0) atomicAdd(metrics + 2, rows);
+      atomicAdd(metrics + 3, se);
+      atomicAdd(metrics + 4, ae);
+    } else {
+      atomicAdd(metrics + 0, se);
+      atomicAdd(metrics + 1, ae);
+    }
   }
 }
 
@@ -612,11 +622,23 @@ void unary_op(int dtype, const void* x, const void* dy, void* y, int64_t n, int 
 
 void mse_loss(int dtype, const void* pred, const void* label, void* grad, float* metrics, int64_t n, float scale,
               hipStream_t st) {
+  mse_loss_full(dtype, dtype, pred, label, grad, metrics, n, scale, 0, 1, 0, st);
+}
+
+void mse_loss_full(int dtype, int label_dtype, const void* pred, const void* label, void* grad, float* metrics,
+                   int64_t n, float scale, int full, int64_t cols, int64_t rows, hipStream_t st) {
   if (n == 0) return;
   by_dtype(dtype, "mse", [&](auto t) {
     using T = decltype(t);
-    hipLaunchKernelGGL(mse_kernel<T>, dim3(std::min(grid1(n), 1024)), dim3(256), 0, st, static_cast<const T*>(pred),
-                       static_cast<const T*>(label), static_cast<T*>(grad), metrics, n, scale);
+    auto go = [&](auto l) {
+      using L = decltype(l);
+      hipLaunchKernelGGL((mse_kernel<T, L>), dim3(std::min(grid1(n), 1024)), dim3(256), 0, st,
+                         static_cast<const T*>(pred), static_cast<const L*>(label), static_cast<T*>(grad), metrics, n,
+                         scale, full, 1.f / static_cast<float>(std::max<int64_t>(cols, 1)), static_cast<float>(rows));
+    };
+    if (label_dtype == dtype) go(T{});
+    else if (label_dtype == kF32) go(float{});
+    else throw std::invalid_argument("mse: label dtype");
   });
   FFK_LAUNCH_CHECK("mse");
 }

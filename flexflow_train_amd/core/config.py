@@ -30,7 +30,7 @@ class FFConfig:
     profiling: bool = False
     perform_fusion: bool = True
     search_budget: int = -1
-    search_time_limit: float = 60.0    # seconds for the whole strategy search (MCMC + Unity)
+    search_time_limit: float = 45.0    # seconds for the whole strategy search (MCMC + Unity + mapping)
     search_alpha: float = 1.2
     search_overlap_backward_update: bool = True
     only_data_parallel: bool = False

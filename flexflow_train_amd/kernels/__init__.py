@@ -15,7 +15,7 @@ import collections
 import importlib
 import math
 import os
-from typing import Optional
+from typing import Dict, Optional
 
 import torch
 
@@ -78,7 +78,7 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-def _check(t: torch.Tensor, name: str, dtype=None, numel=None):
+def _check(t: torch.Tensor, name: str, dtype=None, numel=None, aligned: bool = True):
     if not t.is_cuda:
         raise ValueError(f"{name}: expected a GPU tensor")
     if not t.is_contiguous():
@@ -87,7 +87,7 @@ def _check(t: torch.Tensor, name: str, dtype=None, numel=None):
         raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
     if numel is not None and t.numel() != numel:
         raise ValueError(f"{name}: expected {numel} elements, got {t.numel()}")
-    if t.data_ptr() % 16:
+    if aligned and t.data_ptr() % 16:
         raise ValueError(f"{name}: data pointer must be 16-byte aligned")
 
 
@@ -828,6 +828,83 @@ def mse(pred, label, grad=None, metrics=None, scale: float = 1.0):
     return grad
 
 
+def mse_full(pred, label, grad, metrics, scale: float, cols: int, rows: int):
+    """grad = scale * (pred - label) and the loss-metrics block updated in the
+    same pass (loss += sq err / cols, count += rows, sq / abs error sums);
+    ``label`` fp32 or pred's dtype."""
+    if label.dtype not in (pred.dtype, torch.float32) or label.numel() != pred.numel():
+        raise ValueError("mse: label must match pred (same numel, pred dtype or fp32)")
+    _check(metrics, "metrics", torch.float32, None, aligned=False)
+    if metrics.numel() < 5:
+        raise ValueError("mse: the metrics block needs 5 slots")
+    ext().mse_loss_full(_dt(pred), _dt(label), pred.data_ptr(), label.data_ptr(), _p(grad), metrics.data_ptr(),
+                        pred.numel(), float(scale), 1, int(cols), int(rows), _stream())
+    STATS["mse"] += 1
+    return grad
+
+
+def narrow_ok(x, w) -> bool:
+    """The narrow-Linear kernels' shapes: bf16, N <= 8, K % 8, K * N <= 16384."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and available()):
+        return False
+    K, N = w.shape
+    return (x.dim() == 2 and x.shape[1] == K and 1 <= N <= 8 and K % 8 == 0 and K * N <= 16384 and x.is_contiguous()
+            and w.is_contiguous() and x.data_ptr() % 16 == 0)
+
+
+def narrow_linear_fwd(x, w, bias=None, act: str = "none", pre=None):
+    """y = act(x @ w + bias) for a narrow w [K, N <= 8]; ``pre`` (optional,
+    [M, N] bf16) receives the pre-activation."""
+    if not narrow_ok(x, w):
+        raise ValueError("narrow_linear_fwd: unsupported shapes / dtypes")
+    M, N = x.shape[0], w.shape[1]
+    y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    if bias is not None:
+        bias = bias.float().contiguous()
+    if pre is not None:
+        _check(pre, "pre", x.dtype, M * N, aligned=False)
+    ext().narrow_linear_fwd(x.data_ptr(), w.data_ptr(), _p(bias), y.data_ptr(), _p(pre), M, w.shape[0], N,
+                            ACT_CODES[act], _stream())
+    STATS["narrow_linear"] += 1
+    return y
+
+
+def narrow_linear_bwd(x, w, dy, pre=None, act: str = "none", dw=None, wbeta: float = 0.0, db=None, dx=None,
+                      dx_beta: float = 0.0, need_dx: bool = True):
+    """Backward of ``narrow_linear_fwd``: g = dy * act'(pre); dw = wbeta dw +
+    x^T g (fp32 or bf16), db += colsum(g) (fp32), dx = g w^T (+ dx_beta dx).
+    Returns dx (None when not needed)."""
+    M, K, N = x.shape[0], w.shape[0], w.shape[1]
+    if not narrow_ok(x, w) or dy.shape != (M, N) or dy.dtype != torch.bfloat16 or not dy.is_contiguous():
+        raise ValueError("narrow_linear_bwd: unsupported shapes / dtypes")
+    if act != "none":
+        if pre is None:
+            raise ValueError("narrow_linear_bwd: an activation needs the saved pre-activation")
+        _check(pre, "pre", torch.bfloat16, M * N, aligned=False)
+    if db is not None:
+        _check(db, "db", torch.float32, N, aligned=False)
+    code = ACT_CODES[act]
+    st = _stream()
+    if dw is not None or db is not None:
+        if dw is not None and (tuple(dw.shape) != (K, N) or not dw.is_contiguous()
+                               or dw.dtype not in (torch.float32, torch.bfloat16)):
+            raise ValueError("narrow_linear_bwd: dW must be a contiguous [K, N] fp32 / bf16 tensor")
+        blocks = int(ext().narrow_wgrad_blocks(M))
+        part = torch.empty(blocks * (K + 1) * N, device=x.device, dtype=torch.float32)
+        ext().narrow_linear_wgrad(x.data_ptr(), dy.data_ptr(), _p(pre), part.data_ptr(), blocks, _p(dw),
+                                  _dt(dw) if dw is not None else 0, float(wbeta), _p(db), M, K, N, code, st)
+    if not need_dx:
+        return None
+    if dx is None:
+        dx = torch.empty(M, K, device=x.device, dtype=x.dtype)
+        dx_beta = 0.0
+    else:
+        _check(dx, "dx", torch.bfloat16, M * K)
+    ext().narrow_linear_dgrad(dy.data_ptr(), _p(pre), w.data_ptr(), dx.data_ptr(), M, K, N, code, float(dx_beta), st)
+    STATS["narrow_linear"] += 1
+    return dx
+
+
 INIT_KINDS = {"uniform": 0, "normal": 1, "truncated_normal": 2, "constant": 3}
 
 
@@ -1080,12 +1157,31 @@ def conv32_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups:
     STATS["conv32_wgrad"] += 1
 
 
+_BN_WS: Dict[tuple, torch.Tensor] = {}
+
+
+def _bn_workspace(dev, C: int):
+    """(workspace of 35 C floats, clean): a persistent per-(device, stream, C)
+    buffer whose 16 atomic buckets start zero and are left zero by the kernel
+    that consumes them (bn_fold_buckets / bn_bwd_coef), so no memset runs per
+    call.  Inside a graph capture a first use gets a per-call buffer instead
+    (zeroed by the launcher)."""
+    key = (dev, _stream(), C)
+    ws = _BN_WS.get(key)
+    if ws is not None:
+        return ws, 1
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(35 * C, device=dev, dtype=torch.float32), 0
+    ws = _BN_WS[key] = torch.zeros(35 * C, device=dev, dtype=torch.float32)
+    return ws, 1
+
+
 def bn_stats(x, stats):
     _check_nhwc(x, "x")
     C = x.shape[1]
     _check(stats, "stats", torch.float32, 2 * C)
-    ws = torch.empty(32 * C, device=x.device, dtype=torch.float32)
-    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream(), _p(ws))
+    ws, clean = _bn_workspace(x.device, C)
+    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream(), _p(ws), clean)
     STATS["bn_stats"] += 1
 
 
@@ -1144,10 +1240,10 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, wan
     pdt = _dt(gamma) if gamma is not None else DT_BF16
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     dres = torch.empty_like(x, memory_format=torch.channels_last) if want_masked else None
-    ws = torch.empty(35 * C, device=x.device, dtype=torch.float32)
+    ws, clean = _bn_workspace(x.device, C)
     ext().bn_bwd(_p(dy), _p(x), _p(y if relu_code == 1 else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx),
                  _p(dres), _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, relu_code, _stream(),
-                 _p(scale_shift if relu_code == 2 else None))
+                 _p(scale_shift if relu_code == 2 else None), clean)
     STATS["bn_bwd"] += 1
     return dx, dres
 

@@ -40,7 +40,13 @@ class LinearOp(OpImpl):
         x2 = x.reshape(-1, x.shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
-        if x2.is_cuda and x2.dtype in (torch.bfloat16, torch.float32):
+        if x2.is_cuda and W.shape[1] <= 8 and K.narrow_ok(x2, W if W.dtype == x2.dtype else W.to(x2.dtype)):
+            # narrow head (N <= 8, e.g. DLRM's sigmoid output): GEMV-shaped
+            # kernel with bias + activation fused (elementwise.hip narrow_*)
+            Wc = W if W.dtype == x2.dtype else W.to(x2.dtype)
+            pre = torch.empty(x2.shape[0], W.shape[1], device=x2.device, dtype=x2.dtype) if act != "none" else None
+            y = K.narrow_linear_fwd(x2, Wc, bias=b, act=act, pre=pre)
+        elif x2.is_cuda and x2.dtype in (torch.bfloat16, torch.float32):
             # bf16: the autotuned MFMA GEMMs; fp32: the exact-fp32 MFMA kernel
             # (igemm32.hip) -- no library GEMM either way
             Wc = W if W.dtype == x2.dtype else W.to(x2.dtype)
@@ -72,6 +78,22 @@ class LinearOp(OpImpl):
             # the consumer's dX GEMM already applied act' and accumulated db (gemmp epilogue)
             act = "none"
             db = None
+        Wb = W if W.dtype == torch.bfloat16 else None
+        if (dy2.is_cuda and dy2.dtype == torch.bfloat16 and W.shape[1] <= 8 and Wb is not None
+                and K.narrow_ok(x2, Wb) and (pre is None or pre.dtype == torch.bfloat16)
+                and (dW is None or dW.dtype in (torch.float32, torch.bfloat16))):
+            # narrow head: weight / bias / input gradients with act' fused, no
+            # separate activation-gradient or column-sum pass
+            ctx.extra.pop("dact", None)
+            acc = ctx.extra.get("grad_acc", [None])[0] if need_input_grad[0] else None
+            acc_ok = acc is not None and acc.is_cuda and acc.dtype == torch.bfloat16 and acc.is_contiguous()
+            dx = K.narrow_linear_bwd(x2, Wb, dy2, pre=pre, act=act, dw=dW,
+                                     wbeta=ctx.extra.get("wgrad_beta", [1.0])[0], db=db,
+                                     dx=acc.view(-1, W.shape[0]) if acc_ok else None, dx_beta=1.0 if acc_ok else 0.0,
+                                     need_dx=bool(need_input_grad[0]))
+            if acc_ok:
+                return [acc]
+            return [dx.reshape(*dy.shape[:-1], W.shape[0]) if dx is not None else None]
         if (dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float32) and K.available() and dy2.shape[1] % 8 == 0
                 and (pre is None or pre.dtype == dy2.dtype)):
             if act != "none":

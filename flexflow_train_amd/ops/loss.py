@@ -105,14 +105,13 @@ class LossFunction:
             s = (2.0 / (self.global_rows * C)) if lt == "mean_squared_error" else 2.0
             y = labels.reshape(logits.shape)
             if (K.tensorop_ok(logits) and metrics.dtype == torch.float32 and metrics.is_cuda
-                    and logits.numel() > 0):
-                # fused HIP pass: grad + squared/absolute error sums (slots 3,4 adjacent)
-                y = y.to(logits.dtype).contiguous()
+                    and metrics.is_contiguous() and logits.numel() > 0):
+                # one HIP pass: the gradient and every metric slot (loss,
+                # count, squared / absolute error); fp32 labels read as they are
+                if y.dtype not in (logits.dtype, torch.float32):
+                    y = y.float()
                 g = torch.empty_like(logits)
-                before = metrics[M_SQERR].clone()
-                K.mse(logits.contiguous(), y, g, metrics[M_SQERR:], s)
-                metrics[M_LOSS] += (metrics[M_SQERR] - before) / C
-                metrics[M_COUNT] += rows
+                K.mse_full(logits.contiguous(), y.contiguous(), g, metrics, s, C, rows)
                 return g
             p = logits.float()
             y = labels.reshape(p.shape).float()

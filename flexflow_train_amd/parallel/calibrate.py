@@ -205,6 +205,18 @@ def calibrate_for_step(ex, iters: int = 5, timer: Optional[Callable] = None) -> 
     "spec_calibrated", "comparison"} (spec_* as MachineSpecification)."""
     from ..search.native import machine_spec
     sizes_used = step_message_sizes(ex)
+    if timer is None:
+        # every rank must issue the same collectives at the same sizes: the
+        # union over ranks (redistribution messages differ from rank to rank)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            everyone = [None] * dist.get_world_size()
+            dist.all_gather_object(everyone, sizes_used)
+            merged: Dict[str, set] = {}
+            for d in everyone:
+                for k, v in (d or {}).items():
+                    merged.setdefault(k, set()).update(v)
+            sizes_used = {k: sorted(v) for k, v in merged.items()}
     sizes = {k: _sample_sizes(sizes_used.get(k, [])) for k in KINDS}
     samples = measure(ex.dist, sizes, ex.cfg.device, iters=iters, timer=timer)
     fits = fit(samples)

@@ -48,7 +48,7 @@ def _search_local(cg, ffconfig, world: int):
         "world": world,
         "budget": budget,
         "alpha": float(ffconfig.search_alpha),
-        "time_limit": float(getattr(ffconfig, "search_time_limit", 60.0)),
+        "time_limit": float(getattr(ffconfig, "search_time_limit", 45.0)),
         "enable_parameter_parallel": True,
         "enable_attribute_parallel": bool(ffconfig.enable_attribute_parallel),
         "seed": int(ffconfig.seed) & 0x7FFFFFFF,

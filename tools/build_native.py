@@ -140,8 +140,23 @@ def write_ninja(targets: list[str]) -> str:
                   "  description = CC $out"]
         ro = os.path.join("obj", "ffi", "flexflow_runtime_c.cc.o")
         lines.append(f"build {ro}: cxx {os.path.join(ROOT, 'csrc', 'ffi', 'flexflow_runtime_c.cc')}")
+        # the GPU backing (csrc/ffdev) and the kernel objects it calls (not the
+        # pybind bindings): the C API trains on the GPU when one is visible
+        do = os.path.join("obj", "ffdev", "device_exec.cpp.o")
+        lines.append(f"build {do}: hip {os.path.join(ROOT, 'csrc', 'ffdev', 'device_exec.cpp')}")
+        lines.append(f"  hip_flags = $hip_flags {core_inc}")
+        kobjs = []
+        for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip"))):
+            o = os.path.join("obj", "kernels", os.path.basename(s) + ".o")
+            if "kernels" not in targets:
+                lines.append(f"build {o}: hip {s}")
+            kobjs.append(o)
+        lines += ["rule link_hip_so",
+                  f"  command = $hipcc -shared --offload-arch={ARCH} -o $out $in -L{os.path.join(ROCM, 'lib')} "
+                  "-lhipblaslt -lpthread",
+                  "  description = LINK $out"]
         rlib = os.path.join(PKG, "lib", "libflexflow_runtime_c.so")
-        lines.append(f"build {rlib}: link_so {ro} {' '.join(core_objs)}")
+        lines.append(f"build {rlib}: link_hip_so {ro} {do} {' '.join(core_objs)} {' '.join(kobjs)}")
         rexe = os.path.join(ROOT, "bin", "ffc-runtime-c-test")
         lines.append(f"build {rexe}: cc_rt_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_runtime_c.c')} | {rlib}")
         defaults += [rlib, rexe]

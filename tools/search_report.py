@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--configs", default=",".join(CONFIGS))
     ap.add_argument("--worlds", default="4,8")
     ap.add_argument("--budget", type=int, default=400)
+    ap.add_argument("--micro-batches", type=int, default=1,
+                    help="micro-batches per step: pipeline-parallel candidates priced at this count")
     ap.add_argument("--calibrate", default="", help="directory with op_costs_*.json + bench_<config>.json: "
                     "simulated vs measured 1-GPU step time of the bench configs")
     ap.add_argument("--out", default="")
@@ -130,6 +132,7 @@ def main():
             cfg = FFConfig()
             cfg.batch_size = bpg * world
             cfg.search_budget = args.budget
+            cfg.micro_batches = args.micro_batches
             m = FFModel(cfg)
             build(m, bpg * world)
             t0 = time.time()
@@ -139,6 +142,8 @@ def main():
                               "searched_ms": round(1000 * rep["cost"], 3),
                               "predicted_speedup_over_dp": round(rep["predicted_speedup_over_dp"], 3),
                               "algorithm": rep.get("algorithm"), "search_s": round(time.time() - t0, 1),
+                              "micro_batches": args.micro_batches, "pipeline_stages": rep.get("pipeline_stages"),
+                              "mapped_states": rep.get("mapped_states"),
                               "views": len(views), "layer_degrees": layer_kinds(pcg)}), flush=True)
 
 
