@@ -197,6 +197,24 @@ def _release(res):
         torch.cuda.empty_cache()
 
 
+def _memory_record(model, ex, world, bytes_per_param=16.0):
+    """This rank's liveness memory plan of the step (csrc/ffcore/src/
+    memory_plan.cc) next to the allocator's measured peak, GB."""
+    import torch
+    try:
+        from flexflow_train_amd.search import native
+        plans = native.plan_memory(model.pcg, world, model.views, weight_bytes_per_param=bytes_per_param)
+        p = plans[min(ex.dist.rank, len(plans) - 1)]
+        rec = {"planned_arena_gb": round(p["arena_bytes"] / 1e9, 2),
+               "planned_peak_live_gb": round(p["peak_live_bytes"] / 1e9, 2),
+               "per_op_sum_gb": round(p["naive_bytes"] / 1e9, 2)}
+    except Exception as e:  # noqa: BLE001 -- the record must not cost the run
+        rec = {"plan_error": f"{type(e).__name__}: {e}"[:160]}
+    if ex.cfg.device.type == "cuda":
+        rec["measured_peak_gb"] = round(torch.cuda.max_memory_allocated(ex.cfg.device) / 1e9, 2)
+    return rec
+
+
 def _time_steps(args, ex, feeds, labels, global_batch):
     """W untimed warm-up steps, then EXACTLY K timed steps bracketed by a
     barrier + device synchronisation on both sides; max over ranks."""
@@ -300,6 +318,7 @@ def _run_bert(args, world, rank, only_dp: bool):
         "gemm_choices": dict(collections.Counter(gemm_choices().values())),
         "tokens_per_sec": round(t["value"] * args.seq, 1),
         "final_loss": round(pm.loss, 4),
+        "memory": _memory_record(model, ex, world),
     }
     prof = None
     if args.profile:
@@ -431,7 +450,8 @@ def _run_zoo(args, world, rank, only_dp: bool):
     conf = {"model": args.model, "global_batch": global_batch, "parallelism": _parallelism(model, world),
             "strategy_source": model.search_report.get("source", ""), "optimizer": opt,
             "compile_s": round(compile_s, 2), "hipgraph": t["graphed"],
-            "graph_segments": list(getattr(ex, "graph_segments", ())) or None, "final_loss": round(pm.loss, 4)}
+            "graph_segments": list(getattr(ex, "graph_segments", ())) or None, "final_loss": round(pm.loss, 4),
+            "memory": _memory_record(model, ex, world, 16.0 if opt == "adam" else 8.0)}
     conf.update(extra)
     if zname == "gpt":
         conf["tokens_per_sec"] = round(t["value"] * mcfg.sequence_length, 1)

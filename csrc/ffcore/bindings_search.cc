@@ -9,6 +9,7 @@
 
 #include "bindings_ext.h"
 #include "ff/mapping.h"
+#include "ff/memory_plan.h"
 #include "ff/network.h"
 #include "ff/models.h"
 #include "ff/parallelize.h"
@@ -314,6 +315,19 @@ void register_ext_bindings(py::module_& m) {
     auto r = convert_parallel_shape(p, v, t, &n);
     return py::make_tuple(r, n);
   });
+
+  // ---- liveness memory plan (ff/memory_plan.h): JSON list, one per device
+  m.def("plan_memory", [](const ParallelComputationGraph& p, const std::map<int, std::vector<int>>& views, int world,
+                          bool training, double weight_bytes_per_param, bool with_blocks) {
+    MemoryPlanConfig c;
+    c.training = training;
+    c.weight_bytes_per_param = weight_bytes_per_param;
+    Json a = Json::array();
+    for (auto const& pl : plan_memory(p, std::map<int, Placement>(views.begin(), views.end()), world, c))
+      a.push_back(pl.to_json(with_blocks));
+    return a.dump();
+  }, py::arg("pcg"), py::arg("views") = std::map<int, std::vector<int>>{}, py::arg("world") = 1,
+        py::arg("training") = true, py::arg("weight_bytes_per_param") = 16.0, py::arg("with_blocks") = false);
 
   // ---- simulator
   m.def("simulate", [](const ParallelComputationGraph& p, const CostModel& cm, const std::string& sim_cfg,

@@ -86,6 +86,7 @@ struct SearchResult {
   int pipeline_stages = 0;               // > 0: the pipeline plan won (views = stage blocks)
   int micro_batches = 1;                 // costs are per micro-batch of a step of this many
   Json pipeline = Json::array();         // every pipeline candidate priced
+  Json memory_plan;                      // liveness memory plan of the winner (max over devices)
   Json to_json(const ComputationGraph* cg = nullptr) const;
 };
 

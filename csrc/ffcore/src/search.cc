@@ -1,4 +1,5 @@
 #include "ff/search.h"
+#include "ff/memory_plan.h"
 
 #include <chrono>
 #include <cstdio>
@@ -43,6 +44,7 @@ Json SearchResult::to_json(const ComputationGraph* cg) const {
   j["micro_batches"] = static_cast<int64_t>(micro_batches);
   if (pipeline_stages > 0) j["pipeline_stages"] = static_cast<int64_t>(pipeline_stages);
   if (!pipeline.as_array().empty()) j["pipeline_candidates"] = pipeline;
+  if (memory_plan.is_object()) j["memory_plan"] = memory_plan;
   if (cg && !strategy.empty()) j["strategy"] = strategy_to_json(*cg, strategy);
   Json v = Json::object();
   for (auto const& kv : views) v[std::to_string(kv.first)] = Json(std::vector<int64_t>(kv.second.begin(), kv.second.end()));
@@ -388,6 +390,26 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
       }
     } catch (const FFError&) {
     }
+  }
+  // liveness memory plan of the winner: the busiest device's arena
+  try {
+    auto plans = plan_memory(best.pcg, best.views, cfg.world);
+    Json mp = Json::object();
+    double arena = 0, live = 0, weights = 0, naive = 0;
+    for (auto const& p : plans) {
+      arena = std::max(arena, p.arena_bytes);
+      live = std::max(live, p.peak_live_bytes);
+      weights = std::max(weights, p.weight_bytes);
+      naive = std::max(naive, p.naive_bytes);
+    }
+    mp["arena_bytes"] = arena;
+    mp["peak_live_bytes"] = live;
+    mp["weight_bytes"] = weights;
+    mp["naive_bytes"] = naive;
+    mp["devices"] = static_cast<int64_t>(plans.size());
+    mp["fits_hbm"] = arena <= cm.spec().hbm_capacity;
+    best.memory_plan = mp;
+  } catch (const FFError&) {
   }
   best.elapsed = now_s() - t0;
   return best;

@@ -451,21 +451,23 @@ __global__ void bn_fold_buckets_kernel(float* __restrict__ ws, float* __restrict
 }
 
 // rows / vectors per thread and iteration of the reduction and apply passes
-// (FFK_BN_UNROLL: 1, 2 or 4; read once)
+// (FFK_BN_UNROLL: 1, 2 or 4; read once).  1 measured fastest: 5.2-5.6 TB/s
+// at the ResNet-50 layer-1 shapes, 2 and 4 up to 8 % slower, ResNet-50
+// 8143 vs 7950 img/s (profiles/r5/bench_bn_unroll_r5.txt)
 static int bn_unroll() {
   static const int u = [] {
     const char* e = getenv("FFK_BN_UNROLL");
-    const int v = e ? atoi(e) : 4;
-    return v == 1 || v == 2 ? v : 4;
+    const int v = e ? atoi(e) : 1;
+    return v == 2 || v == 4 ? v : 1;
   }();
   return u;
 }
 template <typename F>
 static void with_unroll(F&& f) {
   switch (bn_unroll()) {
-    case 1: f(std::integral_constant<int, 1>{}); break;
     case 2: f(std::integral_constant<int, 2>{}); break;
-    default: f(std::integral_constant<int, 4>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    default: f(std::integral_constant<int, 1>{}); break;
   }
 }
 

@@ -549,7 +549,7 @@ void narrow_linear_dgrad(const void* dy, const void* pre, const void* w, void* d
   FFK_LAUNCH_CHECK("narrow_linear_dgrad");
 }
 
-int narrow_wgrad_blocks(int64_t M) { return static_cast<int>(std::min<int64_t>(256, (M + 31) / 32)); }
+int narrow_wgrad_blocks(int64_t M) { return static_cast<int>(std::min<int64_t>(256, (M + 7) / 8)); }
 
 void narrow_linear_wgrad(const void* x, const void* dy, const void* pre, float* part, int blocks, void* dw,
                          int dw_dtype, float beta, float* db, int64_t M, int64_t K, int64_t N, int act,

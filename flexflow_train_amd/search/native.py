@@ -92,6 +92,15 @@ def sim_config(ffconfig=None, world: int = 1) -> dict:
     return cfg
 
 
+def plan_memory(pcg, world: int = 1, views: Optional[Dict[int, Sequence[int]]] = None, training: bool = True,
+                weight_bytes_per_param: float = 16.0, with_blocks: bool = False):
+    """Liveness-based memory plan of one step per device
+    (csrc/ffcore/src/memory_plan.cc): [{device, weight_bytes,
+    peak_live_bytes, arena_bytes, naive_bytes, [blocks]}]."""
+    return json.loads(C.plan_memory(pcg, {int(k): [int(d) for d in v] for k, v in (views or {}).items()}, int(world),
+                                    bool(training), float(weight_bytes_per_param), bool(with_blocks)))
+
+
 def simulate(pcg, cm, world: int, views: Optional[Dict[int, Sequence[int]]] = None, dot: bool = False,
              network=None, **sim_kw):
     """Simulated iteration; ``views``: PCG node -> placement (device list in

@@ -4,7 +4,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r5g06; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_narrow_gpu.py tests/test_conv_gpu.py > $O/tests.txt 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_narrow_gpu.py tests/test_conv_gpu.py tests/test_runtime_c_gpu.py > $O/tests.txt 2>&1
 rc=$?; tail -15 $O/tests.txt; [ $rc -eq 0 ] || exit $rc
 for U in 1 2 4; do
   FFK_BN_UNROLL=$U timeout -k 10 200 python tools/bench_bn.py > $O/bench_bn_u$U.jsonl 2>&1 || { tail -5 $O/bench_bn_u$U.jsonl; exit 1; }

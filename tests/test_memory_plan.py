@@ -1,0 +1,66 @@
+"""Liveness-based memory plan (csrc/ffcore/src/memory_plan.cc): activations
+live from their forward to their producer's backward, gradients from the
+first consumer's backward to the producer's, weights + optimizer state all
+step; the arena packs blocks whose lifetimes overlap into disjoint bytes."""
+import json
+
+from flexflow_train_amd import _ffcore as C
+from flexflow_train_amd.core import ActiMode, DataType, FFConfig, FFModel
+from flexflow_train_amd.search import native
+
+
+def _mlp(batch=64, width=512, layers=6):
+    m = FFModel(FFConfig())
+    t = m.create_tensor([batch, width], DataType.DT_FLOAT, name="x")
+    for i in range(layers):
+        t = m.dense(t, width, ActiMode.AC_MODE_RELU, name=f"fc{i}")
+    m.softmax(m.dense(t, 10, name="out"), name="sm")
+    return m
+
+
+def test_plan_invariants_one_device():
+    m = _mlp()
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    (p,) = native.plan_memory(pcg, 1, with_blocks=True)
+    assert p["weight_bytes"] > 0
+    assert p["weight_bytes"] <= p["peak_live_bytes"] <= p["arena_bytes"] <= p["naive_bytes"] + 256 * p["num_blocks"]
+    blocks = p["blocks"]
+    # no two blocks alive at the same step share a byte
+    for i, a in enumerate(blocks):
+        for b in blocks[i + 1:]:
+            if a["start"] <= b["end"] and b["start"] <= a["end"]:
+                assert a["offset"] + a["bytes"] <= b["offset"] or b["offset"] + b["bytes"] <= a["offset"], (a, b)
+    # gradients reuse the bytes of activations that died: the arena is below
+    # the sum of every block
+    assert p["arena_bytes"] < p["naive_bytes"]
+
+
+def test_inference_plan_is_smaller():
+    m = _mlp()
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    (train,) = native.plan_memory(pcg, 1, training=True)
+    (infer,) = native.plan_memory(pcg, 1, training=False)
+    assert infer["arena_bytes"] < train["arena_bytes"]
+    assert infer["peak_live_bytes"] - infer["weight_bytes"] < train["peak_live_bytes"] - train["weight_bytes"]
+
+
+def test_data_parallel_halves_activations_not_weights():
+    m = _mlp(batch=128)
+    (one,) = native.plan_memory(C.data_parallel_pcg(m.cg, 1), 1)
+    two = native.plan_memory(C.data_parallel_pcg(m.cg, 2), 2)
+    assert len(two) == 2
+    for p in two:
+        assert abs(p["weight_bytes"] - one["weight_bytes"]) < 1e-6 * one["weight_bytes"]
+        act_one = one["peak_live_bytes"] - one["weight_bytes"]
+        act_two = p["peak_live_bytes"] - p["weight_bytes"]
+        # about half (the unpartitioned input and its partition op stay whole)
+        assert 0.4 * act_one < act_two < 0.7 * act_one, (act_one, act_two)
+
+
+def test_search_report_carries_memory_plan():
+    m = _mlp()
+    cm = native.cost_model(use_profiles=False)
+    _, rep, _ = C.graph_optimize(m.cg, cm, json.dumps({"world": 2, "budget": 4, "time_limit": 10}))
+    rep = json.loads(rep)
+    mp = rep["memory_plan"]
+    assert mp["arena_bytes"] >= mp["peak_live_bytes"] > 0 and mp["devices"] == 2

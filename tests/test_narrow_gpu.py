@@ -36,14 +36,17 @@ def test_narrow_linear_matches_fp32(N, act):
     dx = K.narrow_linear_bwd(x, w, dy, pre=pre, act=act, dw=dw, wbeta=0.0, db=db)
     assert _rel(dx, xf.grad) < 5e-3
     assert _rel(dw, wf.grad) < 5e-3
-    assert _rel(db - 1.0, bf.grad) < 5e-3
+    # db of a 1-wide head is ONE sum of 1000 random-sign terms, each from the
+    # bf16-rounded pre-activation: a cancelling sum, looser bound
+    assert _rel(db - 1.0, bf.grad) < 2e-2
     # accumulate forms: dW += , dX +=
     dw2 = dw.clone()
     acc = torch.randn(M, Kd, device="cuda").bfloat16()
     acc0 = acc.float().clone()
     K.narrow_linear_bwd(x, w, dy, pre=pre, act=act, dw=dw2, wbeta=1.0, dx=acc, dx_beta=1.0)
     assert _rel(dw2, 2 * wf.grad) < 5e-3
-    assert _rel(acc.float() - acc0, xf.grad) < 2e-2
+    # one bf16 rounding of (old + g W^T), computed in fp32
+    assert _rel(acc.float(), acc0 + xf.grad) < 5e-3
 
 
 def test_mse_full_metrics():

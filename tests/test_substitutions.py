@@ -153,7 +153,9 @@ def test_unity_rewrites_beat_mcmc_alone():
     corpus rules that fuse under parallel operators) can."""
     cg = _relu_chain()
     cm = native.cost_model()
-    cfg = {"world": 2, "budget": 12, "time_limit": 60, "seed": 3, "substitution_path": BUNDLED}
+    # pipeline candidates off: this checks the rewrites (a 2-stage split of
+    # this sync-bound chain would win on its own)
+    cfg = {"world": 2, "budget": 12, "time_limit": 60, "seed": 3, "substitution_path": BUNDLED, "pipeline": False}
     _, mrep, _ = C.mcmc_search(cg, cm, json.dumps(cfg))
     pcg, rep, _ = C.graph_optimize(cg, cm, json.dumps(cfg))
     mrep, rep = json.loads(mrep), json.loads(rep)
