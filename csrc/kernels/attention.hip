@@ -55,7 +55,26 @@ struct AttnParams {
   float scale_log2;  // scale * log2(e)
   float inv_scale_log2;  // 1 / scale_log2 (no IEEE divide in the loops)
   int prio;          // raise wave priority around MFMA clusters (FFK_ATTN_PRIO; guide T5)
+  int xcd;           // XCD-local head order of non-causal grids (FFK_ATTN_XCD, default on)
 };
+
+// (head, block) of a non-causal workgroup, grid (blocks, B*H).  Dispatch puts
+// linear id L = x + y * gridDim.x on XCD L % 8, so without a remap the
+// blocks of one head (4 query blocks at S = 512) run on four XCDs and every
+// XCD's L2 fetches that head's K / V.  The bijective remap (mfma.h) gives
+// each XCD a contiguous range of linear ids, i.e. whole heads: a head's K / V
+// come from HBM once and its other blocks hit in the XCD's L2.
+__device__ __forceinline__ void attn_head_block(const AttnParams& P, int& bh, int& blk) {
+  if (!P.xcd) {
+    bh = blockIdx.y;
+    blk = blockIdx.x;
+    return;
+  }
+  const int W = gridDim.x * gridDim.y;
+  const int r = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, W);
+  bh = r / gridDim.x;
+  blk = r % gridDim.x;
+}
 
 __device__ __forceinline__ void prio_hi(const AttnParams& P) {
   if (P.prio) __builtin_amdgcn_s_setprio(1);
@@ -177,8 +196,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   // causal: grid (B*H, q blocks) with the LAST (heaviest) query block of every
   // head dispatched first — longest-first order, so the kernel's tail is the
   // light blocks near the sequence start
-  const int bh = CAUSAL ? blockIdx.x : blockIdx.y, b = bh / P.H, hh = bh % P.H;
-  const int q_blk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.x) * 128;
+  int bh = blockIdx.x, qb = gridDim.y - 1 - blockIdx.y;
+  if (!CAUSAL) attn_head_block(P, bh, qb);
+  const int b = bh / P.H, hh = bh % P.H;
+  const int q_blk = qb * 128;
   const int qw = q_blk + wave * 32;
   const int q = qw + (lane & 31);
   const bool q_ok = q < P.Sq;
@@ -333,8 +354,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(AttnParams P) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];  // [K V] x 2
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
-  const int bh = CAUSAL ? blockIdx.x : blockIdx.y, b = bh / P.H, hh = bh % P.H;
-  const int q_blk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.x) * 128;
+  int bh = blockIdx.x, qb = gridDim.y - 1 - blockIdx.y;
+  if (!CAUSAL) attn_head_block(P, bh, qb);
+  const int b = bh / P.H, hh = bh % P.H;
+  const int q_blk = qb * 128;
   const int qw = q_blk + wave * 32;
   const int q = qw + (lane & 31);
   const bool q_ok = q < P.Sq;
@@ -515,8 +538,10 @@ __global__ __launch_bounds__(256, (D == 64 ? (CAUSAL ? 2 : 3) : 1)) void attn_bw
   constexpr int TILE_BYTES = KV * D * 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[4 * TILE_BYTES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
-  const int bh = CAUSAL ? blockIdx.x : blockIdx.y, b = bh / P.H, hh = bh % P.H;  // longest-first (fwd)
-  const int q_blk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.x) * 128;
+  int bh = blockIdx.x, qb = gridDim.y - 1 - blockIdx.y;   // causal: longest-first (fwd)
+  if (!CAUSAL) attn_head_block(P, bh, qb);
+  const int b = bh / P.H, hh = bh % P.H;
+  const int q_blk = qb * 128;
   const int qw = q_blk + wave * 32;
   const int q = qw + (lane & 31);
   const bool q_ok = q < P.Sq;
@@ -656,8 +681,10 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
   // causal: heads fastest, key block 0 (the most query tiles) first — longest first
-  const int bh = CAUSAL ? blockIdx.x : blockIdx.y, b = bh / P.H, hh = bh % P.H;
-  const int k_blk = (CAUSAL ? blockIdx.y : blockIdx.x) * (4 * KW);
+  int bh = blockIdx.x, kb = blockIdx.y;
+  if (!CAUSAL) attn_head_block(P, bh, kb);
+  const int b = bh / P.H, hh = bh % P.H;
+  const int k_blk = kb * (4 * KW);
   const int kw = k_blk + wave * KW;
 
   // K, V rows as B operands (lane holds row `key`, d = 16ks + 8h ..)
@@ -927,6 +954,9 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
     return e ? atoi(e) : -1;
   }();
   P.prio = prio >= 0 ? prio : (D == 128 ? 1 : 0);
+  // read per call: tools/attn_time.py --xcd-ab switches it inside one process
+  const char* xe = getenv("FFK_ATTN_XCD");
+  P.xcd = xe ? atoi(xe) : 1;
   return P;
 }
 

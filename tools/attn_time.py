@@ -88,6 +88,9 @@ def main():
         return env_ab("FFK_ATTN_FWD_PIPE", "fwd", 50)
     if "--delta-ab" in sys.argv:       # delta fused into the dQ kernel
         return env_ab("FFK_ATTN_BWD_FUSED_DELTA", "bwd", 30)
+    if "--xcd-ab" in sys.argv:         # XCD-local head order (non-causal grids)
+        env_ab("FFK_ATTN_XCD", "fwd", 50)
+        return env_ab("FFK_ATTN_XCD", "bwd", 30)
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     for name, (B, S, H, D, causal) in SHAPES.items():
         g = torch.Generator(device="cuda").manual_seed(0)
