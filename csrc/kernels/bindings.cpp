@@ -226,6 +226,7 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("unary_op", [](int dt, uintptr_t x, uintptr_t dy, uintptr_t y, int64_t n, int op, float s, int bwd,
                        uintptr_t st) { unary_op(dt, P(x), P(dy), P(y), n, op, s, bwd, S(st)); });
+  m.def("zero_fill", [](uintptr_t p, int64_t bytes, uintptr_t st) { zero_fill(P(p), bytes, S(st)); });
   m.def("mse_loss_full", [](int dt, int ldt, uintptr_t p, uintptr_t y, uintptr_t g, uintptr_t metrics, int64_t n,
                             float scale, int full, int64_t cols, int64_t rows, uintptr_t st) {
     mse_loss_full(dt, ldt, P(p), P(y), P(g), F(metrics), n, scale, full, cols, rows, S(st));

@@ -440,12 +440,13 @@ int ew_blocks(int64_t n) { return static_cast<int>(std::min<int64_t>((n + 255) /
 
 }  // namespace
 
-__global__ void bn_fold_buckets_kernel(float* __restrict__ ws, float* __restrict__ stats, int C2, int reset) {
+__global__ void bn_fold_buckets_kernel(float* __restrict__ ws, float* __restrict__ stats, int C2, int reset,
+                                       int overwrite) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C2) return;
   float s = 0.f;
   for (int k = 0; k < kBnBuckets; ++k) s += ws[static_cast<int64_t>(k) * C2 + c];
-  stats[c] += s;
+  stats[c] = overwrite ? s : stats[c] + s;
   if (reset)
     for (int k = 0; k < kBnBuckets; ++k) ws[static_cast<int64_t>(k) * C2 + c] = 0.f;
 }
@@ -473,7 +474,13 @@ static void with_unroll(F&& f) {
 
 void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws, int ws_clean) {
   if (C % 8) throw std::invalid_argument("bn_stats: C must be a multiple of 8");
-  if (M <= 0) return;
+  // ws_clean bit 1: overwrite `stats` instead of accumulating (needs ws)
+  const int overwrite = (ws_clean & 2) && ws ? 1 : 0;
+  ws_clean &= 1;
+  if (M <= 0) {
+    if (overwrite) (void)hipMemsetAsync(stats, 0, sizeof(float) * 2 * C, st);
+    return;
+  }
   const RedGeom r = red_geom(C);
   dim3 grid = red_grid(r, M);
   if (!ws) grid.x = std::min(grid.x, 256u);  // single [2][C] target: bound the same-address atomics
@@ -485,7 +492,7 @@ void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, flo
   });
   if (ws)
     hipLaunchKernelGGL(bn_fold_buckets_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, ws, stats, 2 * C,
-                       ws_clean);
+                       ws_clean, overwrite);
   FFK_LAUNCH_CHECK("bn_stats");
 }
 

@@ -352,6 +352,25 @@ void axpby(int dtype, const void* x, void* y, int64_t n, float a, float b, hipSt
   FFK_LAUNCH_CHECK("axpby");
 }
 
+// zero `bytes` bytes (16-B stores, a byte tail): gradient buffers between
+// steps, without a runtime fill or a torch kernel in the step
+__global__ __launch_bounds__(256) void zero_kernel(unsigned char* __restrict__ p, int64_t n16, int64_t bytes) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<u16x8*>(p)[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (blockIdx.x == 0)
+    for (int64_t b = n16 * 16 + threadIdx.x; b < bytes; b += 256) p[b] = 0;
+}
+
+void zero_fill(void* p, int64_t bytes, hipStream_t st) {
+  if (bytes <= 0) return;
+  if (reinterpret_cast<uintptr_t>(p) % 16) throw std::invalid_argument("zero_fill: pointer must be 16-B aligned");
+  const int64_t n16 = bytes / 16;
+  const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 4096)));
+  hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(256), 0, st, static_cast<unsigned char*>(p), n16, bytes);
+  FFK_LAUNCH_CHECK("zero_fill");
+}
+
 // ------------------------------------------------------------ narrow Linear
 // Linear layers with a narrow output, N <= 8 (DLRM's 1-wide sigmoid head, any
 // width the 16-B-row GEMM epilogues cannot write): GEMV-shaped and bound by
@@ -493,8 +512,17 @@ __global__ __launch_bounds__(256) void narrow_wgrad_finish_kernel(const float* _
                                                                   float* __restrict__ db) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= KN + N) return;
-  float s = 0.f;
-  for (int b = 0; b < blocks; ++b) s += part[static_cast<int64_t>(b) * (KN + N) + i];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // four independent chains: loads in flight
+  const int64_t ld = KN + N;
+  int b = 0;
+  for (; b + 4 <= blocks; b += 4) {
+    s0 += part[(b + 0) * ld + i];
+    s1 += part[(b + 1) * ld + i];
+    s2 += part[(b + 2) * ld + i];
+    s3 += part[(b + 3) * ld + i];
+  }
+  for (; b < blocks; ++b) s0 += part[b * ld + i];
+  const float s = (s0 + s1) + (s2 + s3);
   if (i < KN) {
     if (dw) {
       const float prev = beta != 0.f ? static_cast<float>(dw[i]) * beta : 0.f;
@@ -549,7 +577,7 @@ void narrow_linear_dgrad(const void* dy, const void* pre, const void* w, void* d
   FFK_LAUNCH_CHECK("narrow_linear_dgrad");
 }
 
-int narrow_wgrad_blocks(int64_t M) { return static_cast<int>(std::min<int64_t>(256, (M + 7) / 8)); }
+int narrow_wgrad_blocks(int64_t M) { return static_cast<int>(std::min<int64_t>(64, (M + 15) / 16)); }
 
 void narrow_linear_wgrad(const void* x, const void* dy, const void* pre, float* part, int blocks, void* dw,
                          int dw_dtype, float beta, float* db, int64_t M, int64_t K, int64_t N, int act,

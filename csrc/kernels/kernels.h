@@ -30,6 +30,7 @@ void colsum_act(int dtype, const void* dy, const void* pre, void* dx, float* dbi
 void dropout_fwd(int dtype, const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
 void cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, hipStream_t st);
 void axpby(int dtype, const void* x, void* y, int64_t n, float a, float b, hipStream_t st);
+void zero_fill(void* p, int64_t bytes, hipStream_t st);
 
 // ---- softmax.hip
 // row_stats: optional [M, 3] fp32 scratch; with metrics, per-row metric terms
@@ -259,7 +260,8 @@ void conv32_wgrad(const ConvShape& cs, int groups, const void* x, const void* dy
 
 // ---- bnpool.hip: BatchNorm (training) + pooling over NHWC bf16 [M][C]
 // ws (optional, 32*C floats): 16 atomic buckets -> full-grid reduction (else the grid is capped);
-// ws_clean: ws is zero on entry and is left zero (a persistent workspace: no memset per call)
+// ws_clean bit 0: ws is zero on entry and is left zero (a persistent workspace: no memset per call);
+// bit 1: write stats instead of adding to them
 void bn_stats(const void* x, float* stats, int64_t M, int C, hipStream_t st, float* ws = nullptr, int ws_clean = 0);
 void bn_finalize(const float* stats, const void* gamma, const void* beta, int param_dtype, float* running_mean,
                  float* running_var, float* scale, float* shift, float* mean, float* rstd, int C, double count,

@@ -843,6 +843,17 @@ def mse_full(pred, label, grad, metrics, scale: float, cols: int, rows: int):
     return grad
 
 
+def zero_(t):
+    """t.zero_() on the device by the library's own kernel (16-B stores)."""
+    if t.numel() == 0:
+        return t
+    if not t.is_contiguous() or t.data_ptr() % 16:
+        return t.zero_()
+    ext().zero_fill(t.data_ptr(), t.numel() * t.element_size(), _stream())
+    STATS["zero_fill"] += 1
+    return t
+
+
 def narrow_ok(x, w) -> bool:
     """The narrow-Linear kernels' shapes: bf16, N <= 8, K % 8, K * N <= 16384."""
     if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and available()):
@@ -1166,7 +1177,7 @@ def _bn_workspace(dev, C: int):
     that consumes them (bn_fold_buckets / bn_bwd_coef), so no memset runs per
     call.  Inside a graph capture a first use gets a per-call buffer instead
     (zeroed by the launcher)."""
-    key = (dev, _stream(), C)
+    key = (dev, C)   # one stream runs the BN passes: stream order keeps uses apart
     ws = _BN_WS.get(key)
     if ws is not None:
         return ws, 1
@@ -1176,12 +1187,14 @@ def _bn_workspace(dev, C: int):
     return ws, 1
 
 
-def bn_stats(x, stats):
+def bn_stats(x, stats, overwrite: bool = False):
+    """stats (fp32 [2, C]) += per-channel (sum, sum of squares) of x;
+    ``overwrite``: stats = ... (no zeroing pass needed)."""
     _check_nhwc(x, "x")
     C = x.shape[1]
     _check(stats, "stats", torch.float32, 2 * C)
     ws, clean = _bn_workspace(x.device, C)
-    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream(), _p(ws), clean)
+    ext().bn_stats(_p(x), _p(stats), x.numel() // C, C, _stream(), _p(ws), clean | (2 if overwrite else 0))
     STATS["bn_stats"] += 1
 
 

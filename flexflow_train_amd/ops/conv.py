@@ -67,8 +67,11 @@ _MODE = os.environ.get("FF_CONV1X1", "auto")   # auto | native | gemm
 
 
 def _pointwise(R, S, stride, pad, groups) -> bool:
-    """1x1, unpadded, ungrouped: a GEMM over (strided-subsampled) NHWC pixels."""
-    return R == 1 and S == 1 and tuple(pad) == (0, 0) and groups == 1
+    """1x1, unit-stride, unpadded, ungrouped: a GEMM over the NHWC pixels
+    (views, no copies).  Strided 1x1 convolutions stay on the implicit-GEMM
+    kernels, which read the sampled pixels in place instead of gathering them
+    with a torch copy (and scattering dgrad into a zeroed buffer)."""
+    return R == 1 and S == 1 and tuple(pad) == (0, 0) and groups == 1 and tuple(stride) == (1, 1)
 
 
 def _sub(x: torch.Tensor, stride) -> torch.Tensor:
@@ -143,11 +146,11 @@ class Conv2DOp(OpImpl):
             if _pointwise(R, S, stride, pad, groups) and C % 8 == 0:
                 def via_gemm(st=stats):
                     xs = _sub(xin, stride)
-                    y2 = G.matmul(_rows(xs), wp.view(Kc, C), trans_b=True, bias=bias, act=act)
+                    # hand-written GEMMs only (no library kernel for convolutions)
+                    y2 = G.matmul(_rows(xs), wp.view(Kc, C), trans_b=True, bias=bias, act=act, native_only=True)
                     yv = y2.view(xs.shape[0], xs.shape[2], xs.shape[3], Kc).permute(0, 3, 1, 2)
                     if st is not None:
-                        st.zero_()
-                        K.bn_stats(yv, st)
+                        K.bn_stats(yv, st, overwrite=True)
                     return yv
                 key = ("fwd", tuple(xin.shape), Kc, tuple(stride), act, bias is not None, stats is not None)
                 scratch = None if stats is None else torch.empty_like(stats)
@@ -229,9 +232,10 @@ class Conv2DOp(OpImpl):
                     tmp = torch.zeros_like(dW.view(-1))
                     _pick(key, {"native": lambda: K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad),
                                 "gemm": lambda: G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True,
-                                                         out=tmp.view(Kc, Cp), beta=1.0)})
+                                                         out=tmp.view(Kc, Cp), beta=1.0, native_only=True)})
                 if _CHOICE[key] == "gemm":
-                    G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True, out=dW.view(Kc, Cp), beta=1.0)
+                    G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True, out=dW.view(Kc, Cp), beta=1.0,
+                             native_only=True)
                 else:
                     K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
             elif Cp == xshape[1]:
@@ -252,12 +256,13 @@ class Conv2DOp(OpImpl):
             def dgrad_gemm(out):
                 if tuple(stride) == (1, 1):
                     if out is not None:
-                        G.matmul(_rows(dy), wp.view(Kc, Cp), out=_rows(out), beta=1.0)
+                        G.matmul(_rows(dy), wp.view(Kc, Cp), out=_rows(out), beta=1.0, native_only=True)
                         return out
-                    dx2 = G.matmul(_rows(dy), wp.view(Kc, Cp))
+                    dx2 = G.matmul(_rows(dy), wp.view(Kc, Cp), native_only=True)
                     return dx2.view(xshape[0], xshape[2], xshape[3], Cp).permute(0, 3, 1, 2)
                 # strided: the gradient lands on the sampled pixels only
-                ds = G.matmul(_rows(dy), wp.view(Kc, Cp)).view(dy.shape[0], dy.shape[2], dy.shape[3], Cp)
+                ds = G.matmul(_rows(dy), wp.view(Kc, Cp), native_only=True).view(dy.shape[0], dy.shape[2],
+                                                                                  dy.shape[3], Cp)
                 if out is None:
                     out = torch.empty(tuple(xshape), device=dy.device, dtype=dy.dtype,
                                       memory_format=torch.channels_last).zero_()

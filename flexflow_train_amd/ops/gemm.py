@@ -431,9 +431,12 @@ def _time(fn, iters=5, rounds=2) -> float:
 
 
 # a library GEMM (hipBLASLt / torch.mm) is taken only when it beats the
-# fastest hand-written candidate by more than this fraction: within timing
-# noise the MFMA kernel runs (FF_GEMM_LIB_MARGIN; 0 = the fastest outright)
+# fastest hand-written candidate by more than this fraction AND by more than
+# _LIB_MIN_MS per call: within timing noise, and on the microsecond GEMMs of
+# small MLPs, the MFMA kernel runs (FF_GEMM_LIB_MARGIN / FF_GEMM_LIB_MIN_MS;
+# 0 / 0 = the fastest outright)
 _LIB_MARGIN = float(os.environ.get("FF_GEMM_LIB_MARGIN", "0.03"))
+_LIB_MIN_MS = float(os.environ.get("FF_GEMM_LIB_MIN_MS", "0.004"))
 
 
 def _is_library(name: str) -> bool:
@@ -447,15 +450,16 @@ def _pick_fastest(times: Dict[str, float]) -> str:
     native = {k: v for k, v in times.items() if not _is_library(k)}
     if native:
         nb = min(native, key=native.get)
-        if times[best] >= native[nb] * (1.0 - _LIB_MARGIN):
+        if times[best] >= native[nb] * (1.0 - _LIB_MARGIN) or native[nb] - times[best] < _LIB_MIN_MS:
             return nb
     return best
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias: Optional[torch.Tensor] = None,
            act: str = "none", out: Optional[torch.Tensor] = None, beta: float = 0.0,
-           pre: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = act(op(a) @ op(b) + bias) (+ beta * out).  2-D operands."""
+           pre: Optional[torch.Tensor] = None, native_only: bool = False) -> torch.Tensor:
+    """C = act(op(a) @ op(b) + bias) (+ beta * out).  2-D operands.
+    ``native_only``: hand-written kernels only (no library candidate)."""
     if not a.is_cuda:
         return _blas(a, b, trans_a, trans_b, bias, act, out, beta, pre)
     if a.dtype == torch.float32 and b.dtype == torch.float32 and K.use_hip(a, b):
@@ -471,7 +475,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
     key = (tuple(a.shape), tuple(b.shape), trans_a, trans_b, bias is not None, act,
            None if out is None else out.dtype, bool(beta), pre is not None,
            a.stride(0), b.stride(0), None if out is None else out.stride(0),
-           _align(a), _align(b), None if out is None else _align(out))
+           _align(a), _align(b), None if out is None else _align(out), bool(native_only))
     choice = _CHOICE.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
@@ -480,6 +484,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
             choice = "hip"
         else:
             cands = _candidates(a, b, trans_a, trans_b, bias, act, pre, out, beta)
+            if native_only:
+                cands = {k: v for k, v in cands.items() if not _is_library(k)}
             scratch = None if out is None else out.clone()
             pscratch = None if pre is None else pre.clone()
             times = _time_all({name: (lambda fn=fn: fn(a, b, trans_a, trans_b, bias, act, scratch, beta, pscratch))

@@ -150,8 +150,8 @@ class BatchNormOp(OpImpl):
             if ctx.training:
                 stats = stats_in
                 if stats is None:
-                    stats = torch.zeros(2 * C, device=x.device, dtype=torch.float32)
-                    K.bn_stats(xin, stats)
+                    stats = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+                    K.bn_stats(xin, stats, overwrite=True)
                 scale, shift, mean, rstd = K.bn_finalize(stats, g, b, xin.numel() // C, eps, mom,
                                                          state["running_mean"], state["running_var"])
             else:

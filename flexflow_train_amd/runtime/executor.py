@@ -33,6 +33,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 
 from .. import _ffcore as C
+from .. import kernels as K
 from .. import ops as _ops_pkg  # noqa: F401  (registers operator impls)
 from ..ops import base as opbase
 from ..ops.loss import N_SLOTS, LossFunction, PerfMetrics
@@ -1236,7 +1237,10 @@ class Executor:
         """Reset a flat's gradients.  Sparse flats only hold non-zero rows the
         last backward touched and no update consumed: clear just those."""
         if not f["sparse"]:
-            f["grad"].zero_()
+            if f["grad"].is_cuda and K.available():
+                K.zero_(f["grad"])
+            else:
+                f["grad"].zero_()
             return
         for p in f["params"]:
             if not (0 <= p.final_step < len(self.steps)):

@@ -87,3 +87,11 @@ def test_dlrm_head_runs_native():
     assert K.STATS["mse"] > before.get("mse", 0)
     pm = ex.perf_metrics()
     assert pm.mse_loss > 0
+
+
+def test_zero_fill_kernel():
+    from flexflow_train_amd import kernels as K
+    for n, dt in ((1, torch.bfloat16), (1000003, torch.float32), (4096, torch.bfloat16)):
+        t = torch.randn(n, device="cuda").to(dt)
+        K.zero_(t)
+        assert int((t != 0).sum()) == 0
