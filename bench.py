@@ -463,5 +463,21 @@ def _run_zoo(args, world, rank, only_dp: bool):
             "step": t["step"], "profile": prof, "feeds": feeds, "labels": labels}
 
 
+def _write_autotune_report():
+    """FF_AUTOTUNE_REPORT=<path>: the GEMM autotuner's per-shape candidate
+    times and picks (ops/gemm.py report) written at exit, rank 0."""
+    path = os.environ.get("FF_AUTOTUNE_REPORT")
+    if not path or int(os.environ.get("RANK", "0")) != 0:
+        return
+    try:
+        from flexflow_train_amd.ops import dense, gemm
+        with open(path, "w") as f:
+            f.write(gemm.report() + "\n" + dense.dact_report() + "\n")
+    except Exception as e:  # noqa: BLE001
+        print(f"autotune report: {e}", file=sys.stderr)
+
+
 if __name__ == "__main__":
+    import atexit
+    atexit.register(_write_autotune_report)
     main()

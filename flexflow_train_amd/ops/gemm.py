@@ -207,6 +207,7 @@ def _gp(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1):
 _GT_VARIANT = int(os.environ.get("FF_GEMMT_VARIANT", "3"))
 _GT_DMA = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_DMA", "1") != "0"
 _GT_RS = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_RS", "1") != "0"
+_GT_PERS = _GT_VARIANT != 0 and os.environ.get("FF_GEMMT_PERS", "1") != "0"
 
 
 def _gt(a, b, trans_a, trans_b, bias, act, out, beta, pre, splits=1, variant=None):
@@ -329,6 +330,11 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
                 if _GT_DMA:
                     c[f"u:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=4)))(s)
                     c[f"w:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=6)))(s)
+                if _GT_PERS and (Kd // 64) % s == 0 and Kd // 64 // s >= 2:
+                    # persistent form (variant 5): one workgroup per CU walks its
+                    # tiles, the next tile's loads in flight under this tile's
+                    # epilogue -- for the epilogue-heavy K = 1024 forwards
+                    c[f"v:{s}"] = (lambda s_: (lambda *args: _gt(*args, splits=s_, variant=5)))(s)
                 if _GT_RS and not (trans_a and trans_b):
                     # the padded-image kernel with register staging (variant 10):
                     # 1-11 % ahead of "w" on the weight-gradient and long-K
@@ -495,7 +501,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, bias:
         _CHOICE[key] = choice
     if choice.startswith("hip256") and not K.gemm256_supported(a, b, trans_a, trans_b):
         choice = "hip"
-    if choice[:2] in ("p:", "t:", "u:", "w:", "x:", "s:", "n:") and not K.gemmp_supported(a, b, trans_a, trans_b):
+    if choice[:2] in ("p:", "t:", "u:", "v:", "w:", "x:", "s:", "n:") and not K.gemmp_supported(a, b, trans_a, trans_b):
         choice = "hip"
     return _resolve(choice)(a, b, trans_a, trans_b, bias, act, out, beta, pre)
 
@@ -553,6 +559,8 @@ def _resolve(name: str):
         return lambda *args: _gt(*args, splits=int(arg), variant=6)
     if kind == "x":
         return lambda *args: _gt(*args, splits=int(arg), variant=10)
+    if kind == "v":
+        return lambda *args: _gt(*args, splits=int(arg), variant=5)
     if kind == "s":
         return lambda *args: _gs(*args, splits=int(arg))
     if kind == "n":

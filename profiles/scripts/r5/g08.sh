@@ -18,3 +18,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_rn -o rn -- \
 DB=$(find $O/prof_rn -name "rn_results.db" | head -n 1)
 [ -n "$DB" ] && python3 $R/tools/prof_summary.py $DB --steps 5 --top 40 > $O/rn50_kernels.txt
 head -44 $O/rn50_kernels.txt
+cd $R
+FF_AUTOTUNE_REPORT=$O/autotune_bert.txt timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_bert.jsonl 2>&1 || { tail -20 $O/bench_bert.jsonl; exit 1; }
+tail -1 $O/bench_bert.jsonl | cut -c1-700
+cat $O/autotune_bert.txt
