@@ -56,7 +56,40 @@ struct AttnParams {
   float inv_scale_log2;  // 1 / scale_log2 (no IEEE divide in the loops)
   int prio;          // raise wave priority around MFMA clusters (FFK_ATTN_PRIO; guide T5)
   int xcd;           // XCD-local head order of non-causal grids (FFK_ATTN_XCD, default on)
+  int wide_store;    // 16-B output rows via permlane32_swap (FFK_ATTN_WIDE_STORE, default on)
 };
+
+// Store a wave's 32-row C^T tile (lane & 31 -> row, registers -> d) as rows
+// of bf16, 16 bytes per store.  A lane holds 4 consecutive d of each 8-group
+// (lane half h: d = 8 g + 4 h + e); v_permlane32_swap trades group 2p+1 of
+// the lower half for group 2p of the upper half, so after the swap every
+// lane holds 8 consecutive d (lower half: d 16p..16p+7 = its own group 2p
+// and its partner's; upper half: 16p+8..16p+15) -- half the store
+// instructions of the 8-byte form (the epilogue tail is store-issue bound,
+// guide T21).  Every lane runs the swaps; `ok` guards only the stores.
+template <int DT>
+__device__ __forceinline__ void store_rows16(bf16* row, const f32x16 (&acc)[DT], float mul, int h, bool ok) {
+  auto pk = [](float a, float b) -> unsigned {
+    return static_cast<unsigned>(f2u(a)) | (static_cast<unsigned>(f2u(b)) << 16);
+  };
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+      const int ga = 2 * gp, gb = 2 * gp + 1;
+      const unsigned xa0 = pk(acc[dt][4 * ga + 0] * mul, acc[dt][4 * ga + 1] * mul);
+      const unsigned xa1 = pk(acc[dt][4 * ga + 2] * mul, acc[dt][4 * ga + 3] * mul);
+      const unsigned yb0 = pk(acc[dt][4 * gb + 0] * mul, acc[dt][4 * gb + 1] * mul);
+      const unsigned yb1 = pk(acc[dt][4 * gb + 2] * mul, acc[dt][4 * gb + 3] * mul);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(xa0, yb0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(xa1, yb1, false, false);
+      if (ok) {
+        u32x4t v = {static_cast<unsigned>(s0[0]), static_cast<unsigned>(s1[0]), static_cast<unsigned>(s0[1]),
+                    static_cast<unsigned>(s1[1])};
+        *reinterpret_cast<u32x4t*>(row + dt * 32 + 16 * gp + 8 * h) = v;
+      }
+    }
+}
 
 // (head, block) of a non-causal workgroup, grid (blocks, B*H).  Dispatch puts
 // linear id L = x + y * gridDim.x on XCD L % 8, so without a remap the
@@ -324,8 +357,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
   // ---- epilogue: O = O^T / l, LSE
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (q_ok) {
-    bf16* orow = P.o_out + b * P.o_sb + static_cast<int64_t>(q) * P.o_ss + hh * P.o_sh;
+  bf16* orow = P.o_out + b * P.o_sb + static_cast<int64_t>(q) * P.o_ss + hh * P.o_sh;
+  if (P.wide_store) {
+    store_rows16<DT>(orow, o, inv, h, q_ok);
+  } else if (q_ok) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -335,8 +370,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams P) {
         for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * g4 + e] * inv);
         *reinterpret_cast<bf16x4*>(orow + dt * 32 + 8 * g4 + 4 * h) = v;
       }
-    if (h == 0) P.lse[static_cast<int64_t>(bh) * P.Sq + q] = (lt > 0.f) ? m * P.scale_log2 + log2f(lt) : -INFINITY;
   }
+  if (q_ok && h == 0)
+    P.lse[static_cast<int64_t>(bh) * P.Sq + q] = (lt > 0.f) ? m * P.scale_log2 + log2f(lt) : -INFINITY;
 }
 
 // ===========================================================================
@@ -651,8 +687,10 @@ __global__ __launch_bounds__(256, (D == 64 ? (CAUSAL ? 2 : 3) : 1)) void attn_bw
   } else if (P.dbq) {
     bias_colsum<DT>(dq, P.scale, P.dbq + hh * D, lane);
   }
-  if (q_ok) {
-    bf16* row = P.dq + b * P.dq_sb + static_cast<int64_t>(q) * P.dq_ss + hh * P.dq_sh;
+  bf16* row = P.dq + b * P.dq_sb + static_cast<int64_t>(q) * P.dq_ss + hh * P.dq_sh;
+  if (P.wide_store) {
+    store_rows16<DT>(row, dq, P.scale, h, q_ok);
+  } else if (q_ok) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -899,9 +937,14 @@ __global__ __launch_bounds__(256, (D == 64 && NKT == 1 ? 2 : 1)) void attn_bwd_d
   }
 #pragma unroll
   for (int j = 0; j < NKT; ++j) {
-    if (!k_ok[j]) continue;
     bf16* krow = P.dk + b * P.dk_sb + static_cast<int64_t>(key[j]) * P.dk_ss + hh * P.dk_sh;
     bf16* vrow = P.dv + b * P.dv_sb + static_cast<int64_t>(key[j]) * P.dv_ss + hh * P.dv_sh;
+    if (P.wide_store) {   // every lane swaps; k_ok guards the stores
+      store_rows16<DT>(krow, dk[j], P.scale, h, k_ok[j]);
+      store_rows16<DT>(vrow, dv[j], 1.f, h, k_ok[j]);
+      continue;
+    }
+    if (!k_ok[j]) continue;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -957,6 +1000,8 @@ static AttnParams make_params(const AttnTensors& t, int B, int H, int Sq, int Sk
   // read per call: tools/attn_time.py --xcd-ab switches it inside one process
   const char* xe = getenv("FFK_ATTN_XCD");
   P.xcd = xe ? atoi(xe) : 1;
+  const char* we = getenv("FFK_ATTN_WIDE_STORE");
+  P.wide_store = we ? atoi(we) : 1;
   return P;
 }
 

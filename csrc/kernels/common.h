@@ -26,6 +26,7 @@ typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4t __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
 

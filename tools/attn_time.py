@@ -88,6 +88,9 @@ def main():
         return env_ab("FFK_ATTN_FWD_PIPE", "fwd", 50)
     if "--delta-ab" in sys.argv:       # delta fused into the dQ kernel
         return env_ab("FFK_ATTN_BWD_FUSED_DELTA", "bwd", 30)
+    if "--wide-ab" in sys.argv:        # 16-B output row stores (forward / backward epilogues)
+        env_ab("FFK_ATTN_WIDE_STORE", "fwd", 50)
+        return env_ab("FFK_ATTN_WIDE_STORE", "bwd", 30)
     if "--xcd-ab" in sys.argv:         # XCD-local head order (non-causal grids)
         env_ab("FFK_ATTN_XCD", "fwd", 50)
         return env_ab("FFK_ATTN_XCD", "bwd", 30)
