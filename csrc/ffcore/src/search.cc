@@ -391,9 +391,61 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
     } catch (const FFError&) {
     }
   }
-  // liveness memory plan of the winner: the busiest device's arena
+  // liveness memory plan of the winner: the busiest device's arena.  A
+  // winner that does not fit the HBM is replaced by the fastest candidate
+  // that does -- data parallelism or a pipeline split (stages hold 1/S of the
+  // weights) -- so the 288 GB budget is checked by the search
   try {
+    auto busiest = [](const std::vector<MemoryPlan>& ps) {
+      double a = 0;
+      for (auto const& p : ps) a = std::max(a, p.arena_bytes);
+      return a;
+    };
     auto plans = plan_memory(best.pcg, best.views, cfg.world);
+    const double cap = cm.spec().hbm_capacity;
+    if (cap > 0 && busiest(plans) > cap && cfg.world > 1) {
+      SimConfig sim = cfg.sim;
+      sim.world = cfg.world;
+      const int M = std::max(1, cfg.micro_batches);
+      Simulator S(cm, sim);
+      double best_t = std::numeric_limits<double>::infinity();
+      auto dp = data_parallel_pcg(cg, cfg.world);
+      auto dplans = plan_memory(dp, {}, cfg.world);
+      bool found = false;
+      ParallelComputationGraph fb_pcg;
+      std::map<int, Placement> fb_views;
+      std::vector<MemoryPlan> fb_plans;
+      std::string tag;
+      int stages = 0;
+      if (busiest(dplans) <= cap) {
+        best_t = micro_batched_step_time(S.simulate(dp), M);
+        fb_pcg = dp;
+        fb_plans = dplans;
+        tag = "+memory_fallback_dp";
+        found = true;
+      }
+      for (auto& pl : pipeline_candidates(cg, cm, cfg.world, M, sim)) {
+        auto pp = plan_memory(pl.pcg, pl.views, cfg.world);
+        if (busiest(pp) <= cap && pl.step_time < best_t) {
+          best_t = pl.step_time;
+          fb_pcg = pl.pcg;
+          fb_views = pl.views;
+          fb_plans = pp;
+          tag = "+memory_fallback_pipeline";
+          stages = pl.stages;
+          found = true;
+        }
+      }
+      if (found) {
+        best.pcg = fb_pcg;
+        best.views = fb_views;
+        best.strategy.clear();
+        best.cost = best_t / M;
+        best.pipeline_stages = stages;
+        best.algorithm += tag;
+        plans = fb_plans;
+      }
+    }
     Json mp = Json::object();
     double arena = 0, live = 0, weights = 0, naive = 0;
     for (auto const& p : plans) {

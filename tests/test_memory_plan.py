@@ -64,3 +64,25 @@ def test_search_report_carries_memory_plan():
     rep = json.loads(rep)
     mp = rep["memory_plan"]
     assert mp["arena_bytes"] >= mp["peak_live_bytes"] > 0 and mp["devices"] == 2
+
+
+def test_search_falls_back_when_the_winner_does_not_fit():
+    """A winner whose planned arena exceeds the HBM is replaced by the fastest
+    candidate that fits: with the capacity set between the data-parallel plan
+    (every weight replicated) and a 4-stage pipeline's (1/4 of the weights per
+    device), a model the search would run data-parallel goes to a pipeline."""
+    m = _mlp(batch=256, width=1024, layers=8)
+    cfg = {"world": 4, "budget": 6, "time_limit": 20}
+    cm = native.cost_model(use_profiles=False)
+    _, rep, _ = C.graph_optimize(m.cg, cm, json.dumps(cfg))
+    rep = json.loads(rep)
+    assert "pipeline" not in rep["algorithm"], rep["algorithm"]
+    win = rep["memory_plan"]["arena_bytes"]
+    spec = C.MachineSpecification.mi355x()
+    spec.hbm_capacity = 0.6 * win        # a 4-stage split needs ~1/4 of the weights
+    cm2 = native.cost_model(use_profiles=False, spec=spec)
+    _, rep2, _ = C.graph_optimize(m.cg, cm2, json.dumps(cfg))
+    rep2 = json.loads(rep2)
+    # the simulator's memory penalty or the plan check moves it to a pipeline
+    assert "pipeline" in rep2["algorithm"], rep2["algorithm"]
+    assert rep2["memory_plan"]["fits_hbm"] and rep2["memory_plan"]["arena_bytes"] <= spec.hbm_capacity
