@@ -9,10 +9,11 @@
 //    initialisers (same values as a CPU run with the same seed) and uploaded;
 //  * operators: LINEAR on the exact-fp32 MFMA GEMM (igemm32.hip: bias and the
 //    activation in its epilogue, the pre-activation kept for backward), the
-//    last SOFTMAX fused with sparse cross-entropy (softmax.hip), MSE
-//    (tensorops.hip), element-wise activations / binaries / scalar ops /
-//    reshapes / softmax by the small kernels below; a graph with any other
-//    operator stays on the CPU backing (make_device_backing returns null);
+//    last SOFTMAX fused with sparse cross-entropy, MSE (tensorops.hip),
+//    CONV2D / POOL2D / BATCHNORM (NCHW, direct formulations), element-wise
+//    activations / binaries / scalar ops / reshapes / softmax by the small
+//    kernels below; a graph with any other operator stays on the CPU backing
+//    (make_device_backing returns null);
 //  * the host slots are mirrors: slot() copies a tensor out when the device
 //    copy is newer and marks it written, and the next device step copies
 //    written mirrors back -- the inline-mapping protocol of the reference's
@@ -227,6 +228,247 @@ __global__ __launch_bounds__(256) void k_adam(float* w, const float* g, float* m
   }
 }
 
+// ---- conv2d / pool2d / batch norm, NCHW fp32 (the C API's small CNNs):
+// direct formulations, one thread per output element (forward, dgrad), one
+// block per weight element (wgrad) or channel (bias, batch norm).
+struct CG {
+  int N, C, H, W, O, OH, OW, KH, KW, SH, SW, PH, PW, G;
+};
+__global__ __launch_bounds__(256) void k_conv_fwd(const float* x, const float* w, const float* bias, float* y,
+                                                  float* pre, CG g, int act) {
+  const int64_t total = static_cast<int64_t>(g.N) * g.O * g.OH * g.OW;
+  const int cpg = g.C / g.G, opg = g.O / g.G;
+  GRID_LOOP(i, total) {
+    const int ow = i % g.OW, oh = (i / g.OW) % g.OH, o = (i / (static_cast<int64_t>(g.OW) * g.OH)) % g.O;
+    const int n = static_cast<int>(i / (static_cast<int64_t>(g.OW) * g.OH * g.O));
+    const int grp = o / opg;
+    float acc = bias ? bias[o] : 0.f;
+    for (int ci = 0; ci < cpg; ++ci)
+      for (int kh = 0; kh < g.KH; ++kh) {
+        const int ih = oh * g.SH - g.PH + kh;
+        if (ih < 0 || ih >= g.H) continue;
+        for (int kw = 0; kw < g.KW; ++kw) {
+          const int iw = ow * g.SW - g.PW + kw;
+          if (iw < 0 || iw >= g.W) continue;
+          acc = __builtin_fmaf(x[((static_cast<int64_t>(n) * g.C + grp * cpg + ci) * g.H + ih) * g.W + iw],
+                               w[((static_cast<int64_t>(o) * cpg + ci) * g.KH + kh) * g.KW + kw], acc);
+        }
+      }
+    if (pre) pre[i] = acc;
+    y[i] = d_act(act, acc);
+  }
+}
+// dx += sum over the outputs that read x[n, c, ih, iw]
+__global__ __launch_bounds__(256) void k_conv_dgrad(const float* gy, const float* w, float* dx, CG g) {
+  const int64_t total = static_cast<int64_t>(g.N) * g.C * g.H * g.W;
+  const int cpg = g.C / g.G, opg = g.O / g.G;
+  GRID_LOOP(i, total) {
+    const int iw = i % g.W, ih = (i / g.W) % g.H, c = (i / (static_cast<int64_t>(g.W) * g.H)) % g.C;
+    const int n = static_cast<int>(i / (static_cast<int64_t>(g.W) * g.H * g.C));
+    const int grp = c / cpg, ci = c % cpg;
+    float acc = 0.f;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int th = ih + g.PH - kh;
+      if (th < 0 || th % g.SH) continue;
+      const int oh = th / g.SH;
+      if (oh >= g.OH) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int tw = iw + g.PW - kw;
+        if (tw < 0 || tw % g.SW) continue;
+        const int ow = tw / g.SW;
+        if (ow >= g.OW) continue;
+        for (int oo = 0; oo < opg; ++oo) {
+          const int o = grp * opg + oo;
+          acc = __builtin_fmaf(gy[((static_cast<int64_t>(n) * g.O + o) * g.OH + oh) * g.OW + ow],
+                               w[((static_cast<int64_t>(o) * cpg + ci) * g.KH + kh) * g.KW + kw], acc);
+        }
+      }
+    }
+    dx[i] += acc;
+  }
+}
+// dw[o, ci, kh, kw] += sum_{n, oh, ow} gy * x: one block per weight element
+__global__ __launch_bounds__(256) void k_conv_wgrad(const float* gy, const float* x, float* dw, CG g) {
+  __shared__ float red[256];
+  const int cpg = g.C / g.G, opg = g.O / g.G;
+  const int64_t wi = blockIdx.x;
+  const int kw = wi % g.KW, kh = (wi / g.KW) % g.KH, ci = (wi / (g.KW * g.KH)) % cpg;
+  const int o = static_cast<int>(wi / (static_cast<int64_t>(g.KW) * g.KH * cpg));
+  const int c = (o / opg) * cpg + ci;
+  const int64_t total = static_cast<int64_t>(g.N) * g.OH * g.OW;
+  float acc = 0.f;
+  for (int64_t t = threadIdx.x; t < total; t += 256) {
+    const int ow = t % g.OW, oh = (t / g.OW) % g.OH, n = static_cast<int>(t / (static_cast<int64_t>(g.OW) * g.OH));
+    const int ih = oh * g.SH - g.PH + kh, iw = ow * g.SW - g.PW + kw;
+    if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) continue;
+    acc = __builtin_fmaf(gy[((static_cast<int64_t>(n) * g.O + o) * g.OH + oh) * g.OW + ow],
+                         x[((static_cast<int64_t>(n) * g.C + c) * g.H + ih) * g.W + iw], acc);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (static_cast<int>(threadIdx.x) < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dw[wi] += red[0];
+}
+// db[c] += sum over n and the S spatial positions of g[n, c, :] (one block per channel)
+__global__ __launch_bounds__(256) void k_chan_sum(const float* gsrc, float* db, int N, int C, int64_t S) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int64_t t = threadIdx.x; t < static_cast<int64_t>(N) * S; t += 256) {
+    const int64_t n = t / S, s = t % S;
+    acc += gsrc[(n * C + c) * S + s];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (static_cast<int>(threadIdx.x) < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) db[c] += red[0];
+}
+// pool: aux = argmax input index (max) or the window count (avg), as floats
+__global__ __launch_bounds__(256) void k_pool_fwd(const float* x, float* y, float* pre, float* aux, CG g, int mx,
+                                                  int act) {
+  const int64_t total = static_cast<int64_t>(g.N) * g.C * g.OH * g.OW;
+  GRID_LOOP(i, total) {
+    const int ow = i % g.OW, oh = (i / g.OW) % g.OH;
+    const int64_t nc = i / (static_cast<int64_t>(g.OW) * g.OH);
+    float acc = mx ? -INFINITY : 0.f;
+    int64_t best = -1;
+    int cnt = 0;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int ih = oh * g.SH - g.PH + kh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int iw = ow * g.SW - g.PW + kw;
+        if (iw < 0 || iw >= g.W) continue;
+        const int64_t xi = (nc * g.H + ih) * g.W + iw;
+        const float v = x[xi];
+        if (mx) {
+          if (v > acc) acc = v, best = xi;
+        } else {
+          acc += v;
+          ++cnt;
+        }
+      }
+    }
+    const float o = mx ? acc : acc / static_cast<float>(cnt > 0 ? cnt : 1);
+    aux[i] = static_cast<float>(mx ? best : cnt);
+    if (pre) pre[i] = o;
+    y[i] = d_act(act, o);
+  }
+}
+__global__ __launch_bounds__(256) void k_pool_bwd(const float* dy, const float* pre, const float* aux, float* dx,
+                                                  CG g, int mx, int act) {
+  const int64_t total = static_cast<int64_t>(g.N) * g.C * g.OH * g.OW;
+  GRID_LOOP(i, total) {
+    float gv = dy[i];
+    if (pre) gv *= d_act_grad(act, pre[i]);
+    if (mx) {
+      const int64_t b = static_cast<int64_t>(aux[i]);
+      if (b >= 0) atomicAdd(dx + b, gv);
+      continue;
+    }
+    const int ow = i % g.OW, oh = (i / g.OW) % g.OH;
+    const int64_t nc = i / (static_cast<int64_t>(g.OW) * g.OH);
+    const float share = gv / fmaxf(1.f, aux[i]);
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int ih = oh * g.SH - g.PH + kh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int iw = ow * g.SW - g.PW + kw;
+        if (iw < 0 || iw >= g.W) continue;
+        atomicAdd(dx + (nc * g.H + ih) * g.W + iw, share);
+      }
+    }
+  }
+}
+// batch norm over N and S per channel (one block per channel); aux = {mean, inv std}[C]
+__global__ __launch_bounds__(256) void k_bn_fwd(const float* x, const float* gamma, const float* beta, float* y,
+                                                float* aux, int N, int C, int64_t S, float eps, int relu) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  const int64_t cnt = static_cast<int64_t>(N) * S;
+  auto at = [&](int64_t t) { return (t / S * C + c) * S + t % S; };
+  float s = 0.f;
+  for (int64_t t = threadIdx.x; t < cnt; t += 256) s += x[at(t)];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (static_cast<int>(threadIdx.x) < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  const float mean = red[0] / static_cast<float>(cnt);
+  __syncthreads();
+  float v = 0.f;
+  for (int64_t t = threadIdx.x; t < cnt; t += 256) {
+    const float d = x[at(t)] - mean;
+    v += d * d;
+  }
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (static_cast<int>(threadIdx.x) < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  const float inv = 1.f / sqrtf(red[0] / static_cast<float>(cnt) + eps);
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  for (int64_t t = threadIdx.x; t < cnt; t += 256) {
+    float o = (x[at(t)] - mean) * inv * gm + bt;
+    if (relu && o < 0.f) o = 0.f;
+    y[at(t)] = o;
+  }
+  if (threadIdx.x == 0) {
+    aux[c] = mean;
+    aux[C + c] = inv;
+  }
+}
+__global__ __launch_bounds__(256) void k_bn_bwd(const float* dy, const float* x, const float* y, const float* gamma,
+                                                const float* aux, float* dx, float* dgamma, float* dbeta, int N,
+                                                int C, int64_t S, int relu) {
+  __shared__ float ra[256], rb[256];
+  const int c = blockIdx.x;
+  const int64_t cnt = static_cast<int64_t>(N) * S;
+  auto at = [&](int64_t t) { return (t / S * C + c) * S + t % S; };
+  const float mean = aux[c], inv = aux[C + c];
+  float sg = 0.f, sgx = 0.f;
+  for (int64_t t = threadIdx.x; t < cnt; t += 256) {
+    const int64_t i = at(t);
+    float gv = dy[i];
+    if (relu && y[i] <= 0.f) gv = 0.f;
+    sg += gv;
+    sgx += gv * (x[i] - mean) * inv;
+  }
+  ra[threadIdx.x] = sg;
+  rb[threadIdx.x] = sgx;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (static_cast<int>(threadIdx.x) < k) {
+      ra[threadIdx.x] += ra[threadIdx.x + k];
+      rb[threadIdx.x] += rb[threadIdx.x + k];
+    }
+    __syncthreads();
+  }
+  sg = ra[0];
+  sgx = rb[0];
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] += sgx;
+    if (dbeta) dbeta[c] += sg;
+  }
+  if (!dx) return;
+  const float gm = gamma ? gamma[c] : 1.f, fc = static_cast<float>(cnt);
+  for (int64_t t = threadIdx.x; t < cnt; t += 256) {
+    const int64_t i = at(t);
+    float gv = dy[i];
+    if (relu && y[i] <= 0.f) gv = 0.f;
+    const float xh = (x[i] - mean) * inv;
+    dx[i] += gm * inv * (gv - sg / fc - xh * sgx / fc);
+  }
+}
+
 int grid_of(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))); }
 
 int dact_of(const std::string& s) {
@@ -280,6 +522,17 @@ std::string unsupported(const ComputationGraph& cg, int n) {
     if (!a.empty() && a != "none" && dact_of(a) == A_NONE) return "LINEAR activation " + a;
     return "";
   }
+  if (t == OpType::CONV2D || t == OpType::POOL2D) {
+    const std::string a = node.label.op.s("activation");
+    if (!a.empty() && a != "none" && dact_of(a) == A_NONE) return to_string(t) + " activation " + a;
+    if (cg.shape(cg.layer_data_inputs(n)[0]).dims.size() != 4) return to_string(t) + " on a non-4-D tensor";
+    if (t == OpType::POOL2D) {
+      const std::string pt = node.label.op.s("pool_type");
+      if (pt != "max" && pt != "avg") return "pool type " + pt;
+    }
+    return "";
+  }
+  if (t == OpType::BATCHNORM) return "";
   if (dact_of(t) >= 0 || binary_of(t) >= 0 || scalar_of(t) >= 0 || is_view(t) || t == OpType::SOFTMAX) {
     if (binary_of(t) >= 0) {
       auto ins = cg.layer_data_inputs(n);
@@ -311,9 +564,15 @@ class DeviceTrainingBacking final : public TrainingBacking {
     }
     for (int n : host_.order()) {
       const auto& node = cg_.g.node(n);
-      if (node.label.op.type == OpType::LINEAR && dact_of(node.label.op.s("activation")) != A_NONE)
-        want.push_back({Key{{n, 0}, 2}, host_.slot({n, 0}, false)->numel()});   // pre-activation
-      tmp_elems_ = std::max(tmp_elems_, host_.slot({n, 0}, false)->numel());
+      const OpType t = node.label.op.type;
+      const int64_t ne = host_.slot({n, 0}, false)->numel();
+      if ((t == OpType::LINEAR || t == OpType::CONV2D || t == OpType::POOL2D) &&
+          dact_of(node.label.op.s("activation")) != A_NONE)
+        want.push_back({Key{{n, 0}, 2}, ne});   // pre-activation
+      if (t == OpType::POOL2D) want.push_back({Key{{n, 0}, 3}, ne});   // argmax / window counts
+      if (t == OpType::BATCHNORM)
+        want.push_back({Key{{n, 0}, 3}, 2 * host_.slot(cg_.layer_data_inputs(n)[0], false)->dims.at(1)});
+      tmp_elems_ = std::max(tmp_elems_, ne);
     }
     const ValueRef out = host_.output();
     rows_ = 1;
@@ -396,7 +655,7 @@ class DeviceTrainingBacking final : public TrainingBacking {
  private:
   struct Key {
     ValueRef v;
-    int kind;  // 0 value, 1 gradient, 2 pre-activation
+    int kind;  // 0 value, 1 gradient, 2 pre-activation, 3 operator aux (argmax, BN statistics)
     bool operator<(const Key& o) const { return v < o.v || (v == o.v && kind < o.kind); }
   };
   struct Buf {
@@ -442,6 +701,25 @@ class DeviceTrainingBacking final : public TrainingBacking {
   mutable LocalMetrics metrics_;
 };
 
+CG conv_geom_of(const HostTensor& x, const HostTensor& y, const OpAttrs& op, bool pool) {
+  CG g{};
+  g.N = static_cast<int>(x.dims[0]);
+  g.C = static_cast<int>(x.dims[1]);
+  g.H = static_cast<int>(x.dims[2]);
+  g.W = static_cast<int>(x.dims[3]);
+  g.O = static_cast<int>(y.dims[1]);
+  g.OH = static_cast<int>(y.dims[2]);
+  g.OW = static_cast<int>(y.dims[3]);
+  g.KH = static_cast<int>(op.i("kernel_h"));
+  g.KW = static_cast<int>(op.i("kernel_w"));
+  g.SH = static_cast<int>(op.i("stride_h"));
+  g.SW = static_cast<int>(op.i("stride_w"));
+  g.PH = static_cast<int>(op.i("padding_h"));
+  g.PW = static_cast<int>(op.i("padding_w"));
+  g.G = pool ? 1 : static_cast<int>(op.i("groups"));
+  return g;
+}
+
 void DeviceTrainingBacking::fwd(int n) {
   const auto& node = cg_.g.node(n);
   const OpAttrs& op = node.label.op;
@@ -458,6 +736,28 @@ void DeviceTrainingBacking::fwd(int n) {
     float* pre = a != A_NONE ? buf_.at(Key{o, 2}).p : nullptr;
     ffk::gemm_f32(val(ins[0]), val(ws[0]), y, ws.size() > 1 ? val(ws[1]) : nullptr, pre, rows, outc, in, in, outc,
                   outc, false, false, gemm_act(a), 1.f, 0.f, 1, 1, st_);
+  } else if (t == OpType::CONV2D || t == OpType::POOL2D) {
+    const bool pool = t == OpType::POOL2D;
+    const CG g = conv_geom_of(*host_.slot(ins[0], false), *host_.slot(o, false), op, pool);
+    const int a = dact_of(op.s("activation"));
+    float* pre = a != A_NONE ? buf_.at(Key{o, 2}).p : nullptr;
+    if (pool) {
+      hipLaunchKernelGGL(k_pool_fwd, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), y, pre,
+                         buf_.at(Key{o, 3}).p, g, op.s("pool_type") == "max" ? 1 : 0, a);
+    } else {
+      const auto ws = cg_.layer_weights(n);
+      hipLaunchKernelGGL(k_conv_fwd, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), val(ws[0]),
+                         ws.size() > 1 ? val(ws[1]) : nullptr, y, pre, g, a);
+    }
+  } else if (t == OpType::BATCHNORM) {
+    const auto& xd = host_.slot(ins[0], false)->dims;
+    int64_t S = 1;
+    for (size_t k = 2; k < xd.size(); ++k) S *= xd[k];
+    const auto ws = cg_.layer_weights(n);
+    hipLaunchKernelGGL(k_bn_fwd, dim3(static_cast<unsigned>(xd[1])), dim3(256), 0, st_, val(ins[0]),
+                       ws.size() > 0 ? val(ws[0]) : nullptr, ws.size() > 1 ? val(ws[1]) : nullptr, y,
+                       buf_.at(Key{o, 3}).p, static_cast<int>(xd[0]), static_cast<int>(xd[1]), S,
+                       static_cast<float>(op.f("eps")), op.b("relu") ? 1 : 0);
   } else if (dact_of(t) >= 0) {
     hipLaunchKernelGGL(k_act, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), y, ne, dact_of(t));
   } else if (binary_of(t) >= 0) {
@@ -508,6 +808,40 @@ void DeviceTrainingBacking::bwd(int n) {
     if (float* dx = grad(ins[0]))   // dX += g W^T
       ffk::gemm_f32(g, val(ws[0]), dx, nullptr, nullptr, rows, in, outc, outc, outc, in, false, true, 0, 1.f, 1.f, 1,
                     1, st_);
+  } else if (t == OpType::CONV2D) {
+    const CG g = conv_geom_of(*host_.slot(ins[0], false), *host_.slot(o, false), op, false);
+    const int a = dact_of(op.s("activation"));
+    const float* gy = dy;
+    if (a != A_NONE) {
+      hipLaunchKernelGGL(k_act_grad, dim3(grid_of(ne)), dim3(256), 0, st_, dy, buf_.at(Key{o, 2}).p, tmp_, ne, a);
+      gy = tmp_;
+    }
+    const auto ws = cg_.layer_weights(n);
+    if (float* dw = grad(ws[0]))
+      hipLaunchKernelGGL(k_conv_wgrad, dim3(static_cast<unsigned>(numel(ws[0]))), dim3(256), 0, st_, gy,
+                         val(ins[0]), dw, g);
+    if (ws.size() > 1)
+      if (float* db = grad(ws[1]))
+        hipLaunchKernelGGL(k_chan_sum, dim3(static_cast<unsigned>(g.O)), dim3(256), 0, st_, gy, db, g.N, g.O,
+                           static_cast<int64_t>(g.OH) * g.OW);
+    if (float* dx = grad(ins[0]))
+      hipLaunchKernelGGL(k_conv_dgrad, dim3(grid_of(numel(ins[0]))), dim3(256), 0, st_, gy, val(ws[0]), dx, g);
+  } else if (t == OpType::POOL2D) {
+    const CG g = conv_geom_of(*host_.slot(ins[0], false), *host_.slot(o, false), op, true);
+    const int a = dact_of(op.s("activation"));
+    if (float* dx = grad(ins[0]))
+      hipLaunchKernelGGL(k_pool_bwd, dim3(grid_of(ne)), dim3(256), 0, st_, dy,
+                         a != A_NONE ? buf_.at(Key{o, 2}).p : nullptr, buf_.at(Key{o, 3}).p, dx, g,
+                         op.s("pool_type") == "max" ? 1 : 0, a);
+  } else if (t == OpType::BATCHNORM) {
+    const auto& xd = host_.slot(ins[0], false)->dims;
+    int64_t S = 1;
+    for (size_t k = 2; k < xd.size(); ++k) S *= xd[k];
+    const auto ws = cg_.layer_weights(n);
+    hipLaunchKernelGGL(k_bn_bwd, dim3(static_cast<unsigned>(xd[1])), dim3(256), 0, st_, dy, val(ins[0]), val(o),
+                       ws.size() > 0 ? val(ws[0]) : nullptr, buf_.at(Key{o, 3}).p, grad(ins[0]),
+                       ws.size() > 0 ? grad(ws[0]) : nullptr, ws.size() > 1 ? grad(ws[1]) : nullptr,
+                       static_cast<int>(xd[0]), static_cast<int>(xd[1]), S, op.b("relu") ? 1 : 0);
   } else if (dact_of(t) >= 0) {
     if (float* dx = grad(ins[0]))
       hipLaunchKernelGGL(k_act_bwd, dim3(grid_of(ne)), dim3(256), 0, st_, dy, val(ins[0]), dx, ne, dact_of(t));

@@ -171,6 +171,7 @@ static int test_cnn(flexflow_config_t cfg) {
   flexflow_model_set_adam_optimizer(model, adam);
   int metrics[1] = {METRICS_ACCURACY};
   flexflow_model_compile(model, LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics, 1, COMP_MODE_TRAINING);
+  printf("cnn device %s\n", flexflow_model_get_device(model));
   float img[N * C * H * W];
   int lab[N];
   for (int i = 0; i < N * C * H * W; ++i) img[i] = sinf(0.37f * (float)i);
@@ -248,6 +249,57 @@ static void test_parity(flexflow_config_t cfg) {
   flexflow_model_destroy(model);
 }
 
+/* the CNN path (conv + relu, batch norm, max / avg pooling, flat, dense,
+ * softmax + cross-entropy) for three Adam steps, the conv kernel printed:
+ * GPU and CPU backings must agree (tests/test_runtime_c_gpu.py) */
+static void test_parity_cnn(flexflow_config_t cfg) {
+  enum { N = 4, C = 3, H = 10, W = 10 };
+  flexflow_model_t model = flexflow_model_create(cfg);
+  int dims[4] = {N, C, H, W};
+  flexflow_tensor_t x = flexflow_tensor_create(model, 4, dims, DT_FLOAT, true);
+  flexflow_initializer_t null_init = flexflow_initializer_create_null();
+  flexflow_op_t no_op = {NULL};
+  flexflow_tensor_t t = flexflow_model_add_conv2d(model, x, 6, 3, 3, 1, 1, 1, 1, AC_MODE_RELU, 1, true, no_op,
+                                                  null_init, null_init, "pc1");
+  t = flexflow_model_add_batch_norm(model, t, true, "pbn");
+  t = flexflow_model_add_pool2d(model, t, 2, 2, 2, 2, 0, 0, POOL_MAX, AC_MODE_NONE, "ppool");
+  t = flexflow_model_add_conv2d(model, t, 4, 3, 3, 2, 2, 1, 1, AC_MODE_TANH, 1, true, no_op, null_init, null_init,
+                                "pc2");
+  t = flexflow_model_add_pool2d(model, t, 2, 2, 1, 1, 1, 1, POOL_AVG, AC_MODE_NONE, "pavg");
+  t = flexflow_model_add_flat(model, t, "pflat");
+  t = flexflow_model_add_dense(model, t, 3, AC_MODE_NONE, true, DT_FLOAT, no_op, null_init, null_init,
+                               REG_MODE_NONE, 0.f, "phead");
+  t = flexflow_model_add_softmax(model, t, -1, "psm");
+  flexflow_adam_optimizer_t adam = flexflow_adam_optimizer_create(model, 0.01, 0.9, 0.999, 0.0, 1e-8);
+  flexflow_model_set_adam_optimizer(model, adam);
+  int metrics[1] = {METRICS_ACCURACY};
+  flexflow_model_compile(model, LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics, 1, COMP_MODE_TRAINING);
+  float img[N * C * H * W];
+  int lab[N];
+  for (int i = 0; i < N * C * H * W; ++i) img[i] = sinf(0.23f * (float)i) + 0.1f * cosf(0.05f * (float)i);
+  for (int i = 0; i < N; ++i) lab[i] = i % 3;
+  int ldims[2] = {N, 1};
+  flexflow_tensor_set_tensor_float(x, model, 4, dims, img);
+  flexflow_tensor_set_tensor_int(flexflow_model_get_label_tensor(model), model, 2, ldims, lab);
+  for (int step = 0; step < 3; ++step) {
+    flexflow_model_forward(model, -1);
+    flexflow_model_zero_gradients(model);
+    flexflow_model_backward(model, -1);
+    flexflow_model_update(model);
+  }
+  flexflow_op_t c1 = flexflow_model_get_layer_by_id(model, 0);
+  float w[6 * 3 * 3 * 3];
+  flexflow_parameter_get_weights_float(flexflow_op_get_parameter_by_id(c1, 0), model, w);
+  double sum = 0.0, asum = 0.0;
+  for (int i = 0; i < 6 * 27; ++i) {
+    sum += w[i];
+    asum += fabs(w[i]);
+  }
+  printf("parity_cnn device %s w_sum %.9g w_abs %.9g w_0 %.9g\n", flexflow_model_get_device(model), sum, asum, w[0]);
+  flexflow_adam_optimizer_destroy(adam);
+  flexflow_model_destroy(model);
+}
+
 static void test_configs(void) {
   char* argv[] = {"prog", "-b", "32", "--epochs", "3", "--arch-mlp-bot", "13-512-256-64", "--arch-embedding-size",
                   "1000-1000", "--arch-sparse-feature-size", "64", "--dataset", "/tmp/x.h5", "-ll:gpu", "8"};
@@ -284,6 +336,7 @@ int main(int argc, char** argv) {
   test_mlp(cfg);
   test_cnn(cfg);
   test_parity(cfg);
+  test_parity_cnn(cfg);
   flexflow_config_destroy(cfg);
   finish_flexflow_task();
   printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
