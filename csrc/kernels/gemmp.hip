@@ -532,6 +532,10 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
       n = 256;
     return std::max(8, n);
   }();
+  if (p.variant == 11 && splits == 1 && gemmpp_supported(p)) {
+    gemmpp_launch(p, st);
+    return;
+  }
   if (p.variant == 9 && splits == 1 && gemmn_supported(p)) {
     gemmn_launch(p, st);
     return;

@@ -139,7 +139,8 @@ struct GemmPParams {
                                 // 3 / 4: one wave per SIMD, 128x128 wave tile, B staged
                                 // through registers / by LDS-DMA (gemmt.hip),
                                 // 8: 64x64 tiles for MLP-sized products (gemms.hip),
-                                // 9: eight-wave multistage NT kernel (gemmn.hip; other layouts -> gemmq)
+                                // 9: eight-wave multistage NT kernel (gemmn.hip; other layouts -> gemmq),
+                                // 11: eight-wave ping-pong A B^T kernel (gemmpp.hip; other layouts -> gemmq)
 };
 bool gemmp_supported(int M, int N, int K, int lda, int ldb, bool trans_a, bool trans_b);
 void gemmp_bf16(const GemmPParams& p, hipStream_t st);
@@ -150,6 +151,9 @@ bool gemmt_supported(const GemmPParams& p);
 // eight-wave multistage NT GEMM, variant 9 (gemmn.hip)
 bool gemmn_supported(const GemmPParams& p);
 void gemmn_launch(const GemmPParams& p, hipStream_t st);
+// eight-wave ping-pong A B^T GEMM, variant 11 (gemmpp.hip)
+bool gemmpp_supported(const GemmPParams& p);
+void gemmpp_launch(const GemmPParams& p, hipStream_t st);
 // small-tile (64 x 64) MLP GEMM, variant 8 (gemms.hip)
 bool gemms_supported(const GemmPParams& p);
 void gemms_launch(const GemmPParams& p, int splits, hipStream_t st);

@@ -317,6 +317,11 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
         if trans_b and not trans_a and bias is None and act == "none" and pre is None \
                 and os.environ.get("FF_GEMMN", "1") != "0":
             c["n:1"] = lambda *args: _gt(*args, splits=1, variant=9)
+        if trans_b and not trans_a and act == "none" and pre is None and Kd // 64 >= 2 \
+                and (out is None or out.dtype == torch.bfloat16) and os.environ.get("FF_GEMMPP", "1") != "0":
+            # eight-wave ping-pong A B^T kernel (gemmpp.hip, variant 11): plain,
+            # accumulate (beta) and bias epilogues
+            c["y:1"] = lambda *args: _gt(*args, splits=1, variant=11)
         if _small_mn(M, N) and os.environ.get("FF_GEMMS", "1") != "0":
             c["s:1"] = _gs
             if bias is None and act == "none" and pre is None:
@@ -565,6 +570,8 @@ def _resolve(name: str):
         return lambda *args: _gs(*args, splits=int(arg))
     if kind == "n":
         return lambda *args: _gt(*args, splits=1, variant=9)
+    if kind == "y":
+        return lambda *args: _gt(*args, splits=1, variant=11)
     return lambda *args: _hip256(*args, splits=int(arg))
 
 

@@ -6,6 +6,8 @@ asymmetric (guide: never validate MFMA layouts with symmetric operands).
 """
 import math
 
+import functools
+
 import pytest
 import torch
 
@@ -356,9 +358,9 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
         assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10],
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11],
                          ids=["mfma32x32x16", "mfma16x16x32", "pingpong", "wave128", "wave128dma", "wave128pers",
-                              "wave128dma2", "tile64", "nt8wave", "wave128regstage"])
+                              "wave128dma2", "tile64", "nt8wave", "wave128regstage", "pingpong8"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd,splits", [(512, 768, 256, 1), (264, 520, 512, 1), (1024, 1024, 4096, 8),
                                             (296, 136, 1024, 3), (2048, 1536, 640, 1),
@@ -418,6 +420,26 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
             assert _rel(db, gr.sum(0) + 0.5) < 1e-3
         else:              # the other kernels sum the stored bf16 values
             assert _rel(db, g.float().sum(0) + 0.5) < 1e-4
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 4, 5, 6])
+@pytest.mark.parametrize("M,N,Kd", [(512, 768, 128), (264, 520, 512), (1040, 264, 1216), (2048, 1024, 3072)])
+def test_gemmpp_modes(mode, M, N, Kd):
+    """Eight-wave ping-pong A B^T kernel (gemmpp.hip, variant 11) in every
+    DMA / priority mode (GemmPParams.dbg = 16 | mode): plain, bf16 accumulate
+    and bias epilogues against the fp32 product of the same bf16 operands,
+    partial edge tiles included."""
+    torch.manual_seed(5)
+    a = torch.randn(M, Kd, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(N, Kd, device=DEV, dtype=torch.bfloat16)
+    ref = a.float() @ b.float().t()
+    run = functools.partial(K.gemmp, a, b, trans_b=True, variant=11, _dbg=16 | mode)
+    assert _rel(run(), ref) < 3e-3
+    c = torch.full((M, N), 0.5, device=DEV, dtype=torch.bfloat16)
+    run(beta=1.0, out=c)
+    assert _rel(c, ref + 0.5) < 3e-3
+    bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    assert _rel(run(bias=bias), ref + bias.float()) < 3e-3
 
 
 def test_dropout_and_cast():

@@ -87,8 +87,11 @@ def main():
             for pre, var in variants.items():
                 cands[f"{pre}{sp}"] = (lambda o, sp=sp, var=var:
                                        K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt, splits=sp, variant=var))
-        if tb and not ta:   # the eight-wave NT kernel (gemmn.hip)
+        if tb and not ta:   # the eight-wave NT kernels (gemmn.hip, gemmpp.hip modes 0-3 as y0-y3)
             cands["n1"] = lambda o: K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt, variant=9)
+            for md in (1, 2, 5, 6):   # bits 0-1: DMA split (1: A / B by group, 2: A triple-buffered), bit 2: setprio
+                cands[f"y{md}"] = (lambda o, md=md:
+                                   K.gemmp(a, b, trans_a=ta, trans_b=tb, out=o, beta=bt, variant=11, _dbg=16 | md))
         if args.cands:
             keep = args.cands.split(",")
             cands = {k: v for k, v in cands.items() if k == "blaslt" and "blaslt" in keep
