@@ -37,6 +37,19 @@ namespace {
 constexpr int BM = 128, BK = 64;
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
+// n / d for n < 2^31 as (umulhi(n, m) + n) >> l, l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1 (division by invariant integers)
+struct FastDiv {
+  unsigned m;
+  int l;
+};
+inline FastDiv make_fdiv(unsigned d) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = (((1ull << l) - d) << 32) / d + 1;
+  return FastDiv{static_cast<unsigned>(m), l};
+}
+
 struct ConvArgs {
   const bf16* x;    // FWD/WGRAD input  [N][H][W][C]
   const bf16* w;    // FWD/DGRAD weight [K][R][S][C]
@@ -55,6 +68,9 @@ struct ConvArgs {
   // h % sh == pch, w % sw == pcw (Hc x Wc per image); the K axis runs only over
   // the taps r = rf + i*sh (i < nr), s = sf + j*sw (j < ns) that reach them.
   int par, pch, pcw, Hc, Wc, rf, sf, nr, ns;
+  // magic divisors of the loaders and the operands' byte sizes (buffer range)
+  FastDiv fC, fS, fK, fQ, fP, fW, fH, fWc, fHc, fns, fsh, fsw;
+  unsigned bx, bw, bdy;
 };
 
 // DGRAD output row of local row m (parity classes scatter to the full image)
@@ -63,18 +79,6 @@ __device__ __forceinline__ int64_t dgrad_row(const ConvArgs& g, int m) {
   const int ww = m % g.Wc, t = m / g.Wc, hh = t % g.Hc, n = t / g.Hc;
   return (static_cast<int64_t>(n) * g.H + hh * g.sh + g.pch) * g.W + ww * g.sw + g.pcw;
 }
-// (r, s) of tap index rs of the K axis
-__device__ __forceinline__ void tap_of(const ConvArgs& g, int rs, int& r, int& s) {
-  if (g.par) {
-    const int j = rs % g.ns, i = rs / g.ns;
-    r = g.rf + i * g.sh;
-    s = g.sf + j * g.sw;
-  } else {
-    s = rs % g.S;
-    r = rs / g.S;
-  }
-}
-
 __device__ __forceinline__ float conv_act(int act, float x) {
   switch (act) {
     case 1: return x > 0.f ? x : 0.f;
@@ -85,19 +89,45 @@ __device__ __forceinline__ float conv_act(int act, float x) {
   }
 }
 
-__device__ __forceinline__ bf16x8 ld8(const bf16* p, bool ok) {
-  return ok ? *reinterpret_cast<const bf16x8*>(p) : bf16x8{};
+// Branch-free gathers: every 16-B chunk is one buffer_load_dwordx4 whose
+// offset is replaced by the tensor's byte size when the chunk is padding or
+// past an edge (the buffer range check returns zeros), so the loaders carry
+// no exec-mask branches; 32-bit offsets (check_shape bounds every tensor
+// below 2^31 elements) and host-computed magic divisors (FastDiv) replace the
+// 64-bit multiply-adds and integer divisions of the per-chunk address math.
+__device__ __forceinline__ unsigned fdiv(unsigned n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.l; }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t conv_rsrc(const bf16* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p), static_cast<short>(0), bytes, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 bld8(__amdgpu_buffer_rsrc_t r, int eoff, bool ok, unsigned oob) {
+  const unsigned off = ok ? static_cast<unsigned>(eoff) * 2u : oob;
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// (r, s) of tap index rs of the DGRAD K axis
+__device__ __forceinline__ void tap_of_f(const ConvArgs& g, int rs, int& r, int& s) {
+  if (g.par) {
+    const int i = static_cast<int>(fdiv(static_cast<unsigned>(rs), g.fns)), j = rs - i * g.ns;
+    r = g.rf + i * g.sh;
+    s = g.sf + j * g.sw;
+  } else {
+    r = static_cast<int>(fdiv(static_cast<unsigned>(rs), g.fS));
+    s = rs - r * g.S;
+  }
 }
 
 // ---------------------------------------------------------------------------
 // A operand, K-contiguous image [128 rows = m][64 k], 4 chunks per thread.
 // FWD: m = output pixel (n,p,q), k = (r,s,c).  DGRAD: m = input pixel (n,h,w),
-// k = (r,s,kout).  The pixel decode happens once; the tap decode once per tile.
+// k = (r,s,kout).  The pixel decode happens once; the thread's tap (its k =
+// k0 + 8 (tid & 7)) advances by 64 per K-tile without a division.
 template <int MODE>
 struct AGather {
   bf16x8 reg[4];
-  int64_t base[4];  // element offset of the image n (NHWC / NPQK)
-  int ya[4], xa[4]; // FWD: p*sh-ph, q*sw-pw ; DGRAD: h+ph, w+pw ; INT_MIN = row past M
+  int pix[4];       // FWD: element offset of x[n][ya][xa][0] (may be negative); DGRAD: of dy[n][0][0][0]
+  int ya[4], xa[4]; // FWD: p*sh-ph, q*sw-pw ; DGRAD: h+ph, w+pw ; -2^30 = row past M
+  int k, cc, r, s, rs;   // the thread's K index and its (channel, tap) decode
 
   __device__ __forceinline__ void init(const ConvArgs& g, int m0) {
 #pragma unroll
@@ -106,61 +136,91 @@ struct AGather {
       if (m >= g.M) {
         ya[i] = -0x3fffffff;
         xa[i] = 0;
-        base[i] = 0;
+        pix[i] = 0;
         continue;
       }
       if (MODE == MODE_FWD) {
-        const int q = m % g.Q, t = m / g.Q, p = t % g.P, n = t / g.P;
+        const int t = static_cast<int>(fdiv(static_cast<unsigned>(m), g.fQ)), q = m - t * g.Q;
+        const int n = static_cast<int>(fdiv(static_cast<unsigned>(t), g.fP)), p = t - n * g.P;
         ya[i] = p * g.sh - g.ph;
         xa[i] = q * g.sw - g.pw;
-        base[i] = static_cast<int64_t>(n) * g.H * g.W * g.C;
+        pix[i] = ((n * g.H + ya[i]) * g.W + xa[i]) * g.C;
       } else {
         int w, h, n;
         if (g.par) {
-          const int ww = m % g.Wc, t = m / g.Wc, hh = t % g.Hc;
-          n = t / g.Hc;
+          const int t = static_cast<int>(fdiv(static_cast<unsigned>(m), g.fWc)), ww = m - t * g.Wc;
+          n = static_cast<int>(fdiv(static_cast<unsigned>(t), g.fHc));
+          const int hh = t - n * g.Hc;
           h = hh * g.sh + g.pch;
           w = ww * g.sw + g.pcw;
         } else {
-          const int t = m / g.W;
-          w = m % g.W;
-          h = t % g.H;
-          n = t / g.H;
+          const int t = static_cast<int>(fdiv(static_cast<unsigned>(m), g.fW));
+          w = m - t * g.W;
+          n = static_cast<int>(fdiv(static_cast<unsigned>(t), g.fH));
+          h = t - n * g.H;
         }
         ya[i] = h + g.ph;
         xa[i] = w + g.pw;
-        base[i] = static_cast<int64_t>(n) * g.P * g.Q * g.K;
+        pix[i] = n * g.P * g.Q * g.K;
       }
+    }
+    k = (threadIdx.x & 7) * 8;   // K-tile 0 (FWD / DGRAD never split K)
+    const int CC = MODE == MODE_FWD ? g.C : g.K;
+    const FastDiv fCC = MODE == MODE_FWD ? g.fC : g.fK;
+    rs = static_cast<int>(fdiv(static_cast<unsigned>(k), fCC));
+    cc = k - rs * CC;
+    if (MODE == MODE_FWD) {
+      r = static_cast<int>(fdiv(static_cast<unsigned>(rs), g.fS));
+      s = rs - r * g.S;
+    } else {
+      tap_of_f(g, rs, r, s);
     }
   }
-  __device__ __forceinline__ void load(const ConvArgs& g, int k0) {
-    const int k = k0 + (threadIdx.x & 7) * 8;
+  // load the current K-tile's chunks, then step the tap to the next K-tile
+  __device__ __forceinline__ void load(const ConvArgs& g, __amdgpu_buffer_rsrc_t rsrc, unsigned oob) {
     const bool kok = k < g.KG;
-    const int CC = MODE == MODE_FWD ? g.C : g.K;
-    const int cc = k % CC, rs = k / CC;
-    int r, s;
     if (MODE == MODE_FWD) {
-      s = rs % g.S;
-      r = rs / g.S;
-    } else {
-      tap_of(g, rs, r, s);
-    }
+      const int rr = r * g.dh, ss = s * g.dw;
+      const int delta = (rr * g.W + ss) * g.C + cc;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bool ok = kok;
-      const bf16* src;
-      if (MODE == MODE_FWD) {
-        const int ih = ya[i] + r * g.dh, iw = xa[i] + s * g.dw;
-        ok = ok && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        src = g.x + base[i] + (static_cast<int64_t>(ih) * g.W + iw) * g.C + cc;
-      } else {
-        const int yn = ya[i] - r * g.dh, xn = xa[i] - s * g.dw;
-        const int oh = yn / g.sh, ow = xn / g.sw;
-        ok = ok && yn >= 0 && xn >= 0 && yn == oh * g.sh && xn == ow * g.sw && oh < g.P && ow < g.Q;
-        src = g.dy + base[i] + (static_cast<int64_t>(oh) * g.Q + ow) * g.K + cc;
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = kok && static_cast<unsigned>(ya[i] + rr) < static_cast<unsigned>(g.H) &&
+                        static_cast<unsigned>(xa[i] + ss) < static_cast<unsigned>(g.W);
+        reg[i] = bld8(rsrc, pix[i] + delta, ok, oob);
       }
-      reg[i] = ld8(src, ok);
+    } else {
+      const int rr = r * g.dh, ss = s * g.dw;
+      const bool unit = g.sh == 1 && g.sw == 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int yn = ya[i] - rr, xn = xa[i] - ss;
+        int oh = yn, ow = xn;
+        bool ok = kok && yn >= 0 && xn >= 0;
+        if (!unit) {   // strided: only the parity class's taps reach these rows
+          oh = static_cast<int>(fdiv(static_cast<unsigned>(max(yn, 0)), g.fsh));
+          ow = static_cast<int>(fdiv(static_cast<unsigned>(max(xn, 0)), g.fsw));
+          ok = ok && yn == oh * g.sh && xn == ow * g.sw;
+        }
+        ok = ok && oh < g.P && ow < g.Q;
+        reg[i] = bld8(rsrc, pix[i] + (oh * g.Q + ow) * g.K + cc, ok, oob);
+      }
     }
+    // next K-tile: k += 64 (channel counts are multiples of 8: C = 8 wraps
+    // eight times, C >= 64 at most once)
+    const int CC = MODE == MODE_FWD ? g.C : g.K;
+    k += BK;
+    cc += BK;
+    while (cc >= CC) {
+      cc -= CC;
+      ++rs;
+      if (MODE == MODE_FWD) {
+        if (++s == g.S) {
+          s = 0;
+          ++r;
+        }
+      }
+    }
+    if (MODE == MODE_DGRAD) tap_of_f(g, rs, r, s);
   }
   __device__ __forceinline__ void store(unsigned char* img) const {
 #pragma unroll
@@ -176,12 +236,13 @@ template <int OUTER>
 struct RowStager {
   static constexpr int NL = OUTER / 32;
   bf16x8 reg[NL];
-  __device__ __forceinline__ void load(const bf16* P, int ld, int outer0, int n_outer, int k0, int K) {
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rsrc, unsigned oob, int ld, int outer0, int n_outer,
+                                       int k0, int K) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = threadIdx.x + 256 * i, r = c >> 3, ch = c & 7;
       const bool ok = (outer0 + r < n_outer) && (k0 + ch * 8 < K);
-      reg[i] = ld8(P + static_cast<int64_t>(outer0 + r) * ld + k0 + ch * 8, ok);
+      reg[i] = bld8(rsrc, (outer0 + r) * ld + k0 + ch * 8, ok, oob);
     }
   }
   __device__ __forceinline__ void store(unsigned char* img) const {
@@ -206,39 +267,55 @@ struct ColStager {
   // KIND 2: per-thread tap (fixed across tiles: the thread's chunk column is fixed)
   int tr_, ts_, tc_;
   bool tok_;
+  // KIND 1: per-chunk (kout, tap index) of the chunk's K row, stepped by 64 per tile
+  int kout_[NL], rsi_[NL];
 
   __device__ __forceinline__ void init(const ConvArgs& g, int outer0) {
     if (KIND == 2) {
       const int n = outer0 + (threadIdx.x % CPR) * 8;
       tok_ = n < g.NG;
-      tc_ = n % g.C;
-      const int rs = n / g.C;
-      ts_ = rs % g.S;
-      tr_ = rs / g.S;
+      const int rs = static_cast<int>(fdiv(static_cast<unsigned>(n), g.fC));
+      tc_ = n - rs * g.C;
+      tr_ = static_cast<int>(fdiv(static_cast<unsigned>(rs), g.fS));
+      ts_ = rs - tr_ * g.S;
+    }
+    if (KIND == 1) {   // K-tile 0 (DGRAD never splits K)
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int k = (threadIdx.x + 256 * i) / CPR;
+        rsi_[i] = static_cast<int>(fdiv(static_cast<unsigned>(k), g.fK));
+        kout_[i] = k - rsi_[i] * g.K;
+      }
     }
   }
-  __device__ __forceinline__ void load(const ConvArgs& g, const bf16* P, int ld, int outer0, int n_outer, int k0,
-                                       int K) {
+  __device__ __forceinline__ void load(const ConvArgs& g, __amdgpu_buffer_rsrc_t rsrc, unsigned oob, int ld,
+                                       int outer0, int n_outer, int k0, int K) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = threadIdx.x + 256 * i, r = c / CPR, ch = c % CPR;
       const int k = k0 + r, o = outer0 + ch * 8;
       bool ok = (k < K) && (o < n_outer);
-      const bf16* src;
+      int off;
       if (KIND == 0) {
-        src = P + static_cast<int64_t>(k) * ld + o;
+        off = k * ld + o;
       } else if (KIND == 1) {
-        const int kout = k % g.K, rs = k / g.K;
         int rr, s;
-        tap_of(g, rs, rr, s);
-        src = g.w + ((static_cast<int64_t>(kout) * g.R + rr) * g.S + s) * g.C + o;
+        tap_of_f(g, rsi_[i], rr, s);
+        off = ((kout_[i] * g.R + rr) * g.S + s) * g.C + o;
+        kout_[i] += BK;   // next K-tile (K >= 8: wraps at most 8 times)
+        while (kout_[i] >= g.K) {
+          kout_[i] -= g.K;
+          ++rsi_[i];
+        }
       } else {
-        const int q = k % g.Q, t = k / g.Q, p = t % g.P, n = t / g.P;
+        const int t = static_cast<int>(fdiv(static_cast<unsigned>(k), g.fQ)), q = k - t * g.Q;
+        const int n = static_cast<int>(fdiv(static_cast<unsigned>(t), g.fP)), p = t - n * g.P;
         const int ih = p * g.sh - g.ph + tr_ * g.dh, iw = q * g.sw - g.pw + ts_ * g.dw;
-        ok = ok && tok_ && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        src = g.x + ((static_cast<int64_t>(n) * g.H + ih) * g.W + iw) * g.C + tc_;
+        ok = ok && tok_ && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+             static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
+        off = ((n * g.H + ih) * g.W + iw) * g.C + tc_;
       }
-      reg[i] = ld8(src, ok);
+      reg[i] = bld8(rsrc, off, ok, oob);
     }
   }
   __device__ __forceinline__ void store(unsigned char* img) const {
@@ -293,17 +370,18 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   ColStager<BN, 1> bdg;
   ColStager<BN, 2> bwg;
 
+  const __amdgpu_buffer_rsrc_t rx = conv_rsrc(g.x, g.bx), rw = conv_rsrc(g.w, g.bw), rdy = conv_rsrc(g.dy, g.bdy);
   auto load = [&](int kt) {
     const int k0 = kt * BK;
     if (MODE == MODE_FWD) {
-      afw.load(g, k0);
-      bfw.load(g.w, g.KG, n0, g.NG, k0, g.KG);
+      afw.load(g, rx, g.bx);
+      bfw.load(rw, g.bw, g.KG, n0, g.NG, k0, g.KG);
     } else if (MODE == MODE_DGRAD) {
-      adg.load(g, k0);
-      bdg.load(g, nullptr, 0, n0, g.NG, k0, g.KG);
+      adg.load(g, rdy, g.bdy);
+      bdg.load(g, rw, g.bw, 0, n0, g.NG, k0, g.KG);
     } else {
-      awg.load(g, g.dy, g.K, m0, g.M, k0, g.KG);
-      bwg.load(g, nullptr, 0, n0, g.NG, k0, g.KG);
+      awg.load(g, rdy, g.bdy, g.K, m0, g.M, k0, g.KG);
+      bwg.load(g, rx, g.bx, 0, n0, g.NG, k0, g.KG);
     }
   };
   auto store = [&](unsigned char* buf) {
@@ -320,7 +398,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   };
 
   if (MODE == MODE_FWD) afw.init(g, m0);
-  if (MODE == MODE_DGRAD) adg.init(g, m0);
+  if (MODE == MODE_DGRAD) {
+    adg.init(g, m0);
+    bdg.init(g, n0);
+  }
   if (MODE == MODE_WGRAD) bwg.init(g, n0);
 
   f32x16 acc[NTN][2];
@@ -539,6 +620,19 @@ ConvArgs make_args(const ConvShape& cs) {
   g.sh = cs.sh; g.sw = cs.sw; g.ph = cs.ph; g.pw = cs.pw; g.dh = cs.dh; g.dw = cs.dw;
   g.P = (cs.H + 2 * cs.ph - cs.dh * (cs.R - 1) - 1) / cs.sh + 1;
   g.Q = (cs.W + 2 * cs.pw - cs.dw * (cs.S - 1) - 1) / cs.sw + 1;
+  g.fC = make_fdiv(cs.C);
+  g.fS = make_fdiv(cs.S);
+  g.fK = make_fdiv(cs.K);
+  g.fQ = make_fdiv(g.Q);
+  g.fP = make_fdiv(g.P);
+  g.fW = make_fdiv(cs.W);
+  g.fH = make_fdiv(cs.H);
+  g.fsh = make_fdiv(cs.sh);
+  g.fsw = make_fdiv(cs.sw);
+  g.fWc = g.fHc = g.fns = make_fdiv(1);
+  g.bx = static_cast<unsigned>(static_cast<int64_t>(cs.N) * cs.H * cs.W * cs.C * 2);
+  g.bdy = static_cast<unsigned>(static_cast<int64_t>(cs.N) * g.P * g.Q * cs.K * 2);
+  g.bw = static_cast<unsigned>(static_cast<int64_t>(cs.K) * cs.R * cs.S * cs.C * 2);
   return g;
 }
 
@@ -620,6 +714,9 @@ void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, 
         g.sf = (pcw + g.pw) % g.sw;
         g.nr = g.rf < g.R ? (g.R - 1 - g.rf) / g.sh + 1 : 0;
         g.ns = g.sf < g.S ? (g.S - 1 - g.sf) / g.sw + 1 : 0;
+        g.fWc = make_fdiv(g.Wc);
+        g.fHc = make_fdiv(g.Hc);
+        g.fns = make_fdiv(std::max(g.ns, 1));
         g.M = g.N * g.Hc * g.Wc;
         g.KG = g.nr * g.ns * g.K;
         const int blocks = ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn);
