@@ -184,8 +184,10 @@ struct AGather {
       const int delta = (rr * g.W + ss) * g.C + cc;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bool ok = kok && static_cast<unsigned>(ya[i] + rr) < static_cast<unsigned>(g.H) &&
-                        static_cast<unsigned>(xa[i] + ss) < static_cast<unsigned>(g.W);
+        // bitwise & (no short-circuit): hipcc otherwise branches on kok around the
+        // loads and serialises them with vmcnt(0) waits on the reused registers
+        const bool ok = kok & (static_cast<unsigned>(ya[i] + rr) < static_cast<unsigned>(g.H)) &
+                        (static_cast<unsigned>(xa[i] + ss) < static_cast<unsigned>(g.W));
         reg[i] = bld8(rsrc, pix[i] + delta, ok, oob);
       }
     } else {
@@ -195,13 +197,13 @@ struct AGather {
       for (int i = 0; i < 4; ++i) {
         const int yn = ya[i] - rr, xn = xa[i] - ss;
         int oh = yn, ow = xn;
-        bool ok = kok && yn >= 0 && xn >= 0;
+        bool ok = kok & (yn >= 0) & (xn >= 0);
         if (!unit) {   // strided: only the parity class's taps reach these rows
           oh = static_cast<int>(fdiv(static_cast<unsigned>(max(yn, 0)), g.fsh));
           ow = static_cast<int>(fdiv(static_cast<unsigned>(max(xn, 0)), g.fsw));
-          ok = ok && yn == oh * g.sh && xn == ow * g.sw;
+          ok = ok & (yn == oh * g.sh) & (xn == ow * g.sw);
         }
-        ok = ok && oh < g.P && ow < g.Q;
+        ok = ok & (oh < g.P) & (ow < g.Q);
         reg[i] = bld8(rsrc, pix[i] + (oh * g.Q + ow) * g.K + cc, ok, oob);
       }
     }
@@ -241,7 +243,7 @@ struct RowStager {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = threadIdx.x + 256 * i, r = c >> 3, ch = c & 7;
-      const bool ok = (outer0 + r < n_outer) && (k0 + ch * 8 < K);
+      const bool ok = (outer0 + r < n_outer) & (k0 + ch * 8 < K);
       reg[i] = bld8(rsrc, (outer0 + r) * ld + k0 + ch * 8, ok, oob);
     }
   }
@@ -294,7 +296,7 @@ struct ColStager {
     for (int i = 0; i < NL; ++i) {
       const int c = threadIdx.x + 256 * i, r = c / CPR, ch = c % CPR;
       const int k = k0 + r, o = outer0 + ch * 8;
-      bool ok = (k < K) && (o < n_outer);
+      bool ok = (k < K) & (o < n_outer);
       int off;
       if (KIND == 0) {
         off = k * ld + o;
@@ -311,8 +313,8 @@ struct ColStager {
         const int t = static_cast<int>(fdiv(static_cast<unsigned>(k), g.fQ)), q = k - t * g.Q;
         const int n = static_cast<int>(fdiv(static_cast<unsigned>(t), g.fP)), p = t - n * g.P;
         const int ih = p * g.sh - g.ph + tr_ * g.dh, iw = q * g.sw - g.pw + ts_ * g.dw;
-        ok = ok && tok_ && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
-             static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
+        ok = ok & tok_ & (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H)) &
+             (static_cast<unsigned>(iw) < static_cast<unsigned>(g.W));
         off = ((n * g.H + ih) * g.W + iw) * g.C + tc_;
       }
       reg[i] = bld8(rsrc, off, ok, oob);
