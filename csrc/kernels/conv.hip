@@ -472,13 +472,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   }
 
   bf16* out = static_cast<bf16*>(g.out);
-  float csum[NTN][4][4], csq[NTN][4][4];
-#pragma unroll
-  for (int nt = 0; nt < NTN; ++nt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) csum[nt][g4][e] = csq[nt][g4][e] = 0.f;
 
   // Epilogue through LDS: lanes own one row x 4 columns of the accumulator
   // (8-byte pieces of many rows), so the tile is first written to an LDS
@@ -489,7 +482,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int ml = wm * 64 + mt * 32 + (lane & 31);
-    const bool mok = m0 + ml < g.M;
 #pragma unroll
     for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
@@ -512,58 +504,70 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        if (mok && n < g.NG) {  // NG % 8 == 0: a 4-group is all in or all out
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float r = bf2f(o[e]);  // statistics of the stored (rounded) value
-            csum[nt][g4][e] += r;
-            csq[nt][g4][e] += r * r;
-          }
-        }
         *reinterpret_cast<bf16x4*>(ctile + ml * ROWB + nl * 2) = o;
       }
   }
   __syncthreads();
-  {
-    constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+  // Row-contiguous stores; a thread's chunks are one 8-column group (ch =
+  // tid % CPR) of every (256 / CPR)-th row, so the BN statistics of the stored
+  // (rounded) values accumulate per thread here, then reduce over the lanes of
+  // that group (xor over lane bits >= log2 CPR) and over the 4 waves in LDS
+  // into one partial row per M tile (reduce_rows folds the tiles): no
+  // 320-shuffle column reduction of accumulator layouts.
+  constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+  const bool want_stats = MODE == MODE_FWD && g.stats != nullptr;
+  float cs[8], cq[8];
 #pragma unroll
-    for (int i = 0; i < BM * CPR / 256; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int ml = c / CPR, ch = c % CPR;
-      const int m = m0 + ml, n = n0 + ch * 8;
-      if (m >= g.M || n >= g.NG) continue;
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(ctile + ml * ROWB + ch * 16);
-      bf16* dst = out + (MODE == MODE_DGRAD ? dgrad_row(g, m) : static_cast<int64_t>(m)) * g.NG + n;
-      if (MODE == MODE_DGRAD && g.beta != 0.f) {
-        const bf16x8 old = *reinterpret_cast<const bf16x8*>(dst);
+  for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + g.beta * bf2f(old[e]));
+  for (int i = 0; i < BM * CPR / 256; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int ml = c / CPR, ch = c % CPR;
+    const int m = m0 + ml, n = n0 + ch * 8;
+    if (m >= g.M || n >= g.NG) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(ctile + ml * ROWB + ch * 16);
+    bf16* dst = out + (MODE == MODE_DGRAD ? dgrad_row(g, m) : static_cast<int64_t>(m)) * g.NG + n;
+    if (MODE == MODE_DGRAD && g.beta != 0.f) {
+      const bf16x8 old = *reinterpret_cast<const bf16x8*>(dst);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + g.beta * bf2f(old[e]));
+    }
+    *reinterpret_cast<bf16x8*>(dst) = v;
+    if (MODE == MODE_FWD && want_stats) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float r = bf2f(v[e]);
+        cs[e] += r;
+        cq[e] += r * r;
       }
-      *reinterpret_cast<bf16x8*>(dst) = v;
     }
   }
-  if (MODE == MODE_FWD && g.stats) {
-    // per-wave column partials (no atomics: a slot per (m tile, wave row));
-    // reduce_rows folds them into the [2][K] statistics
-    float* part = g.stats + static_cast<int64_t>(tm * 2 + wm) * 2 * g.NG;
+  if (MODE == MODE_FWD && want_stats) {
 #pragma unroll
-    for (int nt = 0; nt < NTN; ++nt)
+    for (int o = CPR; o < 64; o <<= 1)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], o, 64);
+        cq[e] += __shfl_xor(cq[e], o, 64);
+      }
+    __syncthreads();   // every wave is done reading the C tile: reuse its LDS
+    float* red = reinterpret_cast<float*>(smem);   // [4 waves][CPR groups][16]
+    if (lane < CPR) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float s = csum[nt][g4][e], q = csq[nt][g4][e];
-#pragma unroll
-          for (int o = 1; o < 32; o <<= 1) {
-            s += __shfl_xor(s, o, 64);
-            q += __shfl_xor(q, o, 64);
-          }
-          const int n = n0 + wn * (BN / 2) + nt * 32 + 8 * g4 + 4 * h + e;
-          if ((lane & 31) == 0 && n < g.NG) {
-            part[n] = s;
-            part[g.NG + n] = q;
-          }
-        }
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * CPR + lane) * 16 + e] = cs[e];
+        red[(wave * CPR + lane) * 16 + 8 + e] = cq[e];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < CPR * 16) {
+      const int chv = threadIdx.x >> 4, vv = threadIdx.x & 15;
+      const float t = red[chv * 16 + vv] + red[(CPR + chv) * 16 + vv] + red[(2 * CPR + chv) * 16 + vv] +
+                      red[(3 * CPR + chv) * 16 + vv];
+      const int n = n0 + chv * 8 + (vv & 7);
+      float* part = g.stats + static_cast<int64_t>(tm) * 2 * g.NG;   // one partial row per M tile
+      if (n < g.NG) part[(vv < 8 ? 0 : g.NG) + n] = t;
+    }
   }
 }
 
@@ -687,7 +691,7 @@ void conv2d_fwd(const ConvShape& cs, const void* x, const void* w, const void* b
   FFK_LAUNCH_CHECK("conv2d_fwd");
   if (stats) {
     const int64_t W = 2 * static_cast<int64_t>(g.NG);
-    reduce_rows(stats_ws, stats, gm * 2, W, 0, stats_ws + static_cast<int64_t>(gm) * 2 * W, st);
+    reduce_rows(stats_ws, stats, gm, W, 0, stats_ws + static_cast<int64_t>(gm) * W, st);
     FFK_LAUNCH_CHECK("conv2d_fwd stats");
   }
 }
