@@ -421,24 +421,31 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
     const unsigned char* Bi = Ai + IMG;
     const bool has_next = kt + 1 < kt1;
     if (has_next) load(kt + 1);
+    // every fragment of the K-tile requested before the first MFMA, so the
+    // LDS latency of k-steps 1-3 hides under the earlier k-steps' MFMAs (one
+    // lgkmcnt wait per k-step group instead of an exposed read per k-step)
+    bf16x8 bf[BK / 16][NTN], af[BK / 16][2];
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8 bf[NTN], af[2];
 #pragma unroll
       for (int t = 0; t < NTN; ++t) {
-        if (MODE == MODE_FWD) bf[t] = row_frag<128>(Bi, wn * (BN / 2) + t * 32, ks * 16, lane);
-        else bf[t] = tr_frag_nat<BN * 2>(Bi, ks * 16, wn * (BN / 2) + t * 32, lane);
+        if (MODE == MODE_FWD) bf[ks][t] = row_frag<128>(Bi, wn * (BN / 2) + t * 32, ks * 16, lane);
+        else bf[ks][t] = tr_frag_nat<BN * 2>(Bi, ks * 16, wn * (BN / 2) + t * 32, lane);
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (MODE == MODE_WGRAD) af[t] = tr_frag_nat<256>(Ai, ks * 16, wm * 64 + t * 32, lane);
-        else af[t] = row_frag<128>(Ai, wm * 64 + t * 32, ks * 16, lane);
+        if (MODE == MODE_WGRAD) af[ks][t] = tr_frag_nat<256>(Ai, ks * 16, wm * 64 + t * 32, lane);
+        else af[ks][t] = row_frag<128>(Ai, wm * 64 + t * 32, ks * 16, lane);
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead (hipcc re-sinks them to save registers)
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks)
 #pragma unroll
       for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) acc[nt][mt] = mfma32(bf[nt], af[mt], acc[nt][mt]);
-    }
+        for (int mt = 0; mt < 2; ++mt) acc[nt][mt] = mfma32(bf[ks][nt], af[ks][mt], acc[nt][mt]);
+    __builtin_amdgcn_sched_barrier(0);
     if (has_next) store(smem + ((kt + 1 - kt0) & 1) * (IMG + IMGB));
     __syncthreads();
   }
