@@ -194,8 +194,11 @@ def write_ninja(targets: list[str]) -> str:
         lines.append(f"build {ro}: cxx_san {os.path.join(ROOT, 'csrc', 'ffi', 'flexflow_runtime_c.cc')}")
         rto = os.path.join("obj", "asan", "test_runtime_c.c.o")
         lines.append(f"build {rto}: cc_san {os.path.join(ROOT, 'csrc', 'ffi', 'test_runtime_c.c')}")
+        # no HIP in the sanitizer build: the host-only make_device_backing
+        hb = os.path.join("obj", "asan", "device_backing_host.cc.o")
+        lines.append(f"build {hb}: cxx_san {os.path.join(ROOT, 'csrc', 'ffi', 'device_backing_host.cc')}")
         exe = os.path.join(ROOT, "bin", "asan", "ffc-runtime-c-test")
-        lines.append(f"build {exe}: link_san {rto} {ro} {' '.join(san_objs)}")
+        lines.append(f"build {exe}: link_san {rto} {ro} {hb} {' '.join(san_objs)}")
         defaults.append(exe)
         for s in sorted(glob.glob(os.path.join(ROOT, "csrc", "tools", "*.cc"))):
             o = os.path.join("obj", "asan", "tool_" + os.path.basename(s) + ".o")
