@@ -548,8 +548,15 @@ void gemmp_bf16(const GemmPParams& p, hipStream_t st) {
   // 9 / 11 (eight-wave A B^T kernels) fall back to gemmt for other layouts / epilogues
   if ((p.variant >= 1 && p.variant <= 6) || p.variant == 9 || p.variant == 10 || p.variant == 11) {
     if (p.variant == 2 && small) gemmr_launch(p, splits, n_cu, st);
-    else if (p.variant >= 3 && small && gemmt_supported(p))
-      gemmt_launch(p, splits, p.variant - 3, st);
+    else if (p.variant >= 3 && small && gemmt_supported(p)) {
+      if (p.variant >= 11) {   // the eight-wave kernels' dbg is their mode, not gemmt's ablation bits
+        GemmPParams q = p;
+        q.dbg = 0;
+        gemmt_launch(q, splits, p.variant - 3, st);
+      } else {
+        gemmt_launch(p, splits, p.variant - 3, st);
+      }
+    }
     else gemmq_launch(p, splits, n_cu, st);
     if (splits > 1) splitk_reduce(p.workspace, p.C, p.M, p.N, p.ldc, splits, p.beta, p.out_f32, st);
     return;

@@ -423,7 +423,8 @@ def test_gemmp(ta, tb, M, N, Kd, splits, variant):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 4, 5, 6])
-@pytest.mark.parametrize("M,N,Kd", [(512, 768, 128), (264, 520, 512), (1040, 264, 1216), (2048, 1024, 3072)])
+@pytest.mark.parametrize("M,N,Kd", [(512, 768, 128), (264, 520, 512), (1040, 264, 1216), (2048, 1024, 3072),
+                                    (256, 256, 64), (520, 264, 192)])
 def test_gemmpp_modes(mode, M, N, Kd):
     """Eight-wave ping-pong A B^T kernel (gemmpp.hip, variant 11) in every
     DMA / priority mode (GemmPParams.dbg = 16 | mode): plain, bf16 accumulate
