@@ -315,6 +315,7 @@ def _run_bert(args, world, rank, only_dp: bool):
         "compile_s": round(compile_s, 2),
         "hipgraph": t["graphed"],
         "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
+        "native_replay": getattr(ex, "native_replay", None),
         "gemm_choices": dict(collections.Counter(gemm_choices().values())),
         "tokens_per_sec": round(t["value"] * args.seq, 1),
         "final_loss": round(pm.loss, 4),
@@ -450,7 +451,8 @@ def _run_zoo(args, world, rank, only_dp: bool):
     conf = {"model": args.model, "global_batch": global_batch, "parallelism": _parallelism(model, world),
             "strategy_source": model.search_report.get("source", ""), "optimizer": opt,
             "compile_s": round(compile_s, 2), "hipgraph": t["graphed"],
-            "graph_segments": list(getattr(ex, "graph_segments", ())) or None, "final_loss": round(pm.loss, 4),
+            "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
+            "native_replay": getattr(ex, "native_replay", None), "final_loss": round(pm.loss, 4),
             "memory": _memory_record(model, ex, world, 16.0 if opt == "adam" else 8.0)}
     conf.update(extra)
     if zname == "gpt":

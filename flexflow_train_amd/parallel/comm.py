@@ -60,10 +60,22 @@ class DistContext:
         # captured: in-place collectives become segment boundaries
         self.recorder = None
 
-    def _issue(self, fn, async_op: bool):
+    def _issue(self, fn, async_op: bool, desc=None):
         if self.recorder is not None:
-            return self.recorder.collective(fn, async_op)
+            return self.recorder.collective(fn, async_op, desc)
         return fn()
+
+    @staticmethod
+    def _pg(grp):
+        """The c10d ProcessGroup object behind ``grp`` (None = the default group)."""
+        if grp is not None:
+            return grp
+        from torch.distributed import distributed_c10d
+        return distributed_c10d._get_default_group()
+
+    @staticmethod
+    def _group_rank(grp, rank: int) -> int:
+        return rank if grp is None else dist.get_group_rank(grp, rank)
 
     @classmethod
     def from_env(cls, device: Optional[torch.device] = None, backend: Optional[str] = None) -> "DistContext":
@@ -128,7 +140,8 @@ class DistContext:
         self.stats["all_reduce"] += 1
         self.stats["bytes"] += t.numel() * t.element_size()
         grp = self.group(ranks)
-        return self._issue(lambda: dist.all_reduce(t, group=grp, async_op=async_op), async_op)
+        return self._issue(lambda: dist.all_reduce(t, group=grp, async_op=async_op), async_op,
+                           ("all_reduce", t, None, self._pg(grp), 0))
 
     def reduce_scatter_(self, t: torch.Tensor, ranks: Sequence[int], async_op: bool = False):
         """In-place reduce-scatter of the 1-D ``t``: afterwards chunk i (of
@@ -145,7 +158,8 @@ class DistContext:
             chunk = t.numel() // n
             grp = self.group(ranks)
             out = t[i * chunk:(i + 1) * chunk]
-            return self._issue(lambda: dist.reduce_scatter_tensor(out, t, group=grp, async_op=async_op), async_op)
+            return self._issue(lambda: dist.reduce_scatter_tensor(out, t, group=grp, async_op=async_op), async_op,
+                               ("reduce_scatter", t, out, self._pg(grp), 0))
         return dist.all_reduce(t, group=self.group(ranks), async_op=async_op)
 
     def reduce_(self, t: torch.Tensor, ranks: Sequence[int], dst: int, async_op: bool = False):
@@ -156,7 +170,8 @@ class DistContext:
         self.stats["reduce"] = self.stats.get("reduce", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
         grp = self.group(ranks)
-        return self._issue(lambda: dist.reduce(t, dst=dst, group=grp, async_op=async_op), async_op)
+        return self._issue(lambda: dist.reduce(t, dst=dst, group=grp, async_op=async_op), async_op,
+                           ("reduce", t, None, self._pg(grp), self._group_rank(grp, dst)))
 
     def broadcast_(self, t: torch.Tensor, ranks: Sequence[int], src: int, async_op: bool = False):
         if not self.syncs(ranks):
@@ -164,7 +179,8 @@ class DistContext:
         self.stats["broadcast"] = self.stats.get("broadcast", 0) + 1
         self.stats["bytes"] += t.numel() * t.element_size()
         grp = self.group(ranks)
-        return self._issue(lambda: dist.broadcast(t, src=src, group=grp, async_op=async_op), async_op)
+        return self._issue(lambda: dist.broadcast(t, src=src, group=grp, async_op=async_op), async_op,
+                           ("broadcast", t, None, self._pg(grp), self._group_rank(grp, src)))
 
     def all_gather_(self, t: torch.Tensor, ranks: Sequence[int]):
         """In-place all-gather of the equal chunks of the 1-D ``t`` (chunk i
@@ -179,7 +195,8 @@ class DistContext:
         if t.is_cuda:
             grp = self.group(ranks)
             piece = t[i * chunk:(i + 1) * chunk]
-            self._issue(lambda: dist.all_gather_into_tensor(t, piece, group=grp), False)
+            self._issue(lambda: dist.all_gather_into_tensor(t, piece, group=grp), False,
+                        ("all_gather", piece, t, self._pg(grp), 0))
         else:
             dist.all_gather(list(t.split(chunk)), t[i * chunk:(i + 1) * chunk].clone(), group=self.group(ranks))
 
@@ -429,7 +446,8 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
         out = torch.empty(dst_shape, dtype=xs.dtype, device=xs.device)
         grp = ctx.group(g)
         ctx.note_size("reduce_scatter", inp.numel() * inp.element_size())
-        ctx._issue(lambda: dist.reduce_scatter_tensor(out.view(-1), inp, group=grp), False)
+        ctx._issue(lambda: dist.reduce_scatter_tensor(out.view(-1), inp, group=grp), False,
+                   ("reduce_scatter", inp, out.view(-1), ctx._pg(grp), 0))
         return out.to(dtype)
     if plan.kind == "all_gather":
         g = next(g for g in plan.groups if me in g)
@@ -443,7 +461,8 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
         # dim, one copy (movedim + reshape) otherwise -- no list + cat
         flat = torch.empty((n,) + tuple(xs.shape), dtype=xs.dtype, device=xs.device)
         ctx.note_size("all_gather", flat.numel() * flat.element_size())
-        ctx._issue(lambda: dist.all_gather_into_tensor(flat.view(-1), xs.view(-1), group=grp), False)
+        ctx._issue(lambda: dist.all_gather_into_tensor(flat.view(-1), xs.view(-1), group=grp), False,
+                   ("all_gather", xs.view(-1), flat.view(-1), ctx._pg(grp), 0))
         order = sorted(range(n), key=lambda i: plan.src_boxes[g[i]][plan.gather_dim][0])
         # members holding identical boxes (implicit replicas) appear once
         seen, keep = set(), []
@@ -521,11 +540,13 @@ def _exchange_all_to_all(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext
         ctx.stats["all_to_all_subgroup"] = ctx.stats.get("all_to_all_subgroup", 0) + 1
         ctx.note_size("all_to_all", sendbuf.numel() * sendbuf.element_size())
         ctx._issue(lambda: dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=go, input_split_sizes=gi,
-                                                  group=grp), False)
+                                                  group=grp), False,
+                   ("all_to_all", sendbuf, recvbuf, ctx._pg(grp), 0, list(go), list(gi)))
     else:
         ctx.note_size("all_to_all", sendbuf.numel() * sendbuf.element_size())
         ctx._issue(lambda: dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=out_sizes,
-                                                  input_split_sizes=in_sizes), False)
+                                                  input_split_sizes=in_sizes), False,
+                   ("all_to_all", sendbuf, recvbuf, ctx._pg(None), 0, list(out_sizes), list(in_sizes)))
     if my_dst is None:
         return None
     result = torch.zeros(dst_shape, dtype=dtype, device=device)

@@ -1684,6 +1684,9 @@ class Executor:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize(self.cfg.device)
         self.graph_segments = (rec.n_graphs(), rec.n_collectives())
+        # the chain replays from C++ (csrc/runtime/replay.cpp) when every
+        # collective carries a descriptor and _ffreplay is built
+        self.native_replay = rec.build_native()
         return rec
 
     def zero_metrics(self):

@@ -29,13 +29,36 @@ segmented capture raises ``NotCapturable`` and the caller runs eagerly.
 This is the MI355X replacement of the reference's Legion tracing
 (``begin_trace``/``end_trace`` around every iteration,
 python/flexflow/core/flexflow_cffi.py:562-566) for multi-GPU runs.
+
+When every collective of the chain came with a descriptor (kind, operands,
+process group, root), the chain is also handed to the native replayer
+(``csrc/runtime/replay.cpp``, ``_ffreplay``): one call walks the graph
+launches and issues the RCCL collectives through the C++ ``c10d``
+ProcessGroup, with the interpreter out of the step (``FF_NATIVE_REPLAY=0``
+keeps the Python walk).
 """
 from __future__ import annotations
 
+import os
 import warnings
 from typing import Callable, List, Optional, Tuple
 
 import torch
+
+
+# collective kinds of the native replayer (csrc/runtime/replay.cpp enum Kind)
+NATIVE_KINDS = {"all_reduce": 1, "reduce_scatter": 2, "all_gather": 3, "reduce": 4, "broadcast": 5,
+                "all_to_all": 7}
+
+
+def _native_module():
+    if os.environ.get("FF_NATIVE_REPLAY", "1") == "0":
+        return None
+    try:
+        from .. import _ffreplay
+    except ImportError:
+        return None
+    return _ffreplay
 
 
 class NotCapturable(RuntimeError):
@@ -71,6 +94,7 @@ class SegmentRecorder:
         self.items: List[Tuple] = []
         self.cur: Optional[torch.cuda.CUDAGraph] = None
         self.n_async = 0
+        self._native = None   # _ffreplay.Replayer once built
 
     # ---- capture side
     def begin(self):
@@ -97,14 +121,16 @@ class SegmentRecorder:
                 self.cur = None
         self.items = []
 
-    def collective(self, fn: Callable, async_op: bool):
-        """Cut the current segment; ``fn()`` issues the collective at replay."""
+    def collective(self, fn: Callable, async_op: bool, desc: Optional[Tuple] = None):
+        """Cut the current segment; ``fn()`` issues the collective at replay.
+        ``desc`` = (kind, input, output, process group, group-local root)
+        lets the native replayer issue it without ``fn``."""
         self.end()
         slot = None
         if async_op:
             slot = self.n_async
             self.n_async += 1
-        self.items.append(("coll", fn, slot))
+        self.items.append(("coll", fn, slot, desc))
         self.begin()
         return _PendingWork(self, slot) if async_op else None
 
@@ -120,7 +146,41 @@ class SegmentRecorder:
     def n_collectives(self) -> int:
         return sum(1 for it in self.items if it[0] == "coll")
 
+    def build_native(self) -> bool:
+        """Hand the chain to the native replayer; False (Python walk) when the
+        extension is absent or a collective has no descriptor."""
+        R = _native_module()
+        if R is None:
+            return False
+        rp = R.Replayer()
+        for it in self.items:
+            if it[0] == "graph":
+                rp.add_graph(it[1])
+            elif it[0] == "coll":
+                desc = it[3]
+                if desc is None or desc[0] not in NATIVE_KINDS:
+                    return False
+                kind, a, b, pg, root = desc[:5]
+                out_splits, in_splits = (desc[5], desc[6]) if len(desc) > 6 else ([], [])
+                try:
+                    rp.add_collective(NATIVE_KINDS[kind], pg, a, a if b is None else b, int(root),
+                                      -1 if it[2] is None else int(it[2]), [int(v) for v in out_splits],
+                                      [int(v) for v in in_splits])
+                except TypeError:   # not a c10d ProcessGroup (e.g. a non-member sentinel)
+                    return False
+            else:
+                rp.add_wait(int(it[1]))
+        self._native = rp
+        return True
+
+    @property
+    def native(self) -> bool:
+        return self._native is not None
+
     def replay(self):
+        if self._native is not None:
+            self._native.replay()
+            return
         works = {}
         for it in self.items:
             kind = it[0]

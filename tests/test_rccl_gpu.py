@@ -95,7 +95,8 @@ _CHILD = textwrap.dedent(r'''
             diff = max(float((p[k] - ref_p[k]).abs().max()) for k in ref_p)
             res[f"{name}{'_graph' if graphed else ''}"] = {
                 "max_abs_diff": diff, "syncs": dict(ex.dist.stats),
-                "segments": list(getattr(ex, "graph_segments", ()) or ())}
+                "segments": list(getattr(ex, "graph_segments", ()) or ()),
+                "native_replay": getattr(ex, "native_replay", None)}
     out["train"] = res
     import torch.distributed as dist
     dist.destroy_process_group()
@@ -134,6 +135,8 @@ def _check(out, backend):
             assert s["all_reduce"] > 0, (name, s)
         if name.endswith("_graph"):
             assert r["segments"] and r["segments"][1] > 0, (name, r)
+            if backend == "nccl":   # the segment chain replays from C++ (csrc/runtime/replay.cpp)
+                assert r["native_replay"] is True, (name, r)
 
 
 @pytest.mark.gpu

@@ -160,6 +160,33 @@ def write_ninja(targets: list[str]) -> str:
         rexe = os.path.join(ROOT, "bin", "ffc-runtime-c-test")
         lines.append(f"build {rexe}: cc_rt_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_runtime_c.c')} | {rlib}")
         defaults += [rlib, rexe]
+    if "replay" in targets:
+        # csrc/runtime/replay.cpp -> _ffreplay: the native walker of segmented
+        # distributed steps (hipGraph launches + c10d ProcessGroup collectives);
+        # a host-only torch extension (libtorch / libtorch_hip, no device code)
+        import torch
+        from torch.utils import cpp_extension as cpp
+
+        tinc = " ".join(f"-I{p}" for p in cpp.include_paths(device_type="cuda"))
+        tlib = " ".join(f"-L{p}" for p in cpp.library_paths(device_type="cuda"))
+        abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+        lines += [f"replay_flags = -O2 -std=c++17 -fPIC -DUSE_ROCM=1 -D__HIP_PLATFORM_AMD__=1 "
+                  f"-DTORCH_EXTENSION_NAME=_ffreplay -DTORCH_API_INCLUDE_EXTENSION_H -D_GLIBCXX_USE_CXX11_ABI={abi} "
+                  f"{tinc} {inc}",
+                  "rule cxx_replay",
+                  "  command = $cxx $replay_flags -MMD -MF $out.d -c $in -o $out",
+                  "  depfile = $out.d",
+                  "  deps = gcc",
+                  "  description = CXX(torch) $in",
+                  "rule link_replay",
+                  f"  command = $cxx -shared -o $out $in {tlib} -lc10 -ltorch -ltorch_cpu -ltorch_python -lc10_hip "
+                  "-ltorch_hip",
+                  "  description = LINK $out"]
+        ro = os.path.join("obj", "runtime", "replay.cpp.o")
+        lines.append(f"build {ro}: cxx_replay {os.path.join(ROOT, 'csrc', 'runtime', 'replay.cpp')}")
+        rso = os.path.join(PKG, "_ffreplay" + EXT)
+        lines.append(f"build {rso}: link_replay {ro}")
+        defaults.append(rso)
     if "asan" in targets:
         # host-code sanitizer build (ASan/UBSan for host code): the
         # C++ core + C ABI + native CLIs compiled with -fsanitize=address,undefined
@@ -218,7 +245,7 @@ def write_ninja(targets: list[str]) -> str:
 
 
 def build(targets: list[str] | None = None, jobs: int | None = None, verbose: bool = False) -> None:
-    targets = targets or ["core", "kernels", "tools", "ffi"]
+    targets = targets or ["core", "kernels", "tools", "ffi", "replay"]
     write_ninja(targets)
     ninja = shutil.which("ninja")
     if ninja is None:
