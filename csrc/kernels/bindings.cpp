@@ -290,6 +290,10 @@ PYBIND11_MODULE(_ffkernels, m) {
     c.sh = v[7]; c.sw = v[8]; c.ph = v[9]; c.pw = v[10]; c.dh = v[11]; c.dw = v[12];
     return c;
   };
+  m.def("pad_channels_nhwc", [=](uintptr_t x, uintptr_t y, int64_t N, int C, int H, int W, int64_t sn, int64_t sc,
+                                 int64_t sh, int64_t sw, int Cp, uintptr_t st) {
+    pad_channels_nhwc(P(x), P(y), N, C, H, W, sn, sc, sh, sw, Cp, S(st));
+  });
   m.def("conv2d_stats_ws_floats", [=](std::vector<int> shp) { return conv2d_stats_ws_floats(cshape(shp)); });
   m.def("conv2d_wgrad_ws_floats",
         [=](std::vector<int> shp, int splits) { return conv2d_wgrad_ws_floats(cshape(shp), splits); });

@@ -802,4 +802,42 @@ void conv2d_wgrad(const ConvShape& cs, const void* x, const void* dy, float* dw,
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Channel padding of a convolution input (the RGB stem: 3 channels -> 8, so
+// every 16-B gather chunk holds whole channels): one pass from any 4-d
+// strided bf16 tensor [N][C][H][W] (NCHW or channels_last) to an NHWC image
+// with Cp >= C channels, the pad channels zero; one output pixel (Cp / 8
+// 16-B chunks) per thread.  Replaces a layout copy, a zero fill and a strided
+// copy.
+namespace {
+__global__ __launch_bounds__(256) void pad_channels_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                           int64_t npix, int C, int H, int W, int64_t sn,
+                                                           int64_t sc, int64_t sh, int64_t sw, int Cp) {
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (p >= npix) return;
+  const int w = static_cast<int>(p % W);
+  const int64_t t = p / W;
+  const int h = static_cast<int>(t % H);
+  const int64_t n = t / H;
+  const bf16* src = x + n * sn + h * sh + w * sw;
+  for (int c0 = 0; c0 < Cp; c0 += 8) {
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = c0 + e < C ? src[(c0 + e) * sc] : static_cast<bf16>(0.f);
+    *reinterpret_cast<bf16x8*>(y + p * Cp + c0) = v;
+  }
+}
+}  // namespace
+
+void pad_channels_nhwc(const void* x, void* y, int64_t N, int C, int H, int W, int64_t sn, int64_t sc, int64_t sh,
+                       int64_t sw, int Cp, hipStream_t st) {
+  if (Cp % 8 || Cp < C) throw std::invalid_argument("pad_channels_nhwc: Cp must be a multiple of 8 and >= C");
+  const int64_t npix = N * H * W;
+  if (npix <= 0) return;
+  hipLaunchKernelGGL(pad_channels_kernel, dim3(static_cast<unsigned>((npix + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const bf16*>(x), static_cast<bf16*>(y), npix, C, H, W, sn, sc, sh, sw, Cp);
+  FFK_LAUNCH_CHECK("pad_channels_nhwc");
+}
+
 }  // namespace ffk

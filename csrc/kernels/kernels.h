@@ -239,6 +239,9 @@ void conv2d_fwd(const ConvShape& s, const void* x, const void* w, const void* bi
                 float* stats_ws, int act, hipStream_t st);
 // dx = conv_transpose(dy, w) + beta * dx
 void conv2d_dgrad(const ConvShape& s, const void* dy, const void* w, void* dx, float beta, hipStream_t st);
+// strided bf16 [N][C][H][W] -> NHWC [N][H][W][Cp], pad channels zero (conv.hip)
+void pad_channels_nhwc(const void* x, void* y, int64_t N, int C, int H, int W, int64_t sn, int64_t sc, int64_t sh,
+                       int64_t sw, int Cp, hipStream_t st);
 // dw (fp32, [K][R][S][C]) += wgrad; split-K partial slabs in ws
 // (conv2d_wgrad_ws_floats(s, splits) floats; splits <= 0: auto)
 int64_t conv2d_wgrad_ws_floats(const ConvShape& s, int splits);

@@ -949,6 +949,19 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous(memory_format=torch.channels_last)
 
 
+def pad_channels_nhwc(x: torch.Tensor, Cp: int) -> torch.Tensor:
+    """Any-stride bf16 [N, C, H, W] -> channels_last [N, Cp, H, W] with the
+    channels past C zero, in one pass (conv.hip pad_channels_kernel)."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 4:
+        raise ValueError("pad_channels_nhwc: 4-d bf16 GPU tensor (any strides)")
+    N, C, H, W = x.shape
+    y = torch.empty((N, Cp, H, W), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    sn, sc, sh, sw = x.stride()
+    ext().pad_channels_nhwc(_p(x), _p(y), N, C, H, W, sn, sc, sh, sw, Cp, _stream())
+    STATS["pad_channels"] += 1
+    return y
+
+
 def conv_out_hw(H, W, R, S, sh, sw, ph, pw, dh=1, dw=1):
     return (H + 2 * ph - dh * (R - 1) - 1) // sh + 1, (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
 

@@ -130,15 +130,12 @@ class Conv2DOp(OpImpl):
             wp = W.reshape(Kc, R, S, C)
             if wp.dtype != torch.bfloat16:
                 wp = wp.to(torch.bfloat16)
-            xin = K.nhwc(x)
-            if C % 8:  # RGB stem: zero-pad channels to 8 (input and weight)
-                xp = torch.zeros((x.shape[0], 8, x.shape[2], x.shape[3]), device=x.device,
-                                 dtype=x.dtype).contiguous(memory_format=torch.channels_last)
-                xp[:, :C].copy_(xin)
-                xin = xp
-                wpad = torch.zeros((Kc, R, S, 8), device=x.device, dtype=wp.dtype)
-                wpad[..., :C].copy_(wp)
-                wp = wpad
+            if C % 8:  # RGB stem: zero-pad channels to a multiple of 8 (input and weight), one pass each
+                Cp = (C + 7) // 8 * 8
+                xin = K.pad_channels_nhwc(x, Cp)
+                wp = K.pad_channels_nhwc(wp.permute(0, 3, 1, 2), Cp).permute(0, 2, 3, 1)
+            else:
+                xin = K.nhwc(x)
             stats = None
             if ctx.extra.get("emit_bn_stats"):
                 stats = torch.empty(2 * Kc, device=x.device, dtype=torch.float32)

@@ -241,3 +241,17 @@ def test_pointwise_conv_paths(mode, C, Ko, acc, st):
         assert set(CV._CHOICE.values()) == ({mode} if st == 1 else set())
     finally:
         CV._MODE, CV._CHOICE = old, {}
+
+
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+@pytest.mark.parametrize("C,Cp", [(3, 8), (5, 16), (8, 8)])
+def test_pad_channels_nhwc(layout, C, Cp):
+    """One-pass channel padding (conv.hip pad_channels_kernel) from either
+    layout into a channels_last tensor with zero pad channels."""
+    x = torch.randn(3, C, 17, 11, device=DEV).to(torch.bfloat16)
+    if layout == "nhwc":
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = K.pad_channels_nhwc(x, Cp)
+    assert y.shape == (3, Cp, 17, 11) and y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y[:, :C], x)
+    assert not y[:, C:].any()
