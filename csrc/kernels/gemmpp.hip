@@ -46,7 +46,10 @@
 // 1.92 PFLOP/s (the ping-pong itself is efficient), the fragment reads add
 // 8 %, the LDS-DMA another 33 % -- the load half is bound by the DMA pieces'
 // issue cost (100-185 cycles each beside 24 ds_read_b128), not by their
-// latency (a third A buffer, prefetch distance 2, moved it < 1 %).
+// latency (a third A buffer, prefetch distance 2, moved it < 1 %).  Moving 2-4
+// of each wave's DMA pieces into its compute half did not help either
+// (profiles/r5/ab_gemmpp_cn_r5.txt): what the DMA costs is not issue slots
+// alone but its LDS writes beside the fragment reads.
 #include <utility>
 
 #include "kernels.h"
