@@ -4,5 +4,5 @@
 set -o pipefail
 N=${1:-2}
 MODEL=${2:-bert-large}
-FF_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" \
+FF_BENCH_REHEARSAL=1 FF_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" \
   --master-addr 127.0.0.1 --master-port 29517 bench.py --model "$MODEL" --gpus "$N" --steps 3 --warmup 1
