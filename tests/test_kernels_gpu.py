@@ -18,6 +18,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+# bf16 GEMM outputs against the fp32 product of the same bf16 operands: only
+# the output rounding remains (2^-9 per element, ~1.2e-3 relative Frobenius);
+# fp32 outputs (beta accumulate into fp32) differ by summation order only
+_BF, _F32 = 3e-3, 1e-4
+
+
 def _rel(a, b):
     a = a.float()
     b = b.float()
@@ -160,7 +166,7 @@ def test_embedding(aggr):
         ref = ref.sum(-2)
     elif aggr == "avg":
         ref = ref.mean(-2)
-    assert _rel(out, ref) < 1e-2
+    assert _rel(out, ref) < _BF
     dout = torch.randn_like(out)
     dW = torch.zeros(n, D, device=DEV)
     K.embedding_bwd(idx, dout, dW, aggr)
@@ -168,7 +174,7 @@ def test_embedding(aggr):
     r = Wf[idx]
     r = r.sum(-2) if aggr == "sum" else (r.mean(-2) if aggr == "avg" else r)
     r.backward(dout.float())
-    assert _rel(dW, Wf.grad) < 1e-2
+    assert _rel(dW, Wf.grad) < 1e-5   # fp32 accumulation of the same bf16 gradients
 
 
 @pytest.mark.parametrize("n,rows,D", [(2, 32768, 1024), (5, 3000, 768), (8, 100, 64), (1, 513, 136)])
@@ -293,16 +299,16 @@ def test_gemm(ta, tb, M, N, Kd):
     bf = b.float().t() if tb else b.float()
     ref = af @ bf
     c = K.gemm(a, b, trans_a=ta, trans_b=tb)
-    assert _rel(c, ref) < 1e-2
+    assert _rel(c, ref) < _BF
     bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
     pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     c2 = K.gemm(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
     u = ref + bias.float()
-    assert _rel(pre, u) < 1e-2
-    assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
+    assert _rel(pre, u) < _BF
+    assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < _BF
     c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
     K.gemm(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3)
-    assert _rel(c3, ref + 1) < 1e-2
+    assert _rel(c3, ref + 1) < _F32
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
@@ -320,16 +326,16 @@ def test_gemm_splitk(ta, tb, M, N, Kd, splits):
     n0 = K.STATS["gemm_splitk"]
     c = K.gemm(a, b, trans_a=ta, trans_b=tb, splits=splits)
     assert K.STATS["gemm_splitk"] == n0 + 1
-    assert _rel(c, ref) < 1e-2
+    assert _rel(c, ref) < _BF
     bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
     pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     c2 = K.gemm(a, b, trans_a=ta, trans_b=tb, bias=bias, act="relu", pre=pre, splits=splits)
     u = ref + bias.float()
-    assert _rel(pre, u) < 1e-2
-    assert _rel(c2, torch.relu(u)) < 1e-2
+    assert _rel(pre, u) < _BF
+    assert _rel(c2, torch.relu(u)) < _BF
     c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
     K.gemm(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
-    assert _rel(c3, ref + 1) < 1e-2
+    assert _rel(c3, ref + 1) < _F32
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
@@ -345,17 +351,17 @@ def test_gemm256(ta, tb, M, N, Kd, splits):
     bf = b.float().t() if tb else b.float()
     ref = af @ bf
     c = K.gemm256(a, b, trans_a=ta, trans_b=tb, splits=splits)
-    assert _rel(c, ref) < 1e-2
+    assert _rel(c, ref) < _BF
     c3 = torch.ones(M, N, device=DEV, dtype=torch.float32)
     K.gemm256(a, b, trans_a=ta, trans_b=tb, beta=1.0, out=c3, splits=splits)
-    assert _rel(c3, ref + 1) < 1e-2
+    assert _rel(c3, ref + 1) < _F32
     if splits == 1:
         bias = torch.randn(N, device=DEV, dtype=torch.bfloat16)
         pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         c2 = K.gemm256(a, b, trans_a=ta, trans_b=tb, bias=bias, act="gelu", pre=pre)
         u = ref + bias.float()
-        assert _rel(pre, u) < 1e-2
-        assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < 1e-2
+        assert _rel(pre, u) < _BF
+        assert _rel(c2, torch.nn.functional.gelu(u, approximate="tanh")) < _BF
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11],
@@ -470,7 +476,7 @@ def test_bmm(ta, tb, Z, M, N, Kd):
     assert K.bmm_supported(a, b, ta, tb)
     ref = (a.float().transpose(-1, -2) if ta else a.float()) @ (b.float().transpose(-1, -2) if tb else b.float())
     c = K.bmm(a, b, ta, tb)
-    assert _rel(c, ref) < 1e-2
+    assert _rel(c, ref) < _BF
     acc = torch.ones(Z, M, N, device=DEV, dtype=torch.float32)
     K.bmm(a, b, ta, tb, out=acc, beta=1.0)
-    assert _rel(acc, ref + 1) < 1e-2
+    assert _rel(acc, ref + 1) < _F32
