@@ -303,6 +303,13 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("conv2d_dgrad", [=](std::vector<int> shp, uintptr_t dy, uintptr_t w, uintptr_t dx, float beta,
                             uintptr_t st) { conv2d_dgrad(cshape(shp), P(dy), P(w), P(dx), beta, S(st)); });
+  m.def("conv2d_dgrad_bn_ws_floats", [=](std::vector<int> shp) { return conv2d_dgrad_bn_ws_floats(cshape(shp)); });
+  m.def("conv2d_dgrad_bn", [=](std::vector<int> shp, uintptr_t dy, uintptr_t w, uintptr_t dx, uintptr_t x,
+                               uintptr_t mean, uintptr_t rstd, uintptr_t ss, uintptr_t sums, uintptr_t ws,
+                               uintptr_t st) {
+    ConvBnBwd b{P(x), F(mean), F(rstd), F(ss), F(sums), F(ws)};
+    conv2d_dgrad(cshape(shp), P(dy), P(w), P(dx), 0.f, S(st), &b);
+  });
   m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws, int splits,
                             uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), F(ws), splits, S(st)); });
   m.def("gemm_f32", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int64_t M, int64_t N,
@@ -335,10 +342,12 @@ PYBIND11_MODULE(_ffkernels, m) {
                        int relu, uintptr_t st) { bn_apply(P(x), P(res), F(scale), F(shift), P(y), M, C, relu, S(st)); });
   m.def("bn_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t g, int pdt,
                      uintptr_t dx, uintptr_t dres, uintptr_t dg, uintptr_t db, uintptr_t ws, int64_t M, int C,
-                     int relu, uintptr_t st, uintptr_t ss, int ws_clean) {
+                     int relu, uintptr_t st, uintptr_t ss, int ws_clean, uintptr_t pre_sums) {
     bn_bwd(P(dy), P(x), P(y), F(mean), F(rstd), P(g), pdt, P(dx), P(dres), F(dg), F(db), F(ws), M, C, relu, S(st),
-           F(ss), ws_clean);
-  });
+           F(ss), ws_clean, F(pre_sums));
+  }, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("g"), py::arg("pdt"),
+     py::arg("dx"), py::arg("dres"), py::arg("dg"), py::arg("db"), py::arg("ws"), py::arg("M"), py::arg("C"),
+     py::arg("relu"), py::arg("st"), py::arg("ss"), py::arg("ws_clean"), py::arg("pre_sums") = 0);
   // pool geometry: [N,H,W,C,R,S,sh,sw,ph,pw,avg,count_pad]
   auto pshape = [](const std::vector<int>& v) {
     if (v.size() != 12) throw std::invalid_argument("pool shape must have 12 entries");

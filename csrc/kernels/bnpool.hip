@@ -237,11 +237,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 // also dgamma += sum(g*xhat), dbeta += sum(g).
 __global__ void bn_bwd_coef_kernel(float* __restrict__ sums, const float* __restrict__ mean,
                                    const float* __restrict__ rstd, const void* gamma, int pdt, float* __restrict__ coef,
-                                   float* dgamma, float* dbeta, int C, float inv_count, int reset) {
+                                   float* dgamma, float* dbeta, int C, float inv_count, int reset, int nb) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s1 = 0.f, s2 = 0.f;
-  for (int k = 0; k < kBnBuckets; ++k) {
+  for (int k = 0; k < nb; ++k) {
     s1 += sums[static_cast<int64_t>(k) * 2 * C + c];
     s2 += sums[static_cast<int64_t>(k) * 2 * C + C + c];
   }
@@ -520,21 +520,26 @@ void bn_apply(const void* x, const void* residual, const float* scale, const flo
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
-            int relu, hipStream_t st, const float* scale_shift, int ws_clean) {
+            int relu, hipStream_t st, const float* scale_shift, int ws_clean, const float* pre_sums) {
   if (C % 8) throw std::invalid_argument("bn_bwd: C must be a multiple of 8");
   if (relu == 1 && !y) throw std::invalid_argument("bn_bwd: ReLU mask from y needs y");
   if (relu == 2 && !scale_shift) throw std::invalid_argument("bn_bwd: ReLU mask from x needs the scale / shift");
   if (M <= 0) return;
   const RedGeom r = red_geom(C);
-  if (!ws_clean) (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
-  with_unroll([&](auto uu) {
-    hipLaunchKernelGGL((bn_reduce_kernel<1, decltype(uu)::value>), red_grid(r, M), dim3(256), 0, st,
-                       static_cast<const bf16*>(x), static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean,
-                       rstd, ws, M, C, r.GL, relu, scale_shift, kBnBuckets);
-  });
   float* coef = ws + 2 * C * kBnBuckets;
-  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, mean, rstd, gamma,
-                     param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M), ws_clean);
+  if (pre_sums) {   // sums reduced by the consumer convolution's dgrad epilogue (conv.hip)
+    hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, const_cast<float*>(pre_sums),
+                       mean, rstd, gamma, param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M), 0, 1);
+  } else {
+    if (!ws_clean) (void)hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * kBnBuckets, st);
+    with_unroll([&](auto uu) {
+      hipLaunchKernelGGL((bn_reduce_kernel<1, decltype(uu)::value>), red_grid(r, M), dim3(256), 0, st,
+                         static_cast<const bf16*>(x), static_cast<const bf16*>(dy), static_cast<const bf16*>(y), mean,
+                         rstd, ws, M, C, r.GL, relu, scale_shift, kBnBuckets);
+    });
+    hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ws, mean, rstd, gamma,
+                       param_dtype, coef, dgamma, dbeta, C, static_cast<float>(1.0 / M), ws_clean, kBnBuckets);
+  }
   const int64_t nvec = M * C / 8;
   with_unroll([&](auto uu) {
     constexpr int U = decltype(uu)::value;

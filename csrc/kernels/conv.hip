@@ -71,6 +71,14 @@ struct ConvArgs {
   // magic divisors of the loaders and the operands' byte sizes (buffer range)
   FastDiv fC, fS, fK, fQ, fP, fW, fH, fWc, fHc, fns, fsh, fsw;
   unsigned bx, bw, bdy;
+  // DGRAD of a convolution fed by a BatchNorm (+ReLU): the epilogue also
+  // reduces that BN's backward sums over the stored gradient g (masked by the
+  // forward's ReLU, recomputed from the BN input): sum g and sum g * xhat,
+  // one partial row per M tile into `stats` (bn_reduce's pass then skipped)
+  const bf16* bnx;            // BN input [N][H][W][C] (null: no BN sums)
+  const float* bnmean;        // [C]
+  const float* bnrstd;        // [C]
+  const float* bnss;          // [2][C] scale, shift (null: no ReLU mask)
 };
 
 // DGRAD output row of local row m (parity classes scatter to the full image)
@@ -514,6 +522,30 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
         *reinterpret_cast<bf16x4*>(ctile + ml * ROWB + nl * 2) = o;
       }
   }
+  constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
+  constexpr int NCH = BM * CPR / 256;   // chunks per thread
+  const bool want_stats = (MODE == MODE_FWD || MODE == MODE_DGRAD) && g.stats != nullptr;
+  // BN backward sums (DGRAD): a thread's chunks all sit in channel group
+  // tid % CPR; its BN parameters and the BN input under its chunks are
+  // requested here, before the barrier, so their latency hides behind it
+  float bmu[8], brs[8], bsc[8], bsh[8];
+  bf16x8 bxr[MODE == MODE_DGRAD ? NCH : 1];
+  if (MODE == MODE_DGRAD && want_stats) {
+    const int n = n0 + (threadIdx.x % CPR) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int m = m0 + (threadIdx.x + 256 * i) / CPR;
+      if (m < g.M && n < g.NG) bxr[i] = *reinterpret_cast<const bf16x8*>(g.bnx + static_cast<int64_t>(m) * g.NG + n);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = n + e < g.NG;
+      bmu[e] = ok ? g.bnmean[n + e] : 0.f;
+      brs[e] = ok ? g.bnrstd[n + e] : 0.f;
+      bsc[e] = ok && g.bnss ? g.bnss[n + e] : 0.f;
+      bsh[e] = ok && g.bnss ? g.bnss[g.NG + n + e] : 1.f;   // no mask: x*0 + 1 > 0
+    }
+  }
   __syncthreads();
   // Row-contiguous stores; a thread's chunks are one 8-column group (ch =
   // tid % CPR) of every (256 / CPR)-th row, so the BN statistics of the stored
@@ -521,8 +553,6 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   // that group (xor over lane bits >= log2 CPR) and over the 4 waves in LDS
   // into one partial row per M tile (reduce_rows folds the tiles): no
   // 320-shuffle column reduction of accumulator layouts.
-  constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
-  const bool want_stats = MODE == MODE_FWD && g.stats != nullptr;
   float cs[8], cq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
@@ -540,6 +570,15 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
       for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + g.beta * bf2f(old[e]));
     }
     *reinterpret_cast<bf16x8*>(dst) = v;
+    if (MODE == MODE_DGRAD && want_stats) {   // beta == 0 and no parity classes (host checked)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xe = bf2f(bxr[MODE == MODE_DGRAD ? i : 0][e]);
+        const float gr = xe * bsc[e] + bsh[e] > 0.f ? bf2f(v[e]) : 0.f;
+        cs[e] += gr;
+        cq[e] += gr * (xe - bmu[e]) * brs[e];
+      }
+    }
     if (MODE == MODE_FWD && want_stats) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -549,7 +588,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
       }
     }
   }
-  if (MODE == MODE_FWD && want_stats) {
+  if (want_stats) {
 #pragma unroll
     for (int o = CPR; o < 64; o <<= 1)
 #pragma unroll
@@ -703,7 +742,8 @@ void conv2d_fwd(const ConvShape& cs, const void* x, const void* w, const void* b
   }
 }
 
-void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, float beta, hipStream_t st) {
+void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, float beta, hipStream_t st,
+                  const ConvBnBwd* bn_sums) {
   check_shape(cs, "conv2d_dgrad");
   ConvArgs g = make_args(cs);
   g.dy = static_cast<const bf16*>(dy);
@@ -712,7 +752,18 @@ void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, 
   g.beta = beta;
   g.NG = g.C;
   const int bn = g.NG <= 64 ? 64 : 128;
-  if ((g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1) {
+  const bool strided = (g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1;
+  if (bn_sums) {
+    if (strided || beta != 0.f || !bn_sums->x || !bn_sums->mean || !bn_sums->rstd || !bn_sums->sums ||
+        !bn_sums->ws)
+      throw std::invalid_argument("conv2d_dgrad: BN sums need a stride-1 dgrad without accumulation");
+    g.bnx = static_cast<const bf16*>(bn_sums->x);
+    g.bnmean = bn_sums->mean;
+    g.bnrstd = bn_sums->rstd;
+    g.bnss = bn_sums->scale_shift;
+    g.stats = bn_sums->ws;
+  }
+  if (strided) {
     // strided: one launch per output-parity class, each a dense implicit GEMM
     // over only the taps that reach it (no MFMA work on structural zeros)
     g.par = 1;
@@ -740,9 +791,20 @@ void conv2d_dgrad(const ConvShape& cs, const void* dy, const void* w, void* dx, 
   }
   g.M = g.N * g.H * g.W;
   g.KG = g.R * g.S * g.K;
-  const int blocks = ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn);
+  const int gm = (g.M + BM - 1) / BM;
+  const int blocks = gm * ((g.NG + bn - 1) / bn);
   launch<MODE_DGRAD>(g, bn, blocks, st);
   FFK_LAUNCH_CHECK("conv2d_dgrad");
+  if (bn_sums) {
+    const int64_t W = 2 * static_cast<int64_t>(g.NG);
+    reduce_rows(bn_sums->ws, bn_sums->sums, gm, W, 0, bn_sums->ws + static_cast<int64_t>(gm) * W, st);
+    FFK_LAUNCH_CHECK("conv2d_dgrad bn sums");
+  }
+}
+
+int conv2d_dgrad_bn_ws_floats(const ConvShape& cs) {
+  const int64_t M = static_cast<int64_t>(cs.N) * cs.H * cs.W;
+  return static_cast<int>((((M + BM - 1) / BM) + kMaxChunks) * 2 * cs.C);
 }
 
 namespace {

@@ -238,7 +238,20 @@ int conv2d_stats_ws_floats(const ConvShape& s);
 void conv2d_fwd(const ConvShape& s, const void* x, const void* w, const void* bias, void* y, float* stats,
                 float* stats_ws, int act, hipStream_t st);
 // dx = conv_transpose(dy, w) + beta * dx
-void conv2d_dgrad(const ConvShape& s, const void* dy, const void* w, void* dx, float beta, hipStream_t st);
+// BN backward sums fused into a dgrad (stride 1, beta 0): sums [2][C] = sum g,
+// sum g * (x - mean) * rstd with g the ReLU-masked dx; ws holds
+// conv2d_dgrad_bn_ws_floats floats
+struct ConvBnBwd {
+  const void* x;
+  const float* mean;
+  const float* rstd;
+  const float* scale_shift;   // null: no ReLU mask
+  float* sums;
+  float* ws;
+};
+int conv2d_dgrad_bn_ws_floats(const ConvShape& s);
+void conv2d_dgrad(const ConvShape& s, const void* dy, const void* w, void* dx, float beta, hipStream_t st,
+                  const ConvBnBwd* bn_sums = nullptr);
 // strided bf16 [N][C][H][W] -> NHWC [N][H][W][Cp], pad channels zero (conv.hip)
 void pad_channels_nhwc(const void* x, void* y, int64_t N, int C, int H, int W, int64_t sn, int64_t sc, int64_t sh,
                        int64_t sw, int Cp, hipStream_t st);
@@ -281,7 +294,8 @@ void bn_apply(const void* x, const void* residual, const float* scale, const flo
 // scale_shift ([2][C]: scale, shift) — y is not read
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             int param_dtype, void* dx, void* dres, float* dgamma, float* dbeta, float* ws, int64_t M, int C,
-            int relu, hipStream_t st, const float* scale_shift = nullptr, int ws_clean = 0);
+            int relu, hipStream_t st, const float* scale_shift = nullptr, int ws_clean = 0,
+            const float* pre_sums = nullptr);   // [2][C] sums from the consumer's dgrad: no reduction pass
 struct PoolShape {
   int N = 0, H = 0, W = 0, C = 0, R = 1, S = 1, sh = 1, sw = 1, ph = 0, pw = 0;
   int avg = 0, count_pad = 0;

@@ -997,7 +997,13 @@ def conv2d_fwd(x, w, bias=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), act: str 
     return y
 
 
-def conv2d_dgrad(dy, w, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), out=None, beta: float = 0.0):
+def conv2d_dgrad(dy, w, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), out=None, beta: float = 0.0,
+                 bn=None):
+    """dx of a convolution.  ``bn = (x, mean, rstd, scale_shift or None)`` of
+    the BatchNorm(+ReLU) that produced the conv input: the epilogue also
+    reduces that BN's backward sums over the ReLU-masked dx (fp32 [2, C]:
+    sum g, sum g * xhat), returned as ``dx._ff_bn_sums = (sums, x)`` for
+    ``bn_bwd(pre_sums=...)`` (stride-1 convs, no accumulation)."""
     _check_nhwc(dy, "dy")
     K_, R, S, C = w.shape
     _check(w, "w", torch.bfloat16)
@@ -1012,6 +1018,24 @@ def conv2d_dgrad(dy, w, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), out=None
         _check_nhwc(out, "dx")
         if tuple(out.shape) != tuple(x_shape):
             raise ValueError("conv2d_dgrad: out has the wrong shape")
+    if bn is not None:
+        bx, mean, rstd, ss = bn
+        C = x_shape[1]
+        if beta != 0.0 or tuple(stride) != (1, 1) or tuple(dil) != (1, 1):
+            raise ValueError("conv2d_dgrad: BN sums need a stride-1 dgrad without accumulation")
+        _check_nhwc(bx, "bn x")
+        if tuple(bx.shape) != tuple(x_shape):
+            raise ValueError("conv2d_dgrad: BN input shape mismatch")
+        for name, t, n in (("mean", mean, C), ("rstd", rstd, C), ("scale_shift", ss, 2 * C)):
+            if t is not None:
+                _check(t, name, torch.float32, n)
+        sums = torch.empty(2 * C, device=dy.device, dtype=torch.float32)
+        ws = torch.empty(ext().conv2d_dgrad_bn_ws_floats(g), device=dy.device, dtype=torch.float32)
+        ext().conv2d_dgrad_bn(g, _p(dy), _p(w), _p(out), _p(bx), _p(mean), _p(rstd), _p(ss), _p(sums), _p(ws),
+                              _stream())
+        out._ff_bn_sums = (sums, bx)
+        STATS["conv2d_dgrad_bn"] += 1
+        return out
     ext().conv2d_dgrad(g, _p(dy), _p(w), _p(out), float(beta), _stream())
     STATS["conv2d_dgrad"] += 1
     return out
@@ -1246,7 +1270,7 @@ def bn_apply(x, scale, shift, relu: bool, residual=None):
 
 
 def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, want_masked: bool = False,
-           scale_shift=None):
+           scale_shift=None, pre_sums=None):
     """-> (dx, masked dy or None).  With ``relu`` the mask comes from ``y``,
     or — when ``y`` is None — is recomputed from ``x`` with the forward's
     ``scale_shift`` (fp32 [2, C]: scale, shift), so y is never re-read."""
@@ -1266,10 +1290,14 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, relu: bool, dgamma=None, dbeta=None, wan
     pdt = _dt(gamma) if gamma is not None else DT_BF16
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     dres = torch.empty_like(x, memory_format=torch.channels_last) if want_masked else None
+    if pre_sums is not None:
+        _check(pre_sums, "pre_sums", torch.float32, 2 * C)
+        if want_masked:
+            raise ValueError("bn_bwd: precomputed sums cannot serve the residual form")
     ws, clean = _bn_workspace(x.device, C)
     ext().bn_bwd(_p(dy), _p(x), _p(y if relu_code == 1 else None), _p(mean), _p(rstd), _p(gamma), pdt, _p(dx),
                  _p(dres), _p(dgamma), _p(dbeta), _p(ws), x.numel() // C, C, relu_code, _stream(),
-                 _p(scale_shift if relu_code == 2 else None), clean)
+                 _p(scale_shift if relu_code == 2 else None), clean, _p(pre_sums))
     STATS["bn_bwd"] += 1
     return dx, dres
 

@@ -32,6 +32,14 @@ from .base import OpImpl, acc_grad, register
 _ACTS = {"none": lambda t: t, "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
          "gelu": lambda t: F.gelu(t, approximate="tanh")}
 
+# FF_CONV_BN_BWD=1: a BatchNorm(+ReLU) feeding a stride-1 convolution takes its
+# backward sums from that conv's dgrad epilogue (conv.hip ConvBnBwd) instead of
+# its own reduction pass.  Off by default: on ResNet-50 the epilogue's extra
+# BN-input read and per-tile partial rows cost the dgrad kernels more than the
+# skipped bn_reduce passes save (+3.2 / -2.9 ms per 5 steps,
+# profiles/r5/ab_conv_bn_bwd_r5.txt)
+_CONV_BN_BWD = os.environ.get("FF_CONV_BN_BWD", "0") == "1"
+
 
 def _geom(ctx):
     # an H-sharded input (attribute parallelism) arrives with its halo rows
@@ -55,9 +63,16 @@ def _pick(key, cands):
         if len(cands) == 1 or torch.cuda.is_current_stream_capturing() or _MODE != "auto":
             c = "gemm" if (_MODE == "gemm" and "gemm" in cands) else "native"
         else:
-            # eager clock (these convolutions run for hundreds of microseconds)
+            # eager clock (these convolutions run for hundreds of microseconds);
+            # candidates interleaved over three passes, best of each kept, so a
+            # clock or power transient during one candidate's turn does not
+            # decide the pick (one-shot picks flipped run to run: 7 wgrads per
+            # ResNet-50 step moved between the two paths, profiles/r5/g35_*)
             from .gemm import _time
-            times = {name: _time(fn, iters=3) for name, fn in cands.items()}
+            times = {name: float("inf") for name in cands}
+            for _ in range(3):
+                for name, fn in cands.items():
+                    times[name] = min(times[name], _time(fn, iters=3, rounds=1))
             c = min(times, key=times.get)
         _CHOICE[key] = c
     return c
@@ -159,7 +174,11 @@ class Conv2DOp(OpImpl):
                 y = K.conv2d_fwd(xin, wp, bias, stride, pad, act=act, stats=stats)
             if stats is not None:
                 y._ff_bn_stats = stats
-            return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape))
+            bnsrc = None
+            if (_CONV_BN_BWD and ctx.training and ctx.extra.get("emit_bn_bwd_sums") and halo is None
+                    and tuple(stride) == (1, 1) and C % 8 == 0):
+                bnsrc = getattr(x, "_ff_bn_bwd", None)   # set by the producing BatchNorm
+            return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape), bnsrc)
         if self._native32(x, act):
             wp = W.reshape(Kc, R, S, C)   # physical [K][R][S][C/groups]
             if wp.dtype != x.dtype:
@@ -203,7 +222,7 @@ class Conv2DOp(OpImpl):
 
         if saved[0] == "hip32":
             return self._backward32(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act)
-        _, xin, wp, y, xshape = saved
+        _, xin, wp, y, xshape, bnsrc = saved
         Kc, R, S, Cp = wp.shape
         dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))
         if act != "none":
@@ -249,6 +268,7 @@ class Conv2DOp(OpImpl):
         acc = ctx.extra.get("grad_acc", [None])[0]
         use_acc = (acc is not None and ctx.extra.get("halo") is None and acc.is_cuda and acc.dtype == torch.bfloat16 and tuple(acc.shape) == tuple(xshape)
                    and acc.is_contiguous(memory_format=torch.channels_last))
+        fuse_bn = bnsrc is not None and not use_acc
         if _pointwise(R, S, stride, pad, 1):
             def dgrad_gemm(out):
                 if tuple(stride) == (1, 1):
@@ -275,6 +295,9 @@ class Conv2DOp(OpImpl):
                             "gemm": lambda: dgrad_gemm(tmp)})
             if _CHOICE[key] == "gemm":
                 return [dgrad_gemm(acc if use_acc else None)]
+        if fuse_bn:
+            # the producing BN's backward sums come out of this dgrad's epilogue
+            return [K.conv2d_dgrad(dy, wp, xshape, stride, pad, bn=bnsrc)]
         if use_acc:
             K.conv2d_dgrad(dy, wp, xshape, stride, pad, out=acc, beta=1.0)
             return [acc]

@@ -17,6 +17,11 @@ from .. import kernels as K
 from .base import OpImpl, acc_grad, register
 
 
+def _bn_sums_from_conv() -> bool:
+    from . import conv
+    return conv._CONV_BN_BWD
+
+
 def _ln_axes_are_trailing(ctx, x):
     axes = sorted(int(a) % x.dim() for a in ctx.a("axes", [-1]))
     return axes == list(range(x.dim() - len(axes), x.dim())), len(axes)
@@ -168,6 +173,10 @@ class BatchNormOp(OpImpl):
                 # rows 0 and 1 of bn_finalize's [4, C] buffer): y is not kept
                 assert shift.data_ptr() == scale.data_ptr() + 4 * C
                 ss = torch.as_strided(scale, (2 * C,), (1,))
+            if (ctx.training and not fused and ctx.extra.get("bn_sums_from_conv") and _bn_sums_from_conv()
+                    and (ss is not None or not relu)):
+                # the consuming conv's dgrad reduces this BN's backward sums (conv.hip)
+                y._ff_bn_bwd = (xin, mean, rstd, ss)
             return [y], ("hip", xin, y if (relu and ss is None) else None, mean, rstd, g, relu, fused, ss)
         train = ctx.training
         xf = x.float()
@@ -188,8 +197,10 @@ class BatchNormOp(OpImpl):
         if saved[0] == "hip":
             _, xin, y, mean, rstd, g, relu, fused, ss = saved
             dyn = K.nhwc(dy.to(torch.bfloat16))
+            pre = getattr(dyn, "_ff_bn_sums", None)
+            pre = pre[0] if pre is not None and pre[1] is xin and not fused else None
             dx, dres = K.bn_bwd(dyn, xin, y, mean, rstd, g, relu, dgamma=dg, dbeta=db, want_masked=fused,
-                                scale_shift=ss)
+                                scale_shift=ss, pre_sums=pre)
             return [dx, dres] if fused else [dx]
         _, x, res, g, b, relu = saved
         eps = float(ctx.a("eps", 1e-5))

@@ -623,6 +623,23 @@ class Executor:
             else:
                 keep.append(s)
         self.steps = keep
+        # * BATCHNORM (no residual) whose only consumer is a CONV2D on the same
+        #   layout: that conv's dgrad epilogue reduces the BN's backward sums
+        #   (``emit_bn_bwd_sums``), so the BN backward skips its reduction pass
+        uses = {}
+        for s in self.steps:
+            for v in s.inputs:
+                uses.setdefault(v, []).append(s)
+        for s in self.steps:
+            if (s.kind != "compute" or s.op_type != "BATCHNORM" or len(s.inputs) != 1 or len(s.outputs) != 1
+                    or s.ctx.extra.get("residual_relu") or s.ctx.sum_degree != 1):
+                continue
+            v = s.outputs[0]
+            u = uses.get(v, [])
+            if (len(u) == 1 and u[0].kind == "compute" and u[0].op_type == "CONV2D" and v != self.loss_value
+                    and u[0].ctx.sum_degree == 1 and u[0].inputs[0] == v and lay[v] == lay[s.inputs[0]]):
+                u[0].ctx.extra["emit_bn_bwd_sums"] = True
+                s.ctx.extra["bn_sums_from_conv"] = True
 
     def _fuse_linear_dact(self):
         """LINEAR(act) -> LINEAR: the second layer's input-gradient GEMM

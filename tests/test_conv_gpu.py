@@ -118,6 +118,47 @@ def test_batchnorm_fwd_bwd(C, relu, residual):
         torch.testing.assert_close(db2, db, rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("C,Ko,R,relu", [(64, 64, 3, True), (128, 256, 1, True), (200, 72, 3, False),
+                                          (2048, 512, 1, True)])
+def test_dgrad_bn_sums(C, Ko, R, relu):
+    """A BN(+ReLU) -> conv pair: the dgrad epilogue's BN backward sums
+    (conv.hip, ConvBnBwd) give the same BN backward as bn_bwd's own
+    reduction pass."""
+    torch.manual_seed(4)
+    N, H, W = 3, 9, 11
+    xb = _rand_nhwc((N, C, H, W), 2.0) + 0.3
+    g = (1 + 0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16)
+    stats = torch.zeros(2 * C, device=DEV)
+    K.bn_stats(xb, stats)
+    scale, shift, mean, rstd = K.bn_finalize(stats, g, b, xb.numel() // C, 1e-5, 0.0, None, None)
+    ss = torch.as_strided(scale, (2 * C,), (1,)) if relu else None
+    w = (torch.randn(Ko, R, R, C, device=DEV) / (R * R * C) ** 0.5).to(torch.bfloat16).contiguous()
+    pad = (R // 2, R // 2)
+    dyc = _rand_nhwc((N, Ko, H, W))
+    n0 = K.STATS["conv2d_dgrad_bn"]
+    dx = K.conv2d_dgrad(dyc, w, tuple(xb.shape), (1, 1), pad, bn=(xb, mean, rstd, ss))
+    assert K.STATS["conv2d_dgrad_bn"] == n0 + 1
+    torch.testing.assert_close(dx.float(), K.conv2d_dgrad(dyc, w, tuple(xb.shape), (1, 1), pad).float(),
+                               rtol=0, atol=0)
+    sums, src = dx._ff_bn_sums
+    assert src is xb
+    # fp32 reference of the sums from the stored gradient
+    xf = xb.float()
+    gm = dx.float() * ((xf * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)) > 0).float() if relu else dx.float()
+    xhat = (xf - mean.view(1, -1, 1, 1)) * rstd.view(1, -1, 1, 1)
+    torch.testing.assert_close(sums[:C], gm.sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(sums[C:], (gm * xhat).sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    outs = []
+    for pre in (None, sums):
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        d, _ = K.bn_bwd(dx, xb, None, mean, rstd, g, relu, dgamma=dg, dbeta=db, scale_shift=ss, pre_sums=pre)
+        outs.append((d.float(), dg, db))
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("k,s,p,avg", [((3, 3), (2, 2), (1, 1), False), ((2, 2), (2, 2), (0, 0), False),
                                        ((3, 3), (1, 1), (1, 1), True), ((7, 7), (1, 1), (0, 0), True),
                                        ((3, 3), (2, 2), (0, 0), True)])
