@@ -61,10 +61,22 @@ RedGeom red_geom(int C) {
   r.RL = 256 / r.GL;
   return r;
 }
+// target workgroups of a reduction pass (FFK_BN_RED_BLOCKS, read once).
+// 1024 (4 per CU): ResNet-50 8910 img/s vs 8794 at 2048, 8596 at 4096, 8257
+// at 8192 (interleaved on one box, profiles/r5/ab_bn_red_blocks_r5.txt) --
+// fewer, longer-running workgroups mean fewer bucket atomics and LDS tails
+int red_blocks() {
+  static const int b = [] {
+    const char* e = getenv("FFK_BN_RED_BLOCKS");
+    const int v = e ? atoi(e) : 1024;
+    return v >= 256 && v <= 65536 ? v : 1024;
+  }();
+  return b;
+}
 dim3 red_grid(const RedGeom& r, int64_t M) {
   const int gy = (r.G + r.GL - 1) / r.GL;
   int64_t gx = (M + r.RL - 1) / r.RL;
-  const int64_t want = std::max<int64_t>(1, 2048 / gy);
+  const int64_t want = std::max<int64_t>(1, red_blocks() / gy);
   gx = std::min(gx, want);
   return dim3(static_cast<unsigned>(std::max<int64_t>(gx, 1)), gy);
 }
