@@ -475,6 +475,15 @@ static int bn_unroll() {
   }();
   return u;
 }
+// workgroup cap of the BN apply passes (FFK_BN_APPLY_BLOCKS, read once)
+static int bn_apply_blocks(int64_t n) {
+  static const int cap = [] {
+    const char* e = getenv("FFK_BN_APPLY_BLOCKS");
+    const int v = e ? atoi(e) : 8192;
+    return v >= 256 && v <= 65536 ? v : 8192;
+  }();
+  return static_cast<int>(std::min<int64_t>((n + 255) / 256, cap));
+}
 template <typename F>
 static void with_unroll(F&& f) {
   switch (bn_unroll()) {
@@ -523,7 +532,7 @@ void bn_apply(const void* x, const void* residual, const float* scale, const flo
   if (nvec <= 0) return;
   with_unroll([&](auto uu) {
     constexpr int U = decltype(uu)::value;
-    hipLaunchKernelGGL(bn_apply_kernel<U>, dim3(ew_blocks((nvec + U - 1) / U)), dim3(256), 0, st,
+    hipLaunchKernelGGL(bn_apply_kernel<U>, dim3(bn_apply_blocks((nvec + U - 1) / U)), dim3(256), 0, st,
                        static_cast<const bf16*>(x), static_cast<const bf16*>(residual), scale, shift,
                        static_cast<bf16*>(y), nvec, C, relu);
   });
@@ -555,7 +564,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   const int64_t nvec = M * C / 8;
   with_unroll([&](auto uu) {
     constexpr int U = decltype(uu)::value;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<U>, dim3(ew_blocks((nvec + U - 1) / U)), dim3(256), 0, st,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<U>, dim3(bn_apply_blocks((nvec + U - 1) / U)), dim3(256), 0, st,
                        static_cast<const bf16*>(dy), static_cast<const bf16*>(x), static_cast<const bf16*>(y), coef,
                        static_cast<bf16*>(dx), static_cast<bf16*>(dres), nvec, C, relu, scale_shift);
   });
