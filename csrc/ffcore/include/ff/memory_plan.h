@@ -50,6 +50,10 @@ struct MemoryPlanConfig {
   bool training = true;
   double weight_bytes_per_param = 16.0;
   double align = 256.0;   // bytes
+  // activations of node n held live `live_copies[n]` times (default 1): a
+  // pipeline stage keeps the saved activations of several micro-batches
+  // (1F1B: min(m, S - s) on stage s, GPipe: m)
+  std::map<int, double> live_copies;
 };
 
 // one plan per device 0 .. world-1

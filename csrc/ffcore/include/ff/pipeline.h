@@ -25,6 +25,7 @@
 
 #include "ff/computation_graph.h"
 #include "ff/machine.h"
+#include "ff/memory_plan.h"
 #include "ff/simulator.h"
 
 namespace ff {
@@ -44,6 +45,10 @@ struct PipelinePlan {
   std::map<int, Placement> views;       // PCG node -> its stage's device block
   Json to_json(bool with_views = false) const;
 };
+
+// memory plan config of a pipeline plan: stage s keeps min(m, S - s) micro-
+// batches of activations live under 1F1B, m under GPipe
+MemoryPlanConfig pipeline_memory_config(const PipelinePlan& p, bool one_f_one_b = true);
 
 // one optimizer step of m micro-batches under a non-pipelined strategy
 double micro_batched_step_time(const SimResult& one_batch, int micro_batches);

@@ -152,6 +152,8 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
       if (cfg.training) first_bwd = std::min(first_bwd, bwd(c));
     }
     const bool grad = cfg.training && role != NodeRole::INPUT_PATH && has_consumer;
+    auto lc = cfg.live_copies.find(n);
+    const double copies = lc == cfg.live_copies.end() ? 1.0 : std::max(1.0, lc->second);
     for (size_t o = 0; o < node.outputs.size(); ++o) {
       const auto& s = node.outputs[o].shape;
       const double bytes = static_cast<double>(s.piece_shape().size_bytes());
@@ -161,7 +163,7 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
         a.node = n;
         a.output = static_cast<int>(o);
         a.kind = 0;
-        a.bytes = bytes * h.second;
+        a.bytes = bytes * h.second * copies;
         a.start = fwd.at(n);
         // inputs fed to the graph are read by their consumers' backward
         // (weight gradients); every other activation until its producer's
@@ -171,6 +173,7 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
         if (grad) {
           MemBlock g = a;
           g.kind = 1;
+          g.bytes = bytes * h.second;   // one micro-batch's gradient at a time
           g.start = first_bwd;
           g.end = bwd(n);
           plans[h.first].blocks.push_back(g);

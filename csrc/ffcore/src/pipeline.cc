@@ -156,6 +156,14 @@ PipelinePlan price_pipeline(const ComputationGraph& cg, const CostModel& cm, int
   return P;
 }
 
+MemoryPlanConfig pipeline_memory_config(const PipelinePlan& p, bool one_f_one_b) {
+  MemoryPlanConfig c;
+  const int m = std::max(1, p.micro_batches);
+  for (auto const& kv : p.stage_of)
+    c.live_copies[kv.first] = one_f_one_b ? std::min(m, std::max(1, p.stages - kv.second)) : m;
+  return c;
+}
+
 std::vector<PipelinePlan> pipeline_candidates(const ComputationGraph& cg, const CostModel& cm, int world,
                                               int micro_batches, const SimConfig& sim) {
   std::vector<PipelinePlan> out;

@@ -401,7 +401,15 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
       for (auto const& p : ps) a = std::max(a, p.arena_bytes);
       return a;
     };
-    auto plans = plan_memory(best.pcg, best.views, cfg.world);
+    // a pipeline winner keeps several micro-batches of activations per stage
+    MemoryPlanConfig best_mc;
+    if (best.pipeline_stages > 1) {
+      SimConfig psim = cfg.sim;
+      psim.world = cfg.world;
+      for (auto& pl : pipeline_candidates(cg, cm, cfg.world, std::max(1, cfg.micro_batches), psim))
+        if (pl.stages == best.pipeline_stages) best_mc = pipeline_memory_config(pl);
+    }
+    auto plans = plan_memory(best.pcg, best.views, cfg.world, best_mc);
     const double cap = cm.spec().hbm_capacity;
     if (cap > 0 && busiest(plans) > cap && cfg.world > 1) {
       SimConfig sim = cfg.sim;
@@ -425,7 +433,7 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
         found = true;
       }
       for (auto& pl : pipeline_candidates(cg, cm, cfg.world, M, sim)) {
-        auto pp = plan_memory(pl.pcg, pl.views, cfg.world);
+        auto pp = plan_memory(pl.pcg, pl.views, cfg.world, pipeline_memory_config(pl));
         if (busiest(pp) <= cap && pl.step_time < best_t) {
           best_t = pl.step_time;
           fb_pcg = pl.pcg;

@@ -30,7 +30,7 @@ from __future__ import annotations
 import dataclasses
 import math
 import os
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -239,6 +239,9 @@ class Plan:
     src_boxes: Dict[int, Optional[Box]]
     groups: List[Tuple[int, ...]]
     gather_dim: int = -1
+    # per-device index tensors of deduplicated all_gather pieces, built once
+    # (an upload per step would be a pageable copy inside graph capture)
+    index_cache: Dict[Any, torch.Tensor] = dataclasses.field(default_factory=dict, compare=False, repr=False)
 
 
 def _summed_sources(src: Layout, dst: Layout, s_d: int) -> List[int]:
@@ -473,7 +476,16 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
             seen.add(b)
             keep.append(i)
         d = plan.gather_dim
-        sel = flat if keep == list(range(n)) else flat[torch.tensor(keep, device=flat.device)]
+        if keep == list(range(n)):
+            sel = flat
+        elif keep == list(range(keep[0], keep[0] + len(keep))):
+            sel = flat.narrow(0, keep[0], len(keep))
+        else:
+            key = (str(flat.device), tuple(keep))
+            idx = plan.index_cache.get(key)
+            if idx is None:
+                idx = plan.index_cache[key] = torch.tensor(keep, device=flat.device)
+            sel = flat[idx]
         if all(xs.shape[i] == 1 for i in range(d)):
             return sel.reshape(tuple(xs.shape[:d]) + (len(keep) * xs.shape[d],) + tuple(xs.shape[d + 1:]))
         return sel.movedim(0, d).reshape(tuple(xs.shape[:d]) + (len(keep) * xs.shape[d],) + tuple(xs.shape[d + 1:]))
@@ -533,7 +545,16 @@ def _exchange_all_to_all(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext
         # no part; members address each other by group rank (sorted order)
         g = plan.groups[0]
         if me not in g:
-            return None if my_dst is None else torch.zeros(dst_shape, dtype=dtype, device=device)
+            # outside the exchange: any destination box this rank has is served
+            # entirely from its own source piece (a rank that received from
+            # another would be a member)
+            if my_dst is None:
+                return None
+            result = torch.zeros(dst_shape, dtype=dtype, device=device)
+            for c in plan.contributions[me]:
+                assert c.src_rank == me, "non-member of a sub-group all_to_all receives from another rank"
+                result[rel_slices(c.part, my_dst)] += x[rel_slices(c.part, my_src)].to(dtype)
+            return result
         grp = ctx.group(g)
         gi = [in_sizes[m] for m in g]
         go = [out_sizes[m] for m in g]

@@ -1518,10 +1518,16 @@ class Executor:
         t0 = self.tracer.begin("__update__:fwd", "compute", self.step_num) if prof else None
         self.update(lr)
         self.tracer.end(t0)
+        self._after_first_update()
+
+    def _after_first_update(self):
+        """Once per executor, after the first distributed update (plain or
+        pipelined step): the first step tuned every GEMM signature on each
+        rank on its own, so agree on one kernel per signature before later
+        steps / the capture (partial-sum replicas' bias gradients would drift
+        apart otherwise)."""
         if (self.dist.distributed and not getattr(self, "_choices_synced", False)
                 and self.cfg.device.type == "cuda" and not torch.cuda.is_current_stream_capturing()):
-            # the first step tuned every GEMM signature on each rank on its own:
-            # agree on one kernel per signature before later steps / the capture
             from ..ops.gemm import sync_choices
             sync_choices()
             self._choices_synced = True
@@ -1610,6 +1616,7 @@ class Executor:
                 self.backward(g, zero_grads=(n_back == 0), accumulate=(n_back > 0), sync=(n_back == m - 1))
                 n_back += 1
         self.update(lr)
+        self._after_first_update()
 
     def make_graphed_train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, warmup: int = 2):
         """Capture one whole training iteration (forward, loss, backward with

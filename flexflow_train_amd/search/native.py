@@ -93,12 +93,16 @@ def sim_config(ffconfig=None, world: int = 1) -> dict:
 
 
 def plan_memory(pcg, world: int = 1, views: Optional[Dict[int, Sequence[int]]] = None, training: bool = True,
-                weight_bytes_per_param: float = 16.0, with_blocks: bool = False):
+                weight_bytes_per_param: float = 16.0, with_blocks: bool = False,
+                live_copies: Optional[Dict[int, float]] = None):
     """Liveness-based memory plan of one step per device
     (csrc/ffcore/src/memory_plan.cc): [{device, weight_bytes,
-    peak_live_bytes, arena_bytes, naive_bytes, [blocks]}]."""
+    peak_live_bytes, arena_bytes, naive_bytes, [blocks]}].  ``live_copies``:
+    PCG node -> micro-batches of its activations held live at once (a
+    pipeline stage under 1F1B keeps min(m, S - s))."""
     return json.loads(C.plan_memory(pcg, {int(k): [int(d) for d in v] for k, v in (views or {}).items()}, int(world),
-                                    bool(training), float(weight_bytes_per_param), bool(with_blocks)))
+                                    bool(training), float(weight_bytes_per_param), bool(with_blocks),
+                                    {int(k): float(v) for k, v in (live_copies or {}).items()}))
 
 
 def simulate(pcg, cm, world: int, views: Optional[Dict[int, Sequence[int]]] = None, dot: bool = False,

@@ -131,20 +131,20 @@ def save_step_checkpoint(model, root: str, progress: dict, keep: int = 2) -> str
     return path
 
 
-def _assemble_full(path: str, world: int) -> Dict[str, torch.Tensor]:
-    full: Dict[str, torch.Tensor] = {}
+def _rank_files(path: str, world: int):
     for r in range(world):
         f = os.path.join(path, f"rank{r}.pt")
-        if not os.path.exists(f):
-            continue
-        st = torch.load(f, map_location="cpu", weights_only=True)
-        for name, rec in st["params"].items():
-            t = full.get(name)
-            if t is None:
-                t = full[name] = torch.zeros(tuple(rec["logical_shape"]), dtype=torch.float32)
-            box = tuple(slice(lo, hi) for lo, hi in rec["box"])
-            t[box] = rec["tensor"].reshape(t[box].shape)
-    return full
+        if os.path.exists(f):
+            yield r, f
+
+
+def _add_params(full: Dict[str, torch.Tensor], st: dict):
+    for name, rec in st["params"].items():
+        t = full.get(name)
+        if t is None:
+            t = full[name] = torch.zeros(tuple(rec["logical_shape"]), dtype=torch.float32)
+        box = tuple(slice(lo, hi) for lo, hi in rec["box"])
+        t[box] = rec["tensor"].reshape(t[box].shape)
 
 
 def _optimizer_pieces(ex) -> Dict[str, dict]:
@@ -172,23 +172,36 @@ def _optimizer_pieces(ex) -> Dict[str, dict]:
     return out
 
 
-def _assemble_optimizer(path: str, world: int) -> Dict[str, Dict[str, torch.Tensor]]:
-    full: Dict[str, Dict[str, torch.Tensor]] = {}
-    for r in range(world):
-        f = os.path.join(path, f"rank{r}.pt")
-        if not os.path.exists(f):
-            continue
+def _add_opt_pieces(full: Dict[str, Dict[str, torch.Tensor]], st: dict):
+    for name, rec in st.get("opt_pieces", {}).items():
+        box = tuple(slice(lo, hi) for lo, hi in rec["box"])
+        for k, t in rec.items():
+            if k in ("box", "logical_shape"):
+                continue
+            dst = full.setdefault(name, {}).get(k)
+            if dst is None:
+                dst = full[name][k] = torch.zeros(tuple(rec["logical_shape"]), dtype=torch.float32)
+            dst[box] = t.reshape(dst[box].shape)
+
+
+def _assemble_once(path: str, world: int, rng_rank: int):
+    """One pass over the saved rank files (each loaded once, then dropped):
+    the logical weights, the logical optimizer state, the optimizer step
+    counter and the RNG state of ``rng_rank``'s file."""
+    full: Dict[str, torch.Tensor] = {}
+    ofull: Dict[str, Dict[str, torch.Tensor]] = {}
+    steps, rng = None, None
+    for r, f in _rank_files(path, world):
         st = torch.load(f, map_location="cpu", weights_only=True)
-        for name, rec in st.get("opt_pieces", {}).items():
-            box = tuple(slice(lo, hi) for lo, hi in rec["box"])
-            for k, t in rec.items():
-                if k in ("box", "logical_shape"):
-                    continue
-                dst = full.setdefault(name, {}).get(k)
-                if dst is None:
-                    dst = full[name][k] = torch.zeros(tuple(rec["logical_shape"]), dtype=torch.float32)
-                dst[box] = t.reshape(dst[box].shape)
-    return full
+        _add_params(full, st)
+        _add_opt_pieces(ofull, st)
+        opts = st.get("optimizer") or []
+        if steps is None and opts:
+            steps = int(opts[0]["step"])
+        if r == rng_rank:
+            rng = {"rng": st.get("rng")}
+        del st
+    return full, ofull, steps, rng
 
 
 def _restore_rng(st: dict, ex):
@@ -217,7 +230,8 @@ def load_checkpoint(model, path: str, strict: bool = True):
         _restore_rng(st, ex)
         meta["resharded"] = False
     else:
-        full = _assemble_full(path, meta["world"])
+        rng_rank = ex.rank if ex.rank < meta["world"] else 0
+        full, ofull, steps, rng = _assemble_once(path, meta["world"], rng_rank)
         names = set(ex.parameter_names())
         missing = names - set(full)
         if strict and missing:
@@ -231,29 +245,13 @@ def load_checkpoint(model, path: str, strict: bool = True):
         # optimizer state: reassembled per weight and re-sliced like the weights
         opt_ok = not ex.cfg.shard_optimizer and not meta.get("optimizer", {}).get("sharded", False)
         if opt_ok:
-            ofull = _assemble_optimizer(path, meta["world"])
             for n in names & set(ofull):
                 ex.set_optimizer_state(n, ofull[n])
-            steps = _flat_steps(path, meta["world"])
             for f in ex.flats:
                 f["opt"].step_num = steps if steps is not None else ex.step_num
-        r0 = os.path.join(path, f"rank{ex.rank if ex.rank < meta['world'] else 0}.pt")
-        if os.path.exists(r0):
-            _restore_rng(torch.load(r0, map_location="cpu", weights_only=True), ex)
+        if rng is not None:
+            _restore_rng(rng, ex)
         meta["resharded"] = True
         meta["optimizer_resharded"] = opt_ok
     ex.dist.barrier()
     return meta
-
-
-def _flat_steps(path: str, world: int) -> Optional[int]:
-    """The optimizer step counter (Adam's bias correction) of the saved run:
-    every flat of a run steps together, so rank 0's first flat says it."""
-    for r in range(world):
-        f = os.path.join(path, f"rank{r}.pt")
-        if os.path.exists(f):
-            st = torch.load(f, map_location="cpu", weights_only=True)
-            opts = st.get("optimizer") or []
-            if opts:
-                return int(opts[0]["step"])
-    return None

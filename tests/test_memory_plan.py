@@ -86,3 +86,21 @@ def test_search_falls_back_when_the_winner_does_not_fit():
     # the simulator's memory penalty or the plan check moves it to a pipeline
     assert "pipeline" in rep2["algorithm"], rep2["algorithm"]
     assert rep2["memory_plan"]["fits_hbm"] and rep2["memory_plan"]["arena_bytes"] <= spec.hbm_capacity
+
+
+def test_live_copies_scale_activations_not_gradients():
+    """A pipeline stage that keeps k micro-batches of activations live (1F1B:
+    min(m, S - s)) is planned with k copies of each activation block and one
+    of its gradient (csrc/ffcore/src/pipeline.cc pipeline_memory_config)."""
+    m = _mlp()
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    (one,) = native.plan_memory(pcg, 1, with_blocks=True)
+    nodes = {b["node"] for b in one["blocks"] if b["kind"] == 0}
+    (three,) = native.plan_memory(pcg, 1, with_blocks=True, live_copies={n: 3 for n in nodes})
+    act1 = sum(b["bytes"] for b in one["blocks"] if b["kind"] == 0)
+    act3 = sum(b["bytes"] for b in three["blocks"] if b["kind"] == 0)
+    assert abs(act3 - 3 * act1) < 1e-6 * act1
+    g1 = sum(b["bytes"] for b in one["blocks"] if b["kind"] == 1)
+    g3 = sum(b["bytes"] for b in three["blocks"] if b["kind"] == 1)
+    assert g1 == g3
+    assert three["peak_live_bytes"] > one["peak_live_bytes"]

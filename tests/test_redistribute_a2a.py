@@ -32,6 +32,10 @@ def _cases(world):
     if world >= 4:
         # a stage boundary that involves 3 of 4 ranks: a sub-group all_to_all
         cases.append((Layout(S, (2, 1, 1), block=2, start=0), Layout(S, (1, 1, 1), block=1, start=2), "all_to_all"))
+        # replicated on [0, 1] -> 2-way shards on [1, 2]: rank 1 keeps its own
+        # piece while another rank exchanges (it must not come back zero
+        # whether or not it is a member of the exchange)
+        cases.append((Layout(S, (1, 1, 1), block=2, start=0), Layout(S, (2, 1, 1), block=2, start=1), None))
     return cases
 
 
