@@ -67,9 +67,14 @@ def main():
                     help="N > 1: skip timing the step's RCCL collectives (cost-model calibration, outside the "
                          "timed region)")
     ap.add_argument("--ae", action="store_true",
-                    help="N > 1: also run the reference's OSDI'22 AE BERT protocol (scripts/osdi22ae/bert.sh: 12 "
-                         "layers, hidden 1024, 16 heads, seq 512, global batch 8, --budget 30) searched vs data "
-                         "parallel, reported as config.ae_bert (outside the headline timed region)")
+                    help="(default at N > 1 for BERT) also run the reference's OSDI'22 AE BERT protocol "
+                         "(scripts/osdi22ae/bert.sh: 12 layers, hidden 1024, 16 heads, seq 512, global batch 8, "
+                         "--budget 30) searched vs data parallel, reported as config.ae_bert (outside the headline "
+                         "timed region)")
+    ap.add_argument("--no-ae", action="store_true", help="skip the AE protocol at N > 1")
+    ap.add_argument("--ae-deadline-s", type=float, default=float(os.environ.get("FF_AE_DEADLINE_S", "300")),
+                    help="start the AE protocol only if the run so far took less than this many seconds (keeps the "
+                         "whole command inside the driver's bench timeout)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32"],
                     help="compute dtype (float32: the exact-fp32 MFMA kernels; the headline metric is bf16)")
     ap.add_argument("--layers", type=int, default=None, help="override (debug only; invalidates the metric)")
@@ -87,6 +92,7 @@ def main():
     args = ap.parse_args()
 
     os.environ["FF_GEMM"] = args.gemm
+    t_start = time.time()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,8 +118,13 @@ def main():
         except Exception as e:  # noqa: BLE001 -- never costs the headline
             res["config"]["comm_calibration"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     ae = None
-    if world > 1 and args.ae and args.model in ("bert-large", "bert-base"):
-        ae = _run_ae(args, world, rank, res)
+    if world > 1 and not args.no_ae and args.model in ("bert-large", "bert-base"):
+        # every rank decides from rank 0's clock, so all of them take the same branch
+        spent = res["ex"].dist.max_scalar(time.time() - t_start)
+        if spent < args.ae_deadline_s:
+            ae = _run_ae(args, world, rank, res)
+        else:
+            ae = {"skipped": f"run took {spent:.0f} s before the protocol (deadline {args.ae_deadline_s:.0f} s)"}
     speed = {}
     if world > 1 and args.strategy == "search":
         pred = res["search"].get("predicted_speedup_over_dp")
@@ -132,6 +143,11 @@ def main():
     if rank == 0:
         conf = res["config"]
         conf.update(speed)
+        if ae is not None and ae.get("speedup_over_dp") is not None:
+            # the measured searched-vs-DP ratio of the reference's AE protocol
+            # (the headline's 64 sequences per GPU leave the search nothing to
+            # win over DP; at 1 sequence per GPU it picks tensor / head splits)
+            conf["ae_speedup_over_dp"] = ae["speedup_over_dp"]
         if ae is not None:
             conf["ae_bert"] = ae
         print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(res["value"], 2),
@@ -213,6 +229,24 @@ def _memory_record(model, ex, world, bytes_per_param=16.0):
     if ex.cfg.device.type == "cuda":
         rec["measured_peak_gb"] = round(torch.cuda.max_memory_allocated(ex.cfg.device) / 1e9, 2)
     return rec
+
+
+def _search_record(model, world):
+    """What the strategy search did: wall time, states / strategies priced,
+    iterations against the budget, whether it ended on its time limit, and
+    whether the machine mapping (per-op device placement) won."""
+    rep = dict(model.search_report or {})
+    if world <= 1 or not rep:
+        return None
+    cfg = model.ffconfig
+    limit = float(getattr(cfg, "search_time_limit", 45.0))
+    out = {"s": round(float(rep.get("elapsed", 0.0)), 2), "algorithm": rep.get("algorithm"),
+           "evaluated": rep.get("evaluated"), "iterations": rep.get("iterations"),
+           "budget": int(cfg.search_budget or 0), "mapped_states": rep.get("mapped_states"),
+           "mapping_won": bool(model.views) or "+mapping" in str(rep.get("algorithm", "")),
+           "predicted_speedup_over_dp": rep.get("predicted_speedup_over_dp")}
+    out["time_limited"] = out["s"] >= 0.98 * limit
+    return out
 
 
 def _time_steps(args, ex, feeds, labels, global_batch):
@@ -320,6 +354,7 @@ def _run_bert(args, world, rank, only_dp: bool):
         "tokens_per_sec": round(t["value"] * args.seq, 1),
         "final_loss": round(pm.loss, 4),
         "memory": _memory_record(model, ex, world),
+        "search": _search_record(model, world),
     }
     prof = None
     if args.profile:
@@ -453,7 +488,8 @@ def _run_zoo(args, world, rank, only_dp: bool):
             "compile_s": round(compile_s, 2), "hipgraph": t["graphed"],
             "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
             "native_replay": getattr(ex, "native_replay", None), "final_loss": round(pm.loss, 4),
-            "memory": _memory_record(model, ex, world, 16.0 if opt == "adam" else 8.0)}
+            "memory": _memory_record(model, ex, world, 16.0 if opt == "adam" else 8.0),
+            "search": _search_record(model, world)}
     conf.update(extra)
     if zname == "gpt":
         conf["tokens_per_sec"] = round(t["value"] * mcfg.sequence_length, 1)

@@ -312,6 +312,25 @@ PYBIND11_MODULE(_ffkernels, m) {
   });
   m.def("conv2d_wgrad", [=](std::vector<int> shp, uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t ws, int splits,
                             uintptr_t st) { conv2d_wgrad(cshape(shp), P(x), P(dy), F(dw), F(ws), splits, S(st)); });
+  m.def("conv2d_grouped_wexp_elems",
+        [=](std::vector<int> shp, int groups) { return conv2d_grouped_wexp_elems(cshape(shp), groups); });
+  m.def("conv2d_grouped_wgrad_ws_floats",
+        [=](std::vector<int> shp, int groups) { return conv2d_grouped_wgrad_ws_floats(cshape(shp), groups); });
+  m.def("conv2d_grouped_expand", [=](std::vector<int> shp, int groups, uintptr_t w, uintptr_t wexp, uintptr_t st) {
+    conv2d_grouped_expand(cshape(shp), groups, P(w), P(wexp), S(st));
+  });
+  m.def("conv2d_grouped_fwd", [=](std::vector<int> shp, int groups, uintptr_t x, uintptr_t wexp, uintptr_t bias,
+                                  uintptr_t y, uintptr_t stats, uintptr_t ws, int act, uintptr_t st) {
+    conv2d_grouped_fwd(cshape(shp), groups, P(x), P(wexp), P(bias), P(y), F(stats), F(ws), act, S(st));
+  });
+  m.def("conv2d_grouped_dgrad", [=](std::vector<int> shp, int groups, uintptr_t dy, uintptr_t wexp, uintptr_t dx,
+                                    float beta, uintptr_t st) {
+    conv2d_grouped_dgrad(cshape(shp), groups, P(dy), P(wexp), P(dx), beta, S(st));
+  });
+  m.def("conv2d_grouped_wgrad", [=](std::vector<int> shp, int groups, uintptr_t x, uintptr_t dy, uintptr_t dw,
+                                    uintptr_t ws, uintptr_t st) {
+    conv2d_grouped_wgrad(cshape(shp), groups, P(x), P(dy), F(dw), F(ws), S(st));
+  });
   m.def("gemm_f32", [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, uintptr_t pre, int64_t M, int64_t N,
                        int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool ta, bool tb, int act, float alpha,
                        float beta, int in_f32, int out_f32, uintptr_t st, int batch, int64_t sa, int64_t sb,

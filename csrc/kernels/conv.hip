@@ -58,7 +58,8 @@ struct ConvArgs {
   const bf16* bias; // FWD only
   float* stats;     // FWD only: per-wave partials [gm*2][2][K] (sum, sum of squares)
   float* wpart;     // WGRAD split-K partial slabs [splits][K][R*S*C] (null: splits == 1)
-  int N, H, W, C, K, R, S, P, Q;
+  int N, H, W, C, K, R, S, P, Q;   // C / K: channels of one (super-)group
+  int ldx, ldk;     // pixel strides (channel counts) of X / dX and of Y / dY
   int sh, sw, ph, pw, dh, dw;
   int M, NG, KG;    // GEMM sizes
   int act;
@@ -152,7 +153,7 @@ struct AGather {
         const int n = static_cast<int>(fdiv(static_cast<unsigned>(t), g.fP)), p = t - n * g.P;
         ya[i] = p * g.sh - g.ph;
         xa[i] = q * g.sw - g.pw;
-        pix[i] = ((n * g.H + ya[i]) * g.W + xa[i]) * g.C;
+        pix[i] = ((n * g.H + ya[i]) * g.W + xa[i]) * g.ldx;
       } else {
         int w, h, n;
         if (g.par) {
@@ -169,7 +170,7 @@ struct AGather {
         }
         ya[i] = h + g.ph;
         xa[i] = w + g.pw;
-        pix[i] = n * g.P * g.Q * g.K;
+        pix[i] = n * g.P * g.Q * g.ldk;
       }
     }
     k = (threadIdx.x & 7) * 8;   // K-tile 0 (FWD / DGRAD never split K)
@@ -189,7 +190,7 @@ struct AGather {
     const bool kok = k < g.KG;
     if (MODE == MODE_FWD) {
       const int rr = r * g.dh, ss = s * g.dw;
-      const int delta = (rr * g.W + ss) * g.C + cc;
+      const int delta = (rr * g.W + ss) * g.ldx + cc;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // bitwise & (no short-circuit): hipcc otherwise branches on kok around the
@@ -212,7 +213,7 @@ struct AGather {
           ok = ok & (yn == oh * g.sh) & (xn == ow * g.sw);
         }
         ok = ok & (oh < g.P) & (ow < g.Q);
-        reg[i] = bld8(rsrc, pix[i] + (oh * g.Q + ow) * g.K + cc, ok, oob);
+        reg[i] = bld8(rsrc, pix[i] + (oh * g.Q + ow) * g.ldk + cc, ok, oob);
       }
     }
     // next K-tile: k += 64 (channel counts are multiples of 8: C = 8 wraps
@@ -323,7 +324,7 @@ struct ColStager {
         const int ih = p * g.sh - g.ph + tr_ * g.dh, iw = q * g.sw - g.pw + ts_ * g.dw;
         ok = ok & tok_ & (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H)) &
              (static_cast<unsigned>(iw) < static_cast<unsigned>(g.W));
-        off = ((n * g.H + ih) * g.W + iw) * g.C + tc_;
+        off = ((n * g.H + ih) * g.W + iw) * g.ldx + tc_;
       }
       reg[i] = bld8(rsrc, off, ok, oob);
     }
@@ -372,6 +373,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
     if (kt0 >= kt1) return;
   }
 
+  // grouped convolutions: blockIdx.z = super-group (a block-diagonal dense
+  // conv over g.C input / g.K output channels at channel offsets cx0 / ck0
+  // of the full tensors, its expanded weight the z-th [K][R][S][C] block)
+  const int z = blockIdx.z;
+  const int cx0 = z * g.C, ck0 = z * g.K;
+  const int64_t wz = static_cast<int64_t>(z) * g.K * g.R * g.S * g.C;
+
   // operand stagers
   AGather<MODE_FWD> afw;
   AGather<MODE_DGRAD> adg;
@@ -380,18 +388,22 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   ColStager<BN, 1> bdg;
   ColStager<BN, 2> bwg;
 
-  const __amdgpu_buffer_rsrc_t rx = conv_rsrc(g.x, g.bx), rw = conv_rsrc(g.w, g.bw), rdy = conv_rsrc(g.dy, g.bdy);
+  // the buffer ranges start at the super-group's channel offset: a chunk
+  // past the tensor's end still reads the range check's zeros
+  const unsigned bxz = g.bx - 2u * cx0, bdyz = g.bdy - 2u * ck0;
+  const __amdgpu_buffer_rsrc_t rx = conv_rsrc(g.x + cx0, bxz), rw = conv_rsrc(g.w + wz, g.bw),
+                               rdy = conv_rsrc(g.dy + ck0, bdyz);
   auto load = [&](int kt) {
     const int k0 = kt * BK;
     if (MODE == MODE_FWD) {
-      afw.load(g, rx, g.bx);
+      afw.load(g, rx, bxz);
       bfw.load(rw, g.bw, g.KG, n0, g.NG, k0, g.KG);
     } else if (MODE == MODE_DGRAD) {
-      adg.load(g, rdy, g.bdy);
+      adg.load(g, rdy, bdyz);
       bdg.load(g, rw, g.bw, 0, n0, g.NG, k0, g.KG);
     } else {
-      awg.load(g, rdy, g.bdy, g.K, m0, g.M, k0, g.KG);
-      bwg.load(g, rx, g.bx, 0, n0, g.NG, k0, g.KG);
+      awg.load(g, rdy, bdyz, g.ldk, m0, g.M, k0, g.KG);
+      bwg.load(g, rx, bxz, 0, n0, g.NG, k0, g.KG);
     }
   };
   auto store = [&](unsigned char* buf) {
@@ -463,7 +475,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
   if (MODE == MODE_WGRAD) {
     // one writer per element: split 0 of a single-split launch accumulates into
     // dW directly; otherwise this split's slab (summed by reduce_rows)
-    float* out = g.wpart ? g.wpart + static_cast<int64_t>(split) * g.M * g.NG : static_cast<float*>(g.out);
+    const int64_t slab = static_cast<int64_t>(g.M) * g.NG;
+    float* out = g.wpart ? g.wpart + (static_cast<int64_t>(split) * gridDim.z + z) * slab
+                         : static_cast<float*>(g.out) + z * slab;
     const bool accumulate = g.wpart == nullptr;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -486,7 +500,11 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
     return;
   }
 
-  bf16* out = static_cast<bf16*>(g.out);
+  // FWD writes output channels [ck0, ck0 + K) of Y, DGRAD input channels
+  // [cx0, cx0 + C) of dX
+  const int coff = MODE == MODE_FWD ? ck0 : cx0;
+  const int ldo = MODE == MODE_FWD ? g.ldk : g.ldx;
+  bf16* out = static_cast<bf16*>(g.out) + coff;
 
   // Epilogue through LDS: lanes own one row x 4 columns of the accumulator
   // (8-byte pieces of many rows), so the tile is first written to an LDS
@@ -509,7 +527,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
         if (MODE == MODE_FWD) {
           if (g.bias && n < g.NG) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += bf2f(g.bias[n + e]);
+            for (int e = 0; e < 4; ++e) v[e] += bf2f(g.bias[ck0 + n + e]);
           }
           if (g.act) {
 #pragma unroll
@@ -535,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int m = m0 + (threadIdx.x + 256 * i) / CPR;
-      if (m < g.M && n < g.NG) bxr[i] = *reinterpret_cast<const bf16x8*>(g.bnx + static_cast<int64_t>(m) * g.NG + n);
+      if (m < g.M && n < g.NG) bxr[i] = *reinterpret_cast<const bf16x8*>(g.bnx + static_cast<int64_t>(m) * ldo + coff + n);
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -563,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
     const int m = m0 + ml, n = n0 + ch * 8;
     if (m >= g.M || n >= g.NG) continue;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(ctile + ml * ROWB + ch * 16);
-    bf16* dst = out + (MODE == MODE_DGRAD ? dgrad_row(g, m) : static_cast<int64_t>(m)) * g.NG + n;
+    bf16* dst = out + (MODE == MODE_DGRAD ? dgrad_row(g, m) : static_cast<int64_t>(m)) * ldo + n;
     if (MODE == MODE_DGRAD && g.beta != 0.f) {
       const bf16x8 old = *reinterpret_cast<const bf16x8*>(dst);
 #pragma unroll
@@ -611,8 +629,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs g) {
       const float t = red[chv * 16 + vv] + red[(CPR + chv) * 16 + vv] + red[(2 * CPR + chv) * 16 + vv] +
                       red[(3 * CPR + chv) * 16 + vv];
       const int n = n0 + chv * 8 + (vv & 7);
-      float* part = g.stats + static_cast<int64_t>(tm) * 2 * g.NG;   // one partial row per M tile
-      if (n < g.NG) part[(vv < 8 ? 0 : g.NG) + n] = t;
+      float* part = g.stats + static_cast<int64_t>(tm) * 2 * ldo;   // one partial row per M tile
+      if (n < g.NG) part[(vv < 8 ? 0 : ldo) + coff + n] = t;
     }
   }
 }
@@ -669,6 +687,8 @@ namespace {
 ConvArgs make_args(const ConvShape& cs) {
   ConvArgs g{};
   g.N = cs.N; g.H = cs.H; g.W = cs.W; g.C = cs.C; g.K = cs.K; g.R = cs.R; g.S = cs.S;
+  g.ldx = cs.C;
+  g.ldk = cs.K;
   g.sh = cs.sh; g.sw = cs.sw; g.ph = cs.ph; g.pw = cs.pw; g.dh = cs.dh; g.dw = cs.dw;
   g.P = (cs.H + 2 * cs.ph - cs.dh * (cs.R - 1) - 1) / cs.sh + 1;
   g.Q = (cs.W + 2 * cs.pw - cs.dw * (cs.S - 1) - 1) / cs.sw + 1;
@@ -703,9 +723,9 @@ void check_shape(const ConvShape& cs, const char* who) {
 }
 
 template <int MODE>
-void launch(const ConvArgs& g, int bn, int blocks, hipStream_t st) {
-  if (bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<MODE, 64>), dim3(blocks), dim3(256), 0, st, g);
-  else hipLaunchKernelGGL((conv_igemm_kernel<MODE, 128>), dim3(blocks), dim3(256), 0, st, g);
+void launch(const ConvArgs& g, int bn, int blocks, hipStream_t st, int zgroups = 1) {
+  if (bn == 64) hipLaunchKernelGGL((conv_igemm_kernel<MODE, 64>), dim3(blocks, 1, zgroups), dim3(256), 0, st, g);
+  else hipLaunchKernelGGL((conv_igemm_kernel<MODE, 128>), dim3(blocks, 1, zgroups), dim3(256), 0, st, g);
 }
 
 }  // namespace
@@ -864,6 +884,222 @@ void conv2d_wgrad(const ConvShape& cs, const void* x, const void* dy, float* dw,
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Grouped convolutions (ResNeXt) on the bf16 MFMA kernels above.  `gps`
+// consecutive groups form a super-group of Cs = gps * C/groups input and
+// Ks = gps * K/groups output channels, run as ONE dense implicit GEMM over a
+// block-diagonal expanded weight [Z][Ks][R][S][Cs] (zeros between the
+// groups), blockIdx.z = super-group.  gps is the smallest divisor of
+// `groups` with Cs, Ks multiples of 8 and Ks >= 64 (one 64-wide MFMA tile):
+// ResNeXt-50 32x4d's Cg = 4 runs 16 groups per super-group.  The MFMAs on the
+// zero blocks (gps x the useful work) are cheap next to what these layers
+// move: the 3x3 grouped convs carry 1/8 of a dense 3x3's FLOPs per byte.
+// Parity: conv_2d_kernels.cu:194-196 (cudnnSetConvolutionGroupCount, tensor
+// op math), :279 / :346 / :362.
+namespace {
+struct GroupPlan {
+  int Z, gps, Cs, Ks, Cg, Kg;
+};
+GroupPlan group_plan(const ConvShape& cs, int groups) {
+  if (groups <= 0 || cs.C % groups || cs.K % groups)
+    throw std::invalid_argument("conv2d_grouped: groups must divide C and K");
+  GroupPlan p{};
+  p.Cg = cs.C / groups;
+  p.Kg = cs.K / groups;
+  for (int gps = 1; gps <= groups; ++gps) {
+    if (groups % gps) continue;
+    const int Cs = gps * p.Cg, Ks = gps * p.Kg;
+    if (Cs % 8 || Ks % 8) continue;
+    if (Ks < 64 && gps != groups) continue;
+    p.gps = gps;
+    p.Cs = Cs;
+    p.Ks = Ks;
+    p.Z = groups / gps;
+    return p;
+  }
+  throw std::invalid_argument("conv2d_grouped: no super-group with channel counts that are multiples of 8");
+}
+// the per-super-group dense shape; pixel strides are the full channel counts
+ConvArgs grouped_args(const ConvShape& cs, const GroupPlan& p) {
+  ConvShape s = cs;
+  s.C = p.Cs;
+  s.K = p.Ks;
+  ConvArgs g = make_args(s);
+  g.ldx = cs.C;
+  g.ldk = cs.K;
+  g.bx = static_cast<unsigned>(static_cast<int64_t>(cs.N) * cs.H * cs.W * cs.C * 2);
+  g.bdy = static_cast<unsigned>(static_cast<int64_t>(cs.N) * g.P * g.Q * cs.K * 2);
+  return g;
+}
+
+// wexp[k][rs][cl] = w[k][rs][cl - (kl / Kg) * Cg] on the diagonal block, else 0
+__global__ __launch_bounds__(256) void group_expand_kernel(const bf16* __restrict__ w, bf16* __restrict__ wexp,
+                                                           int64_t n, int RS, int Cs, int Ks, int Cg, int Kg) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int cl = static_cast<int>(i % Cs);
+  const int64_t t = i / Cs;   // k * RS + rs
+  const int rs = static_cast<int>(t % RS);
+  const int64_t k = t / RS;
+  const int kl = static_cast<int>(k % Ks);
+  const int c0 = (kl / Kg) * Cg;
+  wexp[i] = (cl >= c0 && cl < c0 + Cg) ? w[(k * RS + rs) * Cg + (cl - c0)] : static_cast<bf16>(0.f);
+}
+// dw[k][rs][c] += dwexp[k][rs][(kl / Kg) * Cg + c]
+__global__ __launch_bounds__(256) void group_compress_kernel(const float* __restrict__ dwexp, float* __restrict__ dw,
+                                                             int64_t n, int RS, int Cs, int Ks, int Cg, int Kg) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = static_cast<int>(i % Cg);
+  const int64_t t = i / Cg;
+  const int rs = static_cast<int>(t % RS);
+  const int64_t k = t / RS;
+  const int kl = static_cast<int>(k % Ks);
+  dw[i] += dwexp[(k * RS + rs) * Cs + (kl / Kg) * Cg + c];
+}
+}  // namespace
+
+int64_t conv2d_grouped_wexp_elems(const ConvShape& cs, int groups) {
+  const GroupPlan p = group_plan(cs, groups);
+  return static_cast<int64_t>(cs.K) * cs.R * cs.S * p.Cs;
+}
+
+void conv2d_grouped_expand(const ConvShape& cs, int groups, const void* w, void* wexp, hipStream_t st) {
+  const GroupPlan p = group_plan(cs, groups);
+  const int64_t n = static_cast<int64_t>(cs.K) * cs.R * cs.S * p.Cs;
+  hipLaunchKernelGGL(group_expand_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const bf16*>(w), static_cast<bf16*>(wexp), n, cs.R * cs.S, p.Cs, p.Ks, p.Cg, p.Kg);
+  FFK_LAUNCH_CHECK("conv2d_grouped_expand");
+}
+
+void conv2d_grouped_fwd(const ConvShape& cs, int groups, const void* x, const void* wexp, const void* bias, void* y,
+                        float* stats, float* stats_ws, int act, hipStream_t st) {
+  check_shape(cs, "conv2d_grouped_fwd");
+  if (stats && !stats_ws) throw std::invalid_argument("conv2d_grouped_fwd: statistics need a workspace");
+  const GroupPlan p = group_plan(cs, groups);
+  ConvArgs g = grouped_args(cs, p);
+  g.x = static_cast<const bf16*>(x);
+  g.w = static_cast<const bf16*>(wexp);
+  g.bias = static_cast<const bf16*>(bias);
+  g.out = y;
+  g.stats = stats ? stats_ws : nullptr;
+  g.act = act;
+  g.M = g.N * g.P * g.Q;
+  g.NG = g.K;
+  g.KG = g.R * g.S * g.C;
+  const int bn = g.NG <= 64 ? 64 : 128;
+  const int gm = (g.M + BM - 1) / BM;
+  launch<MODE_FWD>(g, bn, gm * ((g.NG + bn - 1) / bn), st, p.Z);
+  FFK_LAUNCH_CHECK("conv2d_grouped_fwd");
+  if (stats) {
+    const int64_t W = 2 * static_cast<int64_t>(cs.K);
+    reduce_rows(stats_ws, stats, gm, W, 0, stats_ws + static_cast<int64_t>(gm) * W, st);
+    FFK_LAUNCH_CHECK("conv2d_grouped_fwd stats");
+  }
+}
+
+void conv2d_grouped_dgrad(const ConvShape& cs, int groups, const void* dy, const void* wexp, void* dx, float beta,
+                          hipStream_t st) {
+  check_shape(cs, "conv2d_grouped_dgrad");
+  const GroupPlan p = group_plan(cs, groups);
+  ConvArgs g = grouped_args(cs, p);
+  g.dy = static_cast<const bf16*>(dy);
+  g.w = static_cast<const bf16*>(wexp);
+  g.out = dx;
+  g.beta = beta;
+  g.NG = g.C;
+  const int bn = g.NG <= 64 ? 64 : 128;
+  const bool strided = (g.sh > 1 || g.sw > 1) && g.dh == 1 && g.dw == 1;
+  if (strided) {
+    g.par = 1;
+    for (int pch = 0; pch < g.sh; ++pch)
+      for (int pcw = 0; pcw < g.sw; ++pcw) {
+        g.pch = pch;
+        g.pcw = pcw;
+        g.Hc = (g.H - pch + g.sh - 1) / g.sh;
+        g.Wc = (g.W - pcw + g.sw - 1) / g.sw;
+        if (g.Hc <= 0 || g.Wc <= 0) continue;
+        g.rf = (pch + g.ph) % g.sh;
+        g.sf = (pcw + g.pw) % g.sw;
+        g.nr = g.rf < g.R ? (g.R - 1 - g.rf) / g.sh + 1 : 0;
+        g.ns = g.sf < g.S ? (g.S - 1 - g.sf) / g.sw + 1 : 0;
+        g.fWc = make_fdiv(g.Wc);
+        g.fHc = make_fdiv(g.Hc);
+        g.fns = make_fdiv(std::max(g.ns, 1));
+        g.M = g.N * g.Hc * g.Wc;
+        g.KG = g.nr * g.ns * g.K;
+        launch<MODE_DGRAD>(g, bn, ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn), st, p.Z);
+      }
+    FFK_LAUNCH_CHECK("conv2d_grouped_dgrad");
+    return;
+  }
+  g.M = g.N * g.H * g.W;
+  g.KG = g.R * g.S * g.K;
+  launch<MODE_DGRAD>(g, bn, ((g.M + BM - 1) / BM) * ((g.NG + bn - 1) / bn), st, p.Z);
+  FFK_LAUNCH_CHECK("conv2d_grouped_dgrad");
+}
+
+namespace {
+WgradPlan grouped_wgrad_plan(const ConvShape& cs, const GroupPlan& gp) {
+  ConvArgs g = grouped_args(cs, gp);
+  const int M = gp.Ks, NG = cs.R * cs.S * gp.Cs;
+  const int64_t KG = static_cast<int64_t>(g.N) * g.P * g.Q;
+  WgradPlan p;
+  p.bn = NG <= 64 ? 64 : 128;
+  p.tiles = ((M + BM - 1) / BM) * ((NG + p.bn - 1) / p.bn);
+  const int nk = static_cast<int>((KG + BK - 1) / BK);
+  const int64_t tz = static_cast<int64_t>(p.tiles) * gp.Z;
+  int splits = static_cast<int>((2048 + tz - 1) / tz);
+  splits = std::min(splits, std::max(1, nk / 8));
+  const int64_t slab = static_cast<int64_t>(gp.Z) * M * NG * 4;
+  splits = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(splits, (int64_t(256) << 20) / slab)));
+  splits = std::max(1, std::min(splits, nk));
+  p.kt_per_split = (nk + splits - 1) / splits;
+  p.splits = (nk + p.kt_per_split - 1) / p.kt_per_split;
+  return p;
+}
+}  // namespace
+
+int64_t conv2d_grouped_wgrad_ws_floats(const ConvShape& cs, int groups) {
+  const GroupPlan gp = group_plan(cs, groups);
+  const WgradPlan p = grouped_wgrad_plan(cs, gp);
+  const int64_t W = static_cast<int64_t>(cs.K) * cs.R * cs.S * gp.Cs;   // the expanded gradient (all super-groups)
+  // expanded gradient + split slabs + the two-pass reduce scratch
+  return W + (p.splits > 1 ? static_cast<int64_t>(p.splits) * W + (p.splits >= 64 ? kMaxChunks * W : 0) : 0);
+}
+
+void conv2d_grouped_wgrad(const ConvShape& cs, int groups, const void* x, const void* dy, float* dw, float* ws,
+                          hipStream_t st) {
+  check_shape(cs, "conv2d_grouped_wgrad");
+  if (!ws) throw std::invalid_argument("conv2d_grouped_wgrad: needs a workspace");
+  const GroupPlan gp = group_plan(cs, groups);
+  const WgradPlan p = grouped_wgrad_plan(cs, gp);
+  ConvArgs g = grouped_args(cs, gp);
+  const int64_t W = static_cast<int64_t>(cs.K) * cs.R * cs.S * gp.Cs;
+  float* dwexp = ws;
+  g.x = static_cast<const bf16*>(x);
+  g.dy = static_cast<const bf16*>(dy);
+  g.out = dwexp;
+  // every launch writes (never accumulates): one split writes the expanded
+  // gradient itself, several write slabs reduced into it
+  g.wpart = p.splits > 1 ? ws + W : dwexp;
+  g.M = g.K;
+  g.NG = g.R * g.S * g.C;
+  g.KG = g.N * g.P * g.Q;
+  g.kt_per_split = p.kt_per_split;
+  launch<MODE_WGRAD>(g, p.bn, p.tiles * p.splits, st, gp.Z);
+  FFK_LAUNCH_CHECK("conv2d_grouped_wgrad");
+  if (p.splits > 1) {
+    reduce_rows(ws + W, dwexp, p.splits, W, 0, p.splits >= 64 ? ws + W + static_cast<int64_t>(p.splits) * W : nullptr,
+                st);
+    FFK_LAUNCH_CHECK("conv2d_grouped_wgrad reduce");
+  }
+  const int64_t n = static_cast<int64_t>(cs.K) * cs.R * cs.S * gp.Cg;
+  hipLaunchKernelGGL(group_compress_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const float*>(dwexp), dw, n, cs.R * cs.S, gp.Cs, gp.Ks, gp.Cg, gp.Kg);
+  FFK_LAUNCH_CHECK("conv2d_grouped_wgrad compress");
+}
 
 // ---------------------------------------------------------------------------
 // Channel padding of a convolution input (the RGB stem: 3 channels -> 8, so

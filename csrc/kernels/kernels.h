@@ -260,6 +260,20 @@ void pad_channels_nhwc(const void* x, void* y, int64_t N, int C, int H, int W, i
 int64_t conv2d_wgrad_ws_floats(const ConvShape& s, int splits);
 void conv2d_wgrad(const ConvShape& s, const void* x, const void* dy, float* dw, float* ws, int splits,
                   hipStream_t st);
+// Grouped bf16 convolutions on the same MFMA kernels: super-groups of whole
+// groups as block-diagonal dense convs (blockIdx.z), the weight expanded
+// once per step (conv2d_grouped_expand: [K][R][S][C/groups] ->
+// [K][R][S][Cs], conv2d_grouped_wexp_elems elements); wgrad += into the
+// compact fp32 [K][R][S][C/groups] (ws: conv2d_grouped_wgrad_ws_floats)
+int64_t conv2d_grouped_wexp_elems(const ConvShape& s, int groups);
+void conv2d_grouped_expand(const ConvShape& s, int groups, const void* w, void* wexp, hipStream_t st);
+void conv2d_grouped_fwd(const ConvShape& s, int groups, const void* x, const void* wexp, const void* bias, void* y,
+                        float* stats, float* stats_ws, int act, hipStream_t st);
+void conv2d_grouped_dgrad(const ConvShape& s, int groups, const void* dy, const void* wexp, void* dx, float beta,
+                          hipStream_t st);
+int64_t conv2d_grouped_wgrad_ws_floats(const ConvShape& s, int groups);
+void conv2d_grouped_wgrad(const ConvShape& s, int groups, const void* x, const void* dy, float* dw, float* ws,
+                          hipStream_t st);
 
 // ---- igemm32.hip: exact-fp32 MFMA (v_mfma_f32_32x32x2_f32) GEMM and
 // convolutions; fp32 or bf16 inputs (in_f32), fp32 accumulation.

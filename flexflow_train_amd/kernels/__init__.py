@@ -1058,6 +1058,93 @@ def conv2d_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), splits:
     STATS["conv2d_wgrad"] += 1
 
 
+def _grouped_geom(x_shape, K, R, S, stride, pad, dil, groups):
+    N, C, H, W = x_shape
+    if groups <= 0 or C % groups or K % groups:
+        raise ValueError(f"conv2d_grouped: C={C} and K={K} must be multiples of groups={groups}")
+    return [int(N), int(H), int(W), int(C), int(K), int(R), int(S), int(stride[0]), int(stride[1]),
+            int(pad[0]), int(pad[1]), int(dil[0]), int(dil[1])]
+
+
+def conv2d_grouped_expand(w, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1):
+    """Compact bf16 weight [K,R,S,C/groups] -> the block-diagonal super-group
+    weight the grouped kernels read (conv.hip group_plan)."""
+    K_, R, S, Cg = w.shape
+    _check(w, "w", torch.bfloat16)
+    if Cg * groups != x_shape[1]:
+        raise ValueError(f"conv2d_grouped: weight has {Cg} x {groups} input channels, input has {x_shape[1]}")
+    g = _grouped_geom(x_shape, K_, R, S, stride, pad, dil, groups)
+    wexp = torch.empty(ext().conv2d_grouped_wexp_elems(g, int(groups)), device=w.device, dtype=torch.bfloat16)
+    ext().conv2d_grouped_expand(g, int(groups), _p(w), _p(wexp), _stream())
+    return wexp
+
+
+def conv2d_grouped_fwd(x, w, bias=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1, act: str = "none",
+                       stats=None, wexp=None):
+    """Grouped bf16 convolution on the MFMA implicit-GEMM kernels: x [N,C,H,W]
+    channels_last, w [K,R,S,C/groups] -> (y channels_last, the expanded
+    weight, reused by the dgrad)."""
+    _check_nhwc(x, "x")
+    K_, R, S, Cg = w.shape
+    g = _grouped_geom(x.shape, K_, R, S, stride, pad, dil, groups)
+    if wexp is None:
+        wexp = conv2d_grouped_expand(w, x.shape, stride, pad, dil, groups)
+    P, Q = conv_out_hw(x.shape[2], x.shape[3], R, S, *stride, *pad, *dil)
+    if bias is not None:
+        _check(bias, "bias", torch.bfloat16, K_)
+    if stats is not None:
+        _check(stats, "stats", torch.float32, 2 * K_)
+    y = torch.empty((x.shape[0], K_, P, Q), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    ws = None
+    if stats is not None:
+        ws = torch.empty(ext().conv2d_stats_ws_floats(g), device=x.device, dtype=torch.float32)
+    ext().conv2d_grouped_fwd(g, int(groups), _p(x), _p(wexp), _p(bias), _p(y), _p(stats), _p(ws), ACT_CODES[act],
+                             _stream())
+    STATS["conv2d_grouped_fwd"] += 1
+    return y, wexp
+
+
+def conv2d_grouped_dgrad(dy, wexp, w_shape, x_shape, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1,
+                         out=None, beta: float = 0.0):
+    """dx of a grouped convolution from the expanded weight."""
+    _check_nhwc(dy, "dy")
+    K_, R, S, Cg = w_shape
+    g = _grouped_geom(x_shape, K_, R, S, stride, pad, dil, groups)
+    P, Q = conv_out_hw(x_shape[2], x_shape[3], R, S, *stride, *pad, *dil)
+    if tuple(dy.shape) != (x_shape[0], K_, P, Q) or Cg * groups != x_shape[1]:
+        raise ValueError(f"conv2d_grouped_dgrad: dy {tuple(dy.shape)} / weight {tuple(w_shape)} do not match "
+                         f"{tuple(x_shape)}")
+    if wexp.numel() != ext().conv2d_grouped_wexp_elems(g, int(groups)) or wexp.dtype != torch.bfloat16:
+        raise ValueError("conv2d_grouped_dgrad: wexp is not this convolution's expanded weight")
+    if out is None:
+        out = torch.empty(tuple(x_shape), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        beta = 0.0
+    else:
+        _check_nhwc(out, "dx")
+        if tuple(out.shape) != tuple(x_shape):
+            raise ValueError("conv2d_grouped_dgrad: out has the wrong shape")
+    ext().conv2d_grouped_dgrad(g, int(groups), _p(dy), _p(wexp), _p(out), float(beta), _stream())
+    STATS["conv2d_grouped_dgrad"] += 1
+    return out
+
+
+def conv2d_grouped_wgrad(x, dy, dw, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups: int = 1):
+    """dw (fp32, [K][R][S][C/groups] contiguous) += grouped wgrad."""
+    _check_nhwc(x, "x")
+    _check_nhwc(dy, "dy")
+    K_ = dy.shape[1]
+    g = _grouped_geom(x.shape, K_, R, S, stride, pad, dil, groups)
+    P, Q = conv_out_hw(x.shape[2], x.shape[3], R, S, *stride, *pad, *dil)
+    if tuple(dy.shape) != (x.shape[0], K_, P, Q):
+        raise ValueError("conv2d_grouped_wgrad: dy shape mismatch")
+    if (not dw.is_cuda or dw.dtype != torch.float32 or not dw.is_contiguous()
+            or dw.numel() != K_ * R * S * (x.shape[1] // groups)):
+        raise ValueError("conv2d_grouped_wgrad: dw must be a contiguous fp32 [K,R,S,C/groups] buffer")
+    ws = torch.empty(ext().conv2d_grouped_wgrad_ws_floats(g, int(groups)), device=x.device, dtype=torch.float32)
+    ext().conv2d_grouped_wgrad(g, int(groups), _p(x), _p(dy), _p(dw), _p(ws), _stream())
+    STATS["conv2d_grouped_wgrad"] += 1
+
+
 def _rm2d(t: torch.Tensor) -> torch.Tensor:
     """A 2-D operand the kernels can address as rows of unit-stride elements
     (size-1 dims may carry any stride)."""

@@ -15,8 +15,10 @@ activation and, when the executor pairs the conv with a following
 BatchNorm (``emit_bn_stats``), the per-channel statistics that BN needs.
 Backward = dgrad implicit GEMM + split-K wgrad accumulating in fp32 straight
 into the flat gradient buffer.  Inputs with fewer than 8 channels (the RGB
-stem) are zero-padded to 8.  Grouped convolutions and CPU tensors run
-through PyTorch (the weight is viewed back to OIHW).
+stem) are zero-padded to 8.  bf16 grouped convolutions (ResNeXt) run on the
+same MFMA kernels as block-diagonal super-group convs (conv.hip
+group_plan); fp32 models on igemm32.hip; CPU tensors through PyTorch (the
+weight is viewed back to OIHW).
 """
 from __future__ import annotations
 
@@ -126,6 +128,20 @@ class Conv2DOp(OpImpl):
                 and K.use_hip(x))
 
     @staticmethod
+    def _native_grouped(x, W, groups, act):
+        """bf16 grouped convolutions (ResNeXt) on the MFMA implicit-GEMM
+        kernels: super-groups of whole groups whose channel counts are
+        multiples of 8 (conv.hip group_plan)."""
+        if not (groups > 1 and x.is_cuda and x.dtype == torch.bfloat16 and act in ("none", "relu", "sigmoid", "tanh")
+                and K.use_hip(x)):
+            return False
+        C, Kc = x.shape[1], W.shape[0]
+        if C % groups or Kc % groups:
+            return False
+        cg, kg = C // groups, Kc // groups
+        return any(groups % g == 0 and (g * cg) % 8 == 0 and (g * kg) % 8 == 0 for g in range(1, groups + 1))
+
+    @staticmethod
     def _native32(x, act):
         """fp32 models and grouped convolutions (ResNeXt): the exact-fp32 MFMA
         implicit GEMM (igemm32.hip), any channel count per group."""
@@ -179,6 +195,18 @@ class Conv2DOp(OpImpl):
                     and tuple(stride) == (1, 1) and C % 8 == 0):
                 bnsrc = getattr(x, "_ff_bn_bwd", None)   # set by the producing BatchNorm
             return [y], ("hip", xin, wp, y if act != "none" else None, tuple(x.shape), bnsrc)
+        if self._native_grouped(x, W, groups, act):
+            wp = W.reshape(Kc, R, S, C)   # physical [K][R][S][C/groups]
+            wp = (wp if wp.dtype == torch.bfloat16 else wp.to(torch.bfloat16)).contiguous()
+            xin = K.nhwc(x)
+            stats = None
+            if ctx.extra.get("emit_bn_stats"):
+                stats = torch.empty(2 * Kc, device=x.device, dtype=torch.float32)
+            bias = None if b is None else b.to(torch.bfloat16).contiguous()
+            y, wexp = K.conv2d_grouped_fwd(xin, wp, bias, stride, pad, groups=groups, act=act, stats=stats)
+            if stats is not None:
+                y._ff_bn_stats = stats
+            return [y], ("hipg", xin, wexp, y if act != "none" else None, tuple(x.shape), groups, tuple(wp.shape))
         if self._native32(x, act):
             wp = W.reshape(Kc, R, S, C)   # physical [K][R][S][C/groups]
             if wp.dtype != x.dtype:
@@ -222,6 +250,8 @@ class Conv2DOp(OpImpl):
 
         if saved[0] == "hip32":
             return self._backward32(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act)
+        if saved[0] == "hipg":
+            return self._backward_grouped(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act)
         _, xin, wp, y, xshape, bnsrc = saved
         Kc, R, S, Cp = wp.shape
         dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))
@@ -303,6 +333,36 @@ class Conv2DOp(OpImpl):
             return [acc]
         return [K.conv2d_dgrad(dy, wp, xshape, stride, pad)]
 
+
+    @staticmethod
+    def _backward_grouped(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act):
+        _, xin, wexp, y, xshape, groups, wshape = saved
+        Kc, R, S, Cg = wshape
+        dy = K.nhwc(grad_outputs[0].to(torch.bfloat16))
+        if act == "relu":
+            dy = torch.where(y > 0, dy, torch.zeros((), device=dy.device, dtype=dy.dtype))
+        elif act in ("sigmoid", "tanh"):
+            yf = y.float()
+            d = yf * (1 - yf) if act == "sigmoid" else 1 - yf * yf
+            dy = (dy.float() * d).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if len(weight_grads) > 1 and weight_grads[1] is not None:
+            K.colsum_act(dy.permute(0, 2, 3, 1).reshape(-1, Kc), None, "none", weight_grads[1], write_dx=False)
+        dW = weight_grads[0]
+        if dW is not None:
+            if dW.dtype == torch.float32 and dW.is_contiguous():
+                K.conv2d_grouped_wgrad(xin, dy, dW.view(-1), R, S, stride, pad, groups=groups)
+            else:
+                tmp = torch.zeros(dW.numel(), device=dy.device, dtype=torch.float32)
+                K.conv2d_grouped_wgrad(xin, dy, tmp, R, S, stride, pad, groups=groups)
+                acc_grad(dW, tmp.view(dW.shape))
+        if not need_input_grad[0]:
+            return [None]
+        acc = ctx.extra.get("grad_acc", [None])[0]
+        if (acc is not None and ctx.extra.get("halo") is None and acc.is_cuda and acc.dtype == torch.bfloat16
+                and tuple(acc.shape) == tuple(xshape) and acc.is_contiguous(memory_format=torch.channels_last)):
+            K.conv2d_grouped_dgrad(dy, wexp, wshape, xshape, stride, pad, groups=groups, out=acc, beta=1.0)
+            return [acc]
+        return [K.conv2d_grouped_dgrad(dy, wexp, wshape, xshape, stride, pad, groups=groups)]
 
     @staticmethod
     def _backward32(ctx, saved, grad_outputs, weight_grads, need_input_grad, stride, pad, act):

@@ -47,7 +47,7 @@ def test_bench_multi_rank_emits_comm_calibration_and_ae():
     simulator's predicted step beside the measured one, and (--ae) the
     OSDI'22 AE BERT protocol's searched-vs-DP ratio."""
     args = ["--model", "bert-base", "--layers", "2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2",
-            "--seq", "64", "--no-dp-compare", "--ae"]
+            "--seq", "64", "--no-dp-compare"]
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args, env=_env(),
                        capture_output=True, text=True, timeout=900, cwd="/tmp")
     assert p.returncode == 0, p.stderr[-3000:]
@@ -61,3 +61,30 @@ def test_bench_multi_rank_emits_comm_calibration_and_ae():
     assert "error" not in ae, ae
     assert ae["global_batch"] == 8 and ae["layers"] == 12
     assert ae["searched_samples_per_sec"] > 0 and ae["dp_samples_per_sec"] > 0 and ae["speedup_over_dp"] > 0
+
+
+def test_bench_eight_ranks_reports_measured_speedups():
+    """The driver's 8-GPU line, rehearsed on 8 gloo ranks: the AE protocol runs
+    by default at N > 1 (no --ae), and the line carries the measured
+    searched-vs-DP ratios (headline and AE config), the collectives'
+    calibration and what the search did."""
+    args = ["--model", "bert-base", "--layers", "2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2",
+            "--seq", "64"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"] + args,
+                       env=_env(OMP_NUM_THREADS="1"), capture_output=True, text=True, timeout=1500, cwd="/tmp")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    r = lines[0]
+    assert r["n_gpus"] == 8 and r["world_size"] == 8
+    c = r["config"]
+    assert "error" not in c["comm_calibration"], c["comm_calibration"]
+    s = c["search"]
+    assert s["evaluated"] > 0 and s["s"] > 0 and "time_limited" in s and "mapping_won" in s
+    # the headline ratio is measured whenever the search left data parallelism
+    if not c["parallelism"].startswith("dp"):
+        assert c["dp_samples_per_sec"] > 0 and c["dp_reference"].startswith("measured")
+    ae = c["ae_bert"]
+    assert "error" not in ae and "skipped" not in ae, ae
+    assert ae["searched_samples_per_sec"] > 0 and ae["dp_samples_per_sec"] > 0
+    assert c["ae_speedup_over_dp"] == ae["speedup_over_dp"] > 0

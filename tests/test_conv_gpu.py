@@ -28,6 +28,12 @@ def _rand_nhwc(shape, scale=1.0):
     return (torch.randn(shape, device=DEV) * scale).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
 
+def _relerr(a, ref):
+    """Relative Frobenius error against an fp64 reference (on the CPU)."""
+    a, ref = a.double().cpu(), ref.double().cpu()
+    return ((a - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_and_stats(case):
     torch.manual_seed(0)
@@ -37,12 +43,15 @@ def test_conv_fwd_and_stats(case):
     b = (torch.randn(Ko, device=DEV) * 0.1).to(torch.bfloat16)
     stats = torch.zeros(2 * Ko, device=DEV)
     y = K.conv2d_fwd(x, w, b, (st, st), (pd, pd), act="relu", stats=stats)
-    ref = torch.relu(F.conv2d(x.float(), w.float().permute(0, 3, 1, 2), b.float(), stride=st, padding=pd))
+    # fp64 reference on the same bf16 inputs: the bound is the bf16 output
+    # rounding (relative RMS ~1.1e-3), so a 1 % error in one tile phase fails
+    ref = torch.relu(F.conv2d(x.double().cpu(), w.double().cpu().permute(0, 3, 1, 2), b.double().cpu(), stride=st,
+                              padding=pd))
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
-    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
-    yf = y.float()
-    torch.testing.assert_close(stats[:Ko], yf.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
-    torch.testing.assert_close(stats[Ko:], (yf * yf).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    assert _relerr(y, ref) < 5e-3
+    yd = y.double().cpu()
+    assert _relerr(stats[:Ko], yd.sum((0, 2, 3))) < 1e-5
+    assert _relerr(stats[Ko:], (yd * yd).sum((0, 2, 3))) < 1e-5
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -51,22 +60,22 @@ def test_conv_dgrad_wgrad(case):
     N, C, H, W, Ko, R, S, st, pd = case
     x = _rand_nhwc((N, C, H, W))
     w = (torch.randn(Ko, R, S, C, device=DEV) * (1.0 / (R * S * C) ** 0.5)).to(torch.bfloat16).contiguous()
-    xr = x.float().requires_grad_(True)
-    wr = w.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    xr = x.double().cpu().requires_grad_(True)
+    wr = w.double().cpu().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
     yr = F.conv2d(xr, wr, stride=st, padding=pd)
     dy = _rand_nhwc(yr.shape)
-    yr.backward(dy.float())
+    yr.backward(dy.double().cpu())
     dx = K.conv2d_dgrad(dy, w, tuple(x.shape), (st, st), (pd, pd))
-    torch.testing.assert_close(dx.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    assert _relerr(dx, xr.grad) < 5e-3
     # accumulate form
     acc = dx.clone(memory_format=torch.channels_last)
     K.conv2d_dgrad(dy, w, tuple(x.shape), (st, st), (pd, pd), out=acc, beta=1.0)
-    torch.testing.assert_close(acc.float(), 2 * xr.grad, rtol=3e-2, atol=6e-2)
+    assert _relerr(acc, 2 * xr.grad) < 5e-3
     dw_ref = wr.grad.permute(0, 2, 3, 1).contiguous()  # -> [K, R, S, C]
     for splits in (0, 1, 3):
         dw = torch.full((Ko * R * S * C,), 0.5, device=DEV)
         K.conv2d_wgrad(x, dy, dw, R, S, (st, st), (pd, pd), splits=splits)
-        torch.testing.assert_close(dw.view_as(dw_ref) - 0.5, dw_ref, rtol=1e-2, atol=5e-2)
+        assert _relerr(dw.view_as(dw_ref).double().cpu() - 0.5, dw_ref) < 1e-5
 
 
 @pytest.mark.parametrize("C,relu,residual", [(64, True, False), (24, False, False), (256, True, True), (8, True, False)])
