@@ -76,6 +76,7 @@ struct SearchResult {
   int evaluated = 0;
   int accepted = 0;
   double elapsed = 0;
+  bool time_limited = false;             // ended on SearchConfig::time_limit, not the budget
   Json trace;                            // [[iteration, best cost], ...]
   int rules = 0;                         // Unity: rules tried (built-in + rule set)
   int rule_set_rules = 0;                // Unity: of which from the rule set

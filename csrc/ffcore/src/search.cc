@@ -6,7 +6,11 @@
 #include <cstdlib>
 #include <cmath>
 #include <limits>
+#include <atomic>
+#include <functional>
 #include <mutex>
+#include <optional>
+#include <thread>
 #include <queue>
 #include <random>
 #include <unordered_set>
@@ -30,6 +34,7 @@ Json SearchResult::to_json(const ComputationGraph* cg) const {
   j["evaluated"] = evaluated;
   j["accepted"] = accepted;
   j["elapsed"] = elapsed;
+  j["time_limited"] = time_limited;
   j["trace"] = trace;
   if (rules) {
     j["rules"] = static_cast<int64_t>(rules);
@@ -107,7 +112,10 @@ SearchResult mcmc_search(const ComputationGraph& cg, const CostModel& cm, const 
   R.trace.push_back(Json(std::vector<double>{0.0, best_cost}));
   int it = 0;
   for (; it < cfg.budget && !layers.empty(); ++it) {
-    if (now_s() - t0 > cfg.time_limit) break;
+    if (now_s() - t0 > cfg.time_limit) {
+      R.time_limited = true;
+      break;
+    }
     int id = layers[rng() % layers.size()];
     auto const& cs = cands[id];
     LayerConfig c = cs[rng() % cs.size()];
@@ -173,13 +181,22 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   MMCache mm_cache;
   double best_so_far = kInf;
   int mapped_states = 0;
-  auto cost_of = [&](const ParallelComputationGraph& g, std::map<int, Placement>* views) -> double {
+  // whole-world price (thread-safe: the cost model memoises under a mutex)
+  auto whole_cost = [&](const ParallelComputationGraph& g) -> double {
     try {
-      const double whole = S.simulate(g).iteration_time;
-      if (views) views->clear();
-      // the DP mapping (~0.1-0.5 s on a BERT-large PCG) runs for every state
-      // whose whole-world cost is within mapping_alpha of the best so far:
-      // the states the queue can still pop ahead of the best
+      return S.simulate(g).iteration_time;
+    } catch (const FFError&) {
+      return kInf;
+    }
+  };
+  // the DP mapping (~0.1-0.5 s on a BERT-large PCG) for every state whose
+  // whole-world cost is within mapping_alpha of the best so far: the states
+  // the queue can still pop ahead of the best.  Runs in candidate order on
+  // one thread (the cache is shared), so the search stays deterministic.
+  auto mapped_cost = [&](const ParallelComputationGraph& g, double whole, std::map<int, Placement>* views) -> double {
+    if (views) views->clear();
+    if (!std::isfinite(whole)) return whole;
+    try {
       if (cfg.use_machine_mapping && cfg.world > 1 && whole <= best_so_far * cfg.mapping_alpha &&
           (cfg.max_mapped_states < 0 || mapped_states < cfg.max_mapped_states)) {
         auto m = get_optimal_machine_mapping(g, cm, cfg.world, MachineMappingOptions{}, &mm_cache);
@@ -196,11 +213,10 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
           }
         }
       }
-      best_so_far = std::min(best_so_far, whole);
-      return whole;
     } catch (const FFError&) {
-      return kInf;
     }
+    best_so_far = std::min(best_so_far, whole);
+    return whole;
   };
   auto rules = generate_parallelization_substitutions(initial, cfg.world);
   rules.insert(rules.end(), extra_rules.begin(), extra_rules.end());
@@ -210,6 +226,30 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
     R.rule_set_rules = static_cast<int>(rs.size());
   }
   R.rules = static_cast<int>(rules.size());
+  // candidate rewrites of a popped state are applied, checked, hashed and
+  // priced on a pool of threads (FF_SEARCH_THREADS, default up to 16): one
+  // pop of a 24-layer BERT-large PCG expands ~10^3 rewrites, each a graph
+  // copy + hash + simulation.  A network model with its own route cache
+  // (not thread-safe) keeps the search on one thread.
+  int nthreads = static_cast<int>(std::thread::hardware_concurrency());
+  if (const char* e = getenv("FF_SEARCH_THREADS")) nthreads = std::atoi(e);
+  nthreads = std::max(1, std::min(nthreads, 16));
+  if (sim.network) nthreads = 1;
+  auto parallel_for = [&](size_t n, const std::function<void(size_t)>& fn) {
+    if (nthreads <= 1 || n < 2) {
+      for (size_t i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    const int T = static_cast<int>(std::min<size_t>(nthreads, n));
+    for (int t = 0; t < T; ++t)
+      pool.emplace_back([&] {
+        for (size_t i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i);
+      });
+    for (auto& th : pool) th.join();
+  };
+
   std::vector<ParallelComputationGraph> states;
   std::vector<std::pair<int, int>> parent;   // state -> (parent state, rule index)
   parent.push_back({-1, -1});
@@ -218,7 +258,7 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   std::unordered_set<size_t> seen;
   states.push_back(initial);
   state_views.emplace_back();
-  double c0 = cost_of(initial, &state_views[0]);
+  double c0 = mapped_cost(initial, whole_cost(initial), &state_views[0]);
   R.data_parallel_cost = c0;
   pq.push({c0, 0});
   seen.insert(initial.structural_hash());
@@ -228,8 +268,20 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
   R.trace.push_back(Json(std::vector<double>{0.0, best_cost}));
   int it = 0;
   double prof[5] = {0, 0, 0, 0, 0};
+  bool timed_out = false;
+  struct Cand {
+    int rule;
+    const PCGPatternMatch* match;
+    std::optional<ParallelComputationGraph> g;
+    size_t hash = 0;
+    bool ok = false;
+    double whole = kInf;
+  };
   for (; it < cfg.budget && !pq.empty(); ++it) {
-    if (now_s() - t0 > cfg.time_limit) break;
+    if (now_s() - t0 > cfg.time_limit) {
+      timed_out = true;
+      break;
+    }
     State s = pq.top();
     pq.pop();
     if (s.cost < best_cost) {
@@ -241,48 +293,68 @@ SearchResult unity_search(const ParallelComputationGraph& initial, const CostMod
     }
     const ParallelComputationGraph cur = states[s.id];
     const PatternMatchIndex ix(cur);
-    for (size_t ri = 0; ri < rules.size(); ++ri) {
-      auto const& rule = rules[ri];
-      if (now_s() - t0 > cfg.time_limit) break;
-      double tm = now_s();
-      auto matches = find_pattern_matches(rule.pattern, cur, ix, 4096);
-      prof[4] += now_s() - tm;
-      for (auto const& m : matches) {
-        if (now_s() - t0 > cfg.time_limit) break;
-        double ta = now_s();
-        auto next = apply_substitution(cur, rule, m);
-        prof[0] += now_s() - ta;
-        if (!next) continue;
-        ta = now_s();
-        if (next->num_operator_nodes() > cfg.max_num_ops) continue;
-        if (!fits_world(*next, cfg.world)) continue;
-        prof[1] += now_s() - ta;
-        ta = now_s();
-        size_t h = next->structural_hash();
-        prof[2] += now_s() - ta;
-        if (!seen.insert(h).second) continue;
-        std::map<int, Placement> v;
-        ta = now_s();
-        double c = cost_of(*next, &v);
-        prof[3] += now_s() - ta;
-        ++R.evaluated;
-        if (!std::isfinite(c) || c > cfg.threshold) continue;
-        states.push_back(std::move(*next));
-        parent.push_back({s.id, static_cast<int>(ri)});
-        state_views.push_back(std::move(v));
-        pq.push({c, static_cast<int>(states.size()) - 1});
-        if (c < best_cost) {
-          best_cost = c;
-          best = static_cast<int>(states.size()) - 1;
-          R.trace.push_back(Json(std::vector<double>{static_cast<double>(it), best_cost}));
-        }
+    // every (rule, match) of this state, in rule order
+    double tm = now_s();
+    std::vector<std::vector<PCGPatternMatch>> matches(rules.size());
+    for (size_t ri = 0; ri < rules.size(); ++ri) matches[ri] = find_pattern_matches(rules[ri].pattern, cur, ix, 4096);
+    std::vector<Cand> cands;
+    for (size_t ri = 0; ri < rules.size(); ++ri)
+      for (auto const& m : matches[ri]) cands.push_back(Cand{static_cast<int>(ri), &m, std::nullopt});
+    prof[4] += now_s() - tm;
+    // apply + checks + hash, in parallel
+    double ta = now_s();
+    parallel_for(cands.size(), [&](size_t i) {
+      if (now_s() - t0 > cfg.time_limit) return;
+      Cand& c = cands[i];
+      auto next = apply_substitution(cur, rules[c.rule], *c.match);
+      if (!next || next->num_operator_nodes() > cfg.max_num_ops || !fits_world(*next, cfg.world)) return;
+      c.hash = next->structural_hash();
+      c.g = std::move(next);
+      c.ok = true;
+    });
+    prof[0] += now_s() - ta;
+    // dedupe in candidate order (deterministic), then price the new ones in parallel
+    std::vector<size_t> fresh;
+    for (size_t i = 0; i < cands.size(); ++i)
+      if (cands[i].ok && seen.insert(cands[i].hash).second) fresh.push_back(i);
+    ta = now_s();
+    parallel_for(fresh.size(), [&](size_t k) {
+      if (now_s() - t0 > cfg.time_limit) return;
+      Cand& c = cands[fresh[k]];
+      c.whole = whole_cost(*c.g);
+    });
+    prof[3] += now_s() - ta;
+    ta = now_s();
+    for (size_t i : fresh) {
+      Cand& c = cands[i];
+      if (!std::isfinite(c.whole)) continue;   // failed, or not priced before the time limit
+      std::map<int, Placement> v;
+      const double cst = mapped_cost(*c.g, c.whole, &v);
+      ++R.evaluated;
+      if (!std::isfinite(cst) || cst > cfg.threshold) continue;
+      states.push_back(std::move(*c.g));
+      parent.push_back({s.id, c.rule});
+      state_views.push_back(std::move(v));
+      pq.push({cst, static_cast<int>(states.size()) - 1});
+      if (cst < best_cost) {
+        best_cost = cst;
+        best = static_cast<int>(states.size()) - 1;
+        R.trace.push_back(Json(std::vector<double>{static_cast<double>(it), best_cost}));
       }
+    }
+    prof[2] += now_s() - ta;
+    if (now_s() - t0 > cfg.time_limit) {
+      timed_out = true;
+      ++it;
+      break;
     }
   }
   if (getenv("FF_SEARCH_PROFILE"))
-    fprintf(stderr, "unity: apply %.2fs checks %.2fs hash %.2fs cost %.2fs match %.2fs total %.2fs\n", prof[0], prof[1],
-            prof[2], prof[3], prof[4], now_s() - t0);
+    fprintf(stderr, "unity: %d threads, apply+hash %.2fs price %.2fs map+insert %.2fs match %.2fs total %.2fs, "
+            "%d pops, %d evaluated, %zu states%s\n", nthreads, prof[0], prof[3], prof[2], prof[4], now_s() - t0, it,
+            R.evaluated, states.size(), timed_out ? " (time limit)" : "");
   R.iterations = it;
+  R.time_limited = timed_out;
   R.mapping_cache_entries = static_cast<int64_t>(mm_cache.results.size());
   R.mapping_cache_hits = static_cast<int64_t>(mm_cache.hits);
   R.mapped_states = mapped_states;
@@ -320,13 +392,18 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
     best.mapping_cache_entries = u.mapping_cache_entries;
     best.mapping_cache_hits = u.mapping_cache_hits;
     best.mapped_states = u.mapped_states;
+    const int evaluated = m.evaluated + u.evaluated;
+    const bool limited = m.time_limited || u.time_limited;
     if (u.cost < best.cost * 0.999) {
       u.data_parallel_cost = m.data_parallel_cost;
       u.strategy.clear();
       u.algorithm = "mcmc+unity";
-      u.evaluated += m.evaluated;
       best = u;
     }
+    best.evaluated = evaluated;   // every strategy / state priced by either phase
+    best.time_limited = limited;
+  } else if (uc.budget > 0) {
+    best.time_limited = true;     // the MCMC phase left Unity no time
   }
   // final machine mapping (the reference's Unity cost is the mapping DP's;
   // here per-state costs use whole-world placements and the DP, ~0.1 s on a
