@@ -30,6 +30,20 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
+def _rel64(a, b):
+    """Relative Frobenius error in fp64 (references computed in fp64)."""
+    a = a.double()
+    b = b.double()
+    return ((a - b).norm() / (b.norm() + 1e-300)).item()
+
+
+# non-GEMM bf16 kernels against fp64 references on the same bf16 inputs: the
+# bound is the output rounding plus the bf16 rounding of the kernels' own
+# intermediates (attention's P / dS operands), measured at 1.6-2.5e-3
+# (profiles/r6/g01_tol_probe.jsonl); a 1 % error in one tile phase fails
+_BF_OP = 5e-3
+
+
 @pytest.mark.parametrize("N", [1024, 768, 4096, 200 * 8])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_layernorm_fwd_bwd(N, dtype):
@@ -42,20 +56,22 @@ def test_layernorm_fwd_bwd(N, dtype):
     n0 = K.STATS["layernorm_fwd"]
     y, s, mean, rstd = K.layernorm_fwd(x, g, b, 1e-5, residual=r)
     assert K.STATS["layernorm_fwd"] == n0 + 1
-    xs = (x.float() + r.float()).requires_grad_(True)
-    gf = g.float().requires_grad_(True)
-    bf = b.float().requires_grad_(True)
-    ref = torch.nn.functional.layer_norm(xs, (N,), gf, bf, 1e-5)
-    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
-    assert _rel(y, ref) < tol
+    bf16 = dtype == torch.bfloat16
+    ref = torch.nn.functional.layer_norm(x.double() + r.double(), (N,), g.double(), b.double(), 1e-5)
+    assert _rel64(y, ref) < (_BF_OP if bf16 else 1e-5)
+    # backward against fp64 LN of the sum the kernel stored (and reads back)
+    xs = s.double().requires_grad_(True)
+    gf = g.double().requires_grad_(True)
+    bf = b.double().requires_grad_(True)
+    ref2 = torch.nn.functional.layer_norm(xs, (N,), gf, bf, 1e-5)
     dy = torch.randn(M, N, device=DEV, dtype=dtype)
-    ref.backward(dy.float())
+    ref2.backward(dy.double())
     dg = torch.zeros(N, device=DEV)
     db = torch.zeros(N, device=DEV)
     dx = K.layernorm_bwd(dy, s, mean, rstd, g, dg, db)
-    assert _rel(dx, xs.grad) < (3e-2 if dtype == torch.bfloat16 else 1e-4)
-    assert _rel(dg, gf.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
-    assert _rel(db, bf.grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
+    assert _rel64(dx, xs.grad) < (_BF_OP if bf16 else 1e-4)
+    assert _rel64(dg, gf.grad) < (1e-3 if bf16 else 1e-4)
+    assert _rel64(db, bf.grad) < (1e-5 if bf16 else 1e-4)
 
 
 @pytest.mark.parametrize("act", ["gelu", "relu", "sigmoid", "tanh"])
@@ -199,7 +215,8 @@ def test_embedding_small_table_backward(n, rows, D):
 
 
 def _ref_attn(q, k, v, causal):
-    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))  # [B,H,S,D]
+    """Attention in the inputs' precision (pass fp64 tensors for the bounds)."""
+    qf, kf, vf = (t.transpose(1, 2) for t in (q, k, v))  # [B,H,S,D]
     s = qf @ kf.transpose(-1, -2) / math.sqrt(q.shape[-1])
     if causal:
         Sq, Sk = s.shape[-2:]
@@ -219,18 +236,18 @@ def test_attention_fwd_bwd(causal, D, S, dbias_atomic):
     qkv = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
     o, lse = K.attention_fwd(q, k, v, causal=causal)
-    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    qf, kf, vf = (t.double().requires_grad_(True) for t in (q, k, v))
     ref = _ref_attn(qf, kf, vf, causal)
-    assert _rel(o, ref) < 2e-2, _rel(o, ref)
+    assert _rel64(o, ref) < _BF_OP, _rel64(o, ref)
     do = torch.randn_like(o)
-    ref.backward(do.float())
+    ref.backward(do.double())
     dqkv = torch.empty_like(qkv)
     dbias = [torch.full((H * D,), 0.25, device=DEV) for _ in range(3)]
     K.attention_bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], causal=causal, dbias=dbias,
                     dbias_atomic=dbias_atomic)
-    assert _rel(dqkv[:, :, 2], vf.grad) < 3e-2, "dV"
-    assert _rel(dqkv[:, :, 1], kf.grad) < 3e-2, "dK"
-    assert _rel(dqkv[:, :, 0], qf.grad) < 3e-2, "dQ"
+    assert _rel64(dqkv[:, :, 2], vf.grad) < _BF_OP, "dV"
+    assert _rel64(dqkv[:, :, 1], kf.grad) < _BF_OP, "dK"
+    assert _rel64(dqkv[:, :, 0], qf.grad) < _BF_OP, "dQ"
     # fused projection-bias gradients = column sums over (batch, sequence) of dq / dk / dv
     for i, g in enumerate((qf.grad, kf.grad, vf.grad)):
         ref_sum = g.sum((0, 1)).reshape(-1)
@@ -256,8 +273,8 @@ def test_attention_fwd_pipelined(causal, S, monkeypatch):
     monkeypatch.setenv("FFK_ATTN_FWD_PIPE", "1")
     o1, lse1 = K.attention_fwd(q, k, v, causal=causal)
     torch.cuda.synchronize()
-    ref = _ref_attn(q.float(), k.float(), v.float(), causal)
-    assert _rel(o1, ref) < 2e-2, _rel(o1, ref)
+    ref = _ref_attn(q.double(), k.double(), v.double(), causal)
+    assert _rel64(o1, ref) < _BF_OP, _rel64(o1, ref)
     assert _rel(o1, o0) < 1e-2
     assert torch.allclose(lse1, lse0, rtol=1e-4, atol=1e-3)
 
@@ -282,9 +299,9 @@ def test_attention_bwd_fused_delta(causal, D, S, monkeypatch):
         outs.append(dqkv.float())
     for i, name in enumerate(("dQ", "dK", "dV")):
         assert _rel(outs[1][:, :, i], outs[0][:, :, i]) < 2e-3, name
-    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
-    _ref_attn(qf, kf, vf, causal).backward(do.float())
-    assert _rel(outs[1][:, :, 0], qf.grad) < 3e-2
+    qf, kf, vf = (t.double().requires_grad_(True) for t in (q, k, v))
+    _ref_attn(qf, kf, vf, causal).backward(do.double())
+    assert _rel64(outs[1][:, :, 0], qf.grad) < _BF_OP
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])

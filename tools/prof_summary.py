@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--steps", type=int, default=0,
                     help="keep the last N optimizer steps (segments ending at an adam / sgd update kernel)")
+    ap.add_argument("--marker", default="",
+                    help="regex of a kernel launched exactly once per step (e.g. the loss kernel) that marks the "
+                         "step boundaries instead of the last update kernel (steps with several update launches)")
     a = ap.parse_args()
     cur = sqlite3.connect(a.db).cursor()
     rows = cur.execute("select name, start, end from kernels order by start").fetchall()
@@ -31,7 +34,7 @@ def main():
     if a.steps:
         # a step ends with the same optimizer-update kernel every time: the
         # last update kernel of the trace marks the step boundaries
-        upd = [r[0] for r in rows if re.search(r"adam|sgd", r[0])]
+        upd = [r[0] for r in rows if re.search(a.marker or r"adam|sgd", r[0])]
         marks = [i for i, r in enumerate(rows) if upd and r[0] == upd[-1]]
         n = min(a.steps, len(marks) - 1)
         if n > 0:
