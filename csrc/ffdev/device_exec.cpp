@@ -7,13 +7,19 @@
 //  * every graph tensor and gradient lives in one device arena (256-B
 //    aligned pieces); weights are initialised by the CPU backing's
 //    initialisers (same values as a CPU run with the same seed) and uploaded;
-//  * operators: LINEAR on the exact-fp32 MFMA GEMM (igemm32.hip: bias and the
-//    activation in its epilogue, the pre-activation kept for backward), the
-//    last SOFTMAX fused with sparse cross-entropy, MSE (tensorops.hip),
-//    CONV2D / POOL2D / BATCHNORM (NCHW, direct formulations), element-wise
-//    activations / binaries / scalar ops / reshapes / softmax by the small
-//    kernels below; a graph with any other operator stays on the CPU backing
-//    (make_device_backing returns null);
+//  * operators on the production kernel library (csrc/kernels, fp32 paths):
+//    LINEAR, BATCHMATMUL and MULTIHEAD_ATTENTION on the exact-fp32 MFMA GEMM
+//    (igemm32.hip: bias and the activation in its epilogue, the
+//    pre-activation kept for backward; batched over heads x batch for the
+//    attention scores), LAYERNORM (layernorm.hip), EMBEDDING (embedding.hip),
+//    SOFTMAX (softmax.hip), CONCAT / SPLIT (tensorops.hip slice_copy), bias
+//    gradients (elementwise.hip colsum_act), the last SOFTMAX fused with
+//    sparse cross-entropy, MSE (tensorops.hip); small kernels below for the
+//    shapes those kernels do not take (rows not a multiple of 8), DROPOUT
+//    (the CPU backing's counter-hash mask, bit for bit), CONV2D / POOL2D /
+//    BATCHNORM (NCHW, direct formulations), element-wise activations /
+//    binaries / scalar ops / reshapes; a graph with any other operator stays
+//    on the CPU backing (make_device_backing returns null);
 //  * the host slots are mirrors: slot() copies a tensor out when the device
 //    copy is newer and marks it written, and the next device step copies
 //    written mirrors back -- the inline-mapping protocol of the reference's
@@ -24,6 +30,7 @@
 // read back when asked for.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -469,6 +476,197 @@ __global__ __launch_bounds__(256) void k_bn_bwd(const float* dy, const float* x,
   }
 }
 
+// ---- dropout: the CPU backing's counter-hash mask (local_exec.cc hash_uniform), bit for bit
+__device__ __forceinline__ float d_hash_uniform(uint64_t seed, uint64_t i) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + i + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return static_cast<float>(z >> 40) * (1.0f / 16777216.0f);
+}
+// bwd = 0: y = mask(x) / (1 - p); bwd = 1: y += mask(x) / (1 - p)
+__global__ __launch_bounds__(256) void k_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed,
+                                                 int bwd) {
+  GRID_LOOP(i, n) {
+    const float v = (p > 0.f && d_hash_uniform(seed, static_cast<uint64_t>(i)) < p) ? 0.f : x[i] / (1.f - p);
+    if (bwd) y[i] += v;
+    else y[i] = v;
+  }
+}
+// float-carried indices -> int32 (the embedding kernels' index type)
+__global__ __launch_bounds__(256) void k_f2i(const float* x, int* y, int64_t n) {
+  GRID_LOOP(i, n) y[i] = static_cast<int>(x[i]);
+}
+// embedding for rows of D % 8 != 0 (embedding.hip takes 16-B rows)
+__global__ __launch_bounds__(256) void k_embed_fwd(const int* idx, const float* W, float* y, int64_t B, int L,
+                                                   int64_t D, float s) {
+  GRID_LOOP(i, B * D) {
+    const int64_t b = i / D, d = i % D;
+    float acc = 0.f;
+    for (int l = 0; l < L; ++l) acc += W[static_cast<int64_t>(idx[b * L + l]) * D + d];
+    y[i] = s * acc;
+  }
+}
+__global__ __launch_bounds__(256) void k_embed_bwd(const int* idx, const float* g, float* dW, int64_t B, int L,
+                                                   int64_t D, float s) {
+  GRID_LOOP(i, B * L * D) {
+    const int64_t bl = i / D, d = i % D;
+    atomicAdd(dW + static_cast<int64_t>(idx[bl]) * D + d, s * g[(bl / L) * D + d]);
+  }
+}
+// layer norm over rows of N % 8 != 0 (layernorm.hip takes 16-B rows): one
+// block per row; aux = {mean[R], rstd[R]}
+__global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gamma, const float* beta, float* y,
+                                                float* mean, float* rstd, int64_t N, float eps) {
+  __shared__ float red[256];
+  const float* xr = x + blockIdx.x * N;
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < N; j += 256) s += xr[j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float mu = red[0] / static_cast<float>(N);
+  __syncthreads();
+  float v = 0.f;
+  for (int64_t j = threadIdx.x; j < N; j += 256) v += (xr[j] - mu) * (xr[j] - mu);
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float rs = 1.f / sqrtf(red[0] / static_cast<float>(N) + eps);
+  for (int64_t j = threadIdx.x; j < N; j += 256) {
+    float o = (xr[j] - mu) * rs;
+    if (gamma) o = o * gamma[j] + (beta ? beta[j] : 0.f);
+    y[blockIdx.x * N + j] = o;
+  }
+  if (threadIdx.x == 0) {
+    mean[blockIdx.x] = mu;
+    rstd[blockIdx.x] = rs;
+  }
+}
+__global__ __launch_bounds__(256) void k_ln_bwd(const float* dy, const float* x, const float* gamma,
+                                                const float* mean, const float* rstd, float* dx, float* dgamma,
+                                                float* dbeta, int64_t N) {
+  __shared__ float ra[256], rb[256];
+  const int64_t r = blockIdx.x;
+  const float mu = mean[r], rs = rstd[r];
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t j = threadIdx.x; j < N; j += 256) {
+    const float xh = (x[r * N + j] - mu) * rs, g = dy[r * N + j];
+    const float gg = g * (gamma ? gamma[j] : 1.f);
+    s1 += gg;
+    s2 += gg * xh;
+    if (dgamma) atomicAdd(dgamma + j, g * xh);
+    if (dbeta) atomicAdd(dbeta + j, g);
+  }
+  ra[threadIdx.x] = s1;
+  rb[threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) {
+      ra[threadIdx.x] += ra[threadIdx.x + o];
+      rb[threadIdx.x] += rb[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (!dx) return;
+  const float m1 = ra[0] / static_cast<float>(N), m2 = rb[0] / static_cast<float>(N);
+  for (int64_t j = threadIdx.x; j < N; j += 256) {
+    const float xh = (x[r * N + j] - mu) * rs;
+    const float gg = dy[r * N + j] * (gamma ? gamma[j] : 1.f);
+    dx[r * N + j] += rs * (gg - m1 - xh * m2);
+  }
+}
+// ---- multi-head attention helpers (op_attrs mha layout: weight [P, H], head
+// h's column holds Wq [Eq, k] | Wk [Ek, k] | Wv [Ev, v] | Wo [v, E] row-major)
+// Wd[h][p] = W[p][h] (to = 1: dW[p][h] += dWd[h][p])
+__global__ __launch_bounds__(256) void k_head_major(const float* src, float* dst, int64_t P, int64_t H, int to) {
+  GRID_LOOP(i, P * H) {
+    const int64_t h = i / P, p = i % P;
+    if (to) dst[p * H + h] += src[i];
+    else dst[i] = src[p * H + h];
+  }
+}
+// x[h][r][j] += bias[(off + j) * H + h] for r < R
+__global__ __launch_bounds__(256) void k_head_bias(float* x, const float* bias, int64_t H, int64_t R, int64_t D,
+                                                   int64_t off) {
+  GRID_LOOP(i, H * R * D) {
+    const int64_t j = i % D, h = i / (R * D);
+    x[i] += bias[(off + j) * H + h];
+  }
+}
+// dbias[(off + j) * H + h] += sum_r g[h][r][j]: one thread per (h, j)
+__global__ __launch_bounds__(256) void k_head_bias_grad(const float* g, float* dbias, int64_t H, int64_t R,
+                                                        int64_t D, int64_t off) {
+  GRID_LOOP(i, H * D) {
+    const int64_t h = i / D, j = i % D;
+    const float* gh = g + h * R * D;
+    float s = 0.f;
+    for (int64_t r = 0; r < R; ++r) s += gh[r * D + j];
+    dbias[(off + j) * H + h] += s;
+  }
+}
+// scores -> probabilities in place, rows of Sk: scale, causal mask (query
+// row q = row % Sq sees keys <= q), softmax; one block per row
+__global__ __launch_bounds__(256) void k_attn_softmax(float* p, int64_t Sq, int64_t Sk, float scale, int causal) {
+  __shared__ float red[256];
+  float* r = p + blockIdx.x * Sk;
+  const int64_t q = blockIdx.x % Sq;
+  float m = -INFINITY;
+  for (int64_t j = threadIdx.x; j < Sk; j += 256) {
+    const float v = (causal && j > q) ? -INFINITY : r[j] * scale;
+    r[j] = v;
+    m = fmaxf(m, v);
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  m = red[0];
+  __syncthreads();
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < Sk; j += 256) {
+    const float e = r[j] == -INFINITY ? 0.f : expf(r[j] - m);
+    r[j] = e;
+    s += e;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float inv = 1.f / red[0];
+  for (int64_t j = threadIdx.x; j < Sk; j += 256) r[j] *= inv;
+}
+// dS = P * (dP - rowsum(P * dP)) * scale, in place in dP
+__global__ __launch_bounds__(256) void k_attn_softmax_bwd(const float* p, float* dp, int64_t Sk, float scale) {
+  __shared__ float red[256];
+  const float* pr = p + blockIdx.x * Sk;
+  float* dr = dp + blockIdx.x * Sk;
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < Sk; j += 256) s += pr[j] * dr[j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float dot = red[0];
+  for (int64_t j = threadIdx.x; j < Sk; j += 256) dr[j] = pr[j] * (dr[j] - dot) * scale;
+}
+// y[r][e] += b[e]
+__global__ __launch_bounds__(256) void k_add_rows(float* y, const float* b, int64_t R, int64_t E) {
+  GRID_LOOP(i, R * E) y[i] += b[i % E];
+}
+
 int grid_of(int64_t n) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))); }
 
 int dact_of(const std::string& s) {
@@ -532,7 +730,30 @@ std::string unsupported(const ComputationGraph& cg, int n) {
     }
     return "";
   }
-  if (t == OpType::BATCHNORM) return "";
+  if (t == OpType::BATCHNORM || t == OpType::BATCHMATMUL || t == OpType::CONCAT || t == OpType::SPLIT ||
+      t == OpType::DROPOUT)
+    return "";
+  if (t == OpType::EMBEDDING) {
+    const std::string a = node.label.op.s("aggr");
+    if (a != "none" && a != "sum" && a != "avg") return "embedding aggregation " + a;
+    return "";
+  }
+  if (t == OpType::LAYERNORM) {
+    // the normalised axes must be the trailing ones (rows x N)
+    const auto& d = cg.shape(cg.layer_data_inputs(n)[0]).dims;
+    const int nd = static_cast<int>(d.size());
+    std::vector<int> ax;
+    for (auto a : node.label.op.ints("axes")) ax.push_back(static_cast<int>((a % nd + nd) % nd));
+    std::sort(ax.begin(), ax.end());
+    for (size_t i = 0; i < ax.size(); ++i)
+      if (ax[i] != nd - static_cast<int>(ax.size()) + static_cast<int>(i)) return "layer norm over non-trailing axes";
+    return "";
+  }
+  if (t == OpType::MULTIHEAD_ATTENTION) {
+    const auto ins = cg.layer_data_inputs(n);
+    if (ins.size() != 3 || cg.shape(ins[0]).dims.size() != 3) return "attention inputs";
+    return "";
+  }
   if (dact_of(t) >= 0 || binary_of(t) >= 0 || scalar_of(t) >= 0 || is_view(t) || t == OpType::SOFTMAX) {
     if (binary_of(t) >= 0) {
       auto ins = cg.layer_data_inputs(n);
@@ -548,7 +769,7 @@ class DeviceTrainingBacking final : public TrainingBacking {
  public:
   DeviceTrainingBacking(const ComputationGraph& cg, LocalOptimizer opt, const std::string& loss, uint64_t seed,
                         int dev)
-      : cg_(cg), host_(cg, std::move(opt), loss, seed), dev_(dev) {
+      : cg_(cg), host_(cg, std::move(opt), loss, seed), dev_(dev), seed_(seed) {
     FFD_CHECK(hipSetDevice(dev_));
     FFD_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     // one arena: every value, gradient, pre-activation and optimizer buffer
@@ -572,7 +793,24 @@ class DeviceTrainingBacking final : public TrainingBacking {
       if (t == OpType::POOL2D) want.push_back({Key{{n, 0}, 3}, ne});   // argmax / window counts
       if (t == OpType::BATCHNORM)
         want.push_back({Key{{n, 0}, 3}, 2 * host_.slot(cg_.layer_data_inputs(n)[0], false)->dims.at(1)});
+      if (t == OpType::EMBEDDING)   // int32 copy of the float-carried indices
+        want.push_back({Key{{n, 0}, 3}, host_.slot(cg_.layer_data_inputs(n)[0], false)->numel()});
+      if (t == OpType::LAYERNORM) {
+        const int64_t N = ln_cols(n), R = ne / std::max<int64_t>(N, 1);
+        want.push_back({Key{{n, 0}, 3}, 2 * R});   // mean, rstd
+        if (N % 8 == 0) want.push_back({Key{{n, 0}, 4}, 3 * int64_t(ffk::layernorm_bwd_grid(R, N)) * N});
+      }
+      if (t == OpType::MULTIHEAD_ATTENTION) {
+        const MG g = mha_of(n);
+        const int64_t q = g.H * g.B * g.Sq, k = g.H * g.B * g.Sk, pp = g.H * g.B * g.Sq * g.Sk;
+        for (auto const& kv : std::vector<std::pair<int, int64_t>>{
+                 {10, g.H * g.P}, {11, q * g.kd}, {12, k * g.kd}, {13, k * g.vd}, {14, pp}, {15, q * g.vd},
+                 {16, g.H * g.P}, {17, q * g.vd}, {18, q * g.kd}, {19, k * g.kd}, {20, k * g.vd}, {21, pp}})
+          want.push_back({Key{{n, 0}, kv.first}, kv.second});
+      }
       tmp_elems_ = std::max(tmp_elems_, ne);
+      if (t == OpType::LAYERNORM || t == OpType::SOFTMAX)
+        tmp_elems_ = std::max(tmp_elems_, host_.slot(cg_.layer_data_inputs(n)[0], false)->numel());
     }
     const ValueRef out = host_.output();
     rows_ = 1;
@@ -686,10 +924,53 @@ class DeviceTrainingBacking final : public TrainingBacking {
 
   void fwd(int n);
   void bwd(int n);
+  void mha_fwd(int n);
+  void mha_bwd(int n);
+
+  // multi-head attention geometry (local_exec.cc MhaGeom)
+  struct MG {
+    int64_t B, Sq, Sk, Eq, Ek, Ev, E, H, kd, vd, P;
+    int64_t off_q() const { return 0; }
+    int64_t off_k() const { return Eq * kd; }
+    int64_t off_v() const { return Eq * kd + Ek * kd; }
+    int64_t off_o() const { return Eq * kd + Ek * kd + Ev * vd; }
+  };
+  MG mha_of(int n) {
+    const auto& op = cg_.g.node(n).label.op;
+    const auto ins = cg_.layer_data_inputs(n);
+    const auto& q = host_.slot(ins[0], false)->dims;
+    MG g{};
+    g.B = q[0];
+    g.Sq = q[1];
+    g.Eq = q[2];
+    g.Sk = host_.slot(ins[1], false)->dims[1];
+    g.Ek = host_.slot(ins[1], false)->dims[2];
+    g.Ev = host_.slot(ins[2], false)->dims[2];
+    g.E = op.i("embed_dim");
+    g.H = op.i("num_heads");
+    g.kd = op.i("kdim") > 0 ? op.i("kdim") : g.E / g.H;
+    g.vd = op.i("vdim") > 0 ? op.i("vdim") : g.E / g.H;
+    g.P = g.Eq * g.kd + g.Ek * g.kd + g.Ev * g.vd + g.vd * g.E;
+    return g;
+  }
+  // layer norm: elements per normalised row (the trailing axes)
+  int64_t ln_cols(int n) {
+    const auto& op = cg_.g.node(n).label.op;
+    const auto& d = host_.slot(cg_.layer_data_inputs(n)[0], false)->dims;
+    const int nd = static_cast<int>(d.size());
+    int64_t N = 1;
+    for (auto a : op.ints("axes")) N *= d[(a % nd + nd) % nd];
+    return N;
+  }
+  float* aux(int n, int kind) { return buf_.at(Key{{n, 0}, kind}).p; }
+  uint64_t op_seed(int n) const {
+    return seed_ * 7919ull + static_cast<uint64_t>(n) * 104729ull + static_cast<uint64_t>(step_);
+  }
 
   const ComputationGraph& cg_;
   LocalTrainingBacking host_;
   int dev_;
+  uint64_t seed_;
   hipStream_t st_ = nullptr;
   float* arena_ = nullptr;
   float *tmp_ = nullptr, *tmp2_ = nullptr, *metrics_d_ = nullptr;
@@ -771,12 +1052,179 @@ void DeviceTrainingBacking::fwd(int n) {
   } else if (t == OpType::SOFTMAX) {
     const auto& d = host_.slot(o, false)->dims;
     const int64_t cols = d.empty() ? 1 : d.back();
-    hipLaunchKernelGGL(k_softmax, dim3(static_cast<unsigned>(ne / cols)), dim3(256), 0, st_, val(ins[0]), y, cols);
+    ffk::softmax_fwd(kDtF32, val(ins[0]), y, static_cast<int>(ne / cols), static_cast<int>(cols), st_);
+  } else if (t == OpType::EMBEDDING) {
+    const auto ws = cg_.layer_weights(n);
+    const auto& wd = host_.slot(ws[0], false)->dims;   // [entries, D]
+    const int64_t E = wd[0], D = wd[1], nidx = numel(ins[0]);
+    const std::string aggr = op.s("aggr");
+    const auto& id = host_.slot(ins[0], false)->dims;
+    const int L = aggr == "none" ? 1 : static_cast<int>(id.back());
+    int* idx = reinterpret_cast<int*>(aux(n, 3));
+    hipLaunchKernelGGL(k_f2i, dim3(grid_of(nidx)), dim3(256), 0, st_, val(ins[0]), idx, nidx);
+    if (D % 8 == 0)
+      ffk::embedding_fwd(kDtF32, 32, idx, val(ws[0]), y, nidx / L, L, static_cast<int>(D),
+                         aggr == "none" ? 0 : aggr == "sum" ? 1 : 2, E, st_);
+    else
+      hipLaunchKernelGGL(k_embed_fwd, dim3(grid_of(ne)), dim3(256), 0, st_, idx, val(ws[0]), y, nidx / L, L, D,
+                         aggr == "avg" ? 1.f / static_cast<float>(L) : 1.f);
+  } else if (t == OpType::LAYERNORM) {
+    const auto ws = cg_.layer_weights(n);
+    const int64_t N = ln_cols(n), R = ne / N;
+    const float* gm = ws.size() > 0 ? val(ws[0]) : nullptr;
+    const float* bt = ws.size() > 1 ? val(ws[1]) : nullptr;
+    float* st = aux(n, 3);
+    if (N % 8 == 0)
+      ffk::layernorm_fwd(kDtF32, val(ins[0]), nullptr, nullptr, gm, bt, y, st, st + R, static_cast<int>(R),
+                         static_cast<int>(N), static_cast<float>(op.f("eps")), st_);
+    else
+      hipLaunchKernelGGL(k_ln_fwd, dim3(static_cast<unsigned>(R)), dim3(256), 0, st_, val(ins[0]), gm, bt, y, st,
+                         st + R, N, static_cast<float>(op.f("eps")));
+  } else if (t == OpType::BATCHMATMUL) {
+    const auto& a = host_.slot(ins[0], false)->dims;
+    const int nd = static_cast<int>(a.size());
+    const int64_t M = a[nd - 2], K = a[nd - 1], N = host_.slot(ins[1], false)->dims.back();
+    const int64_t Bt = numel(ins[0]) / (M * K);
+    ffk::gemm_f32(val(ins[0]), val(ins[1]), y, nullptr, nullptr, M, N, K, K, N, N, false, false, 0, 1.f, 0.f, 1, 1,
+                  st_, static_cast<int>(Bt), M * K, K * N, M * N);
+  } else if (t == OpType::CONCAT || t == OpType::SPLIT) {
+    const bool cat = t == OpType::CONCAT;
+    const auto& big = cat ? host_.slot(o, false)->dims : host_.slot(ins[0], false)->dims;
+    const int nd = static_cast<int>(big.size());
+    const int ax = static_cast<int>((op.i("axis") % nd + nd) % nd);
+    int64_t outer = 1, inner = 1;
+    for (int k = 0; k < ax; ++k) outer *= big[k];
+    for (int k = ax + 1; k < nd; ++k) inner *= big[k];
+    int64_t off = 0;
+    const size_t pieces = cat ? ins.size() : node.outputs.size();
+    for (size_t j = 0; j < pieces; ++j) {
+      const ValueRef pv = cat ? ins[j] : ValueRef{n, static_cast<int>(j)};
+      const int64_t len = host_.slot(pv, false)->dims[ax];
+      if (cat) ffk::slice_copy(kDtF32, val(pv), y, outer, len, inner, big[ax], off, 0, 0, st_);
+      else ffk::slice_copy(kDtF32, val(ins[0]), val(pv), outer, len, inner, big[ax], off, 1, 0, st_);
+      if (!cat) mark(pv, 0);
+      off += len;
+    }
+  } else if (t == OpType::DROPOUT) {
+    hipLaunchKernelGGL(k_dropout, dim3(grid_of(ne)), dim3(256), 0, st_, val(ins[0]), y, ne,
+                       static_cast<float>(op.f("rate")), op_seed(n), 0);
+  } else if (t == OpType::MULTIHEAD_ATTENTION) {
+    mha_fwd(n);
   } else {
     throw FFError("device backing: no device implementation for " + to_string(t));
   }
   FFD_CHECK(hipGetLastError());
   mark(o, 0);
+}
+
+// ---- multi-head attention (local_exec.cc mha_fwd / mha_bwd) on batched
+// fp32 MFMA GEMMs: per-head projections over all B * S rows, scores and
+// P @ V batched over heads x batch, the weight handled head-major (Wd[h][p])
+void DeviceTrainingBacking::mha_fwd(int n) {
+  const auto& op = cg_.g.node(n).label.op;
+  const auto ins = cg_.layer_data_inputs(n);
+  const auto ws = cg_.layer_weights(n);
+  const MG g = mha_of(n);
+  const ValueRef o{n, 0};
+  float* y = val(o);
+  float *Wd = aux(n, 10), *Q = aux(n, 11), *Kt = aux(n, 12), *V = aux(n, 13), *P = aux(n, 14), *O = aux(n, 15);
+  const int64_t rq = g.B * g.Sq, rk = g.B * g.Sk;
+  hipLaunchKernelGGL(k_head_major, dim3(grid_of(g.P * g.H)), dim3(256), 0, st_, val(ws[0]), Wd, g.P, g.H, 0);
+  for (int64_t h = 0; h < g.H; ++h) {
+    const float* Wh = Wd + h * g.P;
+    ffk::gemm_f32(val(ins[0]), Wh + g.off_q(), Q + h * rq * g.kd, nullptr, nullptr, rq, g.kd, g.Eq, g.Eq, g.kd,
+                  g.kd, false, false, 0, 1.f, 0.f, 1, 1, st_);
+    ffk::gemm_f32(val(ins[1]), Wh + g.off_k(), Kt + h * rk * g.kd, nullptr, nullptr, rk, g.kd, g.Ek, g.Ek, g.kd,
+                  g.kd, false, false, 0, 1.f, 0.f, 1, 1, st_);
+    ffk::gemm_f32(val(ins[2]), Wh + g.off_v(), V + h * rk * g.vd, nullptr, nullptr, rk, g.vd, g.Ev, g.Ev, g.vd,
+                  g.vd, false, false, 0, 1.f, 0.f, 1, 1, st_);
+  }
+  if (ws.size() > 1) {   // input bias [2k + v, H]
+    hipLaunchKernelGGL(k_head_bias, dim3(grid_of(g.H * rq * g.kd)), dim3(256), 0, st_, Q, val(ws[1]), g.H, rq, g.kd,
+                       int64_t(0));
+    hipLaunchKernelGGL(k_head_bias, dim3(grid_of(g.H * rk * g.kd)), dim3(256), 0, st_, Kt, val(ws[1]), g.H, rk, g.kd,
+                       g.kd);
+    hipLaunchKernelGGL(k_head_bias, dim3(grid_of(g.H * rk * g.vd)), dim3(256), 0, st_, V, val(ws[1]), g.H, rk, g.vd,
+                       2 * g.kd);
+  }
+  const int hb = static_cast<int>(g.H * g.B);
+  ffk::gemm_f32(Q, Kt, P, nullptr, nullptr, g.Sq, g.Sk, g.kd, g.kd, g.kd, g.Sk, false, true, 0, 1.f, 0.f, 1, 1, st_,
+                hb, g.Sq * g.kd, g.Sk * g.kd, g.Sq * g.Sk);
+  hipLaunchKernelGGL(k_attn_softmax, dim3(static_cast<unsigned>(hb * g.Sq)), dim3(256), 0, st_, P, g.Sq, g.Sk,
+                     1.f / std::sqrt(static_cast<float>(g.kd)), op.b("causal") ? 1 : 0);
+  ffk::gemm_f32(P, V, O, nullptr, nullptr, g.Sq, g.vd, g.Sk, g.Sk, g.vd, g.vd, false, false, 0, 1.f, 0.f, 1, 1, st_,
+                hb, g.Sq * g.Sk, g.Sk * g.vd, g.Sq * g.vd);
+  for (int64_t h = 0; h < g.H; ++h)   // y = sum_h O_h Wo_h
+    ffk::gemm_f32(O + h * rq * g.vd, Wd + h * g.P + g.off_o(), y, nullptr, nullptr, rq, g.E, g.vd, g.vd, g.E, g.E,
+                  false, false, 0, 1.f, h == 0 ? 0.f : 1.f, 1, 1, st_);
+  if (ws.size() > 2)
+    hipLaunchKernelGGL(k_add_rows, dim3(grid_of(rq * g.E)), dim3(256), 0, st_, y, val(ws[2]), rq, g.E);
+}
+
+void DeviceTrainingBacking::mha_bwd(int n) {
+  const auto ins = cg_.layer_data_inputs(n);
+  const auto ws = cg_.layer_weights(n);
+  const MG g = mha_of(n);
+  const float* G = grad({n, 0});
+  float *Wd = aux(n, 10), *Q = aux(n, 11), *Kt = aux(n, 12), *V = aux(n, 13), *P = aux(n, 14), *O = aux(n, 15);
+  float *dWd = aux(n, 16), *dO = aux(n, 17), *dQ = aux(n, 18), *dK = aux(n, 19), *dV = aux(n, 20), *dP = aux(n, 21);
+  const int64_t rq = g.B * g.Sq, rk = g.B * g.Sk;
+  const int hb = static_cast<int>(g.H * g.B);
+  if (ws.size() > 2)
+    if (float* db = grad(ws[2])) {
+      if (g.E % 8 == 0) ffk::colsum_act(kDtF32, G, nullptr, nullptr, db, rq, g.E, 0, 0.f, st_);
+      else hipLaunchKernelGGL(k_colsum, dim3(static_cast<unsigned>((g.E + 255) / 256)), dim3(256), 0, st_, G, db,
+                              rq, g.E);
+    }
+  for (int64_t h = 0; h < g.H; ++h) {
+    // dWo_h = O_h^T G ; dO_h = G Wo_h^T
+    ffk::gemm_f32(O + h * rq * g.vd, G, dWd + h * g.P + g.off_o(), nullptr, nullptr, g.vd, g.E, rq, g.vd, g.E, g.E,
+                  true, false, 0, 1.f, 0.f, 1, 1, st_);
+    ffk::gemm_f32(G, Wd + h * g.P + g.off_o(), dO + h * rq * g.vd, nullptr, nullptr, rq, g.vd, g.E, g.E, g.E, g.vd,
+                  false, true, 0, 1.f, 0.f, 1, 1, st_);
+  }
+  // dP = dO V^T, dV = P^T dO, dS = softmax'(dP) * scale, dQ = dS K, dK = dS^T Q
+  ffk::gemm_f32(dO, V, dP, nullptr, nullptr, g.Sq, g.Sk, g.vd, g.vd, g.vd, g.Sk, false, true, 0, 1.f, 0.f, 1, 1, st_,
+                hb, g.Sq * g.vd, g.Sk * g.vd, g.Sq * g.Sk);
+  ffk::gemm_f32(P, dO, dV, nullptr, nullptr, g.Sk, g.vd, g.Sq, g.Sk, g.vd, g.vd, true, false, 0, 1.f, 0.f, 1, 1, st_,
+                hb, g.Sq * g.Sk, g.Sq * g.vd, g.Sk * g.vd);
+  hipLaunchKernelGGL(k_attn_softmax_bwd, dim3(static_cast<unsigned>(hb * g.Sq)), dim3(256), 0, st_, P, dP, g.Sk,
+                     1.f / std::sqrt(static_cast<float>(g.kd)));
+  ffk::gemm_f32(dP, Kt, dQ, nullptr, nullptr, g.Sq, g.kd, g.Sk, g.Sk, g.kd, g.kd, false, false, 0, 1.f, 0.f, 1, 1,
+                st_, hb, g.Sq * g.Sk, g.Sk * g.kd, g.Sq * g.kd);
+  ffk::gemm_f32(dP, Q, dK, nullptr, nullptr, g.Sk, g.kd, g.Sq, g.Sk, g.kd, g.kd, true, false, 0, 1.f, 0.f, 1, 1, st_,
+                hb, g.Sq * g.Sk, g.Sq * g.kd, g.Sk * g.kd);
+  float *dxq = grad(ins[0]), *dxk = grad(ins[1]), *dxv = grad(ins[2]);
+  for (int64_t h = 0; h < g.H; ++h) {
+    float* dWh = dWd + h * g.P;
+    const float* Wh = Wd + h * g.P;
+    ffk::gemm_f32(val(ins[0]), dQ + h * rq * g.kd, dWh + g.off_q(), nullptr, nullptr, g.Eq, g.kd, rq, g.Eq, g.kd,
+                  g.kd, true, false, 0, 1.f, 0.f, 1, 1, st_);
+    ffk::gemm_f32(val(ins[1]), dK + h * rk * g.kd, dWh + g.off_k(), nullptr, nullptr, g.Ek, g.kd, rk, g.Ek, g.kd,
+                  g.kd, true, false, 0, 1.f, 0.f, 1, 1, st_);
+    ffk::gemm_f32(val(ins[2]), dV + h * rk * g.vd, dWh + g.off_v(), nullptr, nullptr, g.Ev, g.vd, rk, g.Ev, g.vd,
+                  g.vd, true, false, 0, 1.f, 0.f, 1, 1, st_);
+    if (dxq)
+      ffk::gemm_f32(dQ + h * rq * g.kd, Wh + g.off_q(), dxq, nullptr, nullptr, rq, g.Eq, g.kd, g.kd, g.kd, g.Eq,
+                    false, true, 0, 1.f, 1.f, 1, 1, st_);
+    if (dxk)
+      ffk::gemm_f32(dK + h * rk * g.kd, Wh + g.off_k(), dxk, nullptr, nullptr, rk, g.Ek, g.kd, g.kd, g.kd, g.Ek,
+                    false, true, 0, 1.f, 1.f, 1, 1, st_);
+    if (dxv)
+      ffk::gemm_f32(dV + h * rk * g.vd, Wh + g.off_v(), dxv, nullptr, nullptr, rk, g.Ev, g.vd, g.vd, g.vd, g.Ev,
+                    false, true, 0, 1.f, 1.f, 1, 1, st_);
+  }
+  if (ws.size() > 1)
+    if (float* dbi = grad(ws[1])) {
+      hipLaunchKernelGGL(k_head_bias_grad, dim3(grid_of(g.H * g.kd)), dim3(256), 0, st_, dQ, dbi, g.H, rq, g.kd,
+                         int64_t(0));
+      hipLaunchKernelGGL(k_head_bias_grad, dim3(grid_of(g.H * g.kd)), dim3(256), 0, st_, dK, dbi, g.H, rk, g.kd,
+                         g.kd);
+      hipLaunchKernelGGL(k_head_bias_grad, dim3(grid_of(g.H * g.vd)), dim3(256), 0, st_, dV, dbi, g.H, rk, g.vd,
+                         2 * g.kd);
+    }
+  if (float* dW = grad(ws[0]))
+    hipLaunchKernelGGL(k_head_major, dim3(grid_of(g.P * g.H)), dim3(256), 0, st_, dWd, dW, g.P, g.H, 1);
 }
 
 void DeviceTrainingBacking::bwd(int n) {
@@ -785,6 +1233,26 @@ void DeviceTrainingBacking::bwd(int n) {
   const OpType t = op.type;
   const auto ins = cg_.layer_data_inputs(n);
   const ValueRef o{n, 0};
+  if (t == OpType::SPLIT) {   // every output's gradient back into its slice of the input's
+    float* dx = grad(ins[0]);
+    if (!dx) return;
+    const auto& big = host_.slot(ins[0], false)->dims;
+    const int nd = static_cast<int>(big.size());
+    const int ax = static_cast<int>((op.i("axis") % nd + nd) % nd);
+    int64_t outer = 1, inner = 1;
+    for (int k = 0; k < ax; ++k) outer *= big[k];
+    for (int k = ax + 1; k < nd; ++k) inner *= big[k];
+    int64_t off = 0;
+    for (size_t j = 0; j < node.outputs.size(); ++j) {
+      const ValueRef pv{n, static_cast<int>(j)};
+      const int64_t len = host_.slot(pv, false)->dims[ax];
+      if (const float* g = grad(pv)) ffk::slice_copy(kDtF32, g, dx, outer, len, inner, big[ax], off, 0, 1, st_);
+      off += len;
+    }
+    FFD_CHECK(hipGetLastError());
+    mark(ins[0], 1);
+    return;
+  }
   float* dy = grad(o);
   if (!dy) return;
   const int64_t ne = numel(o);
@@ -802,9 +1270,11 @@ void DeviceTrainingBacking::bwd(int n) {
       ffk::gemm_f32(val(ins[0]), g, dw, nullptr, nullptr, in, outc, rows, in, outc, outc, true, false, 0, 1.f, 1.f, 1,
                     1, st_);
     if (ws.size() > 1)
-      if (float* db = grad(ws[1]))
-        hipLaunchKernelGGL(k_colsum, dim3(static_cast<unsigned>((outc + 255) / 256)), dim3(256), 0, st_, g, db, rows,
-                           outc);
+      if (float* db = grad(ws[1])) {
+        if (outc % 8 == 0) ffk::colsum_act(kDtF32, g, nullptr, nullptr, db, rows, outc, 0, 0.f, st_);
+        else hipLaunchKernelGGL(k_colsum, dim3(static_cast<unsigned>((outc + 255) / 256)), dim3(256), 0, st_, g, db,
+                                rows, outc);
+      }
     if (float* dx = grad(ins[0]))   // dX += g W^T
       ffk::gemm_f32(g, val(ws[0]), dx, nullptr, nullptr, rows, in, outc, outc, outc, in, false, true, 0, 1.f, 1.f, 1,
                     1, st_);
@@ -859,9 +1329,71 @@ void DeviceTrainingBacking::bwd(int n) {
   } else if (t == OpType::SOFTMAX) {
     const auto& d = host_.slot(o, false)->dims;
     const int64_t cols = d.empty() ? 1 : d.back();
+    if (float* dx = grad(ins[0])) {   // softmax.hip writes dx: through tmp, then accumulated
+      ffk::softmax_bwd(kDtF32, dy, val(o), tmp_, static_cast<int>(ne / cols), static_cast<int>(cols), st_);
+      hipLaunchKernelGGL(k_axpy, dim3(grid_of(ne)), dim3(256), 0, st_, tmp_, dx, ne, 1.f);
+    }
+  } else if (t == OpType::EMBEDDING) {
+    const auto ws = cg_.layer_weights(n);
+    if (float* dw = grad(ws[0])) {
+      const auto& wd = host_.slot(ws[0], false)->dims;
+      const int64_t E = wd[0], D = wd[1], nidx = numel(ins[0]);
+      const std::string aggr = op.s("aggr");
+      const int L = aggr == "none" ? 1 : static_cast<int>(host_.slot(ins[0], false)->dims.back());
+      const int* idx = reinterpret_cast<const int*>(aux(n, 3));
+      if (D % 8 == 0)
+        ffk::embedding_bwd(kDtF32, 32, idx, dy, dw, nidx / L, L, static_cast<int>(D),
+                           aggr == "none" ? 0 : aggr == "sum" ? 1 : 2, E, nullptr, 1, st_);
+      else
+        hipLaunchKernelGGL(k_embed_bwd, dim3(grid_of(nidx * D)), dim3(256), 0, st_, idx, dy, dw, nidx / L, L, D,
+                           aggr == "avg" ? 1.f / static_cast<float>(L) : 1.f);
+    }
+  } else if (t == OpType::LAYERNORM) {
+    const auto ws = cg_.layer_weights(n);
+    const int64_t N = ln_cols(n), R = ne / N;
+    const float* gm = ws.size() > 0 ? val(ws[0]) : nullptr;
+    float* dg = ws.size() > 0 ? grad(ws[0]) : nullptr;
+    float* dbt = ws.size() > 1 ? grad(ws[1]) : nullptr;
+    const float* st = aux(n, 3);
+    float* dx = grad(ins[0]);
+    if (N % 8 == 0) {   // layernorm.hip writes dx: through tmp, then accumulated
+      ffk::layernorm_bwd(kDtF32, dy, val(ins[0]), st, st + R, gm, tmp_, dg, dbt, aux(n, 4), static_cast<int>(R),
+                         static_cast<int>(N), st_);
+      if (dx) hipLaunchKernelGGL(k_axpy, dim3(grid_of(ne)), dim3(256), 0, st_, tmp_, dx, ne, 1.f);
+    } else {
+      hipLaunchKernelGGL(k_ln_bwd, dim3(static_cast<unsigned>(R)), dim3(256), 0, st_, dy, val(ins[0]), gm, st, st + R,
+                         dx, dg, dbt, N);
+    }
+  } else if (t == OpType::BATCHMATMUL) {
+    const auto& a = host_.slot(ins[0], false)->dims;
+    const int nd = static_cast<int>(a.size());
+    const int64_t M = a[nd - 2], K = a[nd - 1], N = host_.slot(ins[1], false)->dims.back();
+    const int Bt = static_cast<int>(numel(ins[0]) / (M * K));
+    if (float* da = grad(ins[0]))   // dA += G B^T
+      ffk::gemm_f32(dy, val(ins[1]), da, nullptr, nullptr, M, K, N, N, N, K, false, true, 0, 1.f, 1.f, 1, 1, st_, Bt,
+                    M * N, K * N, M * K);
+    if (float* db = grad(ins[1]))   // dB += A^T G
+      ffk::gemm_f32(val(ins[0]), dy, db, nullptr, nullptr, K, N, M, K, N, N, true, false, 0, 1.f, 1.f, 1, 1, st_, Bt,
+                    M * K, M * N, K * N);
+  } else if (t == OpType::CONCAT) {
+    const auto& big = host_.slot(o, false)->dims;
+    const int nd = static_cast<int>(big.size());
+    const int ax = static_cast<int>((op.i("axis") % nd + nd) % nd);
+    int64_t outer = 1, inner = 1;
+    for (int k = 0; k < ax; ++k) outer *= big[k];
+    for (int k = ax + 1; k < nd; ++k) inner *= big[k];
+    int64_t off = 0;
+    for (auto const& v : ins) {
+      const int64_t len = host_.slot(v, false)->dims[ax];
+      if (float* dx = grad(v)) ffk::slice_copy(kDtF32, dy, dx, outer, len, inner, big[ax], off, 1, 1, st_);
+      off += len;
+    }
+  } else if (t == OpType::DROPOUT) {
     if (float* dx = grad(ins[0]))
-      hipLaunchKernelGGL(k_softmax_bwd, dim3(static_cast<unsigned>(ne / cols)), dim3(256), 0, st_, dy, val(o), dx,
-                         cols);
+      hipLaunchKernelGGL(k_dropout, dim3(grid_of(ne)), dim3(256), 0, st_, dy, dx, ne,
+                         static_cast<float>(op.f("rate")), op_seed(n), 1);
+  } else if (t == OpType::MULTIHEAD_ATTENTION) {
+    mha_bwd(n);
   }
   FFD_CHECK(hipGetLastError());
   for (auto const& v : ins)

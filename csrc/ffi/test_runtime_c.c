@@ -300,6 +300,89 @@ static void test_parity_cnn(flexflow_config_t cfg) {
   flexflow_model_destroy(model);
 }
 
+
+/* a 2-layer BERT-style encoder through the C API (embedding, multi-head
+ * attention with biases, residual adds, layer norms, GELU FFN with dropout,
+ * split + concat, a batch-matmul side branch over a reshaped view, the
+ * vocabulary head + softmax cross-entropy) for three Adam steps: the GPU
+ * backing (production kernels) and the CPU backing must agree
+ * (tests/test_runtime_c_gpu.py) */
+static void test_parity_bert(flexflow_config_t cfg) {
+  enum { BB = 4, S = 16, V = 40, D = 32, HEADS = 4, FF = 64 };
+  flexflow_model_t model = flexflow_model_create(cfg);
+  int dims[2] = {BB, S};
+  flexflow_tensor_t tok = flexflow_tensor_create(model, 2, dims, DT_INT32, false);
+  flexflow_initializer_t null_init = flexflow_initializer_create_null();
+  flexflow_op_t no_op = {NULL};
+  flexflow_tensor_t x = flexflow_model_add_embedding(model, tok, V, D, AGGR_MODE_NONE, no_op, null_init, "emb");
+  int ln_axes[1] = {-1};
+  for (int l = 0; l < 2; ++l) {
+    char nm[32];
+    snprintf(nm, sizeof nm, "attn%d", l);
+    flexflow_tensor_t a = flexflow_model_add_multihead_attention(model, x, x, x, D, HEADS, D / HEADS, D / HEADS, 0.f,
+                                                                 true, false, false, null_init, nm);
+    x = flexflow_model_add_layer_norm(model, flexflow_model_add_add(model, x, a, false, NULL), 1, ln_axes, true, 1e-5f,
+                                      NULL);
+    flexflow_tensor_t f = flexflow_model_add_dense(model, x, FF, AC_MODE_GELU, true, DT_FLOAT, no_op, null_init,
+                                                   null_init, REG_MODE_NONE, 0.f, NULL);
+    f = flexflow_model_add_dropout(model, f, 0.1f, 3, NULL);
+    f = flexflow_model_add_dense(model, f, D, AC_MODE_NONE, true, DT_FLOAT, no_op, null_init, null_init,
+                                 REG_MODE_NONE, 0.f, NULL);
+    if (l == 0) {   /* split the FFN output in two along the features and put it back */
+      flexflow_tensor_t halves[2];
+      int sizes[2] = {D / 2, D / 2};
+      flexflow_model_add_split(model, f, 2, halves, sizes, 2, NULL);
+      f = flexflow_model_add_concat(model, 2, halves, 2, NULL);
+    } else {        /* x [B,S,D] @ view(x) [B,D,S] -> [B,S,S] -> dense back to D, added in */
+      int rs[3] = {BB, D, S};
+      flexflow_tensor_t xr = flexflow_model_add_reshape(model, x, 3, rs, NULL);
+      flexflow_tensor_t z = flexflow_model_add_batch_matmul(model, x, xr, -1, -1);
+      z = flexflow_model_add_dense(model, z, D, AC_MODE_NONE, false, DT_FLOAT, no_op, null_init, null_init,
+                                   REG_MODE_NONE, 0.f, NULL);
+      f = flexflow_model_add_add(model, f, flexflow_model_add_scalar_multiply(model, z, 0.1f, false, NULL), false,
+                                 NULL);
+    }
+    x = flexflow_model_add_layer_norm(model, flexflow_model_add_add(model, x, f, false, NULL), 1, ln_axes, true, 1e-5f,
+                                      NULL);
+  }
+  flexflow_tensor_t logits = flexflow_model_add_dense(model, x, V, AC_MODE_NONE, true, DT_FLOAT, no_op, null_init,
+                                                      null_init, REG_MODE_NONE, 0.f, "head");
+  flexflow_model_add_softmax(model, logits, -1, "sm");
+  flexflow_adam_optimizer_t adam = flexflow_adam_optimizer_create(model, 0.005, 0.9, 0.999, 0.0, 1e-8);
+  flexflow_model_set_adam_optimizer(model, adam);
+  int metrics[1] = {METRICS_ACCURACY};
+  flexflow_model_compile(model, LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics, 1, COMP_MODE_TRAINING);
+  int ids[BB * S], lab[BB * S];
+  for (int i = 0; i < BB * S; ++i) {
+    ids[i] = (i * 7 + 3) % V;
+    lab[i] = (i * 5 + 1) % V;
+  }
+  flexflow_tensor_set_tensor_int(tok, model, 2, dims, ids);
+  int ldims[3] = {BB, S, 1};
+  flexflow_tensor_set_tensor_int(flexflow_model_get_label_tensor(model), model, 3, ldims, lab);
+  for (int step = 0; step < 3; ++step) {
+    flexflow_model_forward(model, -1);
+    flexflow_model_zero_gradients(model);
+    flexflow_model_backward(model, -1);
+    flexflow_model_update(model);
+  }
+  static float we[V * D], wa[4096];
+  flexflow_parameter_get_weights_float(flexflow_op_get_parameter_by_id(flexflow_model_get_layer_by_id(model, 0), 0),
+                                       model, we);
+  flexflow_parameter_get_weights_float(flexflow_op_get_parameter_by_id(flexflow_model_get_layer_by_id(model, 1), 0),
+                                       model, wa);
+  double se = 0.0, sa = 0.0, aa = 0.0;
+  for (int i = 0; i < V * D; ++i) se += we[i];
+  for (int i = 0; i < 4096; ++i) {
+    sa += wa[i];
+    aa += fabs(wa[i]);
+  }
+  printf("parity_bert device %s emb_sum %.9g attn_sum %.9g attn_abs %.9g attn_0 %.9g\n",
+         flexflow_model_get_device(model), se, sa, aa, wa[0]);
+  flexflow_adam_optimizer_destroy(adam);
+  flexflow_model_destroy(model);
+}
+
 static void test_configs(void) {
   char* argv[] = {"prog", "-b", "32", "--epochs", "3", "--arch-mlp-bot", "13-512-256-64", "--arch-embedding-size",
                   "1000-1000", "--arch-sparse-feature-size", "64", "--dataset", "/tmp/x.h5", "-ll:gpu", "8"};
@@ -337,6 +420,7 @@ int main(int argc, char** argv) {
   test_cnn(cfg);
   test_parity(cfg);
   test_parity_cnn(cfg);
+  test_parity_bert(cfg);
   flexflow_config_destroy(cfg);
   finish_flexflow_task();
   printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
