@@ -43,6 +43,7 @@ import gc
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -75,6 +76,9 @@ def main():
     ap.add_argument("--ae-deadline-s", type=float, default=float(os.environ.get("FF_AE_DEADLINE_S", "300")),
                     help="start the AE protocol only if the run so far took less than this many seconds (keeps the "
                          "whole command inside the driver's bench timeout)")
+    ap.add_argument("--deadline-s", type=float, default=float(os.environ.get("FF_BENCH_DEADLINE_S", "540")),
+                    help="N > 1: wall-clock budget of the whole command; work after the headline still running at "
+                         "this point is abandoned, the line printed with what finished")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32"],
                     help="compute dtype (float32: the exact-fp32 MFMA kernels; the headline metric is bf16)")
     ap.add_argument("--layers", type=int, default=None, help="override (debug only; invalidates the metric)")
@@ -117,16 +121,54 @@ def main():
                                                                   res["ms"], res["model"].ffconfig)
         except Exception as e:  # noqa: BLE001 -- never costs the headline
             res["config"]["comm_calibration"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-    ae = None
-    if world > 1 and not args.no_ae and args.model in ("bert-large", "bert-base"):
-        # every rank decides from rank 0's clock, so all of them take the same branch
-        spent = res["ex"].dist.max_scalar(time.time() - t_start)
-        if spent < args.ae_deadline_s:
-            ae = _run_ae(args, world, rank, res)
-        else:
-            ae = {"skipped": f"run took {spent:.0f} s before the protocol (deadline {args.ae_deadline_s:.0f} s)"}
-    speed = {}
+    # everything after the headline (the DP reference run, the AE protocol)
+    # runs under a watchdog: if it is still going at the deadline -- a slow
+    # search, or a hang in a strategy never run at this scale -- rank 0
+    # prints the line with what finished and every rank exits 0, so the
+    # headline measured above is never lost to the driver's timeout
+    extra = {"speed": {}, "ae": None}
+    emitted = threading.Lock()
+
+    def emit(note=None):
+        if not emitted.acquire(blocking=False):
+            return
+        if rank != 0:
+            return
+        conf = res["config"]
+        conf.update(extra["speed"])
+        ae = extra["ae"]
+        if note:
+            conf["after_headline"] = note
+        if ae is not None and ae.get("speedup_over_dp") is not None:
+            # the measured searched-vs-DP ratio of the reference's AE protocol
+            # (the headline's 64 sequences per GPU leave the search nothing to
+            # win over DP; at 1 sequence per GPU it picks tensor / head splits)
+            conf["ae_speedup_over_dp"] = ae["speedup_over_dp"]
+        if ae is not None:
+            conf["ae_bert"] = ae
+        print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(res["value"], 2),
+                          "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": args.dtype, "data": res["data"], "config": conf,
+                          "world_size": dist_world, "backend": backend}), flush=True)
+
+    done = threading.Event()
+    if world > 1:
+        left = args.deadline_s - (time.time() - t_start)
+
+        def watchdog():
+            if done.wait(max(1.0, left)):
+                return
+            if extra["ae"] is None and not args.no_ae and args.model in ("bert-large", "bert-base"):
+                extra["ae"] = {"error": f"not finished within the {args.deadline_s:.0f} s command deadline"}
+            emit(note=f"stopped at the {args.deadline_s:.0f} s deadline")
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
+
     if world > 1 and args.strategy == "search":
+        speed = extra["speed"]
         pred = res["search"].get("predicted_speedup_over_dp")
         if pred is not None:
             speed["predicted_speedup_over_dp"] = round(float(pred), 3)
@@ -140,21 +182,17 @@ def main():
             speed["dp_samples_per_sec"] = round(dp["value"], 2)
             speed["speedup_over_dp"] = round(sps / dp["value"], 3)
             speed["dp_reference"] = "measured: data-parallel run of the same model / batch after the timed run"
+            _release(dp)
+    if world > 1 and not args.no_ae and args.model in ("bert-large", "bert-base"):
+        # every rank decides from rank 0's clock, so all of them take the same branch
+        spent = _max_over_ranks(res, time.time() - t_start)
+        if spent < args.ae_deadline_s:
+            extra["ae"] = _run_ae(args, world, rank, res)
+        else:
+            extra["ae"] = {"skipped": f"run took {spent:.0f} s before the protocol (deadline {args.ae_deadline_s:.0f} s)"}
+    done.set()
+    emit()
     if rank == 0:
-        conf = res["config"]
-        conf.update(speed)
-        if ae is not None and ae.get("speedup_over_dp") is not None:
-            # the measured searched-vs-DP ratio of the reference's AE protocol
-            # (the headline's 64 sequences per GPU leave the search nothing to
-            # win over DP; at 1 sequence per GPU it picks tensor / head splits)
-            conf["ae_speedup_over_dp"] = ae["speedup_over_dp"]
-        if ae is not None:
-            conf["ae_bert"] = ae
-        print(json.dumps({"metric": "samples_per_sec_whole_node", "value": round(res["value"], 2),
-                          "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(res["ms"], 3), "higher_is_better": True, "scaling": "weak",
-                          "vs_baseline": None, "dtype": args.dtype, "data": res["data"], "config": conf,
-                          "world_size": dist_world, "backend": backend}), flush=True)
         if os.environ.get("FF_GEMM_REPORT"):
             from flexflow_train_amd.ops.dense import dact_report
             from flexflow_train_amd.ops.gemm import report
@@ -180,6 +218,19 @@ def _self_launch(n: int) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
     return subprocess.call(cmd, env=env)
+
+
+def _max_over_ranks(res, v: float) -> float:
+    """max of v over the ranks (the executor's process group; the DP run may
+    have released res["ex"])."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return v
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def _check_world(ex, want: int):

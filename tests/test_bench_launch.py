@@ -88,3 +88,19 @@ def test_bench_eight_ranks_reports_measured_speedups():
     assert "error" not in ae and "skipped" not in ae, ae
     assert ae["searched_samples_per_sec"] > 0 and ae["dp_samples_per_sec"] > 0
     assert c["ae_speedup_over_dp"] == ae["speedup_over_dp"] > 0
+
+
+def test_bench_deadline_keeps_the_headline():
+    """Work after the headline (the DP reference / AE protocol) still running
+    at --deadline-s is abandoned: rank 0 prints the line with what finished
+    and every rank exits 0 (a hang there never costs the measured number)."""
+    args = ["--model", "bert-base", "--layers", "2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2",
+            "--seq", "64", "--no-calibrate", "--deadline-s", "1"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args, env=_env(),
+                       capture_output=True, text=True, timeout=900, cwd="/tmp")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    c = lines[0]["config"]
+    assert lines[0]["value"] > 0 and "deadline" in c["after_headline"]
+    assert "error" in c["ae_bert"]
