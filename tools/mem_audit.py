@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Which tensors a training step really keeps (GPU): after one training
+forward, every distinct storage referenced by the executor's saved-for-
+backward tuples and its value environment, attributed to the step (PCG
+node) that produced it, summed by operator type; next to the liveness
+plan's activation blocks for the same PCG (csrc/ffcore/src/memory_plan.cc)
+and the allocator's live bytes.  Drives the plan's executor-fusion rules.
+
+    python tools/mem_audit.py resnet50 [batch]    |  bert-large [batch]
+"""
+import collections
+import json
+import sys
+
+import numpy as np
+import torch
+
+
+def _tensors(o, out):
+    if torch.is_tensor(o):
+        out.append(o)
+    elif isinstance(o, (list, tuple)):
+        for x in o:
+            _tensors(x, out)
+    elif isinstance(o, dict):
+        for x in o.values():
+            _tensors(x, out)
+
+
+def main():
+    from flexflow_train_amd import _ffcore as C
+    from flexflow_train_amd import models as Z
+    from flexflow_train_amd.core import (AdamOptimizer, FFConfig, FFModel, LossType, MetricsType, SGDOptimizer)
+    from flexflow_train_amd.search import native
+
+    name = sys.argv[1]
+    cfg = FFConfig()
+    m = FFModel(cfg)
+    if name.startswith("bert"):
+        from flexflow_train_amd.models.bert import bert_large, build_bert
+        b = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+        cfg.batch_size = b
+        bc = bert_large(batch_size=b, sequence_length=512)
+        build_bert(m, bc)
+        m.compile(optimizer=AdamOptimizer(m, alpha=1e-4), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY])
+        ex = m.executor
+        dev = ex.cfg.device
+        feeds = {}
+        for n in ex.inputs:
+            shp = ex.local_input_shape(n)
+            hi = bc.vocab_size if n == "input_ids" else (shp[-1] if n == "position_ids" else bc.type_vocab_size)
+            feeds[n] = torch.randint(0, hi, shp, device=dev, dtype=torch.int32)
+        labels = torch.randint(0, bc.vocab_size, ex._loss_layout().piece_shape[:-1], device=dev)
+        wbytes = 16.0
+    else:
+        b = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+        cfg.batch_size = b
+        inputs, out, mc = Z.build(name, m, batch_size=b, image_size=224, num_classes=1000)
+        m.compile(optimizer=SGDOptimizer(m, lr=0.01, momentum=0.9),
+                  loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY, metrics=[MetricsType.METRICS_ACCURACY])
+        ex = m.executor
+        fn, ln = Z.synthetic(name, mc, inputs, np.random.default_rng(0))
+        feeds = {k: ex._local_piece(k, torch.as_tensor(v)) for k, v in fn.items()}
+        labels = ex.local_labels(torch.as_tensor(ln))
+        wbytes = 12.0
+    ex.train_step(feeds, labels)          # autotune / workspaces settle
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    ex.forward(feeds, training=True)
+    torch.cuda.synchronize()
+    live = torch.cuda.memory_allocated() - base
+    seen = {}
+    by_saved = collections.Counter()
+    by_env = collections.Counter()
+    for i, s in enumerate(ex.steps):
+        ts = []
+        _tensors(ex._saved.get(i), ts)
+        for t in ts:
+            if not t.is_cuda:
+                continue
+            k = t.untyped_storage().data_ptr()
+            if k not in seen:
+                seen[k] = t.untyped_storage().nbytes()
+                by_saved[s.op_type] += seen[k]
+    for i, s in enumerate(ex.steps):
+        for o in s.outputs:
+            t = ex._env.get(o)
+            if torch.is_tensor(t) and t.is_cuda:
+                k = t.untyped_storage().data_ptr()
+                if k not in seen:
+                    seen[k] = t.untyped_storage().nbytes()
+                    by_env[s.op_type] += seen[k]
+    (p,) = native.plan_memory(m.pcg, 1, with_blocks=True, weight_bytes_per_param=wbytes)
+    steps = p["steps"]
+    fwd_end = steps // 2 - 1
+    plan = collections.Counter()
+    for blk in p["blocks"]:
+        if blk["kind"] == 0 and blk["start"] <= fwd_end <= blk["end"]:
+            plan[m.pcg.layer_op(blk["node"]).op_type] += blk["bytes"]
+    ops = sorted(set(by_saved) | set(by_env) | set(plan), key=lambda k: -(plan[k] + by_saved[k]))
+    rows = [{"op": k, "plan_gb": round(plan[k] / 1e9, 3), "saved_gb": round(by_saved[k] / 1e9, 3),
+             "env_only_gb": round(by_env[k] / 1e9, 3)} for k in ops]
+    print(json.dumps({"model": name, "batch": b, "allocator_live_after_forward_gb": round(live / 1e9, 3),
+                      "distinct_kept_gb": round(sum(seen.values()) / 1e9, 3),
+                      "plan_activations_at_forward_end_gb": round(sum(plan.values()) / 1e9, 3),
+                      "plan_arena_gb": round(p["arena_bytes"] / 1e9, 3),
+                      "measured_peak_gb": round(torch.cuda.max_memory_allocated() / 1e9, 3)}))
+    for r in rows:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
