@@ -270,7 +270,9 @@ def _memory_record(model, ex, world, bytes_per_param=16.0):
     import torch
     try:
         from flexflow_train_amd.search import native
-        plans = native.plan_memory(model.pcg, world, model.views, weight_bytes_per_param=bytes_per_param)
+        bf16 = getattr(ex.cfg, "compute_dtype", None) == torch.bfloat16
+        plans = native.plan_memory(model.pcg, world, model.views, weight_bytes_per_param=bytes_per_param,
+                                   act_elem_bytes=2.0 if bf16 else 0.0, executor_fusions=True)
         p = plans[min(ex.dist.rank, len(plans) - 1)]
         rec = {"planned_arena_gb": round(p["arena_bytes"] / 1e9, 2),
                "planned_peak_live_gb": round(p["peak_live_bytes"] / 1e9, 2),
@@ -278,7 +280,16 @@ def _memory_record(model, ex, world, bytes_per_param=16.0):
     except Exception as e:  # noqa: BLE001 -- the record must not cost the run
         rec = {"plan_error": f"{type(e).__name__}: {e}"[:160]}
     if ex.cfg.device.type == "cuda":
+        # whole run (includes the GEMM autotuner's candidate outputs in step 1)
         rec["measured_peak_gb"] = round(torch.cuda.max_memory_allocated(ex.cfg.device) / 1e9, 2)
+        if getattr(ex, "_ff_step_peak", None) is not None:
+            # one steady-state eager step after the autotuner settled: what
+            # the step itself holds at its peak (the plan's subject)
+            rec["measured_step_peak_gb"] = round(ex._ff_step_peak / 1e9, 2)
+            planned = rec.get("planned_arena_gb")
+            if planned:
+                rec["plan_error_pct"] = round(100.0 * (planned - rec["measured_step_peak_gb"])
+                                              / rec["measured_step_peak_gb"], 1)
     return rec
 
 
@@ -310,6 +321,15 @@ def _time_steps(args, ex, feeds, labels, global_batch):
     def step():
         ex.train_step(feeds, labels)
 
+    if dev.type == "cuda" and not args.profile:
+        # the step's own memory peak: one eager step to settle the autotuner
+        # and the workspaces, then one measured from a reset peak counter
+        ex.train_step(feeds, labels)
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(dev)
+        ex.train_step(feeds, labels)
+        torch.cuda.synchronize()
+        ex._ff_step_peak = torch.cuda.max_memory_allocated(dev)
     graphed = False
     use_graph = args.graph if args.graph >= 0 else 1
     if use_graph and dev.type == "cuda" and not args.profile:

@@ -319,18 +319,21 @@ void register_ext_bindings(py::module_& m) {
   // ---- liveness memory plan (ff/memory_plan.h): JSON list, one per device
   m.def("plan_memory", [](const ParallelComputationGraph& p, const std::map<int, std::vector<int>>& views, int world,
                           bool training, double weight_bytes_per_param, bool with_blocks,
-                          const std::map<int, double>& live_copies) {
+                          const std::map<int, double>& live_copies, double act_elem_bytes, bool executor_fusions) {
     MemoryPlanConfig c;
     c.training = training;
     c.weight_bytes_per_param = weight_bytes_per_param;
     c.live_copies = live_copies;
+    c.act_elem_bytes = act_elem_bytes;
+    c.executor_fusions = executor_fusions;
     Json a = Json::array();
     for (auto const& pl : plan_memory(p, std::map<int, Placement>(views.begin(), views.end()), world, c))
       a.push_back(pl.to_json(with_blocks));
     return a.dump();
   }, py::arg("pcg"), py::arg("views") = std::map<int, std::vector<int>>{}, py::arg("world") = 1,
         py::arg("training") = true, py::arg("weight_bytes_per_param") = 16.0, py::arg("with_blocks") = false,
-        py::arg("live_copies") = std::map<int, double>{});
+        py::arg("live_copies") = std::map<int, double>{}, py::arg("act_elem_bytes") = 0.0,
+        py::arg("executor_fusions") = false);
 
   // ---- simulator
   m.def("simulate", [](const ParallelComputationGraph& p, const CostModel& cm, const std::string& sim_cfg,

@@ -54,6 +54,20 @@ struct MemoryPlanConfig {
   // pipeline stage keeps the saved activations of several micro-batches
   // (1F1B: min(m, S - s) on stage s, GPipe: m)
   std::map<int, double> live_copies;
+  // bytes per activation / activation-gradient element as the executor
+  // stores them (2: bf16 compute); 0 = the PCG tensor's own dtype
+  double act_elem_bytes = 0.0;
+  // the executor's fusions and saved tensors (runtime/executor.py, the op
+  // implementations), measured by tools/mem_audit.py
+  // (profiles/r6/g04_mem_audit_*.jsonl):
+  //  * BATCHNORM (no ReLU) -> EW_ADD -> RELU runs as one kernel: the BN and
+  //    add outputs (and their gradients) never exist;
+  //  * the final SOFTMAX is fused with the loss: no softmax output, and the
+  //    logits' gradient overwrites the logits (no separate block);
+  //  * LINEAR with an activation keeps its pre-activation too (x2);
+  //  * MULTIHEAD_ATTENTION keeps the q / k / v projections and the
+  //    attention output (flash attention: no score matrix) beside its output
+  bool executor_fusions = false;
 };
 
 // one plan per device 0 .. world-1

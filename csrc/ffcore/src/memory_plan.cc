@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <set>
 
 #include "ff/simulator.h"
 
@@ -93,6 +94,10 @@ void pack(MemoryPlan& m, double align) {
   m.arena_bytes = arena;
 }
 
+TensorShape node_output_piece(const ParallelComputationGraph& pcg, int n) {
+  return pcg.g.node(n).outputs.at(0).shape.piece_shape();
+}
+
 }  // namespace
 
 std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const std::map<int, Placement>& views,
@@ -115,6 +120,54 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
   std::map<int, std::vector<int>> consumers;
   for (int id : order)
     for (auto const& v : pcg.g.node(id).inputs) consumers[v.node].push_back(id);
+
+  // executor fusions (MemoryPlanConfig::executor_fusions): nodes whose
+  // outputs are never materialised, nodes whose gradient overwrites their
+  // output, and per-node multipliers of the kept activation
+  std::set<int> no_act, no_grad;
+  std::map<int, double> act_scale;
+  if (cfg.executor_fusions) {
+    auto type_of = [&](int n) { return pcg.g.node(n).label.op.type; };
+    auto sole = [&](int n) -> int {
+      auto it = consumers.find(n);
+      return it != consumers.end() && it->second.size() == 1 ? it->second[0] : -1;
+    };
+    for (int n : order) {
+      if (roles.at(n) != NodeRole::COMPUTE) continue;
+      const auto& op = pcg.g.node(n).label.op;
+      const OpType t = op.type;
+      if (t == OpType::BATCHNORM && !(op.has("relu") && op.b("relu"))) {
+        const int add = sole(n);
+        if (add >= 0 && type_of(add) == OpType::EW_ADD && !no_act.count(add)) {
+          const int relu = sole(add);
+          if (relu >= 0 && type_of(relu) == OpType::RELU) {
+            no_act.insert(n);
+            no_act.insert(add);
+          }
+        }
+      } else if (t == OpType::SOFTMAX && !consumers.count(n)) {
+        no_act.insert(n);
+        for (auto const& v : pcg.layer_data_inputs(n)) no_grad.insert(v.node);
+      } else if (t == OpType::LINEAR) {
+        const std::string a = op.has("activation") ? op.s("activation") : "none";
+        if (!a.empty() && a != "none") act_scale[n] = 2.0;
+      } else if (t == OpType::MULTIHEAD_ATTENTION) {
+        auto ins = pcg.layer_data_inputs(n);
+        if (ins.size() == 3) {
+          const auto q = pcg.shape(ins[0]).piece_shape(), k = pcg.shape(ins[1]).piece_shape();
+          const auto o = node_output_piece(pcg, n);
+          const int64_t E = op.i("embed_dim"), H = std::max<int64_t>(1, op.i("num_heads"));
+          const int64_t kd = op.i("kdim") > 0 ? op.i("kdim") : E / H, vd = op.i("vdim") > 0 ? op.i("vdim") : E / H;
+          const double Sq = static_cast<double>(q.num_elements()) / std::max<int64_t>(1, q.dims.back());
+          const double Sk = static_cast<double>(k.num_elements()) / std::max<int64_t>(1, k.dims.back());
+          const double hd = static_cast<double>(H) / std::max(1, pcg.shape(ins[0]).discard_copy_degree);
+          const double extra = hd * (Sq * kd + Sk * kd + Sk * vd + Sq * vd);
+          const double out = static_cast<double>(o.num_elements());
+          if (out > 0) act_scale[n] = 1.0 + extra / out;
+        }
+      }
+    }
+  }
 
   for (auto& p : plans) p.steps = steps;
   for (int n : order) {
@@ -154,23 +207,27 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
     const bool grad = cfg.training && role != NodeRole::INPUT_PATH && has_consumer;
     auto lc = cfg.live_copies.find(n);
     const double copies = lc == cfg.live_copies.end() ? 1.0 : std::max(1.0, lc->second);
+    if (no_act.count(n)) continue;
+    const double scale = act_scale.count(n) ? act_scale.at(n) : 1.0;
     for (size_t o = 0; o < node.outputs.size(); ++o) {
       const auto& s = node.outputs[o].shape;
-      const double bytes = static_cast<double>(s.piece_shape().size_bytes());
+      const double bytes = cfg.act_elem_bytes > 0
+                               ? static_cast<double>(s.piece_shape().num_elements()) * cfg.act_elem_bytes
+                               : static_cast<double>(s.piece_shape().size_bytes());
       for (auto const& h : holders(place(n), total_pieces(s))) {
         if (h.first < 0 || h.first >= world) continue;
         MemBlock a;
         a.node = n;
         a.output = static_cast<int>(o);
         a.kind = 0;
-        a.bytes = bytes * h.second * copies;
+        a.bytes = bytes * h.second * copies * scale;
         a.start = fwd.at(n);
         // inputs fed to the graph are read by their consumers' backward
         // (weight gradients); every other activation until its producer's
         a.end = !cfg.training ? last_fwd : role == NodeRole::INPUT_PATH ? std::max(last_fwd, steps - 1 - fwd.at(n))
                                                                         : bwd(n);
         plans[h.first].blocks.push_back(a);
-        if (grad) {
+        if (grad && !no_grad.count(n)) {
           MemBlock g = a;
           g.kind = 1;
           g.bytes = bytes * h.second;   // one micro-batch's gradient at a time

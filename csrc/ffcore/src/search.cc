@@ -478,13 +478,23 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
       for (auto const& p : ps) a = std::max(a, p.arena_bytes);
       return a;
     };
+    // the executor's storage: bf16 activations / gradients when the cost
+    // model prices bf16 compute, its fusions and saved tensors
+    MemoryPlanConfig base_mc;
+    base_mc.executor_fusions = cfg.sim.executor_fusions;
+    base_mc.act_elem_bytes = cfg.sim.bf16_weight_grads ? 2.0 : 0.0;
+    auto with_base = [&](MemoryPlanConfig c) {
+      c.executor_fusions = base_mc.executor_fusions;
+      c.act_elem_bytes = base_mc.act_elem_bytes;
+      return c;
+    };
     // a pipeline winner keeps several micro-batches of activations per stage
-    MemoryPlanConfig best_mc;
+    MemoryPlanConfig best_mc = base_mc;
     if (best.pipeline_stages > 1) {
       SimConfig psim = cfg.sim;
       psim.world = cfg.world;
       for (auto& pl : pipeline_candidates(cg, cm, cfg.world, std::max(1, cfg.micro_batches), psim))
-        if (pl.stages == best.pipeline_stages) best_mc = pipeline_memory_config(pl);
+        if (pl.stages == best.pipeline_stages) best_mc = with_base(pipeline_memory_config(pl));
     }
     auto plans = plan_memory(best.pcg, best.views, cfg.world, best_mc);
     const double cap = cm.spec().hbm_capacity;
@@ -495,7 +505,7 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
       Simulator S(cm, sim);
       double best_t = std::numeric_limits<double>::infinity();
       auto dp = data_parallel_pcg(cg, cfg.world);
-      auto dplans = plan_memory(dp, {}, cfg.world);
+      auto dplans = plan_memory(dp, {}, cfg.world, base_mc);
       bool found = false;
       ParallelComputationGraph fb_pcg;
       std::map<int, Placement> fb_views;
@@ -510,7 +520,7 @@ SearchResult graph_optimize(const ComputationGraph& cg, const CostModel& cm, con
         found = true;
       }
       for (auto& pl : pipeline_candidates(cg, cm, cfg.world, M, sim)) {
-        auto pp = plan_memory(pl.pcg, pl.views, cfg.world, pipeline_memory_config(pl));
+        auto pp = plan_memory(pl.pcg, pl.views, cfg.world, with_base(pipeline_memory_config(pl)));
         if (busiest(pp) <= cap && pl.step_time < best_t) {
           best_t = pl.step_time;
           fb_pcg = pl.pcg;

@@ -94,15 +94,20 @@ def sim_config(ffconfig=None, world: int = 1) -> dict:
 
 def plan_memory(pcg, world: int = 1, views: Optional[Dict[int, Sequence[int]]] = None, training: bool = True,
                 weight_bytes_per_param: float = 16.0, with_blocks: bool = False,
-                live_copies: Optional[Dict[int, float]] = None):
+                live_copies: Optional[Dict[int, float]] = None, act_elem_bytes: float = 0.0,
+                executor_fusions: bool = False):
     """Liveness-based memory plan of one step per device
     (csrc/ffcore/src/memory_plan.cc): [{device, weight_bytes,
     peak_live_bytes, arena_bytes, naive_bytes, [blocks]}].  ``live_copies``:
     PCG node -> micro-batches of its activations held live at once (a
-    pipeline stage under 1F1B keeps min(m, S - s))."""
+    pipeline stage under 1F1B keeps min(m, S - s)).  ``act_elem_bytes``:
+    bytes per activation element as stored (2 for bf16 compute; 0 = the PCG
+    dtype); ``executor_fusions``: model the executor's fused / saved tensors
+    (memory_plan.h)."""
     return json.loads(C.plan_memory(pcg, {int(k): [int(d) for d in v] for k, v in (views or {}).items()}, int(world),
                                     bool(training), float(weight_bytes_per_param), bool(with_blocks),
-                                    {int(k): float(v) for k, v in (live_copies or {}).items()}))
+                                    {int(k): float(v) for k, v in (live_copies or {}).items()},
+                                    float(act_elem_bytes), bool(executor_fusions)))
 
 
 def simulate(pcg, cm, world: int, views: Optional[Dict[int, Sequence[int]]] = None, dot: bool = False,

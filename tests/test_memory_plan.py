@@ -104,3 +104,40 @@ def test_live_copies_scale_activations_not_gradients():
     g3 = sum(b["bytes"] for b in three["blocks"] if b["kind"] == 1)
     assert g1 == g3
     assert three["peak_live_bytes"] > one["peak_live_bytes"]
+
+
+def test_executor_fusion_rules():
+    """executor_fusions + bf16 storage (memory_plan.h): the residual tail
+    BN -> add -> ReLU keeps only the ReLU output, the loss-fused final
+    softmax keeps nothing (the logits' gradient overwrites the logits), a
+    Linear with an activation keeps its pre-activation too, and attention
+    keeps its q / k / v projections and output beside its result -- the
+    rules tools/mem_audit.py measured on the GPU executor."""
+    from flexflow_train_amd import models as Z
+    m = FFModel(FFConfig())
+    Z.build("resnet50", m, batch_size=2, image_size=64, num_classes=10)
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    (p0,) = native.plan_memory(pcg, 1, with_blocks=True)
+    (p1,) = native.plan_memory(pcg, 1, with_blocks=True, act_elem_bytes=2.0, executor_fusions=True)
+    kinds = lambda p, t: {b["kind"] for b in p["blocks"] if pcg.layer_op(b["node"]).op_type == t}
+    assert 0 in kinds(p0, "EW_ADD") and 0 not in kinds(p1, "EW_ADD")
+    assert 0 not in kinds(p1, "SOFTMAX")
+    act = lambda p: sum(b["bytes"] for b in p["blocks"] if b["kind"] == 0)
+    assert act(p1) < 0.5 * act(p0)          # half the bytes per element, and the fused tails gone
+
+    from flexflow_train_amd.models.bert import bert_large, build_bert
+    m = FFModel(FFConfig())
+    build_bert(m, bert_large(batch_size=2, sequence_length=128, num_encoder_layers=1))
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    (p0,) = native.plan_memory(pcg, 1, with_blocks=True, act_elem_bytes=2.0)
+    (p1,) = native.plan_memory(pcg, 1, with_blocks=True, act_elem_bytes=2.0, executor_fusions=True)
+    def act_of(p, t):
+        return sum(b["bytes"] for b in p["blocks"] if b["kind"] == 0 and pcg.layer_op(b["node"]).op_type == t)
+    # self-attention, kdim = vdim = E / H: q, k, v and the attention output = 4x the result
+    assert abs(act_of(p1, "MULTIHEAD_ATTENTION") - 5 * act_of(p0, "MULTIHEAD_ATTENTION")) < 1e-6 * act_of(p1, "MULTIHEAD_ATTENTION")
+    assert act_of(p1, "LINEAR") > act_of(p0, "LINEAR")      # GELU layers keep the pre-activation
+    # the head's logits: no gradient block (the fused softmax + CE writes it in place)
+    head = [n for n in pcg.topo_order() if pcg.layer_op(n).op_type == "SOFTMAX"][0]
+    logits = pcg.layer_data_inputs(head)[0].node
+    assert [b for b in p0["blocks"] if b["node"] == logits and b["kind"] == 1]
+    assert not [b for b in p1["blocks"] if b["node"] == logits and b["kind"] == 1]
