@@ -39,6 +39,7 @@ enum Kind : int {
   kBroadcast = 5,
   kWait = 6,
   kAllToAll = 7,        // out = all_to_all_single(in, out / in split sizes)
+  kSendRecv = 8,        // matched point-to-point pairs (a pipeline-stage boundary), one coalesced group
 };
 
 struct Item {
@@ -50,6 +51,8 @@ struct Item {
   int root = 0;       // group-local root rank (reduce / broadcast)
   int slot = -1;      // async work slot (-1: synchronous), or the slot waited on
   std::vector<int64_t> out_splits, in_splits;   // all-to-all (empty: equal splits)
+  std::vector<int> send_peers, recv_peers;      // send / recv: group ranks
+  std::vector<at::Tensor> sends, recvs;
 };
 
 class Replayer {
@@ -75,6 +78,22 @@ class Replayer {
     it.slot = slot;
     it.out_splits = std::move(out_splits);
     it.in_splits = std::move(in_splits);
+    items_.push_back(std::move(it));
+  }
+  void add_send_recv(const c10::intrusive_ptr<c10d::ProcessGroup>& pg, std::vector<int> send_peers,
+                     std::vector<at::Tensor> sends, std::vector<int> recv_peers, std::vector<at::Tensor> recvs,
+                     int slot) {
+    if (!pg) throw std::invalid_argument("replay: null process group");
+    if (send_peers.size() != sends.size() || recv_peers.size() != recvs.size() || (sends.empty() && recvs.empty()))
+      throw std::invalid_argument("replay: send / recv lists do not match");
+    Item it;
+    it.kind = kSendRecv;
+    it.pg = pg;
+    it.send_peers = std::move(send_peers);
+    it.sends = std::move(sends);
+    it.recv_peers = std::move(recv_peers);
+    it.recvs = std::move(recvs);
+    it.slot = slot;
     items_.push_back(std::move(it));
   }
   void add_wait(int slot) {
@@ -118,6 +137,26 @@ class Replayer {
 
  private:
   static c10::intrusive_ptr<c10d::Work> issue(Item& it) {
+    if (it.kind == kSendRecv) {
+      // RCCL: one coalesced group (ncclGroupStart / End), as
+      // torch.distributed.batch_isend_irecv issues it; other backends (gloo
+      // rehearsals) post every op and wait them all
+      const bool cuda = !it.sends.empty() ? it.sends[0].is_cuda() : (!it.recvs.empty() && it.recvs[0].is_cuda());
+      const bool coalesce = cuda && it.pg->getBackendName() == "nccl";
+      if (coalesce) it.pg->startCoalescing(c10::DeviceType::CUDA);
+      std::vector<c10::intrusive_ptr<c10d::Work>> ws;
+      for (size_t i = 0; i < it.sends.size(); ++i) {
+        std::vector<at::Tensor> v{it.sends[i]};
+        ws.push_back(it.pg->send(v, it.send_peers[i], 0));
+      }
+      for (size_t i = 0; i < it.recvs.size(); ++i) {
+        std::vector<at::Tensor> v{it.recvs[i]};
+        ws.push_back(it.pg->recv(v, it.recv_peers[i], 0));
+      }
+      if (coalesce) return it.pg->endCoalescing(c10::DeviceType::CUDA);
+      for (size_t i = 0; i + 1 < ws.size(); ++i) ws[i]->wait();
+      return ws.back();
+    }
     switch (it.kind) {
       case kAllReduce: {
         std::vector<at::Tensor> v{it.a};
@@ -168,6 +207,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("add_collective", &Replayer::add_collective, py::arg("kind"), py::arg("pg"), py::arg("a"), py::arg("b"),
            py::arg("root"), py::arg("slot"), py::arg("out_splits") = std::vector<int64_t>{},
            py::arg("in_splits") = std::vector<int64_t>{})
+      .def("add_send_recv", &Replayer::add_send_recv, py::arg("pg"), py::arg("send_peers"), py::arg("sends"),
+           py::arg("recv_peers"), py::arg("recvs"), py::arg("slot"))
       .def("add_wait", &Replayer::add_wait)
       .def("replay", &Replayer::replay)
       .def("__len__", &Replayer::size)
@@ -178,4 +219,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("REDUCE") = static_cast<int>(kReduce);
   m.attr("BROADCAST") = static_cast<int>(kBroadcast);
   m.attr("ALL_TO_ALL") = static_cast<int>(kAllToAll);
+  m.attr("SEND_RECV") = static_cast<int>(kSendRecv);
 }

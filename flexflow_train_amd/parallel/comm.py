@@ -18,6 +18,8 @@ to the cheapest primitive that implements it:
     (resharding to a different dim, DLRM table-sharded -> batch-sharded
     embeddings, different machine views); each (receiver, sender) pair moves
     at most one box, zero-size splits for pairs that exchange nothing;
+  * matched send / recv pairs — a pipeline-stage boundary (each receiver
+    fed by one rank of the previous stage, no rank on both sides);
   * batched point-to-point (isend/irecv of the intersecting boxes) — the
     fallback (``FF_REDIST_P2P=1``).
 
@@ -364,6 +366,19 @@ def make_plan(src: Layout, dst: Layout, world: int) -> Plan:
     involved = tuple(sorted({r for r, _ in pairs if any(c.src_rank != r for c in contributions[r])} |
                             {m for r, m in pairs if m != r}))
     sub = [involved] if 1 < len(involved) < world else []
+    # a pipeline-stage boundary: every receiver takes its box from at most one
+    # other rank, every sender feeds at most one, and no rank does both ->
+    # matched send / recv pairs (one xGMI link each), not an all_to_all that
+    # rendezvouses both stages' ranks
+    remote = [(r, m) for r, m in pairs if r != m]
+    senders = [m for _, m in remote]
+    receivers = [r for r, _ in remote]
+    if (remote and len(set(senders)) == len(senders) and len(set(receivers)) == len(receivers)
+            and not set(senders) & set(receivers) and os.environ.get("FF_REDIST_SENDRECV", "1") == "1"
+            and os.environ.get("FF_REDIST_P2P", "0") != "1"):
+        # (the sub-group serves the all_to_all form of the same exchange: gloo
+        # moves device tensors only through collectives)
+        return Plan("send_recv", contributions, dst_boxes, src_boxes, sub)
     if len(pairs) == len(set(pairs)) and os.environ.get("FF_REDIST_P2P", "0") != "1":
         return Plan("all_to_all", contributions, dst_boxes, src_boxes, sub)
     return Plan("p2p", contributions, dst_boxes, src_boxes, [])
@@ -491,6 +506,8 @@ def execute_plan(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_sh
         return sel.movedim(0, d).reshape(tuple(xs.shape[:d]) + (len(keep) * xs.shape[d],) + tuple(xs.shape[d + 1:]))
     if plan.kind == "all_to_all":
         return _exchange_all_to_all(plan, x, ctx, dst_shape, dtype, device)
+    if plan.kind == "send_recv":
+        return _exchange_send_recv(plan, x, ctx, dst_shape, dtype, device)
     # ---- generic point-to-point
     ctx.stats["p2p"] += 1
     ops = []
@@ -579,6 +596,48 @@ def _exchange_all_to_all(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext
         n = out_sizes[m]
         result[rel_slices(c.part, my_dst)] += recvbuf[off:off + n].view([h - l for l, h in c.part]).to(dtype)
         off += n
+    return result
+
+
+def _exchange_send_recv(plan: Plan, x: Optional[torch.Tensor], ctx: DistContext, dst_shape: Sequence[int],
+                        dtype: torch.dtype, device: torch.device) -> Optional[torch.Tensor]:
+    """Matched point-to-point pairs (a pipeline-stage boundary): each sender
+    isends its one piece, each receiver irecvs its one piece, batched into one
+    coalesced group; ranks outside the pairs only copy their own pieces."""
+    if device.type == "cuda" and ctx.backend != "nccl":
+        # gloo point-to-point takes host tensors only: the same boxes through
+        # the (sub-group) all_to_all
+        return _exchange_all_to_all(plan, x, ctx, dst_shape, dtype, device)
+    me = ctx.rank
+    my_dst, my_src = plan.dst_boxes.get(me), plan.src_boxes.get(me)
+    ctx.stats["send_recv"] = ctx.stats.get("send_recv", 0) + 1
+    sends, recvs = [], []
+    for r, cl in plan.contributions.items():
+        for c in cl:
+            if c.src_rank == me and r != me:
+                sends.append((r, x[rel_slices(c.part, my_src)].contiguous()))
+    result = None
+    if my_dst is not None:
+        result = torch.zeros(dst_shape, dtype=dtype, device=device)
+        for c in plan.contributions[me]:
+            if c.src_rank == me:
+                result[rel_slices(c.part, my_dst)] += x[rel_slices(c.part, my_src)].to(dtype)
+            else:
+                buf = torch.empty([h - l for l, h in c.part], dtype=dtype, device=device)
+                recvs.append((c.src_rank, buf, c))
+    if sends or recvs:
+        for _, t in sends:
+            ctx.note_size("send_recv", t.numel() * t.element_size())
+        ops = [dist.P2POp(dist.isend, t, peer) for peer, t in sends] + \
+              [dist.P2POp(dist.irecv, b, peer) for peer, b, _ in recvs]
+
+        def _pairs():
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        ctx._issue(_pairs, False, ("send_recv", [(p, t) for p, t in sends], [(p, b) for p, b, _ in recvs],
+                                    ctx._pg(None), 0))
+    for _, buf, c in recvs:
+        result[rel_slices(c.part, my_dst)] += buf
     return result
 
 

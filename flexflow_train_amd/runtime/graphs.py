@@ -158,6 +158,20 @@ class SegmentRecorder:
                 rp.add_graph(it[1])
             elif it[0] == "coll":
                 desc = it[3]
+                if desc is not None and desc[0] == "send_recv":
+                    # replay.cpp kSendRecv (ncclGroupStart/End through c10d
+                    # coalescing) is opt-in until it has run on more than one
+                    # GPU; by default the step keeps torch's batch_isend_irecv
+                    if os.environ.get("FF_NATIVE_SENDRECV", "0") != "1":
+                        return False
+                    _, sends, recvs, pg = desc[:4]
+                    try:
+                        rp.add_send_recv(pg, [int(p) for p, _ in sends], [t for _, t in sends],
+                                         [int(p) for p, _ in recvs], [t for _, t in recvs],
+                                         -1 if it[2] is None else int(it[2]))
+                    except (TypeError, AttributeError):
+                        return False
+                    continue
                 if desc is None or desc[0] not in NATIVE_KINDS:
                     return False
                 kind, a, b, pg, root = desc[:5]

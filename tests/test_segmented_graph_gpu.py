@@ -67,7 +67,8 @@ def _worker(rank, world, port, model_name, strategy, out_path):
         step()
     last = b.perf_metrics().loss
     if rank == 0:
-        torch.save({"a": pa, "b": pb, "segments": list(b.graph_segments), "first": first, "last": last}, out_path)
+        torch.save({"a": pa, "b": pb, "segments": list(b.graph_segments), "first": first, "last": last,
+                    "native": bool(getattr(b, "native_replay", False)), "stats": dict(b.dist.stats)}, out_path)
     import torch.distributed as dist
 
     dist.barrier()
@@ -101,3 +102,34 @@ def test_segmented_graph_tensor_parallel(tmp_path):
     write_strategy(M.mlp, 2, {"fc0": {"batch": 1, "model": 2, "kind": "column"},
                               "fc1": {"batch": 1, "model": 2, "kind": "row"}}, path)
     _check(_run("mlp", path))
+
+
+def test_segmented_graph_stage_boundary(tmp_path):
+    """Two placement stages (fc0 on rank 0, the rest on rank 1): the stage
+    boundary is a matched send / recv plan (comm.py), captured as a
+    collective item of the segmented graph and replayed natively; the
+    replayed step equals eager steps.  Two gloo ranks share the one GPU here,
+    and gloo moves device tensors only through collectives, so the pair runs
+    as the sub-group all_to_all form (RCCL ranks send / recv)."""
+    import json as _json
+
+    from flexflow_train_amd import _ffcore as C
+    from flexflow_train_amd.core import FFConfig, FFModel
+    from flexflow_train_amd.search.strategy import export_strategy
+
+    m = FFModel(FFConfig())
+    M.mlp(m)
+    s = _json.loads(C.data_parallel_strategy(m.cg, 2))
+    for k in s:
+        s[k]["batch"] = 1
+    pcg = C.lower_strategy(m.cg, _json.dumps(s), 2)[0]
+    views = {}
+    for n in pcg.topo_order():
+        name = pcg.layer_name(n).split(".")[0]
+        views[n] = (0,) if name in ("x", "fc0") else (1,)
+    path = str(tmp_path / "stages.json")
+    export_strategy(path, pcg, views, {"world": 2, "source": "test"})
+    res = _run("mlp", path)
+    _check(res)
+    assert res["stats"].get("all_to_all", 0) + res["stats"].get("send_recv", 0) > 0, res["stats"]
+    assert res["native"], "the segmented step was not replayed natively"
