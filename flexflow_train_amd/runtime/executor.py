@@ -1618,7 +1618,7 @@ class Executor:
         self.update(lr)
         self._after_first_update()
 
-    def make_graphed_train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, warmup: int = 2):
+    def make_graphed_train_step(self, feeds, labels, warmup: int = 2, schedule: str = "1f1b"):
         """Capture one whole training iteration (forward, loss, backward with
         the bucketed RCCL gradient all-reduces, fused optimizer update) into a
         hipGraph and return ``step(feeds=None, labels=None)`` that replays it.
@@ -1627,25 +1627,51 @@ class Executor:
         ``step`` to copy them in).  Adam's learning rate and step counter are
         kept on the device, so replays are exact; the GEMM autotuner settles
         during ``warmup`` (eager) before capture.  This replaces the
-        reference's Legion tracing (begin_trace/end_trace around the loop)."""
+        reference's Legion tracing (begin_trace/end_trace around the loop).
+
+        ``feeds`` / ``labels`` as LISTS (one entry per micro-batch) capture the
+        pipelined step instead (``train_step_pipelined`` with ``schedule``):
+        every micro-batch's forward / backward, the stage-boundary transfers
+        (graph segments cut at each), one synchronisation + update."""
         if self.cfg.device.type != "cuda":
             raise RuntimeError("graph capture needs a GPU")
         if self.cfg.grad_clip > 0:
             raise RuntimeError("gradient clipping syncs with the host; disable it for graph capture")
-        static_feeds = {}
-        for k, v in feeds.items():
-            piece = self._local_piece(k, v)
-            static_feeds[k] = piece.clone() if piece is not None else None
-        static_feeds = {k: v for k, v in static_feeds.items() if v is not None}
-        y = self.local_labels(labels)
-        static_labels = y.clone() if y is not None else None
+        micro = isinstance(feeds, (list, tuple))
+
+        def static_piece_feeds(fd):
+            out = {}
+            for k, v in fd.items():
+                piece = self._local_piece(k, v)
+                if piece is not None:
+                    out[k] = piece.clone()
+            return out
+
+        def static_piece_labels(lb):
+            y = self.local_labels(lb)
+            return y.clone() if y is not None else None
+
+        if micro:
+            if len(feeds) != len(labels) or not feeds:
+                raise ValueError("make_graphed_train_step: one label tensor per micro-batch")
+            static_feeds = [static_piece_feeds(fd) for fd in feeds]
+            static_labels = [static_piece_labels(lb) for lb in labels]
+
+            def run():
+                self.train_step_pipelined(static_feeds, static_labels, schedule=schedule)
+        else:
+            static_feeds = static_piece_feeds(feeds)
+            static_labels = static_piece_labels(labels)
+
+            def run():
+                self.train_step(static_feeds, static_labels)
         for f in self.flats:
             f["opt"].enable_device_hparams()
         side = torch.cuda.Stream(device=self.cfg.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
-                self.train_step(static_feeds, static_labels)
+                run()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize(self.cfg.device)
         # no garbage collection inside the capture: a collected cycle that owns
@@ -1656,25 +1682,33 @@ class Executor:
             if self.dist.distributed:
                 # across ranks: one graph segment between consecutive collectives
                 # (runtime/graphs.py); the RCCL calls are re-issued at replay
-                graph = self._capture_segments(side, static_feeds, static_labels)
+                graph = self._capture_segments(side, run)
                 replay = graph.replay
             else:
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    self.train_step(static_feeds, static_labels)
+                    run()
                 replay = graph.replay
         finally:
             if gc_was_on:
                 gc.enable()
         self._graph = graph
 
-        def step(new_feeds: Optional[Dict[str, torch.Tensor]] = None, new_labels: Optional[torch.Tensor] = None):
+        def copy_in(dst_feeds, dst_labels, new_feeds, new_labels):
             if new_feeds:
                 for k, v in new_feeds.items():
-                    if k in static_feeds:
-                        static_feeds[k].copy_(self._local_piece(k, v), non_blocking=True)
-            if new_labels is not None and static_labels is not None:
-                static_labels.copy_(self.local_labels(new_labels), non_blocking=True)
+                    if k in dst_feeds:
+                        dst_feeds[k].copy_(self._local_piece(k, v), non_blocking=True)
+            if new_labels is not None and dst_labels is not None:
+                dst_labels.copy_(self.local_labels(new_labels), non_blocking=True)
+
+        def step(new_feeds=None, new_labels=None):
+            if micro:
+                for i in range(len(static_feeds)):
+                    copy_in(static_feeds[i], static_labels[i], new_feeds[i] if new_feeds else None,
+                            new_labels[i] if new_labels is not None else None)
+            else:
+                copy_in(static_feeds, static_labels, new_feeds, new_labels)
             replay()
             self.step_num += 1
             for f in self.flats:
@@ -1682,7 +1716,7 @@ class Executor:
 
         return step
 
-    def _capture_segments(self, side, static_feeds, static_labels):
+    def _capture_segments(self, side, run):
         """Capture one training step as hipGraph segments cut at every
         collective (runtime/graphs.SegmentRecorder).  Raises NotCapturable
         (after leaving capture mode cleanly) when the step reaches a
@@ -1693,7 +1727,7 @@ class Executor:
         try:
             with torch.cuda.stream(side):
                 rec.begin()
-                self.train_step(static_feeds, static_labels)
+                run()
                 rec.end()
         except BaseException:
             rec.abort()

@@ -36,7 +36,19 @@ def main():
     name = sys.argv[1]
     cfg = FFConfig()
     m = FFModel(cfg)
-    if name.startswith("bert"):
+    if name.startswith("gpt"):
+        b = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+        cfg.batch_size = b
+        inputs, out, mc = Z.build("gpt", m, batch_size=b, hidden_size=1024, num_layers=24, num_heads=16,
+                                  sequence_length=2048)
+        m.compile(optimizer=AdamOptimizer(m, alpha=1e-4), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_ACCURACY])
+        ex = m.executor
+        fn, ln = Z.synthetic("gpt", mc, inputs, np.random.default_rng(0))
+        feeds = {k: ex._local_piece(k, torch.as_tensor(v)) for k, v in fn.items()}
+        labels = ex.local_labels(torch.as_tensor(ln))
+        wbytes = 16.0
+    elif name.startswith("bert"):
         from flexflow_train_amd.models.bert import bert_large, build_bert
         b = int(sys.argv[2]) if len(sys.argv) > 2 else 64
         cfg.batch_size = b
@@ -67,6 +79,13 @@ def main():
     ex.train_step(feeds, labels)          # autotune / workspaces settle
     torch.cuda.synchronize()
     base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    ex.train_step(feeds, labels)
+    torch.cuda.synchronize()
+    step_peak = torch.cuda.max_memory_allocated()
+    # the persistent part: weights, optimizer state, gradient flats, workspaces
+    state_b = sum(p.master.numel() * p.master.element_size() for p in ex.params if p.group)
+    grads_b = sum(f["grad"].numel() * f["grad"].element_size() for f in ex.flats if torch.is_tensor(f.get("grad")))
     ex.forward(feeds, training=True)
     torch.cuda.synchronize()
     live = torch.cuda.memory_allocated() - base
@@ -91,7 +110,8 @@ def main():
                 if k not in seen:
                     seen[k] = t.untyped_storage().nbytes()
                     by_env[s.op_type] += seen[k]
-    (p,) = native.plan_memory(m.pcg, 1, with_blocks=True, weight_bytes_per_param=wbytes)
+    (p,) = native.plan_memory(m.pcg, 1, with_blocks=True, weight_bytes_per_param=wbytes, act_elem_bytes=2.0,
+                              executor_fusions=True)
     steps = p["steps"]
     fwd_end = steps // 2 - 1
     plan = collections.Counter()
@@ -105,6 +125,11 @@ def main():
                       "distinct_kept_gb": round(sum(seen.values()) / 1e9, 3),
                       "plan_activations_at_forward_end_gb": round(sum(plan.values()) / 1e9, 3),
                       "plan_arena_gb": round(p["arena_bytes"] / 1e9, 3),
+                      "plan_weight_gb": round(p["weight_bytes"] / 1e9, 3),
+                      "base_allocated_after_step_gb": round(base / 1e9, 3),
+                      "step_peak_gb": round(step_peak / 1e9, 3),
+                      "step_peak_over_base_gb": round((step_peak - base) / 1e9, 3),
+                      "masters_gb": round(state_b / 1e9, 3), "grad_flats_gb": round(grads_b / 1e9, 3),
                       "measured_peak_gb": round(torch.cuda.max_memory_allocated() / 1e9, 3)}))
     for r in rows:
         print(json.dumps(r))
