@@ -34,10 +34,11 @@ def main():
     from flexflow_train_amd.search import native
 
     name = sys.argv[1]
+    sys.argv = [a for a in sys.argv if a != "--trace"] + (["--trace"] if "--trace" in sys.argv else [])
     cfg = FFConfig()
     m = FFModel(cfg)
     if name.startswith("gpt"):
-        b = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+        b = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 16
         cfg.batch_size = b
         inputs, out, mc = Z.build("gpt", m, batch_size=b, hidden_size=1024, num_layers=24, num_heads=16,
                                   sequence_length=2048)
@@ -50,7 +51,7 @@ def main():
         wbytes = 16.0
     elif name.startswith("bert"):
         from flexflow_train_amd.models.bert import bert_large, build_bert
-        b = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+        b = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 64
         cfg.batch_size = b
         bc = bert_large(batch_size=b, sequence_length=512)
         build_bert(m, bc)
@@ -66,7 +67,7 @@ def main():
         labels = torch.randint(0, bc.vocab_size, ex._loss_layout().piece_shape[:-1], device=dev)
         wbytes = 16.0
     else:
-        b = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+        b = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 256
         cfg.batch_size = b
         inputs, out, mc = Z.build(name, m, batch_size=b, image_size=224, num_classes=1000)
         m.compile(optimizer=SGDOptimizer(m, lr=0.01, momentum=0.9),
@@ -76,9 +77,28 @@ def main():
         feeds = {k: ex._local_piece(k, torch.as_tensor(v)) for k, v in fn.items()}
         labels = ex.local_labels(torch.as_tensor(ln))
         wbytes = 12.0
+    if "--trace" in sys.argv:
+        torch.cuda.memory._record_memory_history(max_entries=200000)
     ex.train_step(feeds, labels)          # autotune / workspaces settle
     torch.cuda.synchronize()
     base = torch.cuda.memory_allocated()
+    if "--trace" in sys.argv:
+        # the largest blocks alive between steps, with the Python frames that allocated them
+        snap = torch.cuda.memory._snapshot()
+        blocks = []
+        for seg in snap["segments"]:
+            for blk in seg["blocks"]:
+                if blk["state"] == "active_allocated":
+                    fr = [f"{f['filename'].split('/')[-1]}:{f['line']}:{f['name']}" for f in blk.get("frames", [])
+                          if f["filename"].endswith(".py") and "torch/" not in f["filename"]]
+                    blocks.append((blk["size"], fr[:4]))
+        blocks.sort(key=lambda b: -b[0])
+        by_site = collections.Counter()
+        for sz, fr in blocks:
+            by_site[" <- ".join(fr[:3])] += sz
+        for site, sz in by_site.most_common(15):
+            print(json.dumps({"base_site": site, "gb": round(sz / 1e9, 3)}))
+        torch.cuda.memory._record_memory_history(enabled=None)
     torch.cuda.reset_peak_memory_stats()
     ex.train_step(feeds, labels)
     torch.cuda.synchronize()
