@@ -1,5 +1,7 @@
 #include "ff/json.h"
 
+#include <cstdlib>
+
 #include <cmath>
 #include <cstdio>
 #include <sstream>
@@ -261,7 +263,14 @@ struct Parser {
     }
     if (start == i) fail("unexpected character");
     std::string num = s.substr(start, i - start);
-    if (is_float) return Json(std::stod(num));
+    // strtod, not std::stod: a subnormal (e.g. 4.9e-324, which to_json writes
+    // for such doubles) sets ERANGE and std::stod throws; strtod returns it
+    if (is_float) {
+      char* end = nullptr;
+      const double v = std::strtod(num.c_str(), &end);
+      if (end == num.c_str()) fail("bad number");
+      return Json(v);
+    }
     return Json(static_cast<long long>(std::stoll(num)));
   }
 };
