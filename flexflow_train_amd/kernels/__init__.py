@@ -497,6 +497,23 @@ def _splitk_ws(dev, numel: int) -> torch.Tensor:
     return ws
 
 
+_GRAPH_CAPTURED = [False]
+
+
+def note_graph_capture():
+    """A hipGraph now holds workspace pointers: the cache is never trimmed
+    again in this process."""
+    _GRAPH_CAPTURED[0] = True
+
+
+def trim_workspaces():
+    """Drop the cached split-K slabs (the autotuner's candidates leave one per
+    split degree they tried); kernels in use re-create theirs on their next
+    call.  Only between steps, and never once a captured graph may read them."""
+    if not _GRAPH_CAPTURED[0]:
+        _WS_CACHE.clear()
+
+
 def gemm256_supported(a, b, trans_a=False, trans_b=False) -> bool:
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
         return False

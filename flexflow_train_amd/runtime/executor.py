@@ -1213,6 +1213,11 @@ class Executor:
                     impl = opbase.get_impl(s.op_type)
                     t0 = self.tracer.begin(f"{s.name}:bwd", "compute", self.step_num) if prof else None
                     gins = impl.backward(s.ctx, saved, gouts, wgs, need)
+                    # hand-offs of this backward only: left in ctx.extra they would
+                    # keep every step's input gradients / pre-activations alive
+                    # into the next forward (3.2 GB on BERT-large, tools/mem_audit.py)
+                    for k in ("grad_acc", "dact", "dsum_target"):
+                        s.ctx.extra.pop(k, None)
                     self.tracer.end(t0)
                     if self.cfg.sync_debug:
                         self._debug_sync(s, "backward")
@@ -1521,16 +1526,25 @@ class Executor:
         self._after_first_update()
 
     def _after_first_update(self):
-        """Once per executor, after the first distributed update (plain or
-        pipelined step): the first step tuned every GEMM signature on each
-        rank on its own, so agree on one kernel per signature before later
-        steps / the capture (partial-sum replicas' bias gradients would drift
-        apart otherwise)."""
-        if (self.dist.distributed and not getattr(self, "_choices_synced", False)
-                and self.cfg.device.type == "cuda" and not torch.cuda.is_current_stream_capturing()):
+        """Once per executor, after the first update (plain or pipelined
+        step), outside graph capture:
+          * distributed: the first step tuned every GEMM signature on each rank
+            on its own, so agree on one kernel per signature before later steps
+            / the capture (partial-sum replicas' bias gradients would drift
+            apart otherwise);
+          * the autotuner's candidates left split-K slabs of every split degree
+            they tried in the workspace cache (15.5 GB on GPT-3 medium,
+            tools/mem_audit.py): drop them, the chosen kernels re-create theirs."""
+        if self.cfg.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+            return
+        if self.dist.distributed and not getattr(self, "_choices_synced", False):
             from ..ops.gemm import sync_choices
             sync_choices()
             self._choices_synced = True
+        if not getattr(self, "_ws_trimmed", False) and getattr(self, "_graph", None) is None:
+            torch.cuda.synchronize(self.cfg.device)
+            K.trim_workspaces()
+            self._ws_trimmed = True
 
     def _overlap_flats(self) -> List[dict]:
         """Flats whose buckets may be updated during the backward pass: one
@@ -1678,6 +1692,7 @@ class Executor:
         # a HIP event / stream would call its destroy API mid-capture (abort)
         gc_was_on = gc.isenabled()
         gc.disable()
+        K.note_graph_capture()
         try:
             if self.dist.distributed:
                 # across ranks: one graph segment between consecutive collectives
