@@ -559,7 +559,10 @@ def _run_zoo(args, world, rank, only_dp: bool):
             "compile_s": round(compile_s, 2), "hipgraph": t["graphed"],
             "graph_segments": list(getattr(ex, "graph_segments", ())) or None,
             "native_replay": getattr(ex, "native_replay", None), "final_loss": round(pm.loss, 4),
-            "memory": _memory_record(model, ex, world, 16.0 if opt == "adam" else 8.0),
+            # resident bytes per parameter: fp32 master + bf16 copy + gradient
+            # + optimizer state (Adam m, v: 16; SGD momentum: 14; plain SGD: 10)
+            "memory": _memory_record(model, ex, world, 16.0 if opt in ("adam", "adamw") else
+                                     (14.0 if zname in ("resnet50", "resnext50", "inception_v3") else 10.0)),
             "search": _search_record(model, world)}
     conf.update(extra)
     if zname == "gpt":
