@@ -290,6 +290,8 @@ def _memory_record(model, ex, world, bytes_per_param=16.0):
             if planned:
                 rec["plan_error_pct"] = round(100.0 * (planned - rec["measured_step_peak_gb"])
                                               / rec["measured_step_peak_gb"], 1)
+        if getattr(ex, "arena", None) is not None:
+            rec["device_arena"] = ex.arena.stats()
     return rec
 
 
@@ -311,12 +313,32 @@ def _search_record(model, world):
     return out
 
 
-def _time_steps(args, ex, feeds, labels, global_batch):
+def _arena_bytes(model, ex, world, bytes_per_param):
+    """The step's device arena: the liveness plan's peak minus the resident
+    weights / optimizer state (allocated at compile time, outside the
+    arena), +10 % and 2 GiB for workspaces and the block cache's slack."""
+    import torch
+    from flexflow_train_amd.search import native
+    bf16 = getattr(ex.cfg, "compute_dtype", None) == torch.bfloat16
+    plans = native.plan_memory(model.pcg, world, model.views, weight_bytes_per_param=bytes_per_param,
+                               act_elem_bytes=2.0 if bf16 else 0.0, executor_fusions=True)
+    p = plans[min(ex.dist.rank, len(plans) - 1)]
+    return int(max(0.0, p["arena_bytes"] - p["weight_bytes"]) * 1.10 + (2 << 30))
+
+
+def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_param=16.0):
     """W untimed warm-up steps, then EXACTLY K timed steps bracketed by a
     barrier + device synchronisation on both sides; max over ranks."""
     import torch
 
     dev = ex.cfg.device
+    if (dev.type == "cuda" and model is not None and not args.profile
+            and os.environ.get("FF_ARENA", "1") == "1"):
+        # the step runs out of the framework's device arena, sized by the plan
+        try:
+            ex.enable_arena(_arena_bytes(model, ex, ex.dist.world, bytes_per_param))
+        except Exception as e:  # noqa: BLE001 -- the torch allocator serves the step instead
+            print(f"warning: device arena not enabled ({type(e).__name__}: {e})", file=sys.stderr)
 
     def step():
         ex.train_step(feeds, labels)
@@ -404,7 +426,7 @@ def _run_bert(args, world, rank, only_dp: bool):
     lshape = ex._loss_layout().piece_shape[:-1]
     labels = torch.randint(0, bcfg.vocab_size, lshape, generator=g, device=dev, dtype=torch.int64)
 
-    t = _time_steps(args, ex, feeds, labels, global_batch)
+    t = _time_steps(args, ex, feeds, labels, global_batch, model, 16.0)
     pm = ex.perf_metrics()
     conf = {
         "model": args.model + ("" if not args.layers else f"-{args.layers}L(debug)"),
@@ -552,7 +574,8 @@ def _run_zoo(args, world, rank, only_dp: bool):
         labels = ex.local_labels(torch.as_tensor(labels_np))
     del feeds_np, labels_np
 
-    t = _time_steps(args, ex, feeds, labels, global_batch)
+    bpp = 16.0 if opt in ("adam", "adamw") else (14.0 if zname in ("resnet50", "resnext50", "inception_v3") else 10.0)
+    t = _time_steps(args, ex, feeds, labels, global_batch, model, bpp)
     pm = ex.perf_metrics()
     conf = {"model": args.model, "global_batch": global_batch, "parallelism": _parallelism(model, world),
             "strategy_source": model.search_report.get("source", ""), "optimizer": opt,
@@ -561,8 +584,7 @@ def _run_zoo(args, world, rank, only_dp: bool):
             "native_replay": getattr(ex, "native_replay", None), "final_loss": round(pm.loss, 4),
             # resident bytes per parameter: fp32 master + bf16 copy + gradient
             # + optimizer state (Adam m, v: 16; SGD momentum: 14; plain SGD: 10)
-            "memory": _memory_record(model, ex, world, 16.0 if opt in ("adam", "adamw") else
-                                     (14.0 if zname in ("resnet50", "resnext50", "inception_v3") else 10.0)),
+            "memory": _memory_record(model, ex, world, bpp),
             "search": _search_record(model, world)}
     conf.update(extra)
     if zname == "gpt":

@@ -1507,7 +1507,28 @@ class Executor:
             dist.all_reduce(tot)
         return float(tot.sqrt().item())
 
+    def enable_arena(self, nbytes: int):
+        """Run the step's allocations out of one device region of ``nbytes``
+        (runtime/arena.py, csrc/runtime/arena.cpp), sized by the caller from
+        the liveness memory plan.  Eager steps allocate inside it until a
+        graph is captured; captures use it as their pool."""
+        from .arena import Arena
+        self.arena = Arena(self.cfg.device, int(nbytes))
+        return self.arena
+
+    def _arena_ctx(self):
+        import contextlib
+        a = getattr(self, "arena", None)
+        if a is None or getattr(self, "_graph", None) is not None or torch.cuda.is_current_stream_capturing():
+            # after a capture the pool's free blocks belong to the graph
+            return contextlib.nullcontext()
+        return a.use()
+
     def train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
+        with self._arena_ctx():
+            self._train_step(feeds, labels, lr)
+
+    def _train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
         self.forward(feeds, training=True)
         prof = self.cfg.profiling
         t0 = self.tracer.begin("__loss__:fwd", "compute", self.step_num) if prof else None
@@ -1581,6 +1602,10 @@ class Executor:
 
     def train_step_pipelined(self, feeds_list: Sequence[Dict[str, torch.Tensor]], labels_list: Sequence[torch.Tensor],
                              lr: Optional[float] = None, schedule: str = "1f1b"):
+        with self._arena_ctx():
+            self._train_step_pipelined(feeds_list, labels_list, lr, schedule)
+
+    def _train_step_pipelined(self, feeds_list, labels_list, lr=None, schedule: str = "1f1b"):
         """One optimizer step over ``len(feeds_list)`` micro-batches (each of
         the compiled batch shape): gradients accumulated over the
         micro-batches, one synchronisation + update.
@@ -1701,7 +1726,8 @@ class Executor:
                 replay = graph.replay
             else:
                 graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
+                arena = getattr(self, "arena", None)
+                with torch.cuda.graph(graph, pool=arena.pool_id if arena is not None else None):
                     run()
                 replay = graph.replay
         finally:
@@ -1736,7 +1762,8 @@ class Executor:
         collective (runtime/graphs.SegmentRecorder).  Raises NotCapturable
         (after leaving capture mode cleanly) when the step reaches a
         collective that cannot be re-issued from a recorded closure."""
-        rec = SegmentRecorder()
+        arena = getattr(self, "arena", None)
+        rec = SegmentRecorder(pool=arena.pool_id if arena is not None else None)
         torch.cuda.synchronize(self.cfg.device)
         self.dist.recorder = rec
         try:

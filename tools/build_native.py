@@ -160,6 +160,17 @@ def write_ninja(targets: list[str]) -> str:
         rexe = os.path.join(ROOT, "bin", "ffc-runtime-c-test")
         lines.append(f"build {rexe}: cc_rt_exe {os.path.join(ROOT, 'csrc', 'ffi', 'test_runtime_c.c')} | {rlib}")
         defaults += [rlib, rexe]
+    if "kernels" in targets:
+        # csrc/runtime/arena.cpp -> lib/libffarena.so: the step's device arena,
+        # loaded by torch.cuda.memory.CUDAPluggableAllocator (host code only)
+        ao = os.path.join("obj", "runtime", "arena.cpp.o")
+        lines.append(f"build {ao}: hip {os.path.join(ROOT, 'csrc', 'runtime', 'arena.cpp')}")
+        alib = os.path.join(PKG, "lib", "libffarena.so")
+        lines += ["rule link_arena",
+                  f"  command = $hipcc -shared -o $out $in -L{os.path.join(ROCM, 'lib')} -lamdhip64",
+                  "  description = LINK $out"]
+        lines.append(f"build {alib}: link_arena {ao}")
+        defaults.append(alib)
     if "replay" in targets:
         # csrc/runtime/replay.cpp -> _ffreplay: the native walker of segmented
         # distributed steps (hipGraph launches + c10d ProcessGroup collectives);
