@@ -333,7 +333,7 @@ def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_par
 
     dev = ex.cfg.device
     if (dev.type == "cuda" and model is not None and not args.profile
-            and os.environ.get("FF_ARENA", "1") == "1"):
+            and os.environ.get("FF_ARENA", "0") == "1"):
         # the step runs out of the framework's device arena, sized by the plan
         try:
             ex.enable_arena(_arena_bytes(model, ex, ex.dist.world, bytes_per_param))
