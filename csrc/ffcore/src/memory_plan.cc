@@ -124,7 +124,7 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
   // executor fusions (MemoryPlanConfig::executor_fusions): nodes whose
   // outputs are never materialised, nodes whose gradient overwrites their
   // output, and per-node multipliers of the kept activation
-  std::set<int> no_act, no_grad;
+  std::set<int> no_act, no_grad, keep_grad;
   std::map<int, double> act_scale;
   if (cfg.executor_fusions) {
     auto type_of = [&](int n) { return pcg.g.node(n).label.op.type; };
@@ -141,8 +141,12 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
         if (add >= 0 && type_of(add) == OpType::EW_ADD && !no_act.count(add)) {
           const int relu = sole(add);
           if (relu >= 0 && type_of(relu) == OpType::RELU) {
+            // neither output is stored; the fused backward does materialise the
+            // masked gradient of the sum once (handed to the residual branch)
             no_act.insert(n);
             no_act.insert(add);
+            no_grad.insert(n);
+            keep_grad.insert(add);
           }
         }
       } else if (t == OpType::SOFTMAX && !consumers.count(n)) {
@@ -207,7 +211,8 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
     const bool grad = cfg.training && role != NodeRole::INPUT_PATH && has_consumer;
     auto lc = cfg.live_copies.find(n);
     const double copies = lc == cfg.live_copies.end() ? 1.0 : std::max(1.0, lc->second);
-    if (no_act.count(n)) continue;
+    if (no_act.count(n) && !keep_grad.count(n)) continue;
+    const bool store_act = !no_act.count(n);
     const double scale = act_scale.count(n) ? act_scale.at(n) : 1.0;
     for (size_t o = 0; o < node.outputs.size(); ++o) {
       const auto& s = node.outputs[o].shape;
@@ -226,7 +231,7 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
         // (weight gradients); every other activation until its producer's
         a.end = !cfg.training ? last_fwd : role == NodeRole::INPUT_PATH ? std::max(last_fwd, steps - 1 - fwd.at(n))
                                                                         : bwd(n);
-        plans[h.first].blocks.push_back(a);
+        if (store_act) plans[h.first].blocks.push_back(a);
         if (grad && !no_grad.count(n)) {
           MemBlock g = a;
           g.kind = 1;
