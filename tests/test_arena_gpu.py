@@ -7,7 +7,11 @@ the same parameters as the default allocator."""
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
+import os
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("FF_ARENA_TEST", "0") != "1",
+                                 reason="device arena is opt-in (FF_ARENA=1) until its MemPool path is verified")]
 
 
 def test_arena_serves_and_tracks():
