@@ -316,14 +316,14 @@ def _search_record(model, world):
 def _arena_bytes(model, ex, world, bytes_per_param):
     """The step's device arena: the liveness plan's peak minus the resident
     weights / optimizer state (allocated at compile time, outside the
-    arena), +10 % and 2 GiB for workspaces and the block cache's slack."""
+    arena), +15 % and 2 GiB for workspaces and the block cache's slack."""
     import torch
     from flexflow_train_amd.search import native
     bf16 = getattr(ex.cfg, "compute_dtype", None) == torch.bfloat16
     plans = native.plan_memory(model.pcg, world, model.views, weight_bytes_per_param=bytes_per_param,
                                act_elem_bytes=2.0 if bf16 else 0.0, executor_fusions=True)
     p = plans[min(ex.dist.rank, len(plans) - 1)]
-    return int(max(0.0, p["arena_bytes"] - p["weight_bytes"]) * 1.10 + (2 << 30))
+    return int(max(0.0, p["arena_bytes"] - p["weight_bytes"]) * 1.15 + (2 << 30))
 
 
 def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_param=16.0):
@@ -332,8 +332,10 @@ def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_par
     import torch
 
     dev = ex.cfg.device
-    if (dev.type == "cuda" and model is not None and not args.profile
-            and os.environ.get("FF_ARENA", "0") == "1"):
+    # the framework's device arena: on by default on one GPU (verified there);
+    # FF_ARENA=1 / 0 forces it on / off at any N
+    arena_on = os.environ.get("FF_ARENA", "1" if ex.dist.world == 1 else "0") == "1"
+    if dev.type == "cuda" and model is not None and not args.profile and arena_on:
         # the step runs out of the framework's device arena, sized by the plan
         try:
             ex.enable_arena(_arena_bytes(model, ex, ex.dist.world, bytes_per_param))
@@ -343,25 +345,40 @@ def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_par
     def step():
         ex.train_step(feeds, labels)
 
+    def phase(tag):
+        # FF_MEM_PHASES=1: allocated / reserved / arena after each set-up phase (stderr)
+        if os.environ.get("FF_MEM_PHASES") == "1" and dev.type == "cuda":
+            torch.cuda.synchronize()
+            a = getattr(ex, "arena", None)
+            print(f"[mem] {tag}: allocated {torch.cuda.memory_allocated(dev) / 1e9:.2f} GB, "
+                  f"peak {torch.cuda.max_memory_allocated(dev) / 1e9:.2f} GB, "
+                  f"reserved {torch.cuda.memory_reserved(dev) / 1e9:.2f} GB"
+                  + (f", arena {a.stats()}" if a is not None else ""), file=sys.stderr, flush=True)
+
+    phase("compiled")
     if dev.type == "cuda" and not args.profile:
         # the step's own memory peak: one eager step to settle the autotuner
         # and the workspaces, then one measured from a reset peak counter
         ex.train_step(feeds, labels)
+        phase("eager step 1")
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats(dev)
         ex.train_step(feeds, labels)
         torch.cuda.synchronize()
         ex._ff_step_peak = torch.cuda.max_memory_allocated(dev)
+        phase("eager step 2")
     graphed = False
     use_graph = args.graph if args.graph >= 0 else 1
     if use_graph and dev.type == "cuda" and not args.profile:
         try:
             step = ex.make_graphed_train_step(feeds, labels)
             graphed = True
+            phase("captured")
         except Exception as e:  # noqa: BLE001 — fall back to eager execution
             print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
     for _ in range(args.warmup):
         step()
+    phase("warm-up done")
     if dev.type == "cuda":
         torch.cuda.synchronize()
     ex.dist.barrier()

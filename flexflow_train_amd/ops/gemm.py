@@ -305,14 +305,17 @@ def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
         M, Kd = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
         N = b.shape[0] if trans_b else b.shape[1]
         splits, tsplits = {1}, {1}
-        if bias is None and act == "none" and pre is None:
+        tiles = ((M + 255) // 256) * ((N + 255) // 256)
+        # split-K only where the output tiles leave CUs idle: past two waves of
+        # workgroups a split only adds its fp32 partial slab (GPT-3's logits
+        # GEMM at split 2: 13 GB of partials for nothing)
+        if bias is None and act == "none" and pre is None and tiles < 512:
             # powers of two around the grid-filling degree (gemmp: K-tiles must
             # split evenly); gemmt also takes uneven splits, so it adds the
             # degrees that fill one or two waves of workgroups exactly
             d = K.default_splits(M, N, Kd)
             pow2 = {s for s in (2, 4, 8, 16, 32) if d / 3 <= s <= 2 * d and s <= max(1, Kd // 512)}
             splits |= {s for s in pow2 if (Kd // 64) % s == 0}
-            tiles = ((M + 255) // 256) * ((N + 255) // 256)
             tsplits |= pow2 | {s for s in (round(256 / tiles), round(512 / tiles)) if 2 <= s <= max(1, Kd // 512)}
         if trans_b and not trans_a and bias is None and act == "none" and pre is None \
                 and os.environ.get("FF_GEMMN", "1") != "0":

@@ -22,6 +22,7 @@ from typing import Dict, Optional
 import torch
 
 _LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libffarena.so")
+_POOLS: Dict[int, tuple] = {}
 
 
 def available() -> bool:
@@ -34,17 +35,29 @@ class Arena:
             raise RuntimeError(f"arena library missing: {_LIB} (python tools/build_native.py kernels)")
         self.device = torch.device(device)
         self.index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        # torch's device allocator is set up before a MemPool is made on top
+        # of a pluggable one
+        torch.cuda.init()
+        torch.empty(1, device=self.device)
         self._lib = ctypes.CDLL(_LIB)
         self._lib.ff_arena_reserve.argtypes = [ctypes.c_int, ctypes.c_size_t]
         self._lib.ff_arena_reserve.restype = ctypes.c_int
         self._lib.ff_arena_stats.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         self._lib.ff_arena_reset_high.argtypes = [ctypes.c_int]
+        self._lib.ff_arena_reset_counts.argtypes = [ctypes.c_int]
         rc = self._lib.ff_arena_reserve(self.index, int(nbytes))
         if rc != 0:
             raise RuntimeError(f"arena: reserving {nbytes / 1e9:.2f} GB on device {self.index} failed ({rc})")
         self.requested = int(nbytes)
-        self.allocator = torch.cuda.memory.CUDAPluggableAllocator(_LIB, "ff_arena_alloc", "ff_arena_free")
-        self.pool = torch.cuda.MemPool(self.allocator.allocator())
+        # one allocator + MemPool per device for the life of the process (the
+        # native region is never released either): a MemPool that dies
+        # releases its blocks through its allocator, and the pluggable
+        # allocator object may already be gone by then
+        if self.index not in _POOLS:
+            alloc = torch.cuda.memory.CUDAPluggableAllocator(_LIB, "ff_arena_alloc", "ff_arena_free")
+            _POOLS[self.index] = (alloc, torch.cuda.MemPool(alloc.allocator()))
+        self.allocator, self.pool = _POOLS[self.index]
+        self._lib.ff_arena_reset_counts(self.index)
 
     def use(self):
         """Route this thread's allocations on the arena's device to it."""

@@ -21,6 +21,7 @@ local_training_backing.cc:50-163):
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import gc
 import hashlib
@@ -1514,15 +1515,29 @@ class Executor:
         graph is captured; captures use it as their pool."""
         from .arena import Arena
         self.arena = Arena(self.cfg.device, int(nbytes))
+        # torch's block cache files a freed block under the stream that
+        # allocated it and reuses it only on that stream: eager steps, the
+        # capture warm-up and the capture itself all run on this one stream,
+        # so the capture reuses the blocks the eager steps left in the pool
+        self._arena_stream = torch.cuda.Stream(device=self.cfg.device)
         return self.arena
 
+    @contextlib.contextmanager
     def _arena_ctx(self):
-        import contextlib
         a = getattr(self, "arena", None)
         if a is None or getattr(self, "_graph", None) is not None or torch.cuda.is_current_stream_capturing():
             # after a capture the pool's free blocks belong to the graph
-            return contextlib.nullcontext()
-        return a.use()
+            yield
+            return
+        s, cur = self._arena_stream, torch.cuda.current_stream(self.cfg.device)
+        if s == cur:
+            with a.use():
+                yield
+            return
+        s.wait_stream(cur)
+        with torch.cuda.stream(s), a.use():
+            yield
+        cur.wait_stream(s)
 
     def train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
         with self._arena_ctx():
@@ -1706,7 +1721,8 @@ class Executor:
                 self.train_step(static_feeds, static_labels)
         for f in self.flats:
             f["opt"].enable_device_hparams()
-        side = torch.cuda.Stream(device=self.cfg.device)
+        arena = getattr(self, "arena", None)
+        side = self._arena_stream if arena is not None else torch.cuda.Stream(device=self.cfg.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
@@ -1726,8 +1742,8 @@ class Executor:
                 replay = graph.replay
             else:
                 graph = torch.cuda.CUDAGraph()
-                arena = getattr(self, "arena", None)
-                with torch.cuda.graph(graph, pool=arena.pool_id if arena is not None else None):
+                with torch.cuda.graph(graph, pool=arena.pool_id if arena is not None else None,
+                                      stream=side if arena is not None else None):
                     run()
                 replay = graph.replay
         finally:

@@ -7,11 +7,7 @@ the same parameters as the default allocator."""
 import pytest
 import torch
 
-import os
-
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("FF_ARENA_TEST", "0") != "1",
-                                 reason="device arena is opt-in (FF_ARENA=1) until its MemPool path is verified")]
+pytestmark = pytest.mark.gpu
 
 
 def test_arena_serves_and_tracks():
@@ -60,6 +56,7 @@ def _bert(arena_bytes):
         ex.enable_arena(arena_bytes)
     for _ in range(2):
         ex.train_step(feeds, labels)
+    ex._eager_arena = ex.arena.stats() if arena_bytes else None
     step = ex.make_graphed_train_step(feeds, labels, warmup=1)
     for _ in range(3):
         step()
@@ -71,6 +68,10 @@ def test_training_step_out_of_the_arena():
     ex_a, pa = _bert(1 << 30)
     st = ex_a.arena.stats()
     assert st["segments"] > 0 and st["overflow_segments"] == 0, st
+    # the capture reuses the blocks the eager steps left in the pool (same
+    # stream) instead of taking fresh segments next to them
+    eager = ex_a._eager_arena
+    assert st["high_water_gb"] <= 1.25 * eager["high_water_gb"] + 0.05, (eager, st)
     _, pb = _bert(0)
     for n in pa:
         torch.testing.assert_close(pa[n], pb[n], rtol=2e-2, atol=2e-3)

@@ -98,11 +98,20 @@ def main():
             by_site[" <- ".join(fr[:3])] += sz
         for site, sz in by_site.most_common(15):
             print(json.dumps({"base_site": site, "gb": round(sz / 1e9, 3)}))
-        torch.cuda.memory._record_memory_history(enabled=None)
     torch.cuda.reset_peak_memory_stats()
     ex.train_step(feeds, labels)
     torch.cuda.synchronize()
     step_peak = torch.cuda.max_memory_allocated()
+    if "--trace" in sys.argv:
+        # the step's largest single allocations, with the frames that made them
+        snap = torch.cuda.memory._snapshot()
+        evs = [e for tr in snap.get("device_traces", []) for e in tr if e.get("action") == "alloc"]
+        evs.sort(key=lambda e: -e["size"])
+        for e in evs[:12]:
+            fr = [f"{f['filename'].split('/')[-1]}:{f['line']}:{f['name']}" for f in e.get("frames", [])
+                  if f["filename"].endswith(".py") and "torch/" not in f["filename"]]
+            print(json.dumps({"step_alloc_gb": round(e["size"] / 1e9, 3), "site": " <- ".join(fr[:4])}))
+        torch.cuda.memory._record_memory_history(enabled=None)
     # the persistent part: weights, optimizer state, gradient flats, workspaces
     state_b = sum(p.master.numel() * p.master.element_size() for p in ex.params if p.group)
     grads_b = sum(f["grad"].numel() * f["grad"].element_size() for f in ex.flats if torch.is_tensor(f.get("grad")))
