@@ -66,7 +66,11 @@ struct MemoryPlanConfig {
   //    logits' gradient overwrites the logits (no separate block);
   //  * LINEAR with an activation keeps its pre-activation too (x2);
   //  * MULTIHEAD_ATTENTION keeps the q / k / v projections and the
-  //    attention output (flash attention: no score matrix) beside its output
+  //    attention output (flash attention: no score matrix) beside its output;
+  //  * an output that neither its producer's nor any consumer's backward
+  //    reads is freed after its last forward reader (the executor drops it
+  //    from its environment); otherwise it lives until its last reader's
+  //    backward
   bool executor_fusions = false;
 };
 

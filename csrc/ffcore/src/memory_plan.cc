@@ -125,7 +125,10 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
   // outputs are never materialised, nodes whose gradient overwrites their
   // output, and per-node multipliers of the kept activation
   std::set<int> no_act, no_grad, keep_grad;
-  std::map<int, double> act_scale;
+  // own_extra[n]: bytes (as a multiple of the output) n's backward reads
+  // besides its output, alive until bwd(n) -- the pre-activation of a Linear
+  // with an activation, attention's projections and output
+  std::map<int, double> own_extra;
   if (cfg.executor_fusions) {
     auto type_of = [&](int n) { return pcg.g.node(n).label.op.type; };
     auto sole = [&](int n) -> int {
@@ -154,7 +157,7 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
         for (auto const& v : pcg.layer_data_inputs(n)) no_grad.insert(v.node);
       } else if (t == OpType::LINEAR) {
         const std::string a = op.has("activation") ? op.s("activation") : "none";
-        if (!a.empty() && a != "none") act_scale[n] = 2.0;
+        if (!a.empty() && a != "none") own_extra[n] = 1.0;
       } else if (t == OpType::MULTIHEAD_ATTENTION) {
         auto ins = pcg.layer_data_inputs(n);
         if (ins.size() == 3) {
@@ -167,11 +170,70 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
           const double hd = static_cast<double>(H) / std::max(1, pcg.shape(ins[0]).discard_copy_degree);
           const double extra = hd * (Sq * kd + Sk * kd + Sk * vd + Sq * vd);
           const double out = static_cast<double>(o.num_elements());
-          if (out > 0) act_scale[n] = 1.0 + extra / out;
+          if (out > 0) own_extra[n] = extra / out;
         }
       }
     }
   }
+
+  // which saved tensors the executor's backward reads (the op
+  // implementations' saved tuples, flexflow_train_amd/ops/*.py): an output
+  // nobody's backward reads leaves memory after its last forward reader
+  // (runtime/executor.py drops it from the environment); unknown operators
+  // are assumed to read both
+  auto reads_own_output = [&](int n) {
+    const auto& op = pcg.g.node(n).label.op;
+    switch (op.type) {
+      case OpType::LINEAR:
+      case OpType::BATCHMATMUL:
+      case OpType::EW_ADD:
+      case OpType::EW_SUB:
+      case OpType::EW_MUL:
+      case OpType::EW_DIV:
+      case OpType::MULTIHEAD_ATTENTION:
+      case OpType::LAYERNORM:
+      case OpType::POOL2D:
+      case OpType::EMBEDDING:
+      case OpType::CONCAT:
+      case OpType::SPLIT:
+      case OpType::DROPOUT:
+      case OpType::RESHAPE:
+      case OpType::FLAT:
+      case OpType::TRANSPOSE:
+      case OpType::REVERSE:
+      case OpType::GELU:
+      case OpType::IDENTITY:
+        return false;
+      case OpType::CONV2D:
+        return op.has("activation") && op.s("activation") != "none" && !op.s("activation").empty();
+      case OpType::BATCHNORM:
+        return op.has("relu") && op.b("relu");
+      default:
+        return true;
+    }
+  };
+  auto reads_inputs = [&](int c) {
+    switch (pcg.g.node(c).label.op.type) {
+      case OpType::EW_ADD:
+      case OpType::EW_SUB:
+      case OpType::CONCAT:
+      case OpType::SPLIT:
+      case OpType::DROPOUT:
+      case OpType::RESHAPE:
+      case OpType::FLAT:
+      case OpType::TRANSPOSE:
+      case OpType::REVERSE:
+      case OpType::SOFTMAX:
+      case OpType::RELU:
+      case OpType::SIGMOID:
+      case OpType::TANH:
+      case OpType::POOL2D:
+      case OpType::IDENTITY:
+        return false;
+      default:
+        return roles.at(c) != NodeRole::WEIGHT_PATH;
+    }
+  };
 
   for (auto& p : plans) p.steps = steps;
   for (int n : order) {
@@ -213,7 +275,17 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
     const double copies = lc == cfg.live_copies.end() ? 1.0 : std::max(1.0, lc->second);
     if (no_act.count(n) && !keep_grad.count(n)) continue;
     const bool store_act = !no_act.count(n);
-    const double scale = act_scale.count(n) ? act_scale.at(n) : 1.0;
+    const double extra = own_extra.count(n) ? own_extra.at(n) : 0.0;
+    // the output's last reader: n's own backward, a consumer's backward that
+    // reads it, or (executor fusions, nobody's backward reads it) its last
+    // forward consumer.  The loss-fused softmax's logits hold their gradient.
+    int out_end = bwd(n);
+    if (cfg.training && cfg.executor_fusions && role == NodeRole::COMPUTE && !reads_own_output(n) &&
+        !no_grad.count(n)) {
+      out_end = last_fwd;
+      for (int c : consumers[n])
+        if (reads_inputs(c)) out_end = std::max(out_end, bwd(c));
+    }
     for (size_t o = 0; o < node.outputs.size(); ++o) {
       const auto& s = node.outputs[o].shape;
       const double bytes = cfg.act_elem_bytes > 0
@@ -225,13 +297,21 @@ std::vector<MemoryPlan> plan_memory(const ParallelComputationGraph& pcg, const s
         a.node = n;
         a.output = static_cast<int>(o);
         a.kind = 0;
-        a.bytes = bytes * h.second * copies * scale;
+        a.bytes = bytes * h.second * copies;
         a.start = fwd.at(n);
         // inputs fed to the graph are read by their consumers' backward
-        // (weight gradients); every other activation until its producer's
+        // (weight gradients); every other activation until its last reader
         a.end = !cfg.training ? last_fwd : role == NodeRole::INPUT_PATH ? std::max(last_fwd, steps - 1 - fwd.at(n))
-                                                                        : bwd(n);
-        if (store_act) plans[h.first].blocks.push_back(a);
+                                                                        : out_end;
+        if (store_act) {
+          plans[h.first].blocks.push_back(a);
+          if (extra > 0) {
+            MemBlock x = a;
+            x.bytes = a.bytes * extra;
+            x.end = cfg.training ? bwd(n) : last_fwd;
+            plans[h.first].blocks.push_back(x);
+          }
+        }
         if (grad && !no_grad.count(n)) {
           MemBlock g = a;
           g.kind = 1;

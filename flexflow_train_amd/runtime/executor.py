@@ -1022,10 +1022,13 @@ class Executor:
 
     # -------------------------------------------------------------- execution
     def forward(self, feeds: Dict[str, torch.Tensor], training: bool = True, keep_outputs: bool = False,
-                save: Optional[bool] = None):
+                save: Optional[bool] = None, free_env: bool = False):
         """Forward pass.  ``training`` selects training-mode op semantics
         (dropout masks, batch statistics); ``save`` (default: ``training``)
-        keeps each step's saved tensors for a following backward()."""
+        keeps each step's saved tensors for a following backward();
+        ``free_env`` (the training step's own forward) lets each value go
+        after its last forward reader instead of holding every activation
+        to the end of the step."""
         if save is None:
             save = training
         env: Dict[Value, torch.Tensor] = {}
@@ -1051,7 +1054,17 @@ class Executor:
                 env[p.terminal] = p.compute
         self._saved = {}
         prof = self.cfg.profiling
+        # with a backward to follow, a value leaves the environment after its
+        # last forward consumer: from then on only the saved tensors that the
+        # backward reads keep it, so the backward frees activations as it goes
+        # (kept to the end of the step, ResNet-50's peak was every activation
+        # plus the largest gradients: 13.7 vs 12.0 GB planned)
+        drop = self._env_drop_plan() if free_env and save and os.environ.get("FF_FREE_ENV", "1") != "0" else None
         for i, s in enumerate(self.steps):
+            if drop is not None and i:
+                for v in drop[i - 1]:
+                    if v not in self.retain:
+                        env.pop(v, None)
             if training and s is self.softmax_fused_step and self.loss is not None and self.loss.fuses_softmax:
                 continue
             if s.kind == "comm":
@@ -1081,8 +1094,39 @@ class Executor:
                     self.retained[o] = t
             if save:
                 self._saved[i] = saved
+        if drop is not None and self.steps:
+            for v in drop[-1]:
+                if v not in self.retain:
+                    env.pop(v, None)
         self._env = env
         return env.get(self.output_value) if keep_outputs or not training else env.get(self.loss_value)
+
+    def _env_drop_plan(self) -> List[List[Value]]:
+        """Per step, the values whose last forward reader it is (a value no
+        step reads goes right after its producer).  Kept to the end: the loss
+        and output values, parameter terminals, and the inputs / outputs of an
+        in-place step's producer (its in-place check looks them up)."""
+        key = (len(self.steps), id(self.softmax_fused_step), len(self._inplace_prod))
+        cached = getattr(self, "_env_drop", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        last: Dict[Value, int] = {}
+        for i, st in enumerate(self.steps):
+            for o in st.outputs:
+                last.setdefault(o, i)
+            for v in st.inputs:
+                last[v] = max(i, last.get(v, i))
+        keep = {self.loss_value, self.output_value}
+        keep.update(p.terminal for p in self.params if p.group)
+        for j in set(self._inplace_prod.values()):
+            keep.update(self.steps[j].inputs)
+            keep.update(self.steps[j].outputs)
+        plan: List[List[Value]] = [[] for _ in self.steps]
+        for v, i in last.items():
+            if v not in keep:
+                plan[i].append(v)
+        self._env_drop = (key, plan)
+        return plan
 
     def _dtype_of(self, v: Value, x: Optional[torch.Tensor]) -> torch.dtype:
         if x is not None:
@@ -1544,7 +1588,7 @@ class Executor:
             self._train_step(feeds, labels, lr)
 
     def _train_step(self, feeds: Dict[str, torch.Tensor], labels: torch.Tensor, lr: Optional[float] = None):
-        self.forward(feeds, training=True)
+        self.forward(feeds, training=True, free_env=True)
         prof = self.cfg.profiling
         t0 = self.tracer.begin("__loss__:fwd", "compute", self.step_num) if prof else None
         g = self.compute_loss(labels)
@@ -1659,7 +1703,7 @@ class Executor:
         self.peak_live_micro_batches = 0
         for kind, i in order:
             if kind == "F":
-                self.forward(feeds_list[i], training=True)
+                self.forward(feeds_list[i], training=True, free_env=True)
                 g = self.compute_loss(labels_list[i])
                 if g is not None and m > 1:
                     g = g / m

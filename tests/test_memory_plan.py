@@ -141,3 +141,34 @@ def test_executor_fusion_rules():
     logits = pcg.layer_data_inputs(head)[0].node
     assert [b for b in p0["blocks"] if b["node"] == logits and b["kind"] == 1]
     assert not [b for b in p1["blocks"] if b["node"] == logits and b["kind"] == 1]
+
+
+def test_outputs_no_backward_reads_leave_after_forward():
+    """executor_fusions: an output that neither its producer's nor any
+    consumer's backward reads (a Linear feeding only a residual add) leaves
+    at its last forward reader, as the executor drops it from its
+    environment; one a consumer's backward reads (a Linear's input) lives
+    until that backward; the loss-fused logits hold their gradient until the
+    head's backward."""
+    from flexflow_train_amd.models.bert import bert_large, build_bert
+    m = FFModel(FFConfig())
+    build_bert(m, bert_large(batch_size=2, sequence_length=128, num_encoder_layers=1))
+    pcg = C.data_parallel_pcg(m.cg, 1)
+    (p,) = native.plan_memory(pcg, 1, with_blocks=True, act_elem_bytes=2.0, executor_fusions=True)
+    order = pcg.topo_order()
+    N = p["steps"] // 2
+    consumers = {}
+    for n in order:
+        for v in pcg.layer_data_inputs(n):
+            consumers.setdefault(v.node, []).append(n)
+    op = lambda n: pcg.layer_op(n).op_type
+    acts = lambda n: [b for b in p["blocks"] if b["node"] == n and b["kind"] == 0]
+    to_add = [n for n in order if op(n) == "LINEAR" and [op(c) for c in consumers.get(n, [])] == ["EW_ADD"]]
+    assert to_add
+    for n in to_add:
+        assert all(b["end"] < N for b in acts(n)), acts(n)
+    to_linear = [n for n in order if op(n) == "LAYERNORM" and "LINEAR" in [op(c) for c in consumers.get(n, [])]]
+    assert to_linear and all(b["end"] >= N for n in to_linear for b in acts(n))
+    head = [n for n in order if op(n) == "SOFTMAX"][0]
+    logits = pcg.layer_data_inputs(head)[0].node
+    assert acts(logits) and all(b["end"] >= N for b in acts(logits))

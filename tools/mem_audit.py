@@ -98,13 +98,39 @@ def main():
             by_site[" <- ".join(fr[:3])] += sz
         for site, sz in by_site.most_common(15):
             print(json.dumps({"base_site": site, "gb": round(sz / 1e9, 3)}))
+    n0 = 0
+    if "--trace" in sys.argv:
+        n0 = sum(len(tr) for tr in torch.cuda.memory._snapshot().get("device_traces", []))
     torch.cuda.reset_peak_memory_stats()
     ex.train_step(feeds, labels)
     torch.cuda.synchronize()
     step_peak = torch.cuda.max_memory_allocated()
     if "--trace" in sys.argv:
-        # the step's largest single allocations, with the frames that made them
         snap = torch.cuda.memory._snapshot()
+        # what is live at the step's peak: replay the step's alloc / free
+        # events from the live set at its start, grouped by allocation site
+        evs = [e for tr in snap.get("device_traces", []) for e in tr][n0:]
+        live = {}
+        cur = 0
+        best, best_live = -1, {}
+        for e in evs:
+            a = e.get("action")
+            if a == "alloc":
+                live[e["addr"]] = e
+                cur += e["size"]
+                if cur > best:
+                    best, best_live = cur, dict(live)
+            elif a == "free_requested" and e["addr"] in live:
+                cur -= live.pop(e["addr"])["size"]
+        by_site = collections.Counter()
+        for e in best_live.values():
+            fr = [f"{f['filename'].split('/')[-1]}:{f['line']}:{f['name']}" for f in e.get("frames", [])
+                  if f["filename"].endswith(".py") and "torch/" not in f["filename"]]
+            by_site[" <- ".join(fr[:3])] += e["size"]
+        print(json.dumps({"step_peak_new_gb": round(best / 1e9, 3), "sites": len(by_site)}))
+        for site, sz in by_site.most_common(20):
+            print(json.dumps({"peak_site": site, "gb": round(sz / 1e9, 3)}))
+        # the step's largest single allocations, with the frames that made them
         evs = [e for tr in snap.get("device_traces", []) for e in tr if e.get("action") == "alloc"]
         evs.sort(key=lambda e: -e["size"])
         for e in evs[:12]:
