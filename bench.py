@@ -178,11 +178,14 @@ def main():
         elif not args.no_dp_compare:
             sps = res["value"]
             _release(res)
-            dp = runner(args, world, rank, only_dp=True)
-            speed["dp_samples_per_sec"] = round(dp["value"], 2)
-            speed["speedup_over_dp"] = round(sps / dp["value"], 3)
-            speed["dp_reference"] = "measured: data-parallel run of the same model / batch after the timed run"
-            _release(dp)
+            try:
+                dp = runner(args, world, rank, only_dp=True)
+                speed["dp_samples_per_sec"] = round(dp["value"], 2)
+                speed["speedup_over_dp"] = round(sps / dp["value"], 3)
+                speed["dp_reference"] = "measured: data-parallel run of the same model / batch after the timed run"
+                _release(dp)
+            except Exception as e:  # noqa: BLE001 -- reported, never costs the headline line
+                speed["dp_reference"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if world > 1 and not args.no_ae and args.model in ("bert-large", "bert-base"):
         # every rank decides from rank 0's clock, so all of them take the same branch
         spent = _max_over_ranks(res, time.time() - t_start)

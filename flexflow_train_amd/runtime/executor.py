@@ -45,6 +45,7 @@ from ..parallel.sequence import SeqGroup
 from ..ops.moe import ExpertGroup
 from .optimizer import AdamConfig, FlatOptimizer, SGDConfig, ShardedOptimizer
 from .graphs import SegmentRecorder
+from .graphs import _native_module as _native_replay_module
 from .initializers import make_initializer_tensor
 from ..utils.tracing import Tracer
 
@@ -1790,6 +1791,16 @@ class Executor:
                                       stream=side if arena is not None else None):
                     run()
                 replay = graph.replay
+                # one device: the step is one graph, launched by the same
+                # native replayer (csrc/runtime/replay.cpp) as the segmented
+                # multi-rank chain
+                R = _native_replay_module()
+                if R is not None:
+                    rp = R.Replayer()
+                    rp.add_graph(graph)
+                    self._native_replayer = rp
+                    replay = rp.replay
+                    self.native_replay = True
         finally:
             if gc_was_on:
                 gc.enable()

@@ -68,6 +68,8 @@ def test_training_step_out_of_the_arena():
     ex_a, pa = _bert(1 << 30)
     st = ex_a.arena.stats()
     assert st["segments"] > 0 and st["overflow_segments"] == 0, st
+    # the one-device step replays through the native replayer (csrc/runtime/replay.cpp)
+    assert ex_a.native_replay is True
     # the capture reuses the blocks the eager steps left in the pool (same
     # stream) instead of taking fresh segments next to them
     eager = ex_a._eager_arena
