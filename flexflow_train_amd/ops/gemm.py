@@ -267,7 +267,7 @@ def _lt(a, b, trans_a, trans_b, bias, act, out, beta, pre, algo=0):
     return K.blaslt_matmul(a, b, trans_a, trans_b, out, beta, bias, algo)
 
 
-_LT_MAX = int(os.environ.get("FF_GEMM_LT_ALGOS", "4"))
+_LT_MAX = 0 if os.environ.get("FF_LIBRARY_GEMM", "1") == "0" else int(os.environ.get("FF_GEMM_LT_ALGOS", "4"))
 
 
 def _lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre):
@@ -284,7 +284,7 @@ def _lt_candidates(a, b, trans_a, trans_b, bias, act, out, beta, pre):
 
 def _candidates(a, b, trans_a, trans_b, bias, act, pre, out=None, beta=0.0):
     """name -> callable(a, b, ta, tb, bias, act, out, beta, pre) tried by the autotuner."""
-    c = {"hip": _hip, "blas": _blas}
+    c = {"hip": _hip} if _LIB_OFF else {"hip": _hip, "blas": _blas}
     M_, Kd_ = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
     N_ = b.shape[0] if trans_b else b.shape[1]
     for s in _hip_splits(M_, N_, Kd_):
@@ -450,6 +450,11 @@ def _time(fn, iters=5, rounds=2) -> float:
 # small MLPs, the MFMA kernel runs (FF_GEMM_LIB_MARGIN / FF_GEMM_LIB_MIN_MS;
 # 0 / 0 = the fastest outright)
 _LIB_MARGIN = float(os.environ.get("FF_GEMM_LIB_MARGIN", "0.03"))
+# FF_LIBRARY_GEMM=0: hand-written kernels only -- rocBLAS / hipBLASLt are
+# neither timed nor picked wherever a native candidate takes the shape
+_LIB_OFF = os.environ.get("FF_LIBRARY_GEMM", "1") == "0"
+if _LIB_OFF:
+    _LIB_MARGIN = 1.0
 _LIB_MIN_MS = float(os.environ.get("FF_GEMM_LIB_MIN_MS", "0.004"))
 
 
