@@ -164,3 +164,35 @@ def test_logging_categories(monkeypatch):
     from flexflow_train_amd.utils.logging import get_logger
     lg = get_logger("search")
     assert lg.name == "flexflow.search"
+
+
+def test_training_forward_frees_values_after_their_last_reader(monkeypatch):
+    """train_step's forward drops each value after its last forward reader
+    (the backward reads only saved tensors): intermediate values are gone from
+    the environment once the step's forward is done, and the trained
+    parameters are bit-identical to a run that keeps every value."""
+    def run(free):
+        monkeypatch.setenv("FF_FREE_ENV", "1" if free else "0")
+        torch.manual_seed(0)
+        cfg = FFConfig()
+        m = FFModel(cfg)
+        feeds, labels = M.bert_tiny(m)
+        m.compile(optimizer=AdamOptimizer(m, alpha=3e-3), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+                  metrics=[MetricsType.METRICS_SPARSE_CATEGORICAL_CROSSENTROPY])
+        ex = m.executor
+        g = torch.Generator().manual_seed(0)
+        for n in sorted(ex.parameter_names()):
+            ex.set_parameter(n, torch.randn(ex.get_parameter(n).shape, generator=g) * 0.05)
+        ex.forward(feeds, training=True, free_env=True)
+        weights = {p.terminal for p in ex.params}
+        kept = len([v for v in ex._env if v not in weights])
+        ex._saved, ex._env = {}, {}
+        for _ in range(3):
+            ex.train_step(feeds, labels)
+        return kept, {n: ex.get_parameter(n).clone() for n in ex.parameter_names()}
+
+    kept_free, p_free = run(True)
+    kept_all, p_all = run(False)
+    assert kept_free < kept_all / 2, (kept_free, kept_all)
+    for n in p_all:
+        assert torch.equal(p_free[n], p_all[n]), n
