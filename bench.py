@@ -265,6 +265,9 @@ def _release(res):
     if torch.cuda.is_available():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+        if os.environ.get("FF_MEM_PHASES") == "1":
+            print(f"[mem] released: allocated {torch.cuda.memory_allocated() / 1e9:.2f} GB, "
+                  f"reserved {torch.cuda.memory_reserved() / 1e9:.2f} GB", file=sys.stderr, flush=True)
 
 
 def _memory_record(model, ex, world, bytes_per_param=16.0):
@@ -388,8 +391,18 @@ def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_par
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if os.environ.get("FF_STEP_TIMES") == "1":
+        # per-step wall times (stderr), each step synchronised: a diagnostic
+        # run, not the headline's timing
+        for i in range(args.steps):
+            ts = time.perf_counter()
+            step()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            print(f"[step] {i}: {1000 * (time.perf_counter() - ts):.1f} ms", file=sys.stderr, flush=True)
+    else:
+        for _ in range(args.steps):
+            step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     ex.dist.barrier()
