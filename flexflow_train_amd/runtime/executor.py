@@ -1788,7 +1788,8 @@ class Executor:
             else:
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph, pool=arena.pool_id if arena is not None else None,
-                                      stream=side if arena is not None else None):
+                                      stream=side if arena is not None else None,
+                                      capture_error_mode="thread_local"):
                     run()
                 replay = graph.replay
                 # one device: the step is one graph, launched by the same

@@ -99,7 +99,12 @@ class SegmentRecorder:
     # ---- capture side
     def begin(self):
         g = torch.cuda.CUDAGraph()
-        g.capture_begin(pool=self.pool)
+        # thread-local capture: RCCL's watchdog thread polls its works' events
+        # while a segment is being captured; under the default global mode
+        # that query is illegal and aborts the process ("operation not
+        # permitted when stream is capturing"); this thread's own unsafe calls
+        # still fail the capture
+        g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
         self.cur = g
 
     def end(self):

@@ -138,7 +138,7 @@ def profile_op(op, in_shapes, device: torch.device, dtype=torch.bfloat16, warmup
             fn()
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             fn()
         return timeit(graph.replay)
 
