@@ -108,7 +108,11 @@ def main():
 
     res = runner(args, world, rank, only_dp=args.strategy == "dp")
     dist_world, backend = _check_world(res["ex"], args.gpus)
-    if world > 1 and not args.no_calibrate:
+    # FF_BENCH_REHEARSE_MULTI=1 (with FF_DIST_WORLD1=1: RCCL at world 1) runs
+    # the multi-rank flow after the headline -- calibration, the watchdog,
+    # the DP reference and the AE protocol -- on one GPU
+    multi = world > 1 or os.environ.get("FF_BENCH_REHEARSE_MULTI") == "1"
+    if multi and not args.no_calibrate:
         # after the timed steps: the collectives the step issued, timed at its
         # own message sizes on this process group, fitted into the cost model;
         # the simulator's step prediction before / after against the measured
@@ -153,7 +157,7 @@ def main():
                           "world_size": dist_world, "backend": backend}), flush=True)
 
     done = threading.Event()
-    if world > 1:
+    if multi:
         left = args.deadline_s - (time.time() - t_start)
 
         def watchdog():
@@ -167,12 +171,12 @@ def main():
             os._exit(0)
         threading.Thread(target=watchdog, daemon=True).start()
 
-    if world > 1 and args.strategy == "search":
+    if multi and args.strategy == "search":
         speed = extra["speed"]
         pred = res["search"].get("predicted_speedup_over_dp")
         if pred is not None:
             speed["predicted_speedup_over_dp"] = round(float(pred), 3)
-        if res["config"]["parallelism"].startswith("dp"):
+        if res["config"]["parallelism"].startswith("dp") and world > 1:
             speed["speedup_over_dp"] = 1.0
             speed["dp_reference"] = "the searched strategy is data parallel"
         elif not args.no_dp_compare:
@@ -186,7 +190,7 @@ def main():
                 _release(dp)
             except Exception as e:  # noqa: BLE001 -- reported, never costs the headline line
                 speed["dp_reference"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-    if world > 1 and not args.no_ae and args.model in ("bert-large", "bert-base"):
+    if multi and not args.no_ae and args.model in ("bert-large", "bert-base"):
         # every rank decides from rank 0's clock, so all of them take the same branch
         spent = _max_over_ranks(res, time.time() - t_start)
         if spent < args.ae_deadline_s:
