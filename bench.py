@@ -42,6 +42,7 @@ import collections
 import gc
 import json
 import os
+import signal
 import sys
 import threading
 import time
@@ -163,6 +164,12 @@ def main():
         def watchdog():
             if done.wait(max(1.0, left)):
                 return
+            child = extra.get("child")
+            if child is not None and child.poll() is None:
+                try:   # the AE protocol's child ranks go with this process
+                    os.killpg(child.pid, signal.SIGKILL)
+                except OSError:
+                    pass
             if extra["ae"] is None and not args.no_ae and args.model in ("bert-large", "bert-base"):
                 extra["ae"] = {"error": f"not finished within the {args.deadline_s:.0f} s command deadline"}
             emit(note=f"stopped at the {args.deadline_s:.0f} s deadline")
@@ -171,6 +178,9 @@ def main():
             os._exit(0)
         threading.Thread(target=watchdog, daemon=True).start()
 
+    inproc = os.environ.get("FF_AE_INPROCESS") == "1"
+    want_ae = multi and not args.no_ae and args.model in ("bert-large", "bert-base")
+    want_dp = False
     if multi and args.strategy == "search":
         speed = extra["speed"]
         pred = res["search"].get("predicted_speedup_over_dp")
@@ -179,10 +189,15 @@ def main():
         if res["config"]["parallelism"].startswith("dp") and world > 1:
             speed["speedup_over_dp"] = 1.0
             speed["dp_reference"] = "the searched strategy is data parallel"
-        elif not args.no_dp_compare:
+        else:
+            want_dp = not args.no_dp_compare
+    if inproc:
+        # the reference runs in this process, every rank taking part
+        if want_dp:
+            speed = extra["speed"]
             sps = res["value"]
-            _release(res)
             try:
+                _release(res)
                 dp = runner(args, world, rank, only_dp=True)
                 speed["dp_samples_per_sec"] = round(dp["value"], 2)
                 speed["speedup_over_dp"] = round(sps / dp["value"], 3)
@@ -190,13 +205,41 @@ def main():
                 _release(dp)
             except Exception as e:  # noqa: BLE001 -- reported, never costs the headline line
                 speed["dp_reference"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-    if multi and not args.no_ae and args.model in ("bert-large", "bert-base"):
-        # every rank decides from rank 0's clock, so all of them take the same branch
-        spent = _max_over_ranks(res, time.time() - t_start)
-        if spent < args.ae_deadline_s:
-            extra["ae"] = _run_ae(args, world, rank, res)
+        if want_ae:
+            # every rank decides from rank 0's clock, so all of them take the same branch
+            spent = _max_over_ranks(res, time.time() - t_start)
+            if spent < args.ae_deadline_s:
+                extra["ae"] = _run_ae(args, world, rank, res)
+            else:
+                extra["ae"] = {"skipped": f"run took {spent:.0f} s before the protocol "
+                                          f"(deadline {args.ae_deadline_s:.0f} s)"}
+    elif want_dp or want_ae:
+        # the DP reference and the AE protocol as fresh jobs started by rank 0
+        # (_child_bench); the other ranks release their model and wait on the
+        # rendezvous store -- no collective pending on the GPUs (an RCCL kernel
+        # waiting in a collective would share the GPUs with the children)
+        _release(res)
+        if rank == 0:
+            try:
+                if want_dp:
+                    speed = extra["speed"]
+                    try:
+                        left = args.deadline_s - (time.time() - t_start) - 30.0
+                        speed.update(_dp_reference_isolated(args, world, rank, res, extra, left))
+                        speed["speedup_over_dp"] = round(res["value"] / speed["dp_samples_per_sec"], 3)
+                    except Exception as e:  # noqa: BLE001 -- reported, never costs the headline line
+                        speed["dp_reference"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+                if want_ae:
+                    spent = time.time() - t_start
+                    if spent < args.ae_deadline_s:
+                        extra["ae"] = _run_ae_isolated(args, world, rank, res, extra, args.ae_deadline_s - spent)
+                    else:
+                        extra["ae"] = {"skipped": f"run took {spent:.0f} s before the protocol "
+                                                  f"(deadline {args.ae_deadline_s:.0f} s)"}
+            finally:
+                _post_done(world, rank, signal_done=True)
         else:
-            extra["ae"] = {"skipped": f"run took {spent:.0f} s before the protocol (deadline {args.ae_deadline_s:.0f} s)"}
+            _post_done(world, rank, signal_done=False, timeout_s=args.deadline_s)
     done.set()
     emit()
     if rank == 0:
@@ -494,6 +537,119 @@ def _run_bert(args, world, rank, only_dp: bool):
             "profile": prof, "feeds": feeds, "labels": labels}
 
 
+def _post_done(world: int, rank: int, signal_done: bool, timeout_s: float = 600.0):
+    """Rank 0 tells the other ranks (through the rendezvous store, CPU only)
+    that the post-headline jobs are done; they wait for it."""
+    import datetime
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or world == 1:
+        return
+    store = dist.distributed_c10d._get_default_store()
+    if signal_done:
+        store.set("ff_bench_post_done", "1")
+    else:
+        store.set_timeout(datetime.timedelta(seconds=max(60.0, timeout_s)))
+        store.wait(["ff_bench_post_done"])
+
+
+def _child_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                        "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT",
+                        "FF_BENCH_REHEARSE_MULTI")
+           and not k.startswith("TORCHELASTIC_")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def _child_bench(world: int, bench_args, timeout_s: float, extra) -> dict:
+    """One fresh N-rank bench job (torch.distributed.run, its own
+    communicators) started by rank 0; its JSON line.  Killed with its process
+    group at ``timeout_s`` (and by the watchdog at the command deadline)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), "--gpus", str(world),
+           "--no-ae", "--no-calibrate", "--no-dp-compare", "--deadline-s", str(max(10.0, timeout_s - 10.0))]
+    cmd += [str(a) for a in bench_args]
+    child = subprocess.Popen(cmd, env=_child_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+    extra["child"] = child
+    try:
+        try:
+            so, se = child.communicate(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(child.pid, signal.SIGKILL)
+            child.communicate()
+            raise TimeoutError(f"did not finish within {timeout_s:.0f} s")
+    finally:
+        extra["child"] = None
+    lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+    if child.returncode != 0 or not lines:
+        raise RuntimeError(f"exited {child.returncode}: {se.strip()[-240:]}")
+    return json.loads(lines[-1])
+
+
+def _dp_reference_isolated(args, world, rank, res, extra, budget_s: float):
+    """The data-parallel run of the headline's model / batch as a fresh job
+    after this run released its memory (a second model built in the same
+    process is not a clean reference: over gloo it ran ~10x slower, and a
+    fault in it would cost the headline)."""
+    _release(res)
+    if rank != 0:
+        return {}
+    a = ["--model", args.model, "--seq", args.seq, "--dtype", args.dtype, "--steps", args.steps,
+         "--warmup", args.warmup, "--strategy", "dp"]
+    if args.layers:
+        a += ["--layers", args.layers]
+    if args.batch_per_gpu:
+        a += ["--batch-per-gpu", args.batch_per_gpu]
+    d = _child_bench(world, a, budget_s, extra)
+    return {"dp_samples_per_sec": round(float(d["value"]), 2),
+            "dp_reference": "measured: data-parallel run of the same model / batch as a fresh job after the timed run"}
+
+
+def _run_ae_isolated(args, world, rank, res, extra, budget_s: float):
+    """The AE protocol (see _run_ae) in child processes: rank 0 launches the
+    searched and the data-parallel run of the AE configuration as two fresh
+    N-rank jobs and reads their JSON lines, so a fault or an abort in a
+    strategy never run at this scale costs only the protocol, never the
+    headline measured above.  The other ranks release their model and
+    finish; the watchdog kills the children's process group at the command
+    deadline."""
+    _release(res)
+    out = {"layers": 12, "hidden": 1024 if args.model == "bert-large" else 768,
+           "global_batch": max(1, 8 // world) * world, "seq_len": args.seq, "budget": 30,
+           "protocol": "scripts/osdi22ae/bert.sh", "isolated": True}
+    if rank != 0:
+        return out
+    t_end = time.time() + budget_s
+    runs = {}
+    try:
+        for strat in ("search", "dp"):
+            left = t_end - time.time()
+            if left < 20:
+                raise TimeoutError(f"{strat} run: {left:.0f} s left of the protocol's budget")
+            runs[strat] = _child_bench(world, ["--model", args.model, "--layers", 12, "--seq", args.seq,
+                                               "--batch-per-gpu", max(1, 8 // world), "--budget", 30,
+                                               "--dtype", args.dtype, "--steps", min(args.steps, 10),
+                                               "--warmup", min(args.warmup, 3), "--strategy", strat], left, extra)
+        s, d = runs["search"], runs["dp"]
+        out["searched_samples_per_sec"] = round(float(s["value"]), 2)
+        out["parallelism"] = s["config"]["parallelism"]
+        out["predicted_speedup_over_dp"] = (s["config"].get("search") or {}).get("predicted_speedup_over_dp")
+        out["dp_samples_per_sec"] = round(float(d["value"]), 2)
+        out["speedup_over_dp"] = round(out["searched_samples_per_sec"] / out["dp_samples_per_sec"], 3)
+    except Exception as e:  # noqa: BLE001 -- reported, never costs the headline line
+        out["error"] = f"{type(e).__name__}: {e}"[:300]
+        if "search" in runs:
+            out["searched_samples_per_sec"] = round(float(runs["search"]["value"]), 2)
+    return out
+
+
 def _run_ae(args, world, rank, res):
     """The OSDI'22 AE BERT protocol (scripts/osdi22ae/bert.sh:3-7): a 12-layer
     hidden-1024 BERT at global batch 8, the searched strategy (--budget 30)
@@ -648,7 +804,22 @@ def _write_autotune_report():
         print(f"autotune report: {e}", file=sys.stderr)
 
 
+def _shutdown():
+    """Leave the process group explicitly (every rank, after the line is
+    out): left to interpreter teardown, the sub-groups of a searched hybrid
+    strategy were destroyed with live worker threads and the ranks aborted
+    on exit ("terminate called without an active exception", exit 1)."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- the measurement is already printed
+        print(f"warning: process group shutdown: {type(e).__name__}: {e}", file=sys.stderr)
+
+
 if __name__ == "__main__":
     import atexit
     atexit.register(_write_autotune_report)
     main()
+    _shutdown()
