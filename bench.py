@@ -188,7 +188,9 @@ def main():
             speed["predicted_speedup_over_dp"] = round(float(pred), 3)
         if res["config"]["parallelism"].startswith("dp") and world > 1:
             speed["speedup_over_dp"] = 1.0
-            speed["dp_reference"] = "the searched strategy is data parallel"
+            kept = res["search"].get("kept_data_parallel")
+            speed["dp_reference"] = ("the searched strategy is data parallel"
+                                     + (f" (kept: {kept})" if kept else ""))
         else:
             want_dp = not args.no_dp_compare
     if inproc:

@@ -32,6 +32,9 @@ class FFConfig:
     search_budget: int = -1
     search_time_limit: float = 45.0    # seconds for the whole strategy search (MCMC + Unity + mapping)
     search_alpha: float = 1.2
+    # a searched strategy replaces data parallelism only when its predicted
+    # speedup reaches this (smaller predicted gains are within the cost model's error)
+    search_min_speedup: float = 1.02
     search_overlap_backward_update: bool = True
     only_data_parallel: bool = False
     enable_parameter_parallel: bool = False
@@ -140,6 +143,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--budget", "--search-budget", dest="search_budget", type=int)
     a("--search-time-limit", dest="search_time_limit", type=float)
     a("--alpha", "--search-alpha", dest="search_alpha", type=float)
+    a("--search-min-speedup", dest="search_min_speedup", type=float)
     a("--simulator-workspace-size", dest="simulator_work_space_size", type=int)
     a("--import", "--import-strategy", dest="import_strategy_file", type=str)
     a("--export", "--export-strategy", dest="export_strategy_file", type=str)

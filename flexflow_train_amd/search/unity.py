@@ -85,4 +85,15 @@ def search(cg, ffconfig, world: int):
         dist.broadcast_object_list(payload, src=0)
     pcg = C.ParallelComputationGraph.from_json(payload[0])
     views: Dict[int, Tuple[int, ...]] = {int(k): tuple(v) for k, v in payload[1].items()}
-    return pcg, views, payload[2]
+    rep = payload[2]
+    # a predicted gain inside the cost model's error (the calibrated
+    # simulator is within ~3 % of measured steps) does not pay for running a
+    # strategy other than data parallelism: keep DP below search_min_speedup
+    pred = rep.get("predicted_speedup_over_dp") if isinstance(rep, dict) else None
+    min_gain = float(getattr(ffconfig, "search_min_speedup", 1.0) or 1.0)
+    if world > 1 and pred is not None and float(pred) < min_gain:
+        pcg = C.data_parallel_pcg(cg, world)
+        views = {}
+        rep = dict(rep)
+        rep["kept_data_parallel"] = f"predicted speedup {float(pred):.4f} < search_min_speedup {min_gain:g}"
+    return pcg, views, rep
