@@ -98,6 +98,10 @@ def main():
 
     os.environ["FF_GEMM"] = args.gemm
     t_start = time.time()
+    if os.environ.get("FF_HANG_DUMP_S"):
+        # diagnostic: every thread's Python stack to stderr every N seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["FF_HANG_DUMP_S"]), repeat=True)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -580,15 +584,29 @@ def _child_bench(world: int, bench_args, timeout_s: float, extra) -> dict:
     child = subprocess.Popen(cmd, env=_child_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                              start_new_session=True)
     extra["child"] = child
+    t_end = time.time() + timeout_s
     try:
-        try:
-            so, se = child.communicate(timeout=timeout_s)
-        except subprocess.TimeoutExpired:
-            os.killpg(child.pid, signal.SIGKILL)
-            child.communicate()
-            raise TimeoutError(f"did not finish within {timeout_s:.0f} s")
+        while True:
+            # a progress line every 30 s (stderr) while the child job runs;
+            # communicate() may be retried after a timeout without losing output
+            try:
+                so, se = child.communicate(timeout=max(1.0, min(30.0, t_end - time.time())))
+                break
+            except subprocess.TimeoutExpired:
+                if time.time() >= t_end:
+                    os.killpg(child.pid, signal.SIGKILL)
+                    child.communicate()
+                    raise TimeoutError(f"did not finish within {timeout_s:.0f} s")
+                print(f"[bench] child job {' '.join(str(a) for a in bench_args[-2:])} running, "
+                      f"{t_end - time.time():.0f} s left", file=sys.stderr, flush=True)
     finally:
         extra["child"] = None
+    logdir = os.environ.get("FF_BENCH_CHILD_LOG_DIR")
+    if logdir:
+        os.makedirs(logdir, exist_ok=True)
+        tag = "_".join(str(a) for a in bench_args[-2:]).replace("/", "_")
+        with open(os.path.join(logdir, f"child_{tag}_{int(time.time())}.err"), "w") as f:
+            f.write(se)
     lines = [ln for ln in so.splitlines() if ln.startswith("{")]
     if child.returncode != 0 or not lines:
         raise RuntimeError(f"exited {child.returncode}: {se.strip()[-240:]}")
