@@ -9,7 +9,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--model", "bert-base", "--layers", "2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2",
-        "--seq", "64", "--no-dp-compare"]
+        "--seq", "64", "--no-dp-compare", "--no-ae"]
 
 
 def _env(**over):
