@@ -60,6 +60,7 @@ def test_bench_multi_rank_emits_comm_calibration_and_ae():
     ae = r["config"]["ae_bert"]
     assert "error" not in ae, ae
     assert ae["global_batch"] == 8 and ae["layers"] == 12
+    assert ae["isolated"]          # searched / DP runs as fresh child jobs started by rank 0
     assert ae["searched_samples_per_sec"] > 0 and ae["dp_samples_per_sec"] > 0 and ae["speedup_over_dp"] > 0
 
 
