@@ -58,8 +58,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: 128 (BERT; 64 before round 6), 256 "
-                                                                   "(ResNet-50), 1024 (DLRM), 16 (GPT-3 medium); sized "
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: 128 (BERT), 512 (ResNet-50), 1024 (DLRM), "
+                                                                   "32 (GPT-3 medium) -- 64 / 256 / 16 before round 6; sized "
                                                                    "for 288 GB of HBM per GPU (profiles/r6/g40_*, "
                                                                    "profiles/batch_sweep_r3.txt)")
     ap.add_argument("--seq", type=int, default=512)
@@ -733,14 +733,16 @@ def _parallelism(model, world: int) -> str:
 _AE_BUDGET = {"bert": 30, "gpt": 30, "dlrm": 400, "resnet50": 400, "resnext50": 20, "inception_v3": 10}
 
 _ZOO = {
-    # bench name -> (zoo name, per-GPU batch, config overrides, optimizer, extra config for the JSON line)
-    "resnet50": ("resnet50", 256, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
+    # bench name -> (zoo name, per-GPU batch, config overrides, optimizer, extra config for the JSON line);
+    # ResNet-50 512 images (22 GB step) and GPT-3 medium 32 sequences (66 GB) per GPU since round 6: same
+    # box, interleaved, +9 % and +3.4 % over 256 / 16 (profiles/r6/g42_batch_sweep.txt)
+    "resnet50": ("resnet50", 512, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
     # the reference's OSDI'22 AE CNNs (scripts/osdi22ae/resnext-50.sh, inception.sh)
     "resnext50": ("resnext50", 64, dict(image_size=224, num_classes=1000), "sgd", {"image_size": 224}),
     "inception-v3": ("inception_v3", 64, dict(image_size=299, num_classes=1000), "sgd", {"image_size": 299}),
     "dlrm": ("dlrm", 1024, dict(embedding_size=[1000000] * 8, sparse_feature_size=64, mlp_bot=[64, 512, 512, 64],
                                 mlp_top=[576, 1024, 1024, 1024, 1]), "sgd", {"tables": "8x1M", "sparse": 64}),
-    "gpt3-medium": ("gpt", 16, dict(hidden_size=1024, num_layers=24, num_heads=16, sequence_length=2048),
+    "gpt3-medium": ("gpt", 32, dict(hidden_size=1024, num_layers=24, num_heads=16, sequence_length=2048),
                     "adamw", {"seq_len": 2048, "layers": 24, "hidden": 1024}),
 }
 
