@@ -81,6 +81,38 @@ def _pick(key, cands):
 
 
 _MODE = os.environ.get("FF_CONV1X1", "auto")   # auto | native | gemm
+_WGRAD_SPLITS: dict = {}
+# opt-in: on ResNet-50 (512 / GPU) the tuned degrees matched the heuristic
+# (9714-9729 vs 9706-9709 img/s, profiles/r6/g44_wgrad_splits.txt)
+_WGRAD_TUNE = os.environ.get("FF_CONV_WGRAD_TUNE", "0") == "1"
+
+
+def _wgrad(xin, dy, dw, R, S, stride, pad):
+    """Native weight gradient with its split-K degree picked per shape: the
+    kernel's heuristic (~2048 workgroups, >= 8 K-tiles per split) against
+    explicit degrees, timed once outside graph capture on a scratch buffer
+    (candidates interleaved over two passes, best of each); under capture an
+    untuned shape keeps the heuristic."""
+    key = (tuple(xin.shape), int(dy.shape[1]), R, S, tuple(stride), tuple(pad))
+    sp = _WGRAD_SPLITS.get(key)
+    if sp is None:
+        sp = 0
+        if _WGRAD_TUNE and not torch.cuda.is_current_stream_capturing():
+            from .gemm import _time
+            N, _, P, Q = dy.shape
+            nk = (N * P * Q + 63) // 64
+            wbytes = dw.numel() * 4
+            cands = [0] + [c for c in (1, 2, 4, 8, 16, 32, 64) if nk // c >= 4 and c * wbytes <= (512 << 20)]
+            tmp = torch.zeros_like(dw)
+            times = {c: float("inf") for c in cands}
+            for _ in range(2):
+                for c in cands:
+                    times[c] = min(times[c], _time(lambda c_=c: K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad,
+                                                                             splits=c_), iters=3, rounds=1))
+            sp = min(times, key=times.get)
+            del tmp
+        _WGRAD_SPLITS[key] = sp
+    K.conv2d_wgrad(xin, dy, dw, R, S, stride, pad, splits=sp)
 
 
 def _pointwise(R, S, stride, pad, groups) -> bool:
@@ -276,19 +308,19 @@ class Conv2DOp(OpImpl):
                 key = ("wgrad", tuple(xin.shape), Kc, tuple(stride))
                 if key not in _CHOICE:
                     tmp = torch.zeros_like(dW.view(-1))
-                    _pick(key, {"native": lambda: K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad),
+                    _pick(key, {"native": lambda: _wgrad(xin, dy, tmp, R, S, stride, pad),
                                 "gemm": lambda: G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True,
                                                          out=tmp.view(Kc, Cp), beta=1.0, native_only=True)})
                 if _CHOICE[key] == "gemm":
                     G.matmul(_rows(dy), _rows(_sub(xin, stride)), trans_a=True, out=dW.view(Kc, Cp), beta=1.0,
                              native_only=True)
                 else:
-                    K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
+                    _wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
             elif Cp == xshape[1]:
-                K.conv2d_wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
+                _wgrad(xin, dy, dW.view(-1), R, S, stride, pad)
             else:  # padded stem: wgrad into a padded buffer, keep the real channels
                 tmp = torch.zeros(Kc * R * S * Cp, device=dy.device, dtype=torch.float32)
-                K.conv2d_wgrad(xin, dy, tmp, R, S, stride, pad)
+                _wgrad(xin, dy, tmp, R, S, stride, pad)
                 dW.view(Kc, R, S, xshape[1]).add_(tmp.view(Kc, R, S, Cp)[..., :xshape[1]])
         if not need_input_grad[0]:
             return [None]

@@ -72,7 +72,7 @@ def test_conv_dgrad_wgrad(case):
     K.conv2d_dgrad(dy, w, tuple(x.shape), (st, st), (pd, pd), out=acc, beta=1.0)
     assert _relerr(acc, 2 * xr.grad) < 5e-3
     dw_ref = wr.grad.permute(0, 2, 3, 1).contiguous()  # -> [K, R, S, C]
-    for splits in (0, 1, 3):
+    for splits in (0, 1, 3, 8, 64):   # the tuned degrees (ops/conv._wgrad), 64: two-pass slab reduce
         dw = torch.full((Ko * R * S * C,), 0.5, device=DEV)
         K.conv2d_wgrad(x, dy, dw, R, S, (st, st), (pd, pd), splits=splits)
         assert _relerr(dw.view_as(dw_ref).double().cpu() - 0.5, dw_ref) < 1e-5
