@@ -374,16 +374,12 @@ def _search_record(model, world):
 
 
 def _arena_bytes(model, ex, world, bytes_per_param):
-    """The step's device arena: the liveness plan's peak minus the resident
-    weights / optimizer state (allocated at compile time, outside the
-    arena), +15 % and 2 GiB for workspaces and the block cache's slack."""
+    """The step's device arena (runtime/arena.plan_bytes): the liveness plan's
+    peak minus the resident weights / optimizer state, +15 % and 2 GiB."""
     import torch
-    from flexflow_train_amd.search import native
-    bf16 = getattr(ex.cfg, "compute_dtype", None) == torch.bfloat16
-    plans = native.plan_memory(model.pcg, world, model.views, weight_bytes_per_param=bytes_per_param,
-                               act_elem_bytes=2.0 if bf16 else 0.0, executor_fusions=True)
-    p = plans[min(ex.dist.rank, len(plans) - 1)]
-    return int(max(0.0, p["arena_bytes"] - p["weight_bytes"]) * 1.15 + (2 << 30))
+    from flexflow_train_amd.runtime.arena import plan_bytes
+    return plan_bytes(model.pcg, model.views, world, ex.dist.rank, bytes_per_param,
+                      getattr(ex.cfg, "compute_dtype", None) == torch.bfloat16)
 
 
 def _time_steps(args, ex, feeds, labels, global_batch, model=None, bytes_per_param=16.0):

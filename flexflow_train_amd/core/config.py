@@ -72,6 +72,7 @@ class FFConfig:
     # strategy search prices pipeline-parallel stage splits at that count
     micro_batches: int = 1
     enable_hipgraph: bool = True       # fit(): capture the training iteration as a hipGraph (1 GPU)
+    device_arena: bool = False         # 1 GPU: the step allocates from a plan-sized device arena (runtime/arena.py)
     parameter_sync: str = "nccl"       # "nccl" (all-reduce) | "ps" (reference ParamSync::PS)
     cpu_only: bool = False             # run on the host even when a GPU is visible
     local_execution: bool = False      # train on the native C++ CPU executor (lib/local-execution parity)
@@ -179,6 +180,7 @@ def build_arg_parser() -> argparse.ArgumentParser:
     a("--bucket-mb", dest="bucket_mb", type=int)
     a("--micro-batches", dest="micro_batches", type=int)
     a("--disable-hipgraph", dest="enable_hipgraph", action="store_const", const=False)
+    a("--device-arena", dest="device_arena", action="store_const", const=True)
     a("--python-data-loader", dest="native_data_loader", action="store_const", const=False)
     a("--local-execution", dest="local_execution", action="store_const", const=True)
     a("--cpu", dest="cpu_only", action="store_const", const=True)

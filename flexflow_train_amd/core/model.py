@@ -645,6 +645,14 @@ class FFModel:
                                  valid_classes=self.valid_classes)
         self.executor.init_parameters()
         self.executor.constants = dict(self._constants)
+        if (getattr(self.ffconfig, "device_arena", False) and self.executor.cfg.device.type == "cuda"
+                and self.dist.world == 1):
+            # the step's activations / gradients / workspaces out of one
+            # plan-sized device region (runtime/arena.py, csrc/runtime/arena.cpp)
+            from ..runtime import arena as _arena
+            self.executor.enable_arena(_arena.plan_bytes(
+                self.pcg, self.views, 1, 0, _arena.bytes_per_param(self._optimizer.cfg),
+                self.executor.cfg.compute_dtype == torch.bfloat16))
         self.local_backing = None
         if self.ffconfig.local_execution:
             self._init_local_backing(loss_type)

@@ -80,5 +80,27 @@ class Arena:
         self._lib.ff_arena_reset_high(self.index)
 
 
+def bytes_per_param(optimizer_cfg) -> float:
+    """Resident bytes per parameter outside the arena: fp32 master + bf16
+    compute copy + gradient + optimizer state (Adam: two moments, SGD with
+    momentum: one)."""
+    from .optimizer import AdamConfig
+    if isinstance(optimizer_cfg, AdamConfig):
+        return 16.0
+    return 14.0 if getattr(optimizer_cfg, "momentum", 0.0) else 10.0
+
+
+def plan_bytes(pcg, views, world: int, rank: int, bytes_per_param: float, bf16: bool) -> int:
+    """Arena size for one rank's step: the liveness plan's peak
+    (csrc/ffcore/src/memory_plan.cc, executor fusions) minus the resident
+    weights / optimizer state, +15 % and 2 GiB for workspaces and the block
+    cache's slack."""
+    from ..search import native
+    plans = native.plan_memory(pcg, world, views, weight_bytes_per_param=bytes_per_param,
+                               act_elem_bytes=2.0 if bf16 else 0.0, executor_fusions=True)
+    p = plans[min(rank, len(plans) - 1)]
+    return int(max(0.0, p["arena_bytes"] - p["weight_bytes"]) * 1.15 + (2 << 30))
+
+
 def maybe(arena: Optional[Arena]):
     return arena.use() if arena is not None else contextlib.nullcontext()

@@ -77,3 +77,30 @@ def test_training_step_out_of_the_arena():
     _, pb = _bert(0)
     for n in pa:
         torch.testing.assert_close(pa[n], pb[n], rtol=2e-2, atol=2e-3)
+
+
+def test_ffconfig_device_arena():
+    """FFConfig.device_arena: compile() sizes the arena from the liveness plan
+    and the model's training steps (eager and graphed) allocate from it."""
+    import numpy as np
+    from flexflow_train_amd import models as Z
+    from flexflow_train_amd.core import AdamOptimizer, FFConfig, FFModel, LossType, MetricsType
+
+    cfg = FFConfig()
+    cfg.device_arena = True
+    m = FFModel(cfg)
+    inputs, out, mc = Z.build("bert", m, batch_size=4, hidden_size=256, num_encoder_layers=2, num_heads=4,
+                              dim_feedforward=1024, sequence_length=64, vocab_size=512)
+    m.compile(optimizer=AdamOptimizer(m, alpha=1e-3), loss_type=LossType.LOSS_SPARSE_CATEGORICAL_CROSSENTROPY,
+              metrics=[MetricsType.METRICS_ACCURACY])
+    ex = m.executor
+    assert ex.arena is not None
+    fn, ln = Z.synthetic("bert", mc, inputs, np.random.default_rng(0))
+    feeds = {k: ex._local_piece(k, torch.as_tensor(v)) for k, v in fn.items()}
+    labels = ex.local_labels(torch.as_tensor(ln))
+    ex.train_step(feeds, labels)
+    step = ex.make_graphed_train_step(feeds, labels, warmup=1)
+    step()
+    torch.cuda.synchronize()
+    st = ex.arena.stats()
+    assert st["capacity_gb"] > 0 and st["segments"] > 0 and st["overflow_segments"] == 0, st
